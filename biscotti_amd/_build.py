@@ -1,0 +1,118 @@
+"""In-tree build of the native parts of biscotti_amd.
+
+* ``_biscotti_rt``  -- host runtime (C++17, pybind11): crypto, ledger, protocol FSM.
+* ``libbiscotti_hip.so`` -- CDNA4 (gfx950) HIP kernels with a C ABI, loaded through ctypes.
+
+Both land next to this file, so a ``gpurun`` snapshot carries them to the GPU box.  Builds are
+incremental (per-object mtime check) and parallel.
+
+Usage: ``python -m biscotti_amd._build [--runtime] [--kernels] [--force]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+BUILD = PKG.parent / "build"
+RT_NAME = "_biscotti_rt" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
+HIP_LIB = "libbiscotti_hip.so"
+ARCH = os.environ.get("BISCOTTI_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _jobs() -> int:
+    try:
+        n = int(os.environ.get("MAX_JOBS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(n or (os.cpu_count() or 4), 16))
+
+
+def _stale(obj: Path, deps: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[0]} {cmd[-1]}")
+
+
+def _compile_many(jobs: list[tuple[list[str], Path, list[Path]]], force: bool) -> list[Path]:
+    todo = [(c, o) for c, o, deps in jobs if force or _stale(o, deps)]
+    if todo:
+        with cf.ThreadPoolExecutor(_jobs()) as ex:
+            list(ex.map(lambda co: _run(co[0]), todo))
+    return [o for _, o, _ in jobs]
+
+
+def build_runtime(force: bool = False) -> Path:
+    src_dir = CSRC / "runtime"
+    out_dir = BUILD / "runtime"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    import pybind11
+
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{src_dir}"]
+    headers = sorted(src_dir.glob("*.hpp"))
+    flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-sign-compare"]
+    extra = os.environ.get("BISCOTTI_RT_CXXFLAGS", "").split()
+    jobs = []
+    for src in sorted(src_dir.glob("*.cpp")):
+        obj = out_dir / (src.stem + ".o")
+        jobs.append((["g++", *flags, *extra, *inc, "-c", str(src), "-o", str(obj)], obj, [src, *headers]))
+    objs = _compile_many(jobs, force)
+    target = PKG / RT_NAME
+    if force or _stale(target, objs):
+        _run(["g++", "-shared", "-pthread", *extra, "-o", str(target), *map(str, objs)])
+    return target
+
+
+def build_kernels(force: bool = False) -> Path:
+    if not Path(HIPCC).exists() and shutil.which("hipcc") is None:
+        raise RuntimeError("hipcc not found; cannot build the gfx950 kernels")
+    hipcc = HIPCC if Path(HIPCC).exists() else shutil.which("hipcc")
+    src_dir = CSRC / "kernels"
+    out_dir = BUILD / "kernels"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    headers = sorted(src_dir.glob("*.h")) + sorted(src_dir.glob("*.hpp"))
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", f"-I{src_dir}"]
+    extra = os.environ.get("BISCOTTI_HIP_FLAGS", "").split()
+    jobs = []
+    for src in sorted(src_dir.glob("*.hip")):
+        obj = out_dir / (src.stem + ".o")
+        jobs.append(([hipcc, *flags, *extra, "-c", str(src), "-o", str(obj)], obj, [src, *headers]))
+    objs = _compile_many(jobs, force)
+    target = PKG / HIP_LIB
+    if force or _stale(target, objs):
+        _run([hipcc, "-shared", f"--offload-arch={ARCH}", "-o", str(target), *map(str, objs)])
+    return target
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--runtime", action="store_true")
+    ap.add_argument("--kernels", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args(argv)
+    both = not (a.runtime or a.kernels)
+    if a.runtime or both:
+        print("built", build_runtime(a.force))
+    if a.kernels or both:
+        print("built", build_kernels(a.force))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,450 @@
+// pybind11 module `_biscotti_rt`: the native host runtime of biscotti_amd.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <thread>
+
+#include "bn256.hpp"
+#include "hash.hpp"
+#include "keys.hpp"
+#include "ledger.hpp"
+#include "protocol.hpp"
+#include "shares.hpp"
+#include "vrf.hpp"
+
+namespace py = pybind11;
+using namespace bsc;
+
+static Bytes B(const py::bytes& b) {
+  std::string s = b;
+  return Bytes(s.begin(), s.end());
+}
+static py::bytes P(const Bytes& b) { return py::bytes(reinterpret_cast<const char*>(b.data()), b.size()); }
+
+static U256 u256_from_pyint(const py::int_& v) {
+  // accepts non-negative python ints < 2^256
+  py::object to_bytes = v.attr("to_bytes");
+  py::bytes b = to_bytes(32, "big");
+  std::string s = b;
+  return U256::from_be(reinterpret_cast<const u8*>(s.data()));
+}
+static py::int_ pyint_from_u256(const U256& v) {
+  Bytes b(32);
+  v.to_be(b.data());
+  return py::int_(py::module_::import("builtins").attr("int").attr("from_bytes")(P(b), "big"));
+}
+
+// Parallel-for over host threads (VRF proofs, Schnorr signatures of many local peers).
+template <class F>
+static void parallel_for(size_t n, int threads, F f) {
+  if (threads <= 1 || n <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> ts;
+  std::atomic<size_t> next{0};
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&] {
+      for (;;) {
+        size_t i = next.fetch_add(1);
+        if (i >= n) break;
+        f(i);
+      }
+    });
+  for (auto& t : ts) t.join();
+}
+
+struct CommitKey {
+  std::vector<G1> pk;
+  size_t dim() const { return pk.size(); }
+};
+
+static py::array_t<uint32_t> g1_affine_u32(const std::vector<G1>& pts) {
+  // [n, 16] uint32 : Montgomery affine x (8 LE limbs), y (8 LE limbs); infinity -> zeros
+  py::array_t<uint32_t> out({py::ssize_t(pts.size()), py::ssize_t(16)});
+  auto o = out.mutable_unchecked<2>();
+  for (size_t i = 0; i < pts.size(); ++i) {
+    U256 ax, ay;
+    pts[i].to_affine(ax, ay);
+    for (int k = 0; k < 4; ++k) {
+      o(i, 2 * k) = uint32_t(ax.w[k]);
+      o(i, 2 * k + 1) = uint32_t(ax.w[k] >> 32);
+      o(i, 8 + 2 * k) = uint32_t(ay.w[k]);
+      o(i, 8 + 2 * k + 1) = uint32_t(ay.w[k] >> 32);
+    }
+  }
+  return out;
+}
+
+static G1 g1_from_jac_u32(const uint32_t* p) {
+  G1 g;
+  for (int k = 0; k < 4; ++k) {
+    g.x.w[k] = u64(p[2 * k]) | (u64(p[2 * k + 1]) << 32);
+    g.y.w[k] = u64(p[8 + 2 * k]) | (u64(p[8 + 2 * k + 1]) << 32);
+    g.z.w[k] = u64(p[16 + 2 * k]) | (u64(p[16 + 2 * k + 1]) << 32);
+  }
+  return g;
+}
+
+PYBIND11_MODULE(_biscotti_rt, m) {
+  m.doc() = "biscotti_amd native host runtime (crypto, ledger, protocol FSM)";
+
+  // ---------------------------------------------------------------- hashing
+  m.def("sha256", [](py::bytes d) { return P(Sha256::digest(B(d))); });
+  m.def("sha512", [](py::bytes d) { return P(Sha512::digest(B(d))); });
+  m.def("blake2b", [](py::bytes d, int outlen, py::bytes key) {
+    Bytes k = B(key), x = B(d);
+    Blake2b h;
+    h.init(size_t(outlen), k.data(), k.size());
+    h.update(x.data(), x.size());
+    Bytes o(static_cast<size_t>(outlen));
+    h.final(o.data());
+    return P(o);
+  }, py::arg("data"), py::arg("outlen") = 64, py::arg("key") = py::bytes(""));
+  m.def("blake2b_param", [](py::bytes param, py::bytes d) {
+    Bytes p = B(param), x = B(d);
+    if (p.size() != 64) throw std::runtime_error("param block must be 64 bytes");
+    Blake2b h;
+    h.init_param(p.data(), nullptr, 0);
+    h.update(x.data(), x.size());
+    Bytes o(h.outlen);
+    h.final(o.data());
+    return P(o);
+  });
+  m.def("blake2xb", [](py::bytes seed, py::bytes msg, size_t n) {
+    Blake2Xb x(B(seed));
+    x.write(B(msg));
+    Bytes o(n);
+    x.read(o.data(), n);
+    return P(o);
+  });
+
+  // ---------------------------------------------------------------- bn256
+  m.def("bn256_prime", [] { return pyint_from_u256(PRIME()); });
+  m.def("bn256_order", [] { return pyint_from_u256(ORDER()); });
+  m.def("g1_generator", [] { return P(G1::generator().marshal()); });
+  m.def("g1_infinity", [] { return P(G1::infinity().marshal()); });
+  m.def("g1_add", [](py::bytes a, py::bytes b) { return P(G1::unmarshal(B(a)).add(G1::unmarshal(B(b))).marshal()); });
+  m.def("g1_neg", [](py::bytes a) { return P(G1::unmarshal(B(a)).neg().marshal()); });
+  m.def("g1_mul", [](py::bytes a, py::int_ k) { return P(G1::unmarshal(B(a)).mul(u256_from_pyint(k)).marshal()); });
+  m.def("g1_mul_i64", [](py::bytes a, int64_t k) { return P(G1::unmarshal(B(a)).mul_i64(k).marshal()); });
+  m.def("g1_base_mul", [](py::int_ k) { return P(gen_table().mul(u256_from_pyint(k)).marshal()); });
+  m.def("g1_is_valid", [](py::bytes a) {
+    try { G1::unmarshal(B(a)); return true; } catch (...) { return false; }
+  });
+  m.def("g1_affine_mont_u32", [](py::bytes a) { return g1_affine_u32({G1::unmarshal(B(a))}); });
+  m.def("g1_marshal_jac_u32", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> jac) {
+    // [n, 24] Montgomery Jacobian limbs (device layout) -> list of 64-byte marshals
+    if (jac.ndim() != 2 || jac.shape(1) != 24) throw std::runtime_error("expected [n, 24] uint32");
+    py::list out;
+    for (py::ssize_t i = 0; i < jac.shape(0); ++i) out.append(P(g1_from_jac_u32(jac.data(i, 0)).marshal()));
+    return out;
+  });
+  m.def("g1_sum_jac_u32", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> jac) {
+    G1 acc = G1::infinity();
+    for (py::ssize_t i = 0; i < jac.shape(0); ++i) acc = acc.add(g1_from_jac_u32(jac.data(i, 0)));
+    return P(acc.marshal());
+  });
+  m.def("g2_generator", [] { return P(G2::generator().marshal()); });
+  m.def("g2_mul", [](py::bytes a, py::int_ k) { return P(G2::unmarshal(B(a)).mul(u256_from_pyint(k)).marshal()); });
+  m.def("g2_add", [](py::bytes a, py::bytes b) { return P(G2::unmarshal(B(a)).add(G2::unmarshal(B(b))).marshal()); });
+  m.def("g2_is_valid", [](py::bytes a) {
+    try { G2::unmarshal(B(a)); return true; } catch (...) { return false; }
+  });
+  m.def("scalar_from_i64", [](int64_t v) { return P(Scalar::from_i64(v).to_be()); });
+
+  // ---------------------------------------------------------------- Schnorr
+  m.def("schnorr_sign", [](py::bytes msg, py::bytes sk, py::bytes nonce) {
+    return P(schnorr_sign(B(msg), Scalar::from_be(B(sk)), B(nonce)));
+  });
+  m.def("schnorr_verify", [](py::bytes msg, py::bytes pk, py::bytes sig) {
+    return schnorr_verify(B(msg), G1::unmarshal(B(pk)), B(sig));
+  });
+  m.def("schnorr_sign_batch", [](std::vector<py::bytes> msgs, py::bytes sk, std::vector<py::bytes> nonces, int threads) {
+    std::vector<Bytes> ms, ns, out(msgs.size());
+    for (auto& x : msgs) ms.push_back(B(x));
+    for (auto& x : nonces) ns.push_back(B(x));
+    Scalar s = Scalar::from_be(B(sk));
+    (void)gen_table();
+    {
+      py::gil_scoped_release rel;
+      parallel_for(ms.size(), threads, [&](size_t i) { out[i] = schnorr_sign(ms[i], s, ns[i]); });
+    }
+    std::vector<py::bytes> r;
+    for (auto& o : out) r.push_back(P(o));
+    return r;
+  });
+  m.def("client_key_from_entropy", [](py::bytes e) {
+    auto kp = client_key_from_entropy(B(e));
+    return py::make_tuple(P(kp.first.to_be()), P(kp.second.marshal()));
+  });
+
+  // ---------------------------------------------------------------- VRF
+  m.def("vrf_public_key", [](py::bytes seed) { return P(VrfKey::from_seed(B(seed)).pk); });
+  m.def("ed25519_public_key", [](py::bytes seed) { return P(ed25519_public_from_seed(B(seed))); });
+  m.def("vrf_prove", [](py::bytes seed, py::bytes alpha) {
+    auto r = vrf_prove(VrfKey::from_seed(B(seed)), B(alpha));
+    return py::make_tuple(P(r.first), P(r.second));
+  });
+  m.def("vrf_verify", [](py::bytes pk, py::bytes alpha, py::bytes pi) -> py::object {
+    Bytes beta;
+    if (!vrf_verify(B(pk), B(alpha), B(pi), &beta)) return py::none();
+    return P(beta);
+  });
+  m.def("vrf_prove_batch", [](std::vector<py::bytes> seeds, py::bytes alpha, int threads) {
+    std::vector<Bytes> ss;
+    for (auto& s : seeds) ss.push_back(B(s));
+    Bytes a = B(alpha);
+    std::vector<std::pair<Bytes, Bytes>> out(ss.size());
+    {
+      py::gil_scoped_release rel;
+      parallel_for(ss.size(), threads, [&](size_t i) { out[i] = vrf_prove(VrfKey::from_seed(ss[i]), a); });
+    }
+    py::list r;
+    for (auto& o : out) r.append(py::make_tuple(P(o.first), P(o.second)));
+    return r;
+  });
+
+  // ---------------------------------------------------------------- keys
+  py::class_<CommitKey>(m, "CommitKey")
+      .def_static("generate", [](size_t d, int64_t s) {
+        CommitKey k; k.pk = gen_commit_key_g1(d, Scalar::from_i64(s)); return k;
+      }, py::arg("d"), py::arg("secret") = 2)
+      .def_static("load", [](const std::string& path, size_t d, bool check_g2) {
+        CommitKey k; k.pk = read_commit_key(path, d, check_g2); return k;
+      }, py::arg("path"), py::arg("d"), py::arg("check_g2") = false)
+      .def_static("from_points", [](std::vector<py::bytes> pts) {
+        CommitKey k; for (auto& p : pts) k.pk.push_back(G1::unmarshal(B(p))); return k;
+      })
+      .def("__len__", &CommitKey::dim)
+      .def("point", [](const CommitKey& k, size_t i) { return P(k.pk.at(i).marshal()); })
+      .def("affine_mont_u32", [](const CommitKey& k) { return g1_affine_u32(k.pk); })
+      .def("witness_bases_affine_u32", [](const CommitKey& k, int64_t poly, int64_t total) {
+        return g1_affine_u32(witness_bases(k.pk, int64_t(k.pk.size()), poly, total));
+      })
+      .def("commit", [](const CommitKey& k, py::array_t<int64_t, py::array::c_style | py::array::forcecast> c, size_t off) {
+        std::vector<i64> v(c.data(), c.data() + c.size());
+        G1 r;
+        { py::gil_scoped_release rel; r = commit(v, k.pk, off); }
+        return P(r.marshal());
+      }, py::arg("coeffs"), py::arg("offset") = 0)
+      .def("make_shares", [](const CommitKey& k, py::array_t<int64_t, py::array::c_style | py::array::forcecast> c,
+                             int64_t poly, int64_t total) {
+        std::vector<i64> v(c.data(), c.data() + c.size());
+        SharePackage sp;
+        { py::gil_scoped_release rel; sp = make_shares(v, k.pk, poly, total); }
+        size_t nch = sp.chunk_commit.size();
+        py::array_t<int64_t> ys({py::ssize_t(nch), py::ssize_t(total)});
+        std::memcpy(ys.mutable_data(), sp.ys.data(), sp.ys.size() * 8);
+        py::list cc, wit;
+        for (auto& g : sp.chunk_commit) cc.append(P(g.marshal()));
+        for (auto& g : sp.witnesses) wit.append(P(g.marshal()));
+        return py::make_tuple(P(sp.commitment.marshal()), cc, ys, wit);
+      });
+  m.def("write_commit_key", [](const std::string& path, size_t d, int64_t s) { write_commit_key(path, d, Scalar::from_i64(s)); },
+        py::arg("path"), py::arg("d"), py::arg("secret") = 2);
+  m.def("write_client_keys", [](const std::string& path, std::vector<std::pair<py::bytes, py::bytes>> keys) {
+    std::vector<std::pair<Scalar, G1>> ks;
+    for (auto& kv : keys) ks.push_back({Scalar::from_be(B(kv.first)), G1::unmarshal(B(kv.second))});
+    write_client_keys(path, ks);
+  });
+  m.def("read_client_keys", [](const std::string& path) {
+    py::list out;
+    for (auto& kv : read_client_keys(path)) out.append(py::make_tuple(P(kv.first.to_be()), P(kv.second.marshal())));
+    return out;
+  });
+  m.def("base64_encode", [](py::bytes b) { return base64_encode(B(b)); });
+  m.def("base64_decode", [](const std::string& s) { return P(base64_decode(s)); });
+  m.def("key_record_json", [](int64_t id, py::bytes pk, py::bytes sk) { return key_record_json({id, B(pk), B(sk)}); });
+
+  // ---------------------------------------------------------------- shares (exact host reference)
+  m.def("quantize", [](py::array_t<double, py::array::c_style | py::array::forcecast> v, int prec) {
+    std::vector<double> x(v.data(), v.data() + v.size());
+    auto q = quantize(x, prec);
+    py::array_t<int64_t> out(py::ssize_t(q.size()));
+    std::memcpy(out.mutable_data(), q.data(), q.size() * 8);
+    return out;
+  });
+  m.def("chunk_stops", &chunk_stops);
+  m.def("share_xs", &share_xs);
+  m.def("poly_eval", [](std::vector<i64> c, i64 x) { return poly_eval(c.data(), int(c.size()), x); });
+  m.def("poly_quotient", [](std::vector<i64> c, i64 x) { return poly_quotient(c.data(), int(c.size()), x); });
+  m.def("recover_exact", [](std::vector<i64> xs, std::vector<i64> ys, int deg) -> py::object {
+    std::vector<i64> out;
+    if (!recover_exact(xs, ys, deg, &out)) return py::none();
+    return py::cast(out);
+  });
+  m.def("recover_lstsq", &recover_lstsq);
+
+  // ---------------------------------------------------------------- ledger
+  py::class_<Update>(m, "Update")
+      .def(py::init<>())
+      .def_readwrite("source_id", &Update::source_id)
+      .def_readwrite("iteration", &Update::iteration)
+      .def_readwrite("delta", &Update::delta)
+      .def_property("commitment", [](const Update& u) { return P(u.commitment); },
+                    [](Update& u, py::bytes b) { u.commitment = B(b); })
+      .def_readwrite("noise", &Update::noise)
+      .def_readwrite("noised_delta", &Update::noised_delta)
+      .def_readwrite("accepted", &Update::accepted)
+      .def_property("signatures", [](const Update& u) {
+        std::vector<py::bytes> r; for (auto& s : u.signatures) r.push_back(P(s)); return r;
+      }, [](Update& u, std::vector<py::bytes> v) { u.signatures.clear(); for (auto& s : v) u.signatures.push_back(B(s)); })
+      .def("__str__", &update_string);
+  py::class_<BlockData>(m, "BlockData")
+      .def(py::init<>())
+      .def_readwrite("iteration", &BlockData::iteration)
+      .def_property("global_w",
+                    [](const BlockData& d) { return py::array_t<double>(py::ssize_t(d.global_w.size()), d.global_w.data()); },
+                    [](BlockData& d, py::array_t<double, py::array::c_style | py::array::forcecast> a) {
+                      d.global_w.assign(a.data(), a.data() + a.size());
+                    })
+      .def_readwrite("deltas", &BlockData::deltas)
+      .def("gob", [](const BlockData& d) { return P(gob_encode_blockdata(d)); })
+      .def("__str__", &blockdata_string);
+  py::class_<Block>(m, "Block")
+      .def(py::init<>())
+      .def_readwrite("timestamp", &Block::timestamp)
+      .def_readwrite("data", &Block::data)
+      .def_property("prev_hash", [](const Block& b) { return P(b.prev_hash); }, [](Block& b, py::bytes x) { b.prev_hash = B(x); })
+      .def_property("hash", [](const Block& b) { return P(b.hash); }, [](Block& b, py::bytes x) { b.hash = B(x); })
+      .def_readwrite("stake", &Block::stake)
+      .def("compute_hash", [](const Block& b) { return P(b.compute_hash()); })
+      .def("set_hash", &Block::set_hash)
+      .def("serialize", [](const Block& b) { return P(Blockchain::serialize_block(b)); })
+      .def_static("deserialize", [](py::bytes x) {
+        Bytes v = B(x);
+        size_t used = 0;
+        return Blockchain::deserialize_block(v.data(), v.size(), &used);
+      });
+  py::class_<Blockchain>(m, "Blockchain")
+      .def_static("with_genesis", &Blockchain::with_genesis)
+      .def_static("genesis", &Blockchain::genesis)
+      .def_static("load", &Blockchain::load)
+      .def_static("append_to_file", &Blockchain::append_to_file)
+      .def("save", &Blockchain::save)
+      .def("__len__", [](const Blockchain& c) { return c.blocks.size(); })
+      .def("block", [](const Blockchain& c, size_t i) { return c.blocks.at(i); })
+      .def("latest", [](const Blockchain& c) { return c.latest(); })
+      .def("get", [](const Blockchain& c, i64 it) -> py::object {
+        const Block* b = c.get(it);
+        if (!b) return py::none();
+        return py::cast(*b);
+      })
+      .def("add_block", &Blockchain::add_block)
+      .def("append", &Blockchain::append)
+      .def("verify", [](const Blockchain& c) {
+        std::string why;
+        bool ok = c.verify(&why);
+        return py::make_tuple(ok, why);
+      })
+      .def("print_chain", &Blockchain::print_chain)
+      .def("truncate", [](Blockchain& c, size_t n) { if (n < c.blocks.size()) c.blocks.resize(n); });
+  m.def("gob_uint", [](uint64_t x) { Bytes b; gob_put_uint(b, x); return P(b); });
+  m.def("gob_int", [](int64_t x) { Bytes b; gob_put_int(b, x); return P(b); });
+  m.def("gob_float", [](double x) { Bytes b; gob_put_float(b, x); return P(b); });
+  m.def("go_format_float", &go_format_float);
+
+  // ---------------------------------------------------------------- protocol
+  py::class_<ProtocolConfig>(m, "ProtocolConfig")
+      .def(py::init<>())
+      .def_readwrite("num_nodes", &ProtocolConfig::num_nodes)
+      .def_readwrite("num_verifiers", &ProtocolConfig::num_verifiers)
+      .def_readwrite("num_miners", &ProtocolConfig::num_miners)
+      .def_readwrite("num_noisers", &ProtocolConfig::num_noisers)
+      .def_readwrite("secure_agg", &ProtocolConfig::secure_agg)
+      .def_readwrite("noising", &ProtocolConfig::noising)
+      .def_readwrite("verification", &ProtocolConfig::verification)
+      .def_readwrite("epsilon", &ProtocolConfig::epsilon)
+      .def_readwrite("poisoning", &ProtocolConfig::poisoning)
+      .def_readwrite("perc_samples", &ProtocolConfig::perc_samples)
+      .def_readwrite("rand_sample", &ProtocolConfig::rand_sample)
+      .def_readwrite("colluders", &ProtocolConfig::colluders)
+      .def_readwrite("defense", &ProtocolConfig::defense)
+      .def_readwrite("poly_size", &ProtocolConfig::poly_size)
+      .def_readwrite("precision", &ProtocolConfig::precision)
+      .def_readwrite("max_iterations", &ProtocolConfig::max_iterations)
+      .def_readwrite("default_stake", &ProtocolConfig::default_stake)
+      .def_readwrite("stake_unit", &ProtocolConfig::stake_unit)
+      .def_readwrite("seed", &ProtocolConfig::seed)
+      .def_readonly("num_samples", &ProtocolConfig::num_samples)
+      .def_readonly("krum_thresh", &ProtocolConfig::krum_thresh)
+      .def_readonly("total_shares", &ProtocolConfig::total_shares)
+      .def_readonly("shares_per_miner", &ProtocolConfig::shares_per_miner)
+      .def_readonly("miner_share_thresh", &ProtocolConfig::miner_share_thresh)
+      .def_readonly("poisoning_index", &ProtocolConfig::poisoning_index)
+      .def_readonly("collusion_thresh", &ProtocolConfig::collusion_thresh)
+      .def("derive", &ProtocolConfig::derive);
+  py::class_<RoundPlan>(m, "RoundPlan")
+      .def_readonly("iteration", &RoundPlan::iteration)
+      .def_readonly("verifiers", &RoundPlan::verifiers)
+      .def_readonly("miners", &RoundPlan::miners)
+      .def_readonly("workers", &RoundPlan::workers)
+      .def_readonly("leader", &RoundPlan::leader)
+      .def_readonly("live", &RoundPlan::live)
+      .def_readonly("done", &RoundPlan::done);
+  py::class_<RoundFSM::LeaderView>(m, "LeaderView")
+      .def_readonly("leader_online", &RoundFSM::LeaderView::leader_online)
+      .def_readonly("quorum", &RoundFSM::LeaderView::quorum)
+      .def_readonly("node_list", &RoundFSM::LeaderView::node_list)
+      .def_readonly("contributing_miners", &RoundFSM::LeaderView::contributing_miners);
+  py::class_<RoundFSM>(m, "RoundFSM")
+      .def(py::init<const ProtocolConfig&, i64>())
+      .def_readonly("cfg", &RoundFSM::cfg)
+      .def_readwrite("chain", &RoundFSM::chain)
+      .def_readwrite("stake", &RoundFSM::stake)
+      .def_readwrite("iteration", &RoundFSM::iteration)
+      .def_readwrite("addresses", &RoundFSM::addresses)
+      .def_readonly("plan", &RoundFSM::plan)
+      .def("begin_round", &RoundFSM::begin_round, py::return_value_policy::copy)
+      .def("verifier_inbox", &RoundFSM::verifier_inbox)
+      .def("krum_clip", &RoundFSM::krum_clip)
+      .def("approve", [](const RoundFSM& f, const std::map<i64, std::vector<i64>>& acc) {
+        bool online = false;
+        auto a = f.approve(acc, &online);
+        return py::make_tuple(a, online);
+      })
+      .def("route_shares", &RoundFSM::route_shares)
+      .def("leader_view", &RoundFSM::leader_view)
+      .def("route_updates", &RoundFSM::route_updates)
+      .def("make_secagg_block", [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w,
+                                   std::vector<i64> nodes, std::vector<py::bytes> comms, i64 now) {
+        std::vector<Bytes> cs;
+        for (auto& c : comms) cs.push_back(B(c));
+        return f.make_secagg_block(std::vector<double>(w.data(), w.data() + w.size()), nodes, cs, now);
+      })
+      .def("make_plain_block", [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w,
+                                  const std::vector<Update>& ups, i64 now) {
+        return f.make_plain_block(std::vector<double>(w.data(), w.data() + w.size()), ups, now);
+      })
+      .def("make_empty_block", &RoundFSM::make_empty_block)
+      .def("commit_block", &RoundFSM::commit_block)
+      .def("is_poisoner", &RoundFSM::is_poisoner, py::arg("id"), py::arg("fedsys") = false)
+      .def("is_colluder", &RoundFSM::is_colluder)
+      .def("round_seed", &RoundFSM::round_seed);
+  m.def("select_roles", [](const std::map<i64, i64>& stake, py::bytes h, i64 nv, i64 na, i64 n) {
+    std::vector<i64> v, mm;
+    select_roles(stake, B(h), nv, na, n, &v, &mm);
+    return py::make_tuple(v, mm);
+  });
+  m.def("select_noisers", [](const std::map<i64, i64>& stake, py::bytes out, i64 self, i64 nn, i64 n) {
+    return select_noisers(stake, B(out), self, nn, n);
+  });
+  m.def("krum_scores", [](py::array_t<double, py::array::c_style | py::array::forcecast> X, i64 groupsize) {
+    if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
+    return krum_scores(X.data(), X.shape(0), X.shape(1), groupsize);
+  });
+  m.def("krum_select", &krum_select);
+  m.def("seeded_permutation", &seeded_permutation);
+  py::class_<FedSysConfig>(m, "FedSysConfig")
+      .def(py::init<>())
+      .def_readwrite("num_nodes", &FedSysConfig::num_nodes)
+      .def_readwrite("perc_samples", &FedSysConfig::perc_samples)
+      .def_readwrite("rand_sample", &FedSysConfig::rand_sample)
+      .def_readwrite("poisoning", &FedSysConfig::poisoning)
+      .def_readonly("num_samples", &FedSysConfig::num_samples)
+      .def_readonly("random_samples", &FedSysConfig::random_samples)
+      .def("derive", &FedSysConfig::derive);
+  m.def("fedsys_select", &fedsys_select);
+}

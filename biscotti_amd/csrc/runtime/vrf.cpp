@@ -1,0 +1,420 @@
+#include "vrf.hpp"
+
+#include "hash.hpp"
+
+namespace bsc {
+namespace {
+
+// ---------------------------------------------------------------- GF(2^255-19), radix 2^51
+struct Fe { u64 v[5]; };
+constexpr u64 MASK51 = (u64(1) << 51) - 1;
+
+Fe fe_zero() { return Fe{{0, 0, 0, 0, 0}}; }
+Fe fe_one() { return Fe{{1, 0, 0, 0, 0}}; }
+
+Fe fe_carry(Fe a) {
+  for (int k = 0; k < 2; ++k) {
+    u64 c;
+    c = a.v[0] >> 51; a.v[0] &= MASK51; a.v[1] += c;
+    c = a.v[1] >> 51; a.v[1] &= MASK51; a.v[2] += c;
+    c = a.v[2] >> 51; a.v[2] &= MASK51; a.v[3] += c;
+    c = a.v[3] >> 51; a.v[3] &= MASK51; a.v[4] += c;
+    c = a.v[4] >> 51; a.v[4] &= MASK51; a.v[0] += c * 19;
+  }
+  return a;
+}
+Fe fe_add(const Fe& a, const Fe& b) {
+  Fe r;
+  for (int i = 0; i < 5; ++i) r.v[i] = a.v[i] + b.v[i];
+  return fe_carry(r);
+}
+Fe fe_sub(const Fe& a, const Fe& b) {
+  // add 4p to keep limbs positive
+  static const u64 p4[5] = {0x1FFFFFFFFFFFB4ULL * 1, 0x1FFFFFFFFFFFFCULL, 0x1FFFFFFFFFFFFCULL,
+                            0x1FFFFFFFFFFFFCULL, 0x1FFFFFFFFFFFFCULL};
+  Fe r;
+  for (int i = 0; i < 5; ++i) r.v[i] = a.v[i] + p4[i] - b.v[i];
+  return fe_carry(r);
+}
+Fe fe_neg(const Fe& a) { return fe_sub(fe_zero(), a); }
+Fe fe_mul(const Fe& a, const Fe& b) {
+  u128 t[5];
+  const u64 *x = a.v, *y = b.v;
+  u64 y19[5];
+  for (int i = 0; i < 5; ++i) y19[i] = y[i] * 19;
+  t[0] = u128(x[0]) * y[0] + u128(x[1]) * y19[4] + u128(x[2]) * y19[3] + u128(x[3]) * y19[2] + u128(x[4]) * y19[1];
+  t[1] = u128(x[0]) * y[1] + u128(x[1]) * y[0] + u128(x[2]) * y19[4] + u128(x[3]) * y19[3] + u128(x[4]) * y19[2];
+  t[2] = u128(x[0]) * y[2] + u128(x[1]) * y[1] + u128(x[2]) * y[0] + u128(x[3]) * y19[4] + u128(x[4]) * y19[3];
+  t[3] = u128(x[0]) * y[3] + u128(x[1]) * y[2] + u128(x[2]) * y[1] + u128(x[3]) * y[0] + u128(x[4]) * y19[4];
+  t[4] = u128(x[0]) * y[4] + u128(x[1]) * y[3] + u128(x[2]) * y[2] + u128(x[3]) * y[1] + u128(x[4]) * y[0];
+  Fe r;
+  u128 c = 0;
+  for (int i = 0; i < 5; ++i) {
+    t[i] += c;
+    r.v[i] = u64(t[i]) & MASK51;
+    c = t[i] >> 51;
+  }
+  r.v[0] += u64(c) * 19;
+  return fe_carry(r);
+}
+Fe fe_sq(const Fe& a) { return fe_mul(a, a); }
+
+// canonical 32-byte little-endian encoding
+void fe_tobytes(u8 out[32], Fe a) {
+  a = fe_carry(a);
+  // subtract p if a >= p: compute a + 19 and check bit 255
+  u64 q = (a.v[0] + 19) >> 51;
+  q = (a.v[1] + q) >> 51;
+  q = (a.v[2] + q) >> 51;
+  q = (a.v[3] + q) >> 51;
+  q = (a.v[4] + q) >> 51;
+  a.v[0] += 19 * q;
+  u64 c;
+  c = a.v[0] >> 51; a.v[0] &= MASK51; a.v[1] += c;
+  c = a.v[1] >> 51; a.v[1] &= MASK51; a.v[2] += c;
+  c = a.v[2] >> 51; a.v[2] &= MASK51; a.v[3] += c;
+  c = a.v[3] >> 51; a.v[3] &= MASK51; a.v[4] += c;
+  a.v[4] &= MASK51;
+  u8 buf[40] = {0};
+  // pack 255 bits
+  u128 acc = 0;
+  int bits = 0, o = 0;
+  for (int i = 0; i < 5; ++i) {
+    acc |= u128(a.v[i]) << bits;
+    bits += 51;
+    while (bits >= 8) { buf[o++] = u8(acc); acc >>= 8; bits -= 8; }
+  }
+  if (bits > 0) buf[o++] = u8(acc);
+  memcpy(out, buf, 32);
+}
+Fe fe_frombytes(const u8 in[32]) {
+  u8 b[32];
+  memcpy(b, in, 32);
+  b[31] &= 0x7f;
+  Fe r;
+  u64 w[4];
+  for (int i = 0; i < 4; ++i) w[i] = load_le64(b + 8 * i);
+  r.v[0] = w[0] & MASK51;
+  r.v[1] = ((w[0] >> 51) | (w[1] << 13)) & MASK51;
+  r.v[2] = ((w[1] >> 38) | (w[2] << 26)) & MASK51;
+  r.v[3] = ((w[2] >> 25) | (w[3] << 39)) & MASK51;
+  r.v[4] = (w[3] >> 12) & MASK51;
+  return r;
+}
+bool fe_eq(const Fe& a, const Fe& b) {
+  u8 x[32], y[32];
+  fe_tobytes(x, a); fe_tobytes(y, b);
+  return memcmp(x, y, 32) == 0;
+}
+bool fe_iszero(const Fe& a) { return fe_eq(a, fe_zero()); }
+bool fe_isneg(const Fe& a) { u8 x[32]; fe_tobytes(x, a); return x[0] & 1; }
+Fe fe_pow(const Fe& a, const u8 e_le[32]) {
+  Fe r = fe_one();
+  for (int i = 255; i >= 0; --i) {
+    r = fe_sq(r);
+    if ((e_le[i >> 3] >> (i & 7)) & 1) r = fe_mul(r, a);
+  }
+  return r;
+}
+Fe fe_invert(const Fe& a) {
+  u8 e[32];
+  memset(e, 0xff, 32);
+  e[0] = 0xeb;  // p - 2 = 2^255 - 21
+  e[31] = 0x7f;
+  return fe_pow(a, e);
+}
+Fe fe_pow22523(const Fe& a) {
+  u8 e[32];  // (p-5)/8 = 2^252 - 3
+  memset(e, 0xff, 32);
+  e[0] = 0xfd;
+  e[31] = 0x0f;
+  return fe_pow(a, e);
+}
+Fe fe_from_dec(const char* s) {
+  u64 w[4] = {0, 0, 0, 0};
+  for (const char* c = s; *c; ++c) {
+    u128 carry = u64(*c - '0');
+    for (int i = 0; i < 4; ++i) {
+      u128 v = u128(w[i]) * 10 + carry;
+      w[i] = u64(v);
+      carry = v >> 64;
+    }
+  }
+  u8 b[32];
+  for (int i = 0; i < 4; ++i) store_le64(b + 8 * i, w[i]);
+  return fe_frombytes(b);
+}
+
+const Fe& D() { static const Fe d = fe_from_dec("37095705934669439343138083508754565189542113879843219016388785533085940283555"); return d; }
+const Fe& D2() { static const Fe d2 = fe_add(D(), D()); return d2; }
+const Fe& SQRTM1() { static const Fe s = fe_from_dec("19681161376707505956807079304988542015446066515923890162744021073123829784752"); return s; }
+
+// ---------------------------------------------------------------- points (extended coordinates)
+struct Ge { Fe X, Y, Z, T; };
+Ge ge_identity() { return Ge{fe_zero(), fe_one(), fe_one(), fe_zero()}; }
+Ge ge_add(const Ge& p, const Ge& q) {
+  Fe A = fe_mul(fe_sub(p.Y, p.X), fe_sub(q.Y, q.X));
+  Fe B = fe_mul(fe_add(p.Y, p.X), fe_add(q.Y, q.X));
+  Fe C = fe_mul(fe_mul(p.T, D2()), q.T);
+  Fe Dd = fe_mul(fe_add(p.Z, p.Z), q.Z);
+  Fe E = fe_sub(B, A), F = fe_sub(Dd, C), G = fe_add(Dd, C), H = fe_add(B, A);
+  return Ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+Ge ge_neg(const Ge& p) { return Ge{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
+// scalar as 32-byte little-endian
+Ge ge_mul(const Ge& p, const u8 k[32]) {
+  Ge r = ge_identity();
+  for (int i = 255; i >= 0; --i) {
+    r = ge_add(r, r);
+    if ((k[i >> 3] >> (i & 7)) & 1) r = ge_add(r, p);
+  }
+  return r;
+}
+Ge ge_base() {
+  static const Ge b = [] {
+    Fe x = fe_from_dec("15112221349535400772501151409588531511454012693041857206046113283949847762202");
+    Fe y = fe_from_dec("46316835694926478169428394003475163141307993866256225615783033603165251855960");
+    return Ge{x, y, fe_one(), fe_mul(x, y)};
+  }();
+  return b;
+}
+// fixed-base table for B: 64 windows x 16 entries
+struct BaseTable {
+  std::vector<Ge> t;
+  BaseTable() {
+    t.resize(64 * 16);
+    Ge base = ge_base();
+    for (int w = 0; w < 64; ++w) {
+      t[w * 16] = ge_identity();
+      for (int d = 1; d < 16; ++d) t[w * 16 + d] = ge_add(t[w * 16 + d - 1], base);
+      for (int i = 0; i < 4; ++i) base = ge_add(base, base);
+    }
+  }
+};
+Ge ge_mul_base(const u8 k[32]) {
+  static const BaseTable bt;
+  Ge r = ge_identity();
+  for (int w = 0; w < 64; ++w) {
+    int d = (k[w >> 1] >> ((w & 1) * 4)) & 15;
+    if (d) r = ge_add(r, bt.t[w * 16 + d]);
+  }
+  return r;
+}
+Bytes ge_tobytes(const Ge& p) {
+  Fe zi = fe_invert(p.Z);
+  Fe x = fe_mul(p.X, zi), y = fe_mul(p.Y, zi);
+  Bytes out(32);
+  fe_tobytes(out.data(), y);
+  if (fe_isneg(x)) out[31] |= 0x80;
+  return out;
+}
+bool ge_frombytes(Ge& out, const u8 in[32]) {
+  // RFC 8032 5.1.3: reject non-canonical y
+  u8 b[32];
+  memcpy(b, in, 32);
+  int sign = b[31] >> 7;
+  b[31] &= 0x7f;
+  Fe y = fe_frombytes(b);
+  u8 chk[32];
+  fe_tobytes(chk, y);
+  if (memcmp(chk, b, 32) != 0) return false;
+  Fe y2 = fe_sq(y);
+  Fe u = fe_sub(y2, fe_one());
+  Fe v = fe_add(fe_mul(D(), y2), fe_one());
+  Fe v3 = fe_mul(fe_sq(v), v);
+  Fe v7 = fe_mul(fe_sq(v3), v);
+  Fe x = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
+  Fe vx2 = fe_mul(v, fe_sq(x));
+  if (!fe_eq(vx2, u)) {
+    if (fe_eq(vx2, fe_neg(u))) x = fe_mul(x, SQRTM1());
+    else return false;
+  }
+  if (fe_iszero(x) && sign) return false;
+  if (int(fe_isneg(x)) != sign) x = fe_neg(x);
+  out = Ge{x, y, fe_one(), fe_mul(x, y)};
+  return true;
+}
+bool ge_is_identity(const Ge& p) { return fe_iszero(p.X) && fe_eq(p.Y, p.Z); }
+
+// ---------------------------------------------------------------- scalars mod L
+// L = 2^252 + 27742317777372353535851937790883648493 as 4 LE limbs
+const u64 Lw[4] = {0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0x0000000000000000ULL, 0x1000000000000000ULL};
+bool ge_L(const u64 r[4]) {
+  for (int i = 3; i >= 0; --i) {
+    if (r[i] > Lw[i]) return true;
+    if (r[i] < Lw[i]) return false;
+  }
+  return true;
+}
+void subL(u64 r[4]) {
+  u64 br = 0;
+  for (int i = 0; i < 4; ++i) {
+    u128 d = u128(r[i]) - Lw[i] - br;
+    r[i] = u64(d);
+    br = u64(d >> 64) & 1;
+  }
+}
+// reduce an arbitrary little-endian byte string mod L (bitwise long division)
+void sc_reduce(u8 out[32], const u8* in, size_t n) {
+  u64 r[4] = {0, 0, 0, 0};
+  for (size_t bi = n * 8; bi-- > 0;) {
+    u64 bit = (in[bi >> 3] >> (bi & 7)) & 1;
+    // r = 2r + bit
+    u64 c = bit;
+    for (int i = 0; i < 4; ++i) {
+      u64 nc = r[i] >> 63;
+      r[i] = (r[i] << 1) | c;
+      c = nc;
+    }
+    if (ge_L(r)) subL(r);
+  }
+  for (int i = 0; i < 4; ++i) store_le64(out + 8 * i, r[i]);
+}
+// out = (a + b*c) mod L ; all little-endian, a,b 32B, c given as cLen bytes
+void sc_muladd(u8 out[32], const u8 a[32], const u8* b, size_t blen, const u8 c[32]) {
+  // schoolbook product into 96 bytes, then add a, then reduce
+  u64 prod[12] = {0};
+  u64 bw[4] = {0, 0, 0, 0}, cw[4];
+  u8 bb[32] = {0};
+  memcpy(bb, b, blen);
+  for (int i = 0; i < 4; ++i) { bw[i] = load_le64(bb + 8 * i); cw[i] = load_le64(c + 8 * i); }
+  for (int i = 0; i < 4; ++i) {
+    u128 carry = 0;
+    for (int j = 0; j < 4; ++j) {
+      u128 v = u128(bw[i]) * cw[j] + prod[i + j] + carry;
+      prod[i + j] = u64(v);
+      carry = v >> 64;
+    }
+    prod[i + 4] += u64(carry);
+  }
+  u128 carry = 0;
+  for (int i = 0; i < 12; ++i) {
+    u128 v = u128(prod[i]) + (i < 4 ? load_le64(a + 8 * i) : 0) + carry;
+    prod[i] = u64(v);
+    carry = v >> 64;
+  }
+  u8 buf[96];
+  for (int i = 0; i < 12; ++i) store_le64(buf + 8 * i, prod[i]);
+  sc_reduce(out, buf, 96);
+}
+
+void clamp_secret(const Bytes& seed, u8 x[32], u8 prefix[32]) {
+  Bytes h = Sha512::digest(seed);
+  memcpy(x, h.data(), 32);
+  x[0] &= 248;
+  x[31] &= 127;
+  x[31] |= 64;
+  memcpy(prefix, h.data() + 32, 32);
+}
+
+const u8 SUITE = 0x03;
+
+Ge encode_to_curve(const Bytes& pk, const Bytes& alpha) {
+  for (int ctr = 0; ctr < 256; ++ctr) {
+    Sha512 h;
+    u8 pre[2] = {SUITE, 0x01};
+    h.update(pre, 2);
+    h.update(pk);
+    h.update(alpha);
+    u8 tail[2] = {u8(ctr), 0x00};
+    h.update(tail, 2);
+    u8 dig[64];
+    h.final(dig);
+    Ge H;
+    if (ge_frombytes(H, dig)) {
+      H = ge_add(H, H); H = ge_add(H, H); H = ge_add(H, H);  // cofactor 8
+      return H;
+    }
+  }
+  fail("ecvrf: encode_to_curve failed");
+}
+
+Bytes challenge(const Ge& Y, const Ge& H, const Ge& G, const Ge& U, const Ge& V) {
+  Sha512 h;
+  u8 pre[2] = {SUITE, 0x02};
+  h.update(pre, 2);
+  for (const Ge* p : {&Y, &H, &G, &U, &V}) h.update(ge_tobytes(*p));
+  u8 z = 0;
+  h.update(&z, 1);
+  u8 dig[64];
+  h.final(dig);
+  return Bytes(dig, dig + 16);
+}
+
+}  // namespace
+
+Bytes ed25519_public_from_seed(const Bytes& seed32) {
+  if (seed32.size() != 32) fail("ed25519: seed must be 32 bytes");
+  u8 x[32], prefix[32];
+  clamp_secret(seed32, x, prefix);
+  return ge_tobytes(ge_mul_base(x));
+}
+
+VrfKey VrfKey::from_seed(const Bytes& seed32) {
+  VrfKey k;
+  k.seed = seed32;
+  k.pk = ed25519_public_from_seed(seed32);
+  return k;
+}
+
+Bytes vrf_proof_to_hash(const Bytes& pi) {
+  if (pi.size() != 80) fail("ecvrf: bad proof length");
+  Ge G;
+  if (!ge_frombytes(G, pi.data())) fail("ecvrf: bad gamma");
+  G = ge_add(G, G); G = ge_add(G, G); G = ge_add(G, G);
+  Sha512 h;
+  u8 pre[2] = {SUITE, 0x03};
+  h.update(pre, 2);
+  h.update(ge_tobytes(G));
+  u8 z = 0;
+  h.update(&z, 1);
+  Bytes out(64);
+  h.final(out.data());
+  return out;
+}
+
+std::pair<Bytes, Bytes> vrf_prove(const VrfKey& key, const Bytes& alpha) {
+  u8 x[32], prefix[32];
+  clamp_secret(key.seed, x, prefix);
+  Ge H = encode_to_curve(key.pk, alpha);
+  Bytes hstr = ge_tobytes(H);
+  Ge Gamma = ge_mul(H, x);
+  Sha512 kh;
+  kh.update(prefix, 32);
+  kh.update(hstr);
+  u8 kd[64];
+  kh.final(kd);
+  u8 k[32];
+  sc_reduce(k, kd, 64);
+  Ge Y;
+  ge_frombytes(Y, key.pk.data());
+  Bytes c = challenge(Y, H, Gamma, ge_mul_base(k), ge_mul(H, k));
+  u8 s[32];
+  sc_muladd(s, k, c.data(), 16, x);
+  Bytes pi = ge_tobytes(Gamma);
+  pi.insert(pi.end(), c.begin(), c.end());
+  pi.insert(pi.end(), s, s + 32);
+  return {vrf_proof_to_hash(pi), pi};
+}
+
+bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* beta) {
+  if (pk.size() != 32 || pi.size() != 80) return false;
+  Ge Y, Gamma;
+  if (!ge_frombytes(Y, pk.data())) return false;
+  if (!ge_frombytes(Gamma, pi.data())) return false;
+  u8 c[32] = {0}, s[32];
+  memcpy(c, pi.data() + 32, 16);
+  memcpy(s, pi.data() + 48, 32);
+  u64 sw[4];
+  for (int i = 0; i < 4; ++i) sw[i] = load_le64(s + 8 * i);
+  if (ge_L(sw)) return false;
+  Ge H = encode_to_curve(pk, alpha);
+  Ge U = ge_add(ge_mul_base(s), ge_neg(ge_mul(Y, c)));
+  Ge V = ge_add(ge_mul(H, s), ge_neg(ge_mul(Gamma, c)));
+  Bytes c2 = challenge(Y, H, Gamma, U, V);
+  if (memcmp(c2.data(), c, 16) != 0) return false;
+  if (beta) *beta = vrf_proof_to_hash(pi);
+  return true;
+}
+
+}  // namespace bsc

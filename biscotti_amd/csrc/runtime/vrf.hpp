@@ -1,0 +1,30 @@
+// Verifiable random function over Edwards25519.
+//
+// The reference draws committee roles from a coniks-go Edwards25519 VRF
+// (DistSys/vrf.go:3-5,16-32; the library is fetched by `go get`, not vendored).  Its exact byte
+// format cannot be reproduced offline, so this runtime implements the standardised
+// ECVRF-EDWARDS25519-SHA512-TAI construction (RFC 9381): an Edwards25519 VRF with the same
+// properties (uniqueness, pseudorandomness, public verifiability), 80-byte proofs and a
+// 64-byte output.  Lottery code consumes only the output bytes, exactly like
+// getVRFNoisers (DistSys/vrf.go:54-100).
+#pragma once
+#include "common.hpp"
+
+namespace bsc {
+
+struct VrfKey {
+  Bytes seed;  // 32-byte secret seed
+  Bytes pk;    // 32-byte encoded public key
+  static VrfKey from_seed(const Bytes& seed32);
+};
+
+// Returns (beta = 64-byte output, pi = 80-byte proof).
+std::pair<Bytes, Bytes> vrf_prove(const VrfKey& key, const Bytes& alpha);
+// Returns true and fills beta on success.
+bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* beta);
+Bytes vrf_proof_to_hash(const Bytes& pi);
+
+// Plain Ed25519 public-key derivation (RFC 8032), exposed for tests.
+Bytes ed25519_public_from_seed(const Bytes& seed32);
+
+}  // namespace bsc

@@ -1,0 +1,181 @@
+"""BN256 / Schnorr / hashing / VRF tests of the native host runtime.
+
+Golden vectors: the reference's binary key files (tests/fixtures, copied from
+/root/reference/keyGeneration): kyber-produced G1/G2 marshals and (sk, pk = sk*G) pairs.
+"""
+import hashlib
+import random
+
+import pytest
+
+
+def _records(path, size):
+    data = path.read_bytes()
+    step = size + 1
+    assert len(data) % step == 0
+    return [data[i:i + size] for i in range(0, len(data), step)]
+
+
+def test_prime_and_order(rt):
+    u = 6518589491078791937
+    assert rt.bn256_prime() == 36 * u**4 + 36 * u**3 + 24 * u**2 + 6 * u + 1
+    assert rt.bn256_order() == 36 * u**4 + 36 * u**3 + 18 * u**2 + 6 * u + 1
+
+
+def test_generator_marshal_matches_kyber(rt, fixtures):
+    g1 = _records(fixtures / "commitKeyG1", 64)
+    assert g1[0] == rt.g1_generator()
+    p = rt.bn256_prime()
+    assert int.from_bytes(g1[0][:32], "big") == 1 and int.from_bytes(g1[0][32:], "big") == p - 2
+    g2 = _records(fixtures / "commitKeyG2", 129)
+    assert g2[0] == rt.g2_generator()
+
+
+def test_kyber_points_decode(rt, fixtures):
+    for rec in _records(fixtures / "commitKeyG1", 64):
+        assert rt.g1_is_valid(rec)
+    for rec in _records(fixtures / "commitKeyG2", 129):
+        assert rt.g2_is_valid(rec)
+    bad = bytearray(_records(fixtures / "commitKeyG1", 64)[3])
+    bad[63] ^= 1
+    assert not rt.g1_is_valid(bytes(bad))
+
+
+def test_client_keys_sk_times_g(rt, fixtures):
+    pks = _records(fixtures / "pKeyG1", 64)
+    sks = _records(fixtures / "sKeyG1", 32)
+    gen = rt.g1_generator()
+    for sk, pk in zip(sks, pks):
+        s = int.from_bytes(sk, "big")
+        assert rt.g1_mul(gen, s) == pk
+        assert rt.g1_base_mul(s) == pk
+
+
+def test_group_laws(rt):
+    g = rt.g1_generator()
+    order = rt.bn256_order()
+    assert rt.g1_mul(g, order) == rt.g1_infinity()
+    a, b = 123456789, 987654321
+    assert rt.g1_add(rt.g1_mul(g, a), rt.g1_mul(g, b)) == rt.g1_mul(g, a + b)
+    # doubling path inside add, and P + (-P)
+    p = rt.g1_mul(g, 77)
+    assert rt.g1_add(p, p) == rt.g1_mul(g, 154)
+    assert rt.g1_add(p, rt.g1_neg(p)) == rt.g1_infinity()
+    # negative scalar == (Order - |k|) * P (kyber SetInt64 semantics)
+    assert rt.g1_mul_i64(p, -5) == rt.g1_mul(p, order - 5)
+    g2 = rt.g2_generator()
+    assert rt.g2_mul(g2, order) == b"\x00"
+    assert rt.g2_add(rt.g2_mul(g2, 2), rt.g2_mul(g2, 4)) == rt.g2_mul(g2, 6)
+
+
+def test_scalar_marshal(rt):
+    order = rt.bn256_order()
+    assert int.from_bytes(rt.scalar_from_i64(-1), "big") == order - 1
+    assert int.from_bytes(rt.scalar_from_i64(7), "big") == 7
+
+
+def test_schnorr_roundtrip(rt):
+    sk, pk = rt.client_key_from_entropy(b"peer-7")
+    msg = rt.g1_mul(rt.g1_generator(), 4242)  # commitments are what verifiers sign
+    sig = rt.schnorr_sign(msg, sk, b"nonce-entropy")
+    assert len(sig) == 64
+    assert rt.schnorr_verify(msg, pk, sig)
+    assert not rt.schnorr_verify(msg[:-1] + bytes([msg[-1] ^ 1]), pk, sig)
+    sk2, pk2 = rt.client_key_from_entropy(b"peer-8")
+    assert not rt.schnorr_verify(msg, pk2, sig)
+    batch = rt.schnorr_sign_batch([msg, msg[::-1]], sk, [b"a", b"b"], 2)
+    assert rt.schnorr_verify(msg, pk, batch[0]) and rt.schnorr_verify(msg[::-1], pk, batch[1])
+
+
+def test_sha_and_blake2b_against_hashlib(rt):
+    rnd = random.Random(1)
+    for n in [0, 1, 55, 56, 63, 64, 65, 111, 112, 127, 128, 129, 1000]:
+        d = bytes(rnd.getrandbits(8) for _ in range(n))
+        assert rt.sha256(d) == hashlib.sha256(d).digest()
+        assert rt.sha512(d) == hashlib.sha512(d).digest()
+        assert rt.blake2b(d, 64, b"") == hashlib.blake2b(d).digest()
+        assert rt.blake2b(d, 20, b"k" * 64) == hashlib.blake2b(d, digest_size=20, key=b"k" * 64).digest()
+
+
+def _blake2b_param_py(param: bytes, data: bytes) -> bytes:
+    """Independent pure-Python BLAKE2b (RFC 7693) with an explicit parameter block."""
+    M = (1 << 64) - 1
+    IV = [0x6A09E667F3BCC908, 0xBB67AE8584CAA73B, 0x3C6EF372FE94F82B, 0xA54FF53A5F1D36F1,
+          0x510E527FADE682D1, 0x9B05688C2B3E6C1F, 0x1F83D9ABFB41BD6B, 0x5BE0CD19137E2179]
+    S = [[0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15], [14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3],
+         [11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4], [7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8],
+         [9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13], [2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9],
+         [12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11], [13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10],
+         [6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5], [10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0]]
+    rot = lambda x, n: ((x >> n) | (x << (64 - n))) & M
+    h = [IV[i] ^ int.from_bytes(param[8 * i:8 * i + 8], "little") for i in range(8)]
+    outlen = param[0]
+    blocks = [data[i:i + 128] for i in range(0, len(data), 128)] or [b""]
+    t = 0
+    for bi, blk in enumerate(blocks):
+        last = bi == len(blocks) - 1
+        t += len(blk)
+        blk = blk.ljust(128, b"\0")
+        m = [int.from_bytes(blk[8 * i:8 * i + 8], "little") for i in range(16)]
+        v = h + IV
+        v[12] ^= t & M
+        v[13] ^= t >> 64
+        if last:
+            v[14] ^= M
+        for r in range(12):
+            s = S[r % 10]
+            for (a, b, c, d), (x, y) in zip([(0, 4, 8, 12), (1, 5, 9, 13), (2, 6, 10, 14), (3, 7, 11, 15),
+                                              (0, 5, 10, 15), (1, 6, 11, 12), (2, 7, 8, 13), (3, 4, 9, 14)],
+                                             [(s[2 * i], s[2 * i + 1]) for i in range(8)]):
+                v[a] = (v[a] + v[b] + m[x]) & M; v[d] = rot(v[d] ^ v[a], 32)
+                v[c] = (v[c] + v[d]) & M; v[b] = rot(v[b] ^ v[c], 24)
+                v[a] = (v[a] + v[b] + m[y]) & M; v[d] = rot(v[d] ^ v[a], 16)
+                v[c] = (v[c] + v[d]) & M; v[b] = rot(v[b] ^ v[c], 63)
+        h = [h[i] ^ v[i] ^ v[i + 8] for i in range(8)]
+    return b"".join(x.to_bytes(8, "little") for x in h)[:outlen]
+
+
+def test_blake2xb_structure(rt):
+    """blake2xb (kyber XOF) = BLAKE2X over BLAKE2b: keyed root with xof-length 2^32-1, then
+    output nodes B2(leaf=64, node_offset=i, inner=64) of the root digest."""
+    seed, msg = bytes(range(64)), b"commitment-bytes"
+    root = hashlib.blake2b(msg, digest_size=64, key=seed, node_offset=0xFFFFFFFF << 32).digest()
+    out = rt.blake2xb(seed, msg, 200)
+    expect = b""
+    for i in range(4):
+        p = bytearray(64)
+        p[0] = 64
+        p[4] = 64
+        p[8:12] = i.to_bytes(4, "little")
+        p[12:16] = b"\xff\xff\xff\xff"
+        p[17] = 64
+        assert rt.blake2b_param(bytes(p), root) == _blake2b_param_py(bytes(p), root)
+        expect += _blake2b_param_py(bytes(p), root)
+    assert out == expect[:200]
+    # seeds longer than 64 bytes: tail is absorbed as message prefix
+    long_seed = bytes(range(100))
+    root2 = hashlib.blake2b(long_seed[64:] + msg, digest_size=64, key=long_seed[:64],
+                            node_offset=0xFFFFFFFF << 32).digest()
+    p = bytearray(64); p[0] = 64; p[4] = 64; p[12:16] = b"\xff" * 4; p[17] = 64
+    assert rt.blake2xb(long_seed, msg, 64) == _blake2b_param_py(bytes(p), root2)
+
+
+def test_ed25519_rfc8032_vector(rt):
+    seed = bytes.fromhex("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60")
+    assert rt.ed25519_public_key(seed).hex() == "d75a980182b10ab7d54bfed3c964073a0ee172f3daa62325af021a68f707511a"
+
+
+def test_vrf_properties(rt):
+    seed = bytes(range(32))
+    pk = rt.vrf_public_key(seed)
+    beta, pi = rt.vrf_prove(seed, b"block-hash")
+    assert len(beta) == 64 and len(pi) == 80
+    assert rt.vrf_verify(pk, b"block-hash", pi) == beta
+    assert rt.vrf_prove(seed, b"block-hash") == (beta, pi)  # deterministic
+    assert rt.vrf_verify(pk, b"block-hasH", pi) is None
+    bad = bytearray(pi); bad[40] ^= 1
+    assert rt.vrf_verify(pk, b"block-hash", bytes(bad)) is None
+    other = rt.vrf_prove(bytes(32), b"block-hash")[0]
+    assert other != beta
+    batch = rt.vrf_prove_batch([seed, bytes(32)], b"block-hash", 2)
+    assert batch[0] == (beta, pi) and batch[1][0] == other
