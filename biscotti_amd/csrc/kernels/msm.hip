@@ -1,0 +1,364 @@
+// Batched fixed-base multi-scalar multiplication on BN256 G1 for Biscotti's secure aggregation.
+//
+// Reference hot loop: createCommitment / createShareAndWitness (DistSys/kyber.go:533-646),
+// ~180k Go big.Int double-and-add scalar multiplications per worker per round.
+//
+// MI355X design:
+//  * Commitment-key points PK[i] and witness bases B_{j,x} (B_1=PK[0], B_{j+1}=x*B_j+PK[j]) are
+//    fixed for the run, so each gets a signed-window table resident in HBM:
+//        T[base][w][k-1] = k * 2^(8w) * base,  k = 1..128, w = 0..NW-1     (affine, Montgomery)
+//    A scalar |c| < 2^64 is recoded into signed 8-bit digits (d in [-127, 128]); every non-zero
+//    digit costs one mixed (Jacobian + affine) addition and one 64-byte table read.
+//  * One thread per output point.  Threads of one (worker, chunk) group -- 21 witness lanes and
+//    the chunk-commitment lane -- consume the SAME scalar c_j at step j, so digit control flow is
+//    uniform inside a group, and the 21 witness lanes read 21 adjacent table points (1344 B
+//    contiguous, table layout [chunk][j][w][k][x][16]).
+//  * The share values y = p(x) (kyber.go:598-605, exact int64 Horner) are fused into the same
+//    kernel.  Full-vector commitment = sum of chunk commitments (PK slices are consecutive).
+//  * Blocks are remapped XCD-contiguously (chunk-major order), so one chunk's table lines are
+//    pulled into a single XCD's L2.
+#include "bn256_dev.h"
+
+using namespace bn;
+
+namespace {
+
+constexpr int TBL_ENTRIES = 128;  // signed 8-bit digits
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  // bijective: blocks that share an XCD (bid % 8) get a contiguous logical range
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + idx;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ test kernels
+extern "C" __global__ void __launch_bounds__(256) k_fp_mul(const uint32_t* a, const uint32_t* b, uint32_t* out, int n, int op) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fp x = ld_fp(a + 8 * i), y = ld_fp(b + 8 * i), r;
+  switch (op) {
+    case 0: r = fp_mul(x, y); break;
+    case 1: r = fp_add(x, y); break;
+    case 2: r = fp_sub(x, y); break;
+    case 3: r = fp_inv(x); break;
+    default: r = fp_from_mont(x); break;
+  }
+  st_fp(out + 8 * i, r);
+}
+
+// op 0: jac(a)+jac(b) ; 1: jac(a)+aff(b) ; 2: dbl(jac(a)) ; 3: small mul a*k
+extern "C" __global__ void __launch_bounds__(256) k_point_op(const uint32_t* a_aff, const uint32_t* b_aff, const int* ks, uint32_t* out,
+                                      int n, int op) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  aff A = ld_aff(a_aff + 16 * i), Bq = ld_aff(b_aff + 16 * i);
+  jac a = jac_inf();
+  if (!aff_is_inf(A)) { a.x = A.x; a.y = A.y; a.z = fp_one(); }
+  jac b = jac_inf();
+  if (!aff_is_inf(Bq)) { b.x = Bq.x; b.y = Bq.y; b.z = fp_one(); }
+  jac r;
+  switch (op) {
+    case 0: r = jac_add(jac_dbl(a), b); break;  // non-trivial Z on the left operand
+    case 1: r = jac_add_aff(jac_dbl(a), Bq); break;
+    case 2: r = jac_dbl(a); break;
+    default: r = jac_mul_small(a, ks[i]); break;
+  }
+  st_jac(out + 24 * i, r);
+}
+
+// ------------------------------------------------------------------ witness bases
+// out: Jacobian [nchunks][J][T][24], J = poly-1.  Short chunks leave trailing bases = infinity.
+extern "C" __global__ void __launch_bounds__(128) k_witness_bases(const uint32_t* pk_aff, int d, int poly, int T, uint32_t* out) {
+  const int nchunks = (d + poly - 1) / poly;
+  const int J = poly - 1;
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nchunks * T) return;
+  const int k = g / T, s = g % T;
+  const int prev = k * poly;
+  const int L = min(poly, d - prev);
+  const int x = s - 10;  // kyber.go:588
+  jac b = jac_inf();
+  for (int j = 1; j <= J; ++j) {
+    if (j < L) {
+      aff pk = ld_aff(pk_aff + 16 * (prev + j - 1));
+      if (j == 1) {
+        b = jac_add_aff(jac_inf(), pk);
+      } else {
+        b = jac_add_aff(jac_mul_small(b, x), pk);
+      }
+      st_jac(out + 24 * (((size_t)k * J + (j - 1)) * T + s), b);
+    } else {
+      st_jac(out + 24 * (((size_t)k * J + (j - 1)) * T + s), jac_inf());
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fixed-base tables
+// Thread per (base b, window w).  base index b = outer * inner + in; entry (b, w, k) is stored at
+//   table + 16 * (outer * s_outer + w * s_w + (k-1) * s_k + in * s_in)
+// scratch: per thread 128 x 32 u32 (Jacobian + running Z product), in the caller's chunk.
+extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb, int inner, int NW,
+                                      long long s_outer, long long s_w, long long s_k, long long s_in,
+                                      uint32_t* table, uint32_t* scratch) {
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nb * NW) return;
+  const int bl = g / NW, w = g % NW;
+  const int b = b0 + bl;
+  jac P;
+  if (bases_are_jac) {
+    P = ld_jac(bases + 24 * (size_t)b);
+  } else {
+    aff a = ld_aff(bases + 16 * (size_t)b);
+    P = jac_add_aff(jac_inf(), a);
+  }
+  for (int i = 0; i < 8 * w; ++i) P = jac_dbl(P);
+  uint32_t* sc = scratch + (size_t)g * TBL_ENTRIES * 32;
+  jac acc = P;
+  fp prod = fp_one();
+  for (int k = 0; k < TBL_ENTRIES; ++k) {
+    st_jac(sc + 32 * k, acc);
+    st_fp(sc + 32 * k + 24, prod);  // exclusive prefix product of the non-zero Z's before k
+    if (!jac_is_inf(acc)) prod = fp_mul(prod, acc.z);
+    acc = jac_add(acc, P);
+  }
+  fp inv = fp_inv(prod);  // Montgomery's trick: one inversion per (base, window)
+  const int outer = b / inner, in = b % inner;
+  uint32_t* dst0 = table + 16 * (outer * s_outer + w * s_w + in * s_in);
+  for (int k = TBL_ENTRIES - 1; k >= 0; --k) {
+    jac pt = ld_jac(sc + 32 * k);
+    aff o;
+    if (jac_is_inf(pt)) {
+      o.x = fp_zero();
+      o.y = fp_zero();
+    } else {
+      fp zi = fp_mul(inv, ld_fp(sc + 32 * k + 24));  // 1 / z_k
+      inv = fp_mul(inv, pt.z);
+      fp zi2 = fp_sqr(zi);
+      o.x = fp_mul(pt.x, zi2);
+      o.y = fp_mul(pt.y, fp_mul(zi2, zi));
+    }
+    st_aff(dst0 + 16 * (k * s_k), o);
+  }
+}
+
+// ------------------------------------------------------------------ fused shares + commitments
+// coeffs: int64 [*, d] (row stride d); rows: worker rows to process.
+// tbl_pk: [d][NW][128][16]; tbl_wb: [nchunks][J][NW][128][T][16].
+// out_pts: Jacobian [nrows][nchunks][S][24] with S = T+1 (slots 0..T-1 witnesses, slot T the chunk
+// commitment) or S = 1 (commit_only: chunk commitments only).  out_y: int64 [nrows][nchunks][T].
+extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
+    const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
+    int poly, int T, int NW, int commit_only, uint32_t* out_pts, long long* out_y) {
+  const int nchunks = (d + poly - 1) / poly;
+  const int S = commit_only ? 1 : T + 1;
+  const long long total = (long long)nrows * nchunks * S;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const long long g = (long long)lb * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  // chunk-major: consecutive groups share a chunk (and its table lines)
+  const int slot = (int)(g % S);
+  const long long grp = g / S;
+  const int r = (int)(grp % nrows);
+  const int k = (int)(grp / nrows);
+  const int row = rows[r];
+  const int prev = k * poly;
+  const int L = min(poly, d - prev);
+  const bool is_commit = commit_only || slot == T;
+  const int J = poly - 1;
+  const long long* c = coeffs + (size_t)row * d + prev;
+
+  const size_t pk_base_stride = (size_t)NW * TBL_ENTRIES * 16;
+  const size_t wb_w_stride = (size_t)TBL_ENTRIES * T * 16;
+  const size_t wb_j_stride = (size_t)NW * wb_w_stride;
+  const uint32_t* wb_chunk = tbl_wb + (size_t)k * J * wb_j_stride;
+
+  jac acc = jac_inf();
+  // commitment uses c_0..c_{L-1} on PK[prev..]; witness uses c_1..c_{L-1} on B_{1..L-1, x}
+  for (int j = is_commit ? 0 : 1; j < L; ++j) {
+    const long long cj = c[j];
+    if (cj == 0) continue;
+    const bool neg = cj < 0;
+    unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
+    const uint32_t* tb;
+    size_t kstride;
+    size_t wstride;
+    if (is_commit) {
+      tb = tbl_pk + (size_t)(prev + j) * pk_base_stride;
+      kstride = 16;
+      wstride = (size_t)TBL_ENTRIES * 16;
+    } else {
+      tb = wb_chunk + (size_t)(j - 1) * wb_j_stride + (size_t)slot * 16;
+      kstride = (size_t)T * 16;
+      wstride = wb_w_stride;
+    }
+    int carry = 0;
+    for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
+      int dg = (int)(m & 0xFFull) + carry;
+      m >>= 8;
+      if (dg > 128) {
+        dg -= 256;
+        carry = 1;
+      } else {
+        carry = 0;
+      }
+      if (dg == 0) continue;
+      const int ad = dg < 0 ? -dg : dg;
+      aff q = ld_aff(tb + (size_t)w * wstride + (size_t)(ad - 1) * kstride);
+      if ((dg < 0) != neg) q = aff_neg(q);
+      acc = jac_add_aff(acc, q);
+    }
+  }
+  const size_t o = ((size_t)r * nchunks + k) * S + slot;
+  st_jac(out_pts + 24 * o, acc);
+  if (!is_commit && out_y != nullptr) {
+    // y = p(x) exact int64 Horner (kyber.go:598-605 evaluates the same value in float64)
+    const long long x = slot - 10;
+    unsigned long long y = 0;
+    for (int j = L - 1; j >= 0; --j) y = y * (unsigned long long)x + (unsigned long long)c[j];
+    out_y[((size_t)r * nchunks + k) * T + slot] = (long long)y;
+  }
+}
+
+// ------------------------------------------------------------------ reductions
+// out[i] = sum_{r < nrows} pts[(rows[r] * ncols_in + cols[i]) * 24]   (cols == nullptr: cols[i] = i)
+// One thread per output column; used for miner-side share aggregation (aggregateSecret).
+extern "C" __global__ void __launch_bounds__(128) k_sum_rows(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
+                                      int ncols, uint32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncols) return;
+  const int col = cols ? cols[i] : i;
+  jac acc = jac_inf();
+  for (int r = 0; r < nrows; ++r) {
+    const int row = rows ? rows[r] : r;
+    acc = jac_add(acc, ld_jac(pts + 24 * ((size_t)row * ncols_in + col)));
+  }
+  st_jac(out + 24 * (size_t)i, acc);
+}
+
+// Sum of a strided segment per group: out[g] = sum_{k<n} pts[(g*n + k)*stride + off], one block
+// per group, LDS tree.  Used for the full commitment = sum of chunk commitments.
+extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* pts, int n, int stride, int off,
+                                                               uint32_t* out) {
+  __shared__ uint32_t sh[256 * 24];
+  const int g = blockIdx.x;
+  jac acc = jac_inf();
+  for (int k = threadIdx.x; k < n; k += blockDim.x)
+    acc = jac_add(acc, ld_jac(pts + 24 * ((size_t)(g * (size_t)n + k) * stride + off)));
+  for (int t = 0; t < 24; ++t) sh[threadIdx.x * 24 + t] = 0;
+  st_jac(sh + threadIdx.x * 24, acc);
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      jac a = ld_jac(sh + threadIdx.x * 24), b = ld_jac(sh + (threadIdx.x + s) * 24);
+      st_jac(sh + threadIdx.x * 24, jac_add(a, b));
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) st_jac(out + 24 * (size_t)g, ld_jac(sh));
+}
+
+// Jacobian -> kyber marshal (64 B: big-endian affine x || y, Montgomery-decoded; infinity = 0s)
+extern "C" __global__ void __launch_bounds__(64) k_marshal(const uint32_t* pts, int n, uint8_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  aff a = jac_to_aff(ld_jac(pts + 24 * (size_t)i));
+  uint8_t* o = out + 64 * (size_t)i;
+  if (aff_is_inf(a)) {
+    for (int t = 0; t < 64; ++t) o[t] = 0;
+    return;
+  }
+  fp x = fp_from_mont(a.x), y = fp_from_mont(a.y);
+  for (int l = 0; l < 8; ++l) {
+    const uint32_t vx = x.v[7 - l], vy = y.v[7 - l];
+    for (int b = 0; b < 4; ++b) {
+      o[4 * l + b] = (uint8_t)(vx >> (24 - 8 * b));
+      o[32 + 4 * l + b] = (uint8_t)(vy >> (24 - 8 * b));
+    }
+  }
+}
+
+// Jacobian -> affine (Montgomery) [n][16]
+extern "C" __global__ void __launch_bounds__(64) k_to_affine(const uint32_t* pts, int n, uint32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st_aff(out + 16 * (size_t)i, jac_to_aff(ld_jac(pts + 24 * (size_t)i)));
+}
+
+// ------------------------------------------------------------------ C ABI launchers
+// (same translation unit as the kernels: no relocatable device code needed)
+static inline int blocks_for(long long n, int bs) { return (int)((n + bs - 1) / bs); }
+
+extern "C" int bsc_fp_op(const uint32_t* a, const uint32_t* b, uint32_t* out, int n, int op, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_fp_mul, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, a, b, out, n, op);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_point_op(const uint32_t* a, const uint32_t* b, const int* ks, uint32_t* out, int n, int op,
+                            void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_point_op, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, a, b, ks, out, n, op);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_witness_bases(const uint32_t* pk_aff, int d, int poly, int T, uint32_t* out, void* stream) {
+  const int nchunks = (d + poly - 1) / poly;
+  const long long n = (long long)nchunks * T;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_witness_bases, dim3(blocks_for(n, 128)), dim3(128), 0, (hipStream_t)stream, pk_aff, d, poly,
+                     T, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb, int inner, int NW,
+                            long long s_outer, long long s_w, long long s_k, long long s_in, uint32_t* table,
+                            uint32_t* scratch, void* stream) {
+  const long long n = (long long)nb * NW;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_fb_table, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, bases, bases_are_jac, b0,
+                     nb, inner, NW, s_outer, s_w, s_k, s_in, table, scratch);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
+                              const uint32_t* tbl_wb, int poly, int T, int NW, int commit_only, uint32_t* out_pts,
+                              long long* out_y, void* stream) {
+  const int nchunks = (d + poly - 1) / poly;
+  const int S = commit_only ? 1 : T + 1;
+  const long long n = (long long)nrows * nchunks * S;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_shares_msm, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows,
+                     nrows, tbl_pk, tbl_wb, poly, T, NW, commit_only, out_pts, out_y);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_sum_rows(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols, int ncols,
+                            uint32_t* out, void* stream) {
+  if (ncols <= 0) return 0;
+  hipLaunchKernelGGL(k_sum_rows, dim3(blocks_for(ncols, 128)), dim3(128), 0, (hipStream_t)stream, pts, ncols_in,
+                     rows, nrows, cols, ncols, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
+                               void* stream) {
+  if (ngroups <= 0) return 0;
+  hipLaunchKernelGGL(k_segment_sum, dim3(ngroups), dim3(256), 0, (hipStream_t)stream, pts, n, stride, off, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_marshal(const uint32_t* pts, int n, uint8_t* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_marshal, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, pts, n, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_to_affine(const uint32_t* pts, int n, uint32_t* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_to_affine, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, pts, n, out);
+  return (int)hipGetLastError();
+}

@@ -191,8 +191,21 @@ SharePackage make_shares(const std::vector<i64>& c, const std::vector<G1>& pk, i
     sp.commitment = sp.commitment.add(cc);
     for (i64 x : xs) {
       sp.ys.push_back(poly_eval(chunk.data(), L, x));
-      std::vector<i64> q = poly_quotient(chunk.data(), L, x);
-      sp.witnesses.push_back(commit(q, pk, size_t(prev)));
+      // exact quotient in 128-bit (|q| < 2^63 * 10^9 * 10 fits), committed mod Order
+      G1 w = G1::infinity();
+      i128 carry = 0;
+      for (int k = L - 1; k >= 1; --k) {
+        carry = carry * x + chunk[size_t(k)];
+        if (carry != 0) {
+          u128 mag = carry < 0 ? u128(-carry) : u128(carry);
+          U256 m;
+          m.w[0] = u64(mag);
+          m.w[1] = u64(mag >> 64);
+          G1 t = pk[size_t(prev + k - 1)].mul(m);
+          w = w.add(carry < 0 ? t.neg() : t);
+        }
+      }
+      sp.witnesses.push_back(w);
     }
     prev = stop;
   }

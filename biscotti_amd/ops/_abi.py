@@ -1,0 +1,33 @@
+"""ctypes signatures of the C ABI exported by ``libbiscotti_hip.so``."""
+from __future__ import annotations
+
+import ctypes as C
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_longlong
+D = C.c_double
+F = C.c_float
+U64 = C.c_uint64
+
+SIGNATURES = {
+    # msm.hip
+    "bsc_fp_op": [P, P, P, I, I, P],
+    "bsc_point_op": [P, P, P, P, I, I, P],
+    "bsc_witness_bases": [P, I, I, I, P, P],
+    "bsc_fb_table": [P, I, I, I, I, I, L, L, L, L, P, P, P],
+    "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, P, P, P],
+    "bsc_sum_rows": [P, I, P, I, P, I, P, P],
+    "bsc_segment_sum": [P, I, I, I, I, P, P],
+    "bsc_marshal": [P, I, P, P],
+    "bsc_to_affine": [P, I, P, P],
+}
+
+
+def declare(lib) -> None:
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = args
+        fn.restype = C.c_int

@@ -1,0 +1,163 @@
+"""Device-side BN256 G1 engine: fixed-base tables + batched share/commitment MSM on gfx950.
+
+Replaces the reference's per-peer Go big.Int loops (DistSys/kyber.go:533-646) with HBM-resident
+signed-window tables and one fused kernel per round phase (see csrc/kernels/msm.hip).
+
+Tensor conventions (all on the GPU):
+  * field elements: 8 x 32-bit Montgomery limbs stored in ``torch.int32`` (bit patterns)
+  * affine points   [..., 16]  (x, y);  infinity = zeros
+  * Jacobian points [..., 24]  (x, y, z); infinity <=> z == 0
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..native import hip, rt
+
+NW_DEFAULT = 9       # 9 signed 8-bit windows cover any |scalar| < 2^64
+TBL_ENTRIES = 128
+_SCRATCH_BYTES = 1 << 31
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous(), "device kernels need contiguous GPU tensors"
+    return t.data_ptr()
+
+
+def _check(err: int, what: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"HIP launch of {what} failed with hipError {err}")
+
+
+def u32_tensor(a: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
+
+
+class DeviceCommitEngine:
+    """Commitment key + witness-base tables resident on one GPU.
+
+    poly: POLY_SIZE (10); total_shares: TOTAL_SHARES (21) -- x = i - 10 (kyber.go:588).
+    """
+
+    def __init__(self, commit_key, poly: int, total_shares: int, device="cuda", nw: int = NW_DEFAULT):
+        self.device = torch.device(device)
+        self.d = len(commit_key)
+        self.poly = int(poly)
+        self.T = int(total_shares)
+        self.J = self.poly - 1
+        self.nw = int(nw)
+        self.nchunks = (self.d + self.poly - 1) // self.poly
+        lib = hip()
+        self.pk_aff = u32_tensor(commit_key.affine_mont_u32(), self.device)  # [d, 16]
+        # witness bases B_{j,x}: [nchunks][J][T][24]
+        self.wbases = torch.empty((self.nchunks, self.J, self.T, 24), dtype=torch.int32, device=self.device)
+        _check(lib.bsc_witness_bases(_ptr(self.pk_aff), self.d, self.poly, self.T, _ptr(self.wbases), _stream()),
+               "witness_bases")
+        self.tbl_pk = torch.empty((self.d, self.nw, TBL_ENTRIES, 16), dtype=torch.int32, device=self.device)
+        self.tbl_wb = torch.empty((self.nchunks, self.J, self.nw, TBL_ENTRIES, self.T, 16), dtype=torch.int32,
+                                  device=self.device)
+        nw, E, T = self.nw, TBL_ENTRIES, self.T
+        self._build_table(self.pk_aff, False, self.d, 1, (nw * E, E, 1, 0), self.tbl_pk)
+        self._build_table(self.wbases, True, self.nchunks * self.J * self.T, T, (nw * E * T, E * T, T, 1), self.tbl_wb)
+        del self.wbases
+        torch.cuda.synchronize(self.device)
+
+    def table_bytes(self) -> int:
+        return (self.tbl_pk.numel() + self.tbl_wb.numel()) * 4
+
+    def _build_table(self, bases, jac: bool, nbases: int, inner: int, strides, table) -> None:
+        lib = hip()
+        per_thread = TBL_ENTRIES * 32 * 4
+        batch = max(inner, (_SCRATCH_BYTES // (per_thread * self.nw)) // inner * inner)
+        scratch = torch.empty((min(batch, nbases) * self.nw * TBL_ENTRIES * 32,), dtype=torch.int32,
+                              device=self.device)
+        for b0 in range(0, nbases, batch):
+            nb = min(batch, nbases - b0)
+            _check(lib.bsc_fb_table(_ptr(bases), int(jac), b0, nb, inner, self.nw, *strides, _ptr(table),
+                                    _ptr(scratch), _stream()), "fb_table")
+        del scratch
+
+    # ---------------------------------------------------------------- per-round kernels
+    def shares(self, coeffs: torch.Tensor, rows: torch.Tensor, commit_only: bool = False):
+        """Fused chunk commitments (+ witnesses and share values unless commit_only).
+
+        coeffs: int64 [P, d] quantized deltas; rows: int32 [n] rows of `coeffs` to process.
+        Returns (pts [n, nchunks, S, 24] Jacobian with S = 1 or T+1, ys [n, nchunks, T] or None).
+        """
+        assert coeffs.dtype == torch.int64 and coeffs.dim() == 2 and coeffs.shape[1] == self.d
+        assert rows.dtype == torch.int32 and rows.dim() == 1
+        n = rows.numel()
+        if n:
+            assert int(rows.min()) >= 0 and int(rows.max()) < coeffs.shape[0], "row index out of range"
+        S = 1 if commit_only else self.T + 1
+        pts = torch.empty((n, self.nchunks, S, 24), dtype=torch.int32, device=self.device)
+        ys = None if commit_only else torch.empty((n, self.nchunks, self.T), dtype=torch.int64, device=self.device)
+        _check(hip().bsc_shares_msm(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), _ptr(self.tbl_wb),
+                                    self.poly, self.T, self.nw, int(commit_only), _ptr(pts), _ptr(ys), _stream()),
+               "shares_msm")
+        return pts, ys
+
+    def commitments(self, pts: torch.Tensor) -> torch.Tensor:
+        """Full-vector commitment per row = sum of its chunk commitments. Returns Jacobian [n, 24]."""
+        n, nch, S, _ = pts.shape
+        out = torch.empty((n, 24), dtype=torch.int32, device=self.device)
+        _check(hip().bsc_segment_sum(_ptr(pts), n, nch, S, S - 1, _ptr(out), _stream()), "segment_sum")
+        return out
+
+
+def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | None) -> torch.Tensor:
+    """out[i] = sum_r pts[rows[r], cols[i]] for a [R, C, 24] Jacobian tensor."""
+    assert pts.dim() == 3 and pts.shape[2] == 24
+    R, Cn, _ = pts.shape
+    nrows = R if rows is None else rows.numel()
+    ncols = Cn if cols is None else cols.numel()
+    if rows is not None:
+        assert rows.dtype == torch.int32 and (nrows == 0 or int(rows.max()) < R)
+    if cols is not None:
+        assert cols.dtype == torch.int32 and (ncols == 0 or int(cols.max()) < Cn)
+    out = torch.empty((ncols, 24), dtype=torch.int32, device=pts.device)
+    _check(hip().bsc_sum_rows(_ptr(pts), Cn, _ptr(rows), nrows, _ptr(cols), ncols, _ptr(out), _stream()),
+           "sum_rows")
+    return out
+
+
+def marshal(pts: torch.Tensor) -> torch.Tensor:
+    """Jacobian [..., 24] -> kyber marshal bytes uint8 [N, 64] (on device)."""
+    flat = pts.reshape(-1, 24).contiguous()
+    out = torch.empty((flat.shape[0], 64), dtype=torch.uint8, device=pts.device)
+    _check(hip().bsc_marshal(_ptr(flat), flat.shape[0], _ptr(out), _stream()), "marshal")
+    return out
+
+
+def to_affine(pts: torch.Tensor) -> torch.Tensor:
+    flat = pts.reshape(-1, 24).contiguous()
+    out = torch.empty((flat.shape[0], 16), dtype=torch.int32, device=pts.device)
+    _check(hip().bsc_to_affine(_ptr(flat), flat.shape[0], _ptr(out), _stream()), "to_affine")
+    return out
+
+
+def fp_op(a: torch.Tensor, b: torch.Tensor, op: int) -> torch.Tensor:
+    """Element-wise field op on [n, 8] limb tensors (0 mul, 1 add, 2 sub, 3 inv, 4 from_mont)."""
+    assert a.shape == b.shape and a.shape[-1] == 8
+    out = torch.empty_like(a)
+    _check(hip().bsc_fp_op(_ptr(a), _ptr(b), _ptr(out), a.shape[0], op, _stream()), "fp_op")
+    return out
+
+
+def point_op(a_aff: torch.Tensor, b_aff: torch.Tensor, ks: torch.Tensor, op: int) -> torch.Tensor:
+    n = a_aff.shape[0]
+    out = torch.empty((n, 24), dtype=torch.int32, device=a_aff.device)
+    _check(hip().bsc_point_op(_ptr(a_aff), _ptr(b_aff), _ptr(ks), _ptr(out), n, op, _stream()), "point_op")
+    return out
+
+
+def host_commit_key(d: int, secret: int = 2):
+    """Reference commitment key PK[i] = secret^i * G1 (DistSys/publicKey.go:26-61)."""
+    return rt().CommitKey.generate(d, secret)

@@ -1,0 +1,59 @@
+"""Micro-benchmark of the BN256 share/commitment MSM at the MNIST size (d = 7850).
+
+python scripts/bench_msm.py [--rows 35] [--workers 94] [--scale 30000]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import numpy as np
+import torch
+
+from biscotti_amd.native import rt
+from biscotti_amd.ops import bn256 as B
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--d", type=int, default=7850)
+    ap.add_argument("--rows", type=int, default=35)
+    ap.add_argument("--workers", type=int, default=94)
+    ap.add_argument("--scale", type=int, default=30000)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    t0 = time.time()
+    key = rt().CommitKey.generate(a.d, 2)
+    t1 = time.time()
+    eng = B.DeviceCommitEngine(key, 10, 21)
+    torch.cuda.synchronize()
+    t2 = time.time()
+    rng = np.random.default_rng(0)
+    coeffs = torch.from_numpy(rng.integers(-a.scale, a.scale, size=(a.workers, a.d), dtype=np.int64)).cuda()
+    allrows = torch.arange(a.workers, dtype=torch.int32, device="cuda")
+    rows = allrows[: a.rows].contiguous()
+    res = {"d": a.d, "key_gen_s": t1 - t0, "table_build_s": t2 - t1, "table_gb": eng.table_bytes() / 1e9}
+    for name, fn in [
+        ("commit_only_all_workers", lambda: eng.commitments(eng.shares(coeffs, allrows, commit_only=True)[0])),
+        ("shares_approved", lambda: eng.shares(coeffs, rows)),
+    ]:
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.iters):
+            s = time.time()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.time() - s)
+        res[name + "_ms"] = 1e3 * float(np.median(ts))
+    n_mults = a.rows * (a.d + (a.d // 10) * 21 * 9)
+    res["shares_scalar_mults"] = n_mults
+    res["shares_Gmult_per_s"] = n_mults / (res["shares_approved_ms"] / 1e3) / 1e9
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

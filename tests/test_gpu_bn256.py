@@ -1,0 +1,124 @@
+"""Numerics of the gfx950 BN256 kernels against the host runtime / Python big integers."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+P = 65000549695646603732796438742359905742825358107623003571877145026864184071783
+R = 1 << 256
+RINV = pow(R, -1, P)
+
+
+def _limbs(x):
+    return [(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
+
+
+def _from_limbs(row):
+    return sum(int(v) << (32 * i) for i, v in enumerate(row))
+
+
+def _to_dev(vals):
+    a = np.array([_limbs(v) for v in vals], dtype=np.uint32)
+    return torch.from_numpy(a.view(np.int32)).cuda()
+
+
+def _from_dev(t):
+    a = t.cpu().numpy().view(np.uint32)
+    return [_from_limbs(r) for r in a]
+
+
+def test_field_ops_match_bigint():
+    from biscotti_amd.ops import bn256 as B
+    rnd = random.Random(3)
+    xs = [0, 1, P - 1, P - 2, (1 << 255), R % P] + [rnd.randrange(P) for _ in range(2000)]
+    ys = [P - 1, 1, P - 1, 3, (1 << 255) - 1, 7] + [rnd.randrange(P) for _ in range(2000)]
+    a, b = _to_dev(xs), _to_dev(ys)
+    assert _from_dev(B.fp_op(a, b, 0)) == [(x * y * RINV) % P for x, y in zip(xs, ys)]
+    assert _from_dev(B.fp_op(a, b, 1)) == [(x + y) % P for x, y in zip(xs, ys)]
+    assert _from_dev(B.fp_op(a, b, 2)) == [(x - y) % P for x, y in zip(xs, ys)]
+    # Montgomery inverse: inv(xR) = x^-1 R  -> fp_inv works on the raw value: a^(p-2) in Montgomery domain
+    got = _from_dev(B.fp_op(a, b, 3))
+    for x, g in zip(xs[:200], got[:200]):
+        assert g == (pow(x * RINV, P - 2, P) * R) % P
+    assert _from_dev(B.fp_op(a, b, 4)) == [(x * RINV) % P for x in xs]
+
+
+def _aff_dev(rt, pts):
+    arr = np.concatenate([rt.g1_affine_mont_u32(p) for p in pts], axis=0)
+    return torch.from_numpy(arr.view(np.int32)).cuda()
+
+
+def test_point_ops_match_host(rt):
+    from biscotti_amd.ops import bn256 as B
+    g = rt.g1_generator()
+    rnd = random.Random(5)
+    ks_a = [rnd.randrange(1, 1 << 200) for _ in range(64)] + [5, 5, 7]
+    ks_b = [rnd.randrange(1, 1 << 200) for _ in range(64)] + [10, 0, 0]
+    A = [rt.g1_mul(g, k) for k in ks_a]
+    Bp = [rt.g1_mul(g, k) for k in ks_b]
+    a, b = _aff_dev(rt, A), _aff_dev(rt, Bp)
+    small = torch.tensor([rnd.randrange(-1000, 1000) for _ in A], dtype=torch.int32, device="cuda")
+    order = rt.bn256_order()
+    for op in range(4):
+        out = B.marshal(B.point_op(a, b, small, op)).cpu().numpy()
+        for i, (ka, kb) in enumerate(zip(ks_a, ks_b)):
+            if op in (0, 1):
+                k = 2 * ka + kb
+            elif op == 2:
+                k = 2 * ka
+            else:
+                k = ka * int(small[i]) % order
+            assert bytes(out[i]) == rt.g1_mul(g, k % order), (op, i)
+
+
+@pytest.mark.parametrize("d,secret,scale", [(25, 2, 10**4), (57, 2, 10**6), (33, 987654321123, 10**12),
+                                             (40, 2, 2**62)])
+def test_shares_msm_matches_host(rt, d, secret, scale):
+    from biscotti_amd.ops import bn256 as B
+    key = rt.CommitKey.generate(d, secret)
+    eng = B.DeviceCommitEngine(key, poly=10, total_shares=21)
+    rng = np.random.default_rng(d)
+    P_ = 3
+    coeffs = rng.integers(-scale, scale, size=(P_, d), dtype=np.int64)
+    coeffs[0, :7] = 0                     # zero scalars
+    coeffs[1, 3] = 2; coeffs[1, 4] = 1    # collisions with 2^i keys exercise doubling / P == -Q
+    coeffs[2, :] = rng.integers(-3, 3, size=d)
+    ct = torch.from_numpy(coeffs).cuda()
+    rows = torch.tensor([2, 0, 1], dtype=torch.int32, device="cuda")
+    pts, ys = eng.shares(ct, rows)
+    comm = B.marshal(eng.commitments(pts)).cpu().numpy()
+    allb = B.marshal(pts).cpu().numpy().reshape(3, eng.nchunks, 22, 64)
+    ys = ys.cpu().numpy()
+    for r, row in enumerate([2, 0, 1]):
+        commitment, chunk_commits, hys, wits = key.make_shares(coeffs[row], 10, 21)
+        assert bytes(comm[r]) == commitment
+        assert bytes(comm[r]) == key.commit(coeffs[row], 0)
+        np.testing.assert_array_equal(ys[r], hys)
+        for k in range(eng.nchunks):
+            assert bytes(allb[r, k, 21]) == chunk_commits[k]
+            for s in range(21):
+                assert bytes(allb[r, k, s]) == wits[k * 21 + s], (r, k, s)
+    # commit-only pass gives the same chunk commitments
+    pts_c, _ = eng.shares(ct, rows, commit_only=True)
+    np.testing.assert_array_equal(B.marshal(pts_c).cpu().numpy().reshape(3, eng.nchunks, 64), allb[:, :, 21])
+
+
+def test_sum_rows_is_aggregate(rt):
+    from biscotti_amd.ops import bn256 as B
+    d = 30
+    key = rt.CommitKey.generate(d, 3)
+    eng = B.DeviceCommitEngine(key, 10, 21)
+    coeffs = np.random.default_rng(1).integers(-10**5, 10**5, size=(4, d), dtype=np.int64)
+    pts, _ = eng.shares(torch.from_numpy(coeffs).cuda(), torch.arange(4, dtype=torch.int32, device="cuda"))
+    flat = pts.reshape(4, -1, 24)
+    rows = torch.tensor([0, 2, 3], dtype=torch.int32, device="cuda")
+    agg = B.marshal(B.sum_rows(flat, rows, None)).cpu().numpy().reshape(eng.nchunks, 22, 64)
+    summed = coeffs[[0, 2, 3]].sum(0)
+    commitment, chunk_commits, hys, wits = key.make_shares(summed, 10, 21)   # homomorphism
+    for k in range(eng.nchunks):
+        assert bytes(agg[k, 21]) == chunk_commits[k]
+        for s in range(21):
+            assert bytes(agg[k, s]) == wits[k * 21 + s]
