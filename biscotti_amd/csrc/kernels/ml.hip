@@ -1,0 +1,566 @@
+// Learning-side kernels of a Biscotti round (gfx950):
+//   K1  batched softmax-regression local step: minibatch draw, (x-0.5)/0.5 transform, logits
+//       (f32 MFMA), softmax + CE, backward dW (f32 MFMA) / db, clip_grad_norm(100), negate,
+//       fixed-point quantisation -- one workgroup per virtual peer
+//       (ML/Pytorch/client.py:38-65, client_obj.py:73-77, DistSys/kyber.go:698-710)
+//   K3  batched logistic-regression step with DP noise at source (ML/code/logistic_model.py:92-140)
+//   K4  counter-based Gaussian DP noise, averaged over each worker's noisers, added to the delta
+//       (client_obj.py:42-67,97-98; DistSys/main.go:1592-1660,1530-1537)
+//   K5  Multi-Krum: f64-MFMA Gram (split-K) + distances/scores/selection in LDS
+//       (client_obj.py:114-143)
+//   K2  test error / 1->7 attack rate (client.py:146-172)
+//   K12 exact secret recovery (128-bit Newton) + dequantisation + W update (kyber.go:809-857,
+//       honest.go:398-411,442-502)
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u4 {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ u4 philox(u4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    u4 n;
+    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    n.y = (uint32_t)p1;
+    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    n.w = (uint32_t)p0;
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+__device__ __forceinline__ float u01(uint32_t v) { return ((float)(v >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+__device__ __forceinline__ float gauss(uint32_t a, uint32_t b) {
+  const float r = sqrtf(-2.0f * logf(u01(a)));
+  return r * cosf(6.28318530717958647692f * u01(b));
+}
+
+__device__ __forceinline__ long long quantize(float v, double scale) {
+  // Go: int64(float64(delta) * 10^precision) -- truncation toward zero
+  return (long long)((double)v * scale);
+}
+
+}  // namespace
+
+// =====================================================================================
+// K1: softmax regression local step.  D_IN <= 1024, D_OUT <= 16, B <= 16.
+// X: [Ntot, D_IN] fp32 (standardised pixels), y: [Ntot] int32.  Peer p trains on rows
+// [off[p], off[p] + ntrain[p]).  W: [D_OUT*D_IN + D_OUT] fp64 global model (W row-major, b).
+// Outputs: delta fp32 [P, nparam], qdelta int64 [P, nparam], loss fp32 [P].
+// =====================================================================================
+constexpr int SM_MAXK = 1024;
+constexpr int SM_THREADS = 256;
+
+extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
+    const float* X, const int* y, const long long* off, const int* ntrain, const int* pid, const double* W, int D_IN,
+    int D_OUT, int B, int P, unsigned long long seed, int iteration, float max_norm, double qscale, float* delta,
+    long long* qdelta, float* loss) {
+  __shared__ float xs[16 * SM_MAXK];  // minibatch rows, transformed; rows >= B are zero
+  __shared__ float red[4][16][16];    // per-wave partial logits
+  __shared__ float G[16][16];         // (softmax - onehot) / B
+  __shared__ int bidx[16];
+  __shared__ float nrm[SM_THREADS / 64];
+  __shared__ float scale_sh;
+  const int p = blockIdx.x;
+  if (p >= P) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nparam = D_OUT * D_IN + D_OUT;
+  const int n = ntrain[p];
+  // 1. draw B distinct minibatch indices (DataLoader(shuffle=True) takes the first batch)
+  if (tid == 0) {
+    int cnt = 0;
+    uint32_t ctr = 0;
+    while (cnt < B && cnt < n) {
+      u4 r = philox(u4{(uint32_t)pid[p], (uint32_t)iteration, ctr++, 0x5EEDu}, (uint32_t)seed, (uint32_t)(seed >> 32));
+      const uint32_t cand[4] = {r.x, r.y, r.z, r.w};
+      for (int q = 0; q < 4 && cnt < B && cnt < n; ++q) {
+        const int c = (int)(cand[q] % (uint32_t)n);
+        bool dup = false;
+        for (int t = 0; t < cnt; ++t) dup |= bidx[t] == c;
+        if (!dup) bidx[cnt++] = c;
+      }
+    }
+    for (int t = cnt; t < 16; ++t) bidx[t] = -1;
+  }
+  __syncthreads();
+  const int Bq = min(B, n);
+  // 2. stage transformed rows (x - 0.5) / 0.5 (torchvision Normalize(0.5, 0.5)); zero padding
+  for (int i = tid; i < 16 * D_IN; i += SM_THREADS) {
+    const int s = i / D_IN, k = i % D_IN;
+    float v = 0.f;
+    if (s < Bq) v = (X[(off[p] + bidx[s]) * (long long)D_IN + k] - 0.5f) * 2.0f;
+    xs[s * SM_MAXK + k] = v;
+  }
+  __syncthreads();
+  // 3. logits via f32 MFMA 16x16x4: A[s][k] = xs, B[k][c] = W[c][k]; K split over the 4 waves
+  {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ksteps = (D_IN + 3) / 4;
+    const int per = (ksteps + 3) / 4;
+    const int i = lane & 15, kk = lane >> 4;
+    for (int st = wid * per; st < min(ksteps, (wid + 1) * per); ++st) {
+      const int k = st * 4 + kk;
+      const float a = (k < D_IN) ? xs[i * SM_MAXK + k] : 0.f;
+      const float b = (k < D_IN && i < D_OUT) ? (float)W[i * D_IN + k] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wid][(lane >> 4) * 4 + r][lane & 15] = acc[r];
+  }
+  __syncthreads();
+  // 4. softmax + cross-entropy on rows s < Bq (one thread per row)
+  if (tid < 16) {
+    const int s = tid;
+    if (s < Bq) {
+      float lg[16];
+      float mx = -INFINITY;
+      for (int c = 0; c < D_OUT; ++c) {
+        lg[c] = red[0][s][c] + red[1][s][c] + red[2][s][c] + red[3][s][c] + (float)W[D_OUT * D_IN + c];
+        mx = fmaxf(mx, lg[c]);
+      }
+      float se = 0.f;
+      for (int c = 0; c < D_OUT; ++c) se += expf(lg[c] - mx);
+      const int lab = y[off[p] + bidx[s]];
+      for (int c = 0; c < D_OUT; ++c) G[s][c] = (expf(lg[c] - mx) / se - (c == lab ? 1.f : 0.f)) / (float)Bq;
+      for (int c = D_OUT; c < 16; ++c) G[s][c] = 0.f;
+      red[0][s][0] = (mx + logf(se)) - lg[lab];  // per-row CE (red no longer needed)
+    } else {
+      for (int c = 0; c < 16; ++c) G[s][c] = 0.f;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float l = 0.f;
+    for (int s = 0; s < Bq; ++s) l += red[0][s][0];
+    loss[p] = l / (float)max(Bq, 1);
+  }
+  // 5. dW[c][k] = sum_s G[s][c] xs[s][k] via f32 MFMA (M = classes, N = k tiles, K = samples)
+  float* dst = delta + (size_t)p * nparam;
+  float sq = 0.f;
+  {
+    const int ntiles = (D_IN + 15) / 16;
+    const int col = lane & 15, kk = lane >> 4;
+    for (int t = wid; t < ntiles; t += 4) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int s = ks * 4 + kk;
+        const float a = G[s][col];  // A[c = col][s]
+        const int k = t * 16 + col;
+        const float b = (k < D_IN) ? xs[s * SM_MAXK + k] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      }
+      const int k = t * 16 + col;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = (lane >> 4) * 4 + r;
+        if (c < D_OUT && k < D_IN) {
+          dst[c * D_IN + k] = acc[r];
+          sq += acc[r] * acc[r];
+        }
+      }
+    }
+  }
+  if (tid < D_OUT) {
+    float db = 0.f;
+    for (int s = 0; s < 16; ++s) db += G[s][tid];
+    dst[D_OUT * D_IN + tid] = db;
+    sq += db * db;
+  }
+  // 6. clip_grad_norm(max_norm): total L2 norm over W and b
+  for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+  if (lane == 0) nrm[wid] = sq;
+  __syncthreads();
+  if (tid == 0) {
+    const float tot = sqrtf(nrm[0] + nrm[1] + nrm[2] + nrm[3]);
+    const float coef = max_norm / (tot + 1e-6f);
+    scale_sh = coef < 1.f ? coef : 1.f;
+  }
+  __syncthreads();
+  // 7. delta = -grad (client_obj.privateFun), quantised like updateFloatToInt
+  const float sc = -scale_sh;
+  long long* qd = qdelta + (size_t)p * nparam;
+  for (int i = tid; i < nparam; i += SM_THREADS) {
+    const float v = dst[i] * sc;
+    dst[i] = v;
+    qd[i] = quantize(v, qscale);
+  }
+}
+
+// =====================================================================================
+// K3: logistic regression step (creditcard path).  One wave per peer.
+// X: [Ntot, D] fp64 with bias column, y: [Ntot] (+1/-1); peer p samples B rows of
+// [off[p], off[p]+n[p]).  delta = -alpha * g + noise_at_source;  g = X^T(-y/(1+e^{yXw}))/B + lam*w
+// noise = (-alpha/B) * sigma*sqrt(B) * N(0,1)  (getNoise: samples are sums over the batch axis)
+// =====================================================================================
+extern "C" __global__ void __launch_bounds__(64) k_logreg_step(
+    const double* X, const double* y, const long long* off, const int* nrows, const int* pid, const double* W, int D,
+    int B, int P, unsigned long long seed, const int* calls, double alpha, double lammy, const double* sigma, double qscale,
+    float* delta, long long* qdelta) {
+  const int p = blockIdx.x;
+  if (p >= P) return;
+  const int lane = threadIdx.x;
+  __shared__ int bidx[64];
+  __shared__ double res[64];
+  const int n = nrows[p];
+  if (lane == 0) {
+    int cnt = 0;
+    uint32_t ctr = 0;
+    while (cnt < B && cnt < n) {
+      u4 r = philox(u4{(uint32_t)pid[p], (uint32_t)calls[p], ctr++, 0x106u}, (uint32_t)seed, (uint32_t)(seed >> 32));
+      const uint32_t cand[4] = {r.x, r.y, r.z, r.w};
+      for (int q = 0; q < 4 && cnt < B && cnt < n; ++q) {
+        const int c = (int)(cand[q] % (uint32_t)n);
+        bool dup = false;
+        for (int t = 0; t < cnt; ++t) dup |= bidx[t] == c;
+        if (!dup) bidx[cnt++] = c;
+      }
+    }
+  }
+  __syncthreads();
+  const int Bq = min(B, n);
+  if (lane < Bq) {
+    const double* xr = X + (off[p] + bidx[lane]) * (long long)D;
+    double z = 0.0;
+    for (int k = 0; k < D; ++k) z += xr[k] * W[k];
+    const double yy = y[off[p] + bidx[lane]];
+    // -y / exp(logaddexp(0, y*z)) == -y / (1 + exp(y*z))
+    const double t = yy * z;
+    const double lae = t > 0 ? t + log1p(exp(-t)) : log1p(exp(t));
+    res[lane] = -yy / exp(lae);
+  }
+  __syncthreads();
+  for (int k = lane; k < D; k += 64) {
+    double g = 0.0;
+    for (int s = 0; s < Bq; ++s) g += X[(off[p] + bidx[s]) * (long long)D + k] * res[s];
+    g = g / (double)B + lammy * W[k];
+    double v = -alpha * g;
+    if (sigma[p] > 0.0) {
+      u4 r = philox(u4{(uint32_t)k, (uint32_t)(calls[p] % 100), (uint32_t)pid[p], 0xD9u}, (uint32_t)(seed >> 7),
+                    (uint32_t)(seed >> 39));
+      v += (-alpha / (double)B) * sigma[p] * sqrt((double)B) * (double)gauss(r.x, r.y);
+    }
+    delta[(size_t)p * D + k] = (float)v;
+    qdelta[(size_t)p * D + k] = (long long)(v * qscale);
+  }
+}
+
+// =====================================================================================
+// K4: DP noise.  noised[p][i] = delta[p][i] + (1/nn) sum_j scale[j] * N(0,1; key=(seed,noiser_j),
+// ctr=(i, it%100)).  A noiser's vector depends only on (noiser, iteration % 100), like the
+// reference's pre-sampled samples[it % 100] (client_obj.py:61-63,97-98).
+// scale[j] = -sigma_j / sqrt(B)  (sigma_j = 0 for colluding noisers that pre-sampled with eps = 0)
+// =====================================================================================
+extern "C" __global__ void k_dp_noise(const float* delta, int P, int D, const int* noisers, int nn,
+                                      const float* noiser_scale, unsigned long long seed, int iter_mod,
+                                      float* noised) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long long)P * D) return;
+  const int p = (int)(g / D), i = (int)(g % D);
+  float acc = 0.f;
+  for (int j = 0; j < nn; ++j) {
+    const int nid = noisers[p * nn + j];
+    u4 r = philox(u4{(uint32_t)i, (uint32_t)iter_mod, (uint32_t)nid, 0xA11CEu}, (uint32_t)seed, (uint32_t)(seed >> 32));
+    acc += noiser_scale[p * nn + j] * gauss(r.x, r.y);
+  }
+  noised[g] = delta[g] + (nn > 0 ? acc / (float)nn : 0.f);
+}
+
+// =====================================================================================
+// K5a: Gram partials G_part[split][i][j] = sum_{k in split} X[i][k] X[j][k] in f64 via
+// v_mfma_f64_16x16x4f64.  Grid (tiles_i, tiles_j, splits), one wave per block.
+// f64 16x16x4 layout: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15]; D: col=l&15, row=(l>>4)+4*r.
+// =====================================================================================
+extern "C" __global__ void __launch_bounds__(64) k_gram_f64(const float* X, int n, int D, int ksplit,
+                                                           double* part) {
+  const int ti = blockIdx.x, tj = blockIdx.y, sp = blockIdx.z;
+  const int lane = threadIdx.x;
+  const int i = ti * 16 + (lane & 15), j = tj * 16 + (lane & 15), kk = lane >> 4;
+  const int k0 = sp * ksplit, k1 = min(D, k0 + ksplit);
+  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k = k0; k < k1; k += 4) {
+    const int kx = k + kk;
+    const double a = (i < n && kx < k1) ? (double)X[(size_t)i * D + kx] : 0.0;
+    const double b = (j < n && kx < k1) ? (double)X[(size_t)j * D + kx] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  const int npad = gridDim.x * 16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = ti * 16 + (lane >> 4) + 4 * r, col = tj * 16 + (lane & 15);
+    part[((size_t)sp * npad + row) * npad + col] = acc[r];
+  }
+}
+
+// K5b: reduce partials, distances, Krum scores and Multi-Krum selection; one block, n <= 256.
+// score_i = sum(sort(D_i)[1:groupsize-1]);  accept the n_accept lowest scores (index tiebreak).
+extern "C" __global__ void __launch_bounds__(256) k_krum_select(const double* part, int nsplit, int n, int npad,
+                                                               int groupsize, int n_accept, double* dist,
+                                                               double* scores, int* accept) {
+  __shared__ double sq[256];
+  __shared__ double sc[256];
+  const int t = threadIdx.x;
+  for (int idx = t; idx < n * n; idx += blockDim.x) {
+    const int i = idx / n, j = idx % n;
+    double g = 0.0;
+    for (int s = 0; s < nsplit; ++s) g += part[((size_t)s * npad + i) * npad + j];
+    dist[idx] = g;  // temporarily the Gram matrix
+  }
+  __syncthreads();
+  if (t < n) sq[t] = dist[t * n + t];
+  __syncthreads();
+  for (int idx = t; idx < n * n; idx += blockDim.x) {
+    const int i = idx / n, j = idx % n;
+    dist[idx] = sq[i] + sq[j] - 2.0 * dist[idx];
+  }
+  __syncthreads();
+  if (t < n) {
+    // insertion sort of row t in place (global, row is private to this thread)
+    double* row = dist + (size_t)t * n;
+    for (int a = 1; a < n; ++a) {
+      const double v = row[a];
+      int b = a - 1;
+      while (b >= 0 && row[b] > v) {
+        row[b + 1] = row[b];
+        --b;
+      }
+      row[b + 1] = v;
+    }
+    double s = 0.0;
+    for (int k = 1; k < groupsize - 1 && k < n; ++k) s += row[k];
+    sc[t] = s;
+    scores[t] = s;
+  }
+  __syncthreads();
+  if (t < n) {
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += (sc[j] < sc[t]) || (sc[j] == sc[t] && j < t);
+    accept[t] = rank < n_accept ? 1 : 0;
+  }
+}
+
+// =====================================================================================
+// K2: classification error of a softmax model: err[0] += #(argmax != label) over N rows.
+// One wave per row (grid-stride), W staged in LDS.
+// =====================================================================================
+extern "C" __global__ void __launch_bounds__(256) k_eval_error(const float* X, const int* y, int N, int D_IN,
+                                                              int D_OUT, const double* W, int transform,
+                                                              unsigned int* err) {
+  __shared__ float w[16 * SM_MAXK];
+  __shared__ float bsh[16];
+  for (int i = threadIdx.x; i < D_OUT * D_IN; i += blockDim.x) w[i] = (float)W[i];
+  if (threadIdx.x < D_OUT) bsh[threadIdx.x] = (float)W[D_OUT * D_IN + threadIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int waves = blockDim.x >> 6;
+  for (int r = blockIdx.x * waves + wid; r < N; r += gridDim.x * waves) {
+    float acc[16];
+    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+    const float* xr = X + (size_t)r * D_IN;
+    for (int k = lane; k < D_IN; k += 64) {
+      float v = xr[k];
+      if (transform) v = (v - 0.5f) * 2.0f;
+      for (int c = 0; c < D_OUT; ++c) acc[c] += v * w[c * D_IN + k];
+    }
+    for (int c = 0; c < D_OUT; ++c)
+      for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+    if (lane == 0) {
+      int best = 0;
+      float bv = acc[0] + bsh[0];
+      for (int c = 1; c < D_OUT; ++c) {
+        const float v = acc[c] + bsh[c];
+        if (v > bv) { bv = v; best = c; }  // np.argmax: first maximum
+      }
+      if (best != y[r]) atomicAdd(err, 1u);
+    }
+  }
+}
+
+// =====================================================================================
+// K12: exact recovery of the aggregated chunk polynomials from miner shares.
+// ys: int64 [nchunks][npts], xs: int [npts] distinct; deg+1 <= npts.  Newton divided differences
+// in 128-bit on the deg+1 nodes of smallest |x|, verified against every share.  Writes the
+// dequantised aggregate into W_new = W + coeff / 10^prec  (fp64, the reference's mat.Dense.Add).
+// status[k] = 1 exact, 0 inconsistent shares (caller falls back to least squares).
+// =====================================================================================
+namespace {
+__device__ __forceinline__ bool div_small(__int128 a, long long d, __int128* q) {
+  // exact division of a signed 128-bit value by a small non-zero divisor (|d| < 2^31)
+  const bool neg = (a < 0) != (d < 0);
+  unsigned __int128 m = a < 0 ? (unsigned __int128)(-a) : (unsigned __int128)a;
+  const unsigned long long dd = d < 0 ? (unsigned long long)(-d) : (unsigned long long)d;
+  const unsigned long long hi = (unsigned long long)(m >> 64), lo = (unsigned long long)m;
+  const unsigned long long qh = hi / dd;
+  unsigned long long r = hi % dd;
+  unsigned long long t = (r << 32) | (lo >> 32);
+  const unsigned long long q1 = t / dd;
+  r = t % dd;
+  t = (r << 32) | (lo & 0xFFFFFFFFull);
+  const unsigned long long q0 = t / dd;
+  r = t % dd;
+  if (r != 0) return false;
+  unsigned __int128 qq = ((unsigned __int128)qh << 64) | ((unsigned __int128)q1 << 32) | q0;
+  *q = neg ? -(__int128)qq : (__int128)qq;
+  return true;
+}
+}  // namespace
+
+extern "C" __global__ void k_recover(const long long* ys, int nchunks, int npts, const int* xs, int poly, int d,
+                                     const double* W, double qscale, double* W_new, long long* coeffs,
+                                     int* status) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nchunks) return;
+  const int n = poly;  // degree poly-1
+  // node choice: smallest |x| first (stable)
+  int order[32];
+  for (int i = 0; i < npts; ++i) order[i] = i;
+  for (int a = 1; a < npts; ++a) {
+    const int v = order[a];
+    const int av = xs[v] < 0 ? -xs[v] : xs[v];
+    int b = a - 1;
+    while (b >= 0) {
+      const int ob = xs[order[b]] < 0 ? -xs[order[b]] : xs[order[b]];
+      if (ob > av || (ob == av && xs[order[b]] > xs[v])) {
+        order[b + 1] = order[b];
+        --b;
+      } else {
+        break;
+      }
+    }
+    order[b + 1] = v;
+  }
+  __int128 nx[16], dd[16], c[16];
+  bool ok = npts >= n;
+  for (int i = 0; i < n && ok; ++i) {
+    nx[i] = xs[order[i]];
+    dd[i] = ys[(size_t)k * npts + order[i]];
+  }
+  for (int lvl = 1; lvl < n && ok; ++lvl)
+    for (int i = n - 1; i >= lvl && ok; --i) {
+      __int128 q;
+      ok = div_small(dd[i] - dd[i - 1], (long long)(nx[i] - nx[i - lvl]), &q);
+      dd[i] = q;
+    }
+  if (ok) {
+    for (int i = 0; i < n; ++i) c[i] = 0;
+    c[0] = dd[n - 1];
+    int cur = 0;
+    for (int kk = n - 2; kk >= 0; --kk) {
+      for (int j = cur + 1; j >= 1; --j) c[j] = c[j - 1] - nx[kk] * c[j];
+      c[0] = -nx[kk] * c[0] + dd[kk];
+      ++cur;
+    }
+    for (int pt = 0; pt < npts && ok; ++pt) {
+      __int128 acc = 0;
+      for (int j = n - 1; j >= 0; --j) acc = acc * xs[pt] + c[j];
+      ok = acc == (__int128)ys[(size_t)k * npts + pt];
+    }
+  }
+  status[k] = ok ? 1 : 0;
+  const int prev = k * poly;
+  for (int j = 0; j < n; ++j) {
+    const long long v = ok ? (long long)c[j] : 0;
+    coeffs[(size_t)k * n + j] = v;
+    const int idx = prev + j;
+    if (idx < d) W_new[idx] = W[idx] + (double)v / qscale;
+  }
+}
+
+// =====================================================================================
+// Plain aggregation (non-secure-agg / FedSys): W_new = W + sum_r delta64[rows[r]] in fp64,
+// in row order (mat.Dense.Add sequence).
+// =====================================================================================
+extern "C" __global__ void k_add_rows(const float* delta, int D, const int* rows, int nrows, const double* W,
+                                      double* W_new) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= D) return;
+  double acc = W[i];
+  for (int r = 0; r < nrows; ++r) acc += (double)delta[(size_t)rows[r] * D + i];
+  W_new[i] = acc;
+}
+
+// ---------------------------------------------------------------- C ABI launchers
+static inline int nblk(long long n, int bs) { return (int)((n + bs - 1) / bs); }
+
+extern "C" int bsc_softmax_step(const float* X, const int* y, const long long* off, const int* ntrain,
+                                const int* pid, const double* W, int D_IN, int D_OUT, int B, int P, unsigned long long seed,
+                                int iteration, float max_norm, double qscale, float* delta, long long* qdelta,
+                                float* loss, void* stream) {
+  if (D_IN > SM_MAXK || D_OUT > 16 || B > 16) return -1;
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_softmax_step, dim3(P), dim3(SM_THREADS), 0, (hipStream_t)stream, X, y, off, ntrain, pid, W, D_IN,
+                     D_OUT, B, P, seed, iteration, max_norm, qscale, delta, qdelta, loss);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_logreg_step(const double* X, const double* y, const long long* off, const int* nrows,
+                               const int* pid, const double* W, int D, int B, int P, unsigned long long seed, const int* calls,
+                               double alpha, double lammy, const double* sigma, double qscale, float* delta,
+                               long long* qdelta, void* stream) {
+  if (B > 64) return -1;
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_logreg_step, dim3(P), dim3(64), 0, (hipStream_t)stream, X, y, off, nrows, pid, W, D, B, P, seed,
+                     calls, alpha, lammy, sigma, qscale, delta, qdelta);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_dp_noise(const float* delta, int P, int D, const int* noisers, int nn, const float* scale,
+                            unsigned long long seed, int iter_mod, float* noised, void* stream) {
+  const long long n = (long long)P * D;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_dp_noise, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, delta, P, D, noisers, nn,
+                     scale, seed, iter_mod, noised);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_krum(const float* X, int n, int D, int ksplit, double* part, double* dist, double* scores,
+                        int* accept, int groupsize, int n_accept, void* stream) {
+  if (n <= 0) return 0;
+  if (n > 256) return -1;
+  const int tiles = (n + 15) / 16;
+  const int nsplit = (D + ksplit - 1) / ksplit;
+  hipLaunchKernelGGL(k_gram_f64, dim3(tiles, tiles, nsplit), dim3(64), 0, (hipStream_t)stream, X, n, D, ksplit,
+                     part);
+  hipLaunchKernelGGL(k_krum_select, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nsplit, n, tiles * 16,
+                     groupsize, n_accept, dist, scores, accept);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_eval_error(const float* X, const int* y, int N, int D_IN, int D_OUT, const double* W,
+                              int transform, unsigned int* err, void* stream) {
+  if (D_IN > SM_MAXK || D_OUT > 16) return -1;
+  if (N <= 0) return 0;
+  const int blocks = min(1024, nblk(N, 4));
+  hipLaunchKernelGGL(k_eval_error, dim3(blocks), dim3(256), 0, (hipStream_t)stream, X, y, N, D_IN, D_OUT, W,
+                     transform, err);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_recover(const long long* ys, int nchunks, int npts, const int* xs, int poly, int d,
+                           const double* W, double qscale, double* W_new, long long* coeffs, int* status,
+                           void* stream) {
+  if (nchunks <= 0) return 0;
+  if (npts > 32 || poly > 16) return -1;
+  hipLaunchKernelGGL(k_recover, dim3(nblk(nchunks, 64)), dim3(64), 0, (hipStream_t)stream, ys, nchunks, npts, xs,
+                     poly, d, W, qscale, W_new, coeffs, status);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_add_rows(const float* delta, int D, const int* rows, int nrows, const double* W, double* W_new,
+                            void* stream) {
+  if (D <= 0) return 0;
+  hipLaunchKernelGGL(k_add_rows, dim3(nblk(D, 256)), dim3(256), 0, (hipStream_t)stream, delta, D, rows, nrows, W,
+                     W_new);
+  return (int)hipGetLastError();
+}

@@ -146,6 +146,24 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     for (py::ssize_t i = 0; i < jac.shape(0); ++i) acc = acc.add(g1_from_jac_u32(jac.data(i, 0)));
     return P(acc.marshal());
   });
+  m.def("g1_sum_marshaled", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> a) {
+    // a: [R, C, 64] marshaled points -> [C, 64] sums over R (miner-side aggregateSecret on CPU)
+    if (a.ndim() != 3 || a.shape(2) != 64) throw std::runtime_error("expected [R, C, 64] uint8");
+    const py::ssize_t R = a.shape(0), Cn = a.shape(1);
+    py::array_t<uint8_t> out({Cn, py::ssize_t(64)});
+    std::vector<G1> acc(size_t(Cn), G1::infinity());
+    {
+      py::gil_scoped_release rel;
+      for (py::ssize_t c = 0; c < Cn; ++c)
+        for (py::ssize_t r = 0; r < R; ++r)
+          acc[size_t(c)] = acc[size_t(c)].add(G1::unmarshal(Bytes(a.data(r, c, 0), a.data(r, c, 0) + 64)));
+    }
+    for (py::ssize_t c = 0; c < Cn; ++c) {
+      Bytes b = acc[size_t(c)].marshal();
+      std::memcpy(out.mutable_data(c, 0), b.data(), 64);
+    }
+    return out;
+  });
   m.def("g2_generator", [] { return P(G2::generator().marshal()); });
   m.def("g2_mul", [](py::bytes a, py::int_ k) { return P(G2::unmarshal(B(a)).mul(u256_from_pyint(k)).marshal()); });
   m.def("g2_add", [](py::bytes a, py::bytes b) { return P(G2::unmarshal(B(a)).add(G2::unmarshal(B(b))).marshal()); });

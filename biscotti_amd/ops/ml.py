@@ -1,0 +1,280 @@
+"""Learning-side ops of a Biscotti round: local step, DP noise, Multi-Krum, evaluation, recovery.
+
+On a GPU every op launches the gfx950 kernel from ``csrc/kernels/ml.hip`` (there is no eager
+fallback on GPU: a missing library raises).  On CPU the same math runs as a numpy/torch reference
+that draws from the identical Philox4x32-10 streams, so CPU runs reproduce GPU runs up to
+float rounding and GPU numerics tests compare against it.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..native import hip
+
+PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
+PHILOX_W0, PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
+MASK32 = 0xFFFFFFFF
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    if t is None:
+        return None
+    assert t.is_contiguous(), "kernel operands must be contiguous"
+    return t.data_ptr()
+
+
+def _check(err: int, what: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"HIP launch of {what} failed (code {err})")
+
+
+# ---------------------------------------------------------------------------- Philox (numpy)
+def philox4x32(c0, c1, c2, c3, k0: int, k1: int):
+    """Vectorised Philox4x32-10; inputs are uint32-compatible arrays/scalars."""
+    c0, c1, c2, c3 = (np.asarray(v, dtype=np.uint64) & MASK32 for v in (c0, c1, c2, c3))
+    c0, c1, c2, c3 = np.broadcast_arrays(c0, c1, c2, c3)
+    c0, c1, c2, c3 = (x.copy() for x in (c0, c1, c2, c3))
+    k0 = np.uint64(k0 & MASK32)
+    k1 = np.uint64(k1 & MASK32)
+    for _ in range(10):
+        p0 = np.uint64(PHILOX_M0) * c0
+        p1 = np.uint64(PHILOX_M1) * c2
+        n0 = ((p1 >> np.uint64(32)) ^ c1 ^ k0) & np.uint64(MASK32)
+        n1 = p1 & np.uint64(MASK32)
+        n2 = ((p0 >> np.uint64(32)) ^ c3 ^ k1) & np.uint64(MASK32)
+        n3 = p0 & np.uint64(MASK32)
+        c0, c1, c2, c3 = n0, n1, n2, n3
+        k0 = np.uint64((int(k0) + PHILOX_W0) & MASK32)
+        k1 = np.uint64((int(k1) + PHILOX_W1) & MASK32)
+    return c0, c1, c2, c3
+
+
+def _u01(v):
+    return ((np.asarray(v) >> np.uint64(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+
+
+def _gauss(a, b):
+    r = np.sqrt(np.float32(-2.0) * np.log(_u01(a)))
+    return (r * np.cos(np.float32(6.28318530717958647692) * _u01(b))).astype(np.float32)
+
+
+def minibatch_indices(p: int, iteration: int, n: int, B: int, seed: int, tag: int = 0x5EED) -> list[int]:
+    """The B distinct indices the local-step kernel draws for peer p (DataLoader shuffle analogue)."""
+    out: list[int] = []
+    ctr = 0
+    while len(out) < min(B, n):
+        r = philox4x32(p, iteration, ctr, tag, seed & MASK32, (seed >> 32) & MASK32)
+        ctr += 1
+        for v in r:
+            if len(out) >= min(B, n):
+                break
+            c = int(v) % n
+            if c not in out:
+                out.append(c)
+    return out
+
+
+# ---------------------------------------------------------------------------- K1 softmax step
+def softmax_step(X, y, off, ntrain, pid, W, d_in, d_out, B, seed, iteration, max_norm=100.0, qscale=1e4):
+    """Batched local SGD step of SoftmaxModel for every local peer.
+
+    X fp32 [Ntot, d_in]; y int32 [Ntot]; off int64 [P]; ntrain int32 [P]; pid int32 [P] global peer
+    ids (key of each peer's minibatch stream); W fp64 [nparam].
+    Returns (delta fp32 [P, nparam] = -clip(grad), qdelta int64 [P, nparam], loss fp32 [P]).
+    """
+    P = off.numel()
+    nparam = d_out * d_in + d_out
+    dev = X.device
+    delta = torch.empty((P, nparam), dtype=torch.float32, device=dev)
+    qdelta = torch.empty((P, nparam), dtype=torch.int64, device=dev)
+    loss = torch.empty((P,), dtype=torch.float32, device=dev)
+    if dev.type == "cuda":
+        assert X.dtype == torch.float32 and y.dtype == torch.int32 and W.dtype == torch.float64
+        assert off.dtype == torch.int64 and ntrain.dtype == torch.int32 and W.numel() == nparam
+        assert pid.dtype == torch.int32 and pid.numel() == P
+        _check(hip().bsc_softmax_step(_p(X), _p(y), _p(off), _p(ntrain), _p(pid), _p(W), d_in, d_out, B, P, seed & (2**64 - 1),
+                                      iteration, float(max_norm), float(qscale), _p(delta), _p(qdelta), _p(loss),
+                                      _stream()), "softmax_step")
+        return delta, qdelta, loss
+    Wm = W.to(torch.float32)
+    Wt, bt = Wm[: d_out * d_in].view(d_out, d_in), Wm[d_out * d_in:]
+    offs, ns, pids = off.tolist(), ntrain.tolist(), pid.tolist()
+    for p in range(P):
+        idx = minibatch_indices(pids[p], iteration, ns[p], B, seed)
+        rows = torch.tensor([offs[p] + i for i in idx], dtype=torch.long)
+        xb = (X[rows] - 0.5) / 0.5
+        logits = xb @ Wt.T + bt
+        lab = y[rows].long()
+        lossv = torch.nn.functional.cross_entropy(logits, lab)
+        g = (torch.softmax(logits, 1) - torch.nn.functional.one_hot(lab, d_out).float()) / len(idx)
+        dW, db = g.T @ xb, g.sum(0)
+        flat = torch.cat([dW.reshape(-1), db])
+        tot = float(torch.linalg.vector_norm(flat))
+        coef = max_norm / (tot + 1e-6)
+        if coef < 1:
+            flat = flat * coef
+        v = -flat
+        delta[p] = v
+        qdelta[p] = torch.from_numpy((v.double().numpy() * qscale).astype(np.int64))
+        loss[p] = lossv
+    return delta, qdelta, loss
+
+
+# ---------------------------------------------------------------------------- K3 logistic step
+def logreg_step(X, y, off, nrows, pid, W, B, seed, calls, alpha, lammy, sigma, qscale=1e4):
+    """Batched logistic-regression step (creditcard path), DP noise at source when sigma > 0.
+
+    X fp64 [Ntot, D]; y fp64 [Ntot] (+-1); off int64 [P]; nrows int32 [P]; W fp64 [D];
+    calls int32 [P] (per-peer privateFun call counter); sigma fp64 [P].
+    """
+    P, D = off.numel(), X.shape[1]
+    dev = X.device
+    delta = torch.empty((P, D), dtype=torch.float32, device=dev)
+    qdelta = torch.empty((P, D), dtype=torch.int64, device=dev)
+    if dev.type == "cuda":
+        _check(hip().bsc_logreg_step(_p(X), _p(y), _p(off), _p(nrows), _p(pid), _p(W), D, B, P, seed & (2**64 - 1), _p(calls),
+                                     float(alpha), float(lammy), _p(sigma), float(qscale), _p(delta), _p(qdelta),
+                                     _stream()), "logreg_step")
+        return delta, qdelta
+    Xn, yn, Wn = X.numpy(), y.numpy(), W.numpy()
+    for p in range(P):
+        n = int(nrows[p])
+        idx = minibatch_indices(int(pid[p]), int(calls[p]), n, B, seed, tag=0x106)
+        rows = [int(off[p]) + i for i in idx]
+        xb, yb = Xn[rows], yn[rows]
+        t = yb * (xb @ Wn)
+        res = -yb / np.exp(np.logaddexp(0, t))
+        g = xb.T @ res / B + lammy * Wn
+        v = -alpha * g
+        if float(sigma[p]) > 0:
+            r = philox4x32(np.arange(D), int(calls[p]) % 100, int(pid[p]), 0xD9, (seed >> 7) & MASK32, (seed >> 39) & MASK32)
+            v = v + (-alpha / B) * float(sigma[p]) * np.sqrt(B) * _gauss(r[0], r[1]).astype(np.float64)
+        delta[p] = torch.from_numpy(v.astype(np.float32))
+        qdelta[p] = torch.from_numpy((v * qscale).astype(np.int64))
+    return delta, qdelta
+
+
+# ---------------------------------------------------------------------------- K4 DP noise
+def dp_noise(delta, noisers, scales, seed, iteration):
+    """noised = delta + mean_j scales[p, j] * N(0, 1; noiser_j, iteration % 100)."""
+    P, D = delta.shape
+    nn_ = noisers.shape[1] if noisers.dim() == 2 else 0
+    out = torch.empty_like(delta)
+    if delta.device.type == "cuda":
+        _check(hip().bsc_dp_noise(_p(delta), P, D, _p(noisers), nn_, _p(scales), seed & (2**64 - 1), iteration % 100,
+                                  _p(out), _stream()), "dp_noise")
+        return out
+    acc = np.zeros((P, D), dtype=np.float32)
+    idx = np.arange(D)
+    for p in range(P):
+        for j in range(nn_):
+            nid = int(noisers[p, j])
+            r = philox4x32(idx, iteration % 100, nid, 0xA11CE, seed & MASK32, (seed >> 32) & MASK32)
+            acc[p] += np.float32(float(scales[p, j])) * _gauss(r[0], r[1])
+    if nn_:
+        acc /= np.float32(nn_)
+    return delta + torch.from_numpy(acc)
+
+
+def noise_vector(noiser: int, iteration: int, D: int, seed: int) -> np.ndarray:
+    """N(0,1) vector a noiser contributes at `iteration` (before scaling) -- RequestNoise payload."""
+    r = philox4x32(np.arange(D), iteration % 100, noiser, 0xA11CE, seed & MASK32, (seed >> 32) & MASK32)
+    return _gauss(r[0], r[1])
+
+
+# ---------------------------------------------------------------------------- K5 Multi-Krum
+def krum(X, groupsize: int, n_accept: int, ksplit: int = 512):
+    """Multi-Krum over the rows of X (fp32 [n, d]): returns (accept bool [n], scores fp64 [n])."""
+    n, D = X.shape
+    if n == 0:
+        return torch.zeros(0, dtype=torch.bool), torch.zeros(0, dtype=torch.float64)
+    if X.device.type == "cuda":
+        assert n <= 256, "krum kernel handles up to 256 updates per verifier"
+        tiles = (n + 15) // 16
+        nsplit = (D + ksplit - 1) // ksplit
+        part = torch.empty((nsplit, tiles * 16, tiles * 16), dtype=torch.float64, device=X.device)
+        dist = torch.empty((n, n), dtype=torch.float64, device=X.device)
+        scores = torch.empty((n,), dtype=torch.float64, device=X.device)
+        acc = torch.empty((n,), dtype=torch.int32, device=X.device)
+        _check(hip().bsc_krum(_p(X), n, D, ksplit, _p(part), _p(dist), _p(scores), _p(acc), groupsize, n_accept,
+                              _stream()), "krum")
+        return acc.bool(), scores
+    Xd = X.double()
+    sq = (Xd * Xd).sum(1)
+    dist = sq[:, None] + sq[None] - 2 * Xd @ Xd.T
+    srt, _ = torch.sort(dist, dim=1)
+    hi = max(1, min(groupsize - 1, n))
+    scores = srt[:, 1:hi].sum(1) if hi > 1 else torch.zeros(n, dtype=torch.float64)
+    order = sorted(range(n), key=lambda i: (float(scores[i]), i))
+    acc = torch.zeros(n, dtype=torch.bool)
+    acc[order[:n_accept]] = True
+    return acc, scores
+
+
+# ---------------------------------------------------------------------------- K2 evaluation
+def eval_error(X, y, W, d_in, d_out, transform=True) -> float:
+    """1 - accuracy of the softmax model W on (X, y) (client.getTestErr / get17AttackRate)."""
+    N = X.shape[0]
+    if N == 0:
+        return 0.0
+    if X.device.type == "cuda":
+        err = torch.zeros((1,), dtype=torch.int32, device=X.device)
+        _check(hip().bsc_eval_error(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), _p(err), _stream()),
+               "eval_error")
+        return float(err.item()) / N
+    Wm = W.to(torch.float32)
+    xb = (X - 0.5) / 0.5 if transform else X
+    logits = xb @ Wm[: d_out * d_in].view(d_out, d_in).T + Wm[d_out * d_in:]
+    pred = torch.argmax(logits, 1)
+    return float((pred != y.long()).sum()) / N
+
+
+# ---------------------------------------------------------------------------- K12 recovery
+def recover(agg_y, xs, poly: int, d: int, W, qscale=1e4):
+    """Recover the aggregated quantised update from miner shares and apply it to W.
+
+    agg_y int64 [nchunks, npts]; xs int32 [npts].  Returns (W_new fp64 [d], coeffs int64
+    [nchunks, poly], status int32 [nchunks]).
+    """
+    nchunks, npts = agg_y.shape
+    dev = agg_y.device
+    W_new = torch.empty_like(W)
+    coeffs = torch.empty((nchunks, poly), dtype=torch.int64, device=dev)
+    status = torch.empty((nchunks,), dtype=torch.int32, device=dev)
+    if dev.type == "cuda":
+        _check(hip().bsc_recover(_p(agg_y), nchunks, npts, _p(xs), poly, d, _p(W), float(qscale), _p(W_new),
+                                 _p(coeffs), _p(status), _stream()), "recover")
+        return W_new, coeffs, status
+    from ..native import rt
+
+    xl = [int(v) for v in xs]
+    Wn = W.numpy().copy()
+    for k in range(nchunks):
+        r = rt().recover_exact(xl, [int(v) for v in agg_y[k]], poly - 1)
+        status[k] = 1 if r is not None else 0
+        r = r if r is not None else [0] * poly
+        coeffs[k] = torch.tensor(r, dtype=torch.int64)
+        for j in range(poly):
+            i = k * poly + j
+            if i < d:
+                Wn[i] = Wn[i] + float(r[j]) / qscale
+    W_new.copy_(torch.from_numpy(Wn))
+    return W_new, coeffs, status
+
+
+def add_rows(delta, rows, W):
+    """W + sum of delta[rows] (fp64, sequential like mat.Dense.Add)."""
+    D = W.numel()
+    if W.device.type == "cuda":
+        out = torch.empty_like(W)
+        _check(hip().bsc_add_rows(_p(delta), D, _p(rows), rows.numel(), _p(W), _p(out), _stream()), "add_rows")
+        return out
+    acc = W.clone()
+    for r in rows.tolist():
+        acc += delta[r].double()
+    return acc

@@ -1,0 +1,138 @@
+"""Peer <-> rank mapping and the collectives of a Biscotti round.
+
+The reference moves every protocol message as a point-to-point Go net/rpc call (DistSys/main.go,
+SURVEY.md section 2.7).  Here peers are *virtual* and packed into contiguous blocks per rank (one
+process per GPU); per-round traffic is a handful of collectives:
+
+  noised deltas + commitments -> verifiers      all_gather (one-shot, every link at once)
+  accept masks + Schnorr signatures -> workers  all_gather
+  Shamir shares worker -> miner                 all_to_all (personalised, variable sizes)
+  miner aggregates -> leader                    all_gather
+  block (header + GlobalW) leader -> everyone   broadcast
+
+With world size 1 all of these are local no-ops.  Backend "nccl" is RCCL on ROCm (xGMI); "gloo"
+runs the same code on CPU for tests and the plumbing configuration.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Comm:
+    world: int = 1
+    rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    # ------------------------------------------------------------------ setup
+    @staticmethod
+    def init(device: str | None = None, backend: str | None = None) -> "Comm":
+        """Initialise from torchrun-style env vars (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+        want_gpu = device != "cpu" and torch.cuda.is_available()
+        if want_gpu:
+            torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+            dev = torch.device("cuda", torch.cuda.current_device())
+        else:
+            dev = torch.device("cpu")
+        if world > 1 and not dist.is_initialized():
+            be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = {"device_id": dev} if be == "nccl" else {}
+            try:
+                dist.init_process_group(be, rank=rank, world_size=world, **kw)
+            except TypeError:
+                dist.init_process_group(be, rank=rank, world_size=world)
+        be = dist.get_backend() if dist.is_initialized() else "none"
+        return Comm(world, rank, dev, be)
+
+    def shutdown(self) -> None:
+        if self.world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+    # ------------------------------------------------------------------ ownership
+    def peer_range(self, num_peers: int, rank: int | None = None) -> range:
+        r = self.rank if rank is None else rank
+        return range(r * num_peers // self.world, (r + 1) * num_peers // self.world)
+
+    def owner(self, peer: int, num_peers: int) -> int:
+        for r in range(self.world):
+            if peer in self.peer_range(num_peers, r):
+                return r
+        raise ValueError(peer)
+
+    def max_local(self, num_peers: int) -> int:
+        return max(len(self.peer_range(num_peers, r)) for r in range(self.world))
+
+    # ------------------------------------------------------------------ collectives
+    def barrier(self) -> None:
+        if self.world > 1:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """[...] per rank -> [world, ...] (same shape on every rank)."""
+        t = t.contiguous()
+        if self.world == 1:
+            return t.unsqueeze(0)
+        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t)
+        return out
+
+    def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, src)
+        return t
+
+    def broadcast_bytes(self, data: bytes | None, src: int) -> bytes:
+        if self.world == 1:
+            assert data is not None
+            return data
+        n = torch.zeros((1,), dtype=torch.int64, device=self.device)
+        if self.rank == src:
+            n[0] = len(data)
+        dist.broadcast(n, src)
+        buf = torch.empty((int(n.item()),), dtype=torch.uint8, device=self.device)
+        if self.rank == src:
+            buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+        dist.broadcast(buf, src)
+        return data if self.rank == src else bytes(buf.cpu().numpy())
+
+    def all_to_all(self, send: list[torch.Tensor]) -> list[torch.Tensor]:
+        """Personalised exchange of 1-D tensors of one dtype; send[r] goes to rank r.
+
+        Receive sizes are exchanged first (one tiny all_gather), then one all_to_all_single."""
+        assert len(send) == self.world
+        if self.world == 1:
+            return [send[0]]
+        dtype = send[0].dtype
+        sizes = torch.tensor([s.numel() for s in send], dtype=torch.int64, device=self.device)
+        allsizes = self.all_gather(sizes)  # [src, dst]
+        recv_sizes = [int(v) for v in allsizes[:, self.rank].tolist()]
+        inp = torch.cat([s.reshape(-1) for s in send]) if any(s.numel() for s in send) else \
+            torch.empty((0,), dtype=dtype, device=self.device)
+        out = torch.empty((sum(recv_sizes),), dtype=dtype, device=self.device)
+        try:
+            dist.all_to_all_single(out, inp, recv_sizes, [s.numel() for s in send])
+        except (RuntimeError, NotImplementedError):
+            # backends without alltoall: padded all_gather
+            m = max(int(allsizes.max()), 1)
+            pad = torch.zeros((self.world, m), dtype=dtype, device=self.device)
+            for r, s in enumerate(send):
+                pad[r, : s.numel()] = s.reshape(-1)
+            g = self.all_gather(pad)  # [src, dst, m]
+            out = torch.cat([g[src, self.rank, : recv_sizes[src]] for src in range(self.world)])
+        res, o = [], 0
+        for n in recv_sizes:
+            res.append(out[o:o + n])
+            o += n
+        return res

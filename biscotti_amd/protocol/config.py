@@ -1,0 +1,125 @@
+"""Typed run configuration accepting the reference's flag names (DistSys/main.go:613-647)."""
+from __future__ import annotations
+
+import argparse
+from dataclasses import dataclass, field, fields
+
+
+@dataclass
+class RunConfig:
+    # --- reference flags
+    num_nodes: int = 100            # -t
+    node_index: int = -1            # -i  (per-process mode; SPMD runs host several peers per rank)
+    dataset: str = "mnist"          # -d  mnist | creditcard
+    peers_file: str | None = None   # -f
+    my_ip: str = ""                 # -a
+    my_private_ip: str = ""         # -pa
+    port: str = ""                  # -p
+    colluders: int = 0              # -c  percent
+    num_miners: int = 3             # -na
+    num_verifiers: int = 3          # -nv
+    num_noisers: int = 2            # -nn
+    secure_agg: bool = True         # -sa
+    noising: bool = True            # -np
+    verification: bool = True       # -vp
+    epsilon: float = 2.0            # -ep
+    poisoning: float = 0.0          # -po
+    perc_samples: int = 70          # -ns
+    rand_sample: bool = False       # -rs
+    # --- compile-time constants of the reference (main.go:28-58, honest.go:44-57)
+    defense: str = "KRUM"           # POISON_DEFENSE (KRUM | RONI)
+    max_iterations: int = 100       # MAX_ITERATIONS
+    poly_size: int = 10             # POLY_SIZE
+    precision: int = 4              # PRECISION
+    batch_size: int = 10
+    default_stake: int = 10
+    stake_unit: int = 5
+    # --- framework knobs
+    seed: int = 0
+    churn: float = 0.0              # fraction of peers offline per round (fault-tolerance runs)
+    data_dir: str | None = None     # real MNIST .npy shards (reference layout), else synthetic
+    commit_key: str | None = None   # commitKey.json (else generated: PK[i] = 2^i G1, s = 2)
+    pkey_file: str | None = None    # pKeyG1.json (else derived from seed)
+    roles_vrf_proof: bool = True    # getVRFRoles computes (and discards) a proof; keep the work
+    verify_signatures: bool = False  # miners check verifier signatures (commented out in reference, Q5)
+    host_threads: int = 16
+    log_dir: str | None = None
+    trace_file: str | None = None
+    chain_file: str | None = None   # append-only chain persistence (checkpoint / resume)
+    resume: bool = False
+    device: str | None = None       # "cpu" forces the CPU path
+    log_every_peer: bool = False    # one Train Error line per local peer (reference style)
+
+    def protocol(self, rt):
+        pc = rt.ProtocolConfig()
+        pc.num_nodes = self.num_nodes
+        pc.num_verifiers = self.num_verifiers
+        pc.num_miners = self.num_miners
+        pc.num_noisers = self.num_noisers
+        pc.secure_agg = self.secure_agg
+        pc.noising = self.noising
+        pc.verification = self.verification
+        pc.epsilon = self.epsilon
+        pc.poisoning = self.poisoning
+        pc.perc_samples = self.perc_samples
+        pc.rand_sample = self.rand_sample
+        pc.colluders = self.colluders
+        pc.defense = self.defense
+        pc.poly_size = self.poly_size
+        pc.precision = self.precision
+        pc.max_iterations = self.max_iterations
+        pc.default_stake = self.default_stake
+        pc.stake_unit = self.stake_unit
+        pc.seed = self.seed & (2**64 - 1)
+        pc.derive()
+        return pc
+
+
+def _bool(s: str) -> bool:
+    return str(s).lower() in ("1", "true", "t", "yes", "y")
+
+
+def add_reference_flags(ap: argparse.ArgumentParser) -> None:
+    """Register the DistSys flags (single-dash, Go style) on an argparse parser."""
+    ap.add_argument("-t", dest="num_nodes", type=int, default=100, help="total number of nodes")
+    ap.add_argument("-i", dest="node_index", type=int, default=-1, help="this node's index")
+    ap.add_argument("-d", dest="dataset", default="mnist", help="dataset (mnist | creditcard)")
+    ap.add_argument("-f", dest="peers_file", default=None, help="peers file (IP:port per line)")
+    ap.add_argument("-a", dest="my_ip", default="", help="public IP")
+    ap.add_argument("-pa", dest="my_private_ip", default="", help="private IP")
+    ap.add_argument("-p", dest="port", default="", help="port")
+    ap.add_argument("-c", dest="colluders", type=int, default=0, help="colluders (percent)")
+    ap.add_argument("-na", dest="num_miners", type=int, default=3, help="number of aggregators")
+    ap.add_argument("-nv", dest="num_verifiers", type=int, default=3, help="number of verifiers")
+    ap.add_argument("-nn", dest="num_noisers", type=int, default=2, help="number of noisers")
+    ap.add_argument("-sa", dest="secure_agg", type=_bool, default=True, help="secure aggregation on/off")
+    ap.add_argument("-np", dest="noising", type=_bool, default=True, help="noising on/off")
+    ap.add_argument("-vp", dest="verification", type=_bool, default=True, help="verification on/off")
+    ap.add_argument("-ep", dest="epsilon", type=float, default=2.0, help="epsilon")
+    ap.add_argument("-po", dest="poisoning", type=float, default=0.0, help="poisoner fraction")
+    ap.add_argument("-ns", dest="perc_samples", type=int, default=70, help="percent of updates collected")
+    ap.add_argument("-rs", dest="rand_sample", type=_bool, default=False, help="random sampling")
+
+
+def add_framework_flags(ap: argparse.ArgumentParser) -> None:
+    ap.add_argument("--defense", default="KRUM", choices=["KRUM", "RONI"])
+    ap.add_argument("--max-iterations", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--churn", type=float, default=0.0)
+    ap.add_argument("--data-dir", default=None)
+    ap.add_argument("--commit-key", default=None)
+    ap.add_argument("--pkey-file", default=None)
+    ap.add_argument("--no-roles-vrf-proof", dest="roles_vrf_proof", action="store_false")
+    ap.add_argument("--verify-signatures", action="store_true")
+    ap.add_argument("--host-threads", type=int, default=16)
+    ap.add_argument("--log-dir", default=None)
+    ap.add_argument("--trace-file", default=None)
+    ap.add_argument("--chain-file", default=None)
+    ap.add_argument("--resume", action="store_true")
+    ap.add_argument("--device", default=None)
+    ap.add_argument("--log-every-peer", action="store_true")
+
+
+def config_from_args(ns: argparse.Namespace) -> RunConfig:
+    names = {f.name for f in fields(RunConfig)}
+    return RunConfig(**{k: v for k, v in vars(ns).items() if k in names})

@@ -1,0 +1,526 @@
+"""The Biscotti round engine (SPMD over ranks, virtual peers per rank).
+
+One call of :meth:`BiscottiEngine.run_round` performs everything one reference iteration does
+across all N peer processes (DistSys/main.go prepareForNextIteration -> messageSender ->
+VerifyUpdateKRUM -> RegisterSecret -> startShareDeadlineTimer -> createBlockSecAgg -> sendBlock):
+
+  1. roles        native FSM: stake lottery on the latest block hash; noisers by each worker's
+                  own ECVRF output (batched over host threads)
+  2. local step   fused gfx950 kernel for all local workers (softmax / logistic regression)
+  3. commitments  fixed-base MSM (commit-only pass) for every online worker
+  4. noising      counter-based DP noise averaged over each worker's noisers
+  5. verification all_gather of noised deltas + commitments; Multi-Krum (f64 MFMA Gram) on each
+                  rank that hosts a verifier; Schnorr signatures; all_gather of accept masks
+  6. secure agg.  fused share/witness MSM for approved workers; all_to_all of per-miner share
+                  slices; miner-side sums; all_gather of miner aggregates to the leader; exact
+                  recovery + W update
+  7. block        leader builds the block (gob + SHA-256), broadcast, every rank appends and
+                  re-verifies the hash; empty blocks on the reference's timeout paths
+  8. evaluation   test error / attack rate (logged in the reference's line format)
+
+Every decision (roles, inbox, approvals, share routing, leader quorum, block contents) comes from
+the native :class:`RoundFSM`, replicated identically on every rank.
+"""
+from __future__ import annotations
+
+import hashlib
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..native import rt
+from ..ops import bn256 as B
+from ..ops import ml as K
+from ..parallel.comm import Comm
+from ..utils import JsonlWriter, PhaseTimer, get_logger
+from .config import RunConfig
+
+
+def _seed_bytes(seed: int, tag: str, i: int) -> bytes:
+    return hashlib.sha256(f"{seed}:{tag}:{i}".encode()).digest()
+
+
+@dataclass
+class RoundResult:
+    iteration: int
+    block_hash: bytes
+    empty: bool
+    node_list: list = field(default_factory=list)
+    approved: list = field(default_factory=list)
+    verifiers: list = field(default_factory=list)
+    miners: list = field(default_factory=list)
+    test_error: float = float("nan")
+    attack_rate: float = float("nan")
+    phases: dict = field(default_factory=dict)
+    wall: float = 0.0
+
+
+class HostCrypto:
+    """CPU crypto backend (native host BN256): points travel as 64-byte marshals."""
+
+    def __init__(self, key, poly: int, T: int, threads: int):
+        self.key, self.poly, self.T = key, poly, T
+        self.d = len(key)
+        self.nchunks = (self.d + poly - 1) // poly
+        self.threads = threads
+
+    def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
+        q = qdelta.cpu().numpy()
+        return np.stack([np.frombuffer(self.key.commit(q[i], 0), np.uint8) for i in range(q.shape[0])]) \
+            if q.shape[0] else np.zeros((0, 64), np.uint8)
+
+    def shares(self, qdelta: torch.Tensor):
+        q = qdelta.cpu().numpy()
+        n = q.shape[0]
+        pts = np.zeros((n, self.nchunks, self.T + 1, 64), np.uint8)
+        ys = np.zeros((n, self.nchunks, self.T), np.int64)
+        for i in range(n):
+            _, cc, y, wit = self.key.make_shares(q[i], self.poly, self.T)
+            w = np.frombuffer(b"".join(wit), np.uint8).reshape(self.nchunks, self.T, 64)
+            pts[i, :, : self.T] = w
+            pts[i, :, self.T] = np.frombuffer(b"".join(cc), np.uint8).reshape(self.nchunks, 64)
+            ys[i] = y
+        return torch.from_numpy(pts), torch.from_numpy(ys)
+
+    def sum_rows(self, pts: torch.Tensor) -> torch.Tensor:
+        """[R, C, 64] -> [C, 64]"""
+        return torch.from_numpy(rt().g1_sum_marshaled(pts.numpy()))
+
+
+class DeviceCrypto:
+    """GPU crypto backend: HBM-resident tables, Jacobian points [.., 24] int32."""
+
+    def __init__(self, key, poly: int, T: int, device):
+        self.eng = B.DeviceCommitEngine(key, poly, T, device)
+        self.d, self.poly, self.T, self.nchunks = self.eng.d, poly, T, self.eng.nchunks
+
+    def commitments_dev(self, qdelta: torch.Tensor) -> torch.Tensor:
+        n = qdelta.shape[0]
+        if n == 0:
+            return torch.zeros((0, 64), dtype=torch.uint8, device=qdelta.device)
+        rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
+        pts, _ = self.eng.shares(qdelta, rows, commit_only=True)
+        return B.marshal(self.eng.commitments(pts))
+
+    def shares(self, qdelta: torch.Tensor):
+        rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
+        return self.eng.shares(qdelta, rows)
+
+    def sum_rows(self, pts: torch.Tensor) -> torch.Tensor:
+        """[R, C, 24] -> [C, 24]"""
+        return B.sum_rows(pts.contiguous(), None, None)
+
+
+class BiscottiEngine:
+    def __init__(self, cfg: RunConfig, comm: Comm | None = None):
+        self.cfg = cfg
+        self.comm = comm or Comm()
+        self.R = rt()
+        self.dev = self.comm.device if cfg.device != "cpu" else torch.device("cpu")
+        self.gpu = self.dev.type == "cuda"
+        self.N = cfg.num_nodes
+        self.pc = cfg.protocol(self.R)
+        self.local = self.comm.peer_range(self.N)
+        self.lo = self.local.start
+        self.maxlocal = self.comm.max_local(self.N)
+        tag = f"{cfg.log_dir}/log_{self.comm.rank}_{self.N}.log" if cfg.log_dir else None
+        self.log = get_logger("peer", tag)
+        self.trace = JsonlWriter(cfg.trace_file if self.comm.rank == 0 else None)
+        self.timer = PhaseTimer(sync=(lambda: torch.cuda.synchronize(self.dev)) if self.gpu else None)
+        # ---- data / model
+        from ..data import dataset_dims
+        from ..models import make_task
+
+        self.d = dataset_dims(cfg.dataset)[0]
+        fsm_probe = self.R.RoundFSM(self.pc, self.d)
+        poisoned = {p for p in self.local if fsm_probe.is_poisoner(p)}
+        colluders = {p for p in range(self.N) if fsm_probe.is_colluder(p)}
+        self.colluders = colluders
+        self.task = make_task(cfg.dataset, self.local, self.N, self.dev, cfg.seed, poisoned=poisoned,
+                              batch_size=cfg.batch_size, data_dir=cfg.data_dir, epsilon=cfg.epsilon,
+                              colluders=colluders)
+        # ---- ledger / protocol state
+        self.fsm = fsm_probe
+        if cfg.peers_file:
+            with open(cfg.peers_file) as f:
+                addrs = [ln.strip() for ln in f if ln.strip()]
+            if len(addrs) >= self.N:
+                self.fsm.addresses = addrs[: self.N]
+        if cfg.resume and cfg.chain_file:
+            self._resume(cfg.chain_file)
+        self.W = torch.from_numpy(np.array(self.fsm.chain.latest().data.global_w, dtype=np.float64)).to(self.dev)
+        # ---- keys
+        if cfg.commit_key:
+            key = self.R.CommitKey.load(cfg.commit_key, self.d)
+        else:
+            key = self.R.CommitKey.generate(self.d, 2)  # publicKey.go: s = 2
+        self.T = self.pc.total_shares
+        self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
+            HostCrypto(key, cfg.poly_size, self.T, cfg.host_threads)
+        self.nchunks = self.crypto.nchunks
+        if cfg.pkey_file:
+            ks = self.R.read_client_keys(cfg.pkey_file)
+            self.sk = {i: ks[i][0] for i in range(self.N)}
+            self.pk = {i: ks[i][1] for i in range(self.N)}
+        else:
+            self.sk, self.pk = {}, {}
+            for i in range(self.N):
+                s, p = self.R.client_key_from_entropy(_seed_bytes(cfg.seed, "client", i))
+                self.sk[i], self.pk[i] = s, p
+        self.vrf_noise_seed = {i: _seed_bytes(cfg.seed, "vrf-noise", i) for i in self.local}
+        self.vrf_roles_seed = {i: _seed_bytes(cfg.seed, "vrf-roles", i) for i in self.local}
+        self.sigma = self.task.noise_sigma(cfg.epsilon)
+        self.stats = {"unmasked_updates": 0, "total_updates": 0}
+        self.rounds_done = 0
+
+    # ------------------------------------------------------------------ helpers
+    def _resume(self, path: str) -> None:
+        import os
+
+        if not os.path.exists(path):
+            return
+        chain = self.R.Blockchain.load(path)
+        self.fsm.chain = chain
+        last = chain.latest()
+        self.fsm.iteration = last.data.iteration
+        if len(last.stake):
+            self.fsm.stake = dict(last.stake)
+        self.log.info("Resumed chain of %d blocks at iteration %d", len(chain), last.data.iteration)
+
+    def _live_mask(self) -> list[int]:
+        if self.cfg.churn <= 0:
+            return [1] * self.N
+        seed = self.fsm.round_seed(7)
+        perm = self.R.seeded_permutation(self.N, seed)
+        k = int(round(self.cfg.churn * self.N))
+        live = [1] * self.N
+        for p in perm[:k]:
+            live[p] = 0
+        return live
+
+    def _rows_buffer(self, per_peer: dict, width: int, dtype) -> torch.Tensor:
+        """[maxlocal, width] buffer whose row (peer - lo) holds that local peer's vector."""
+        buf = torch.zeros((self.maxlocal, width), dtype=dtype, device=self.dev)
+        for p, v in per_peer.items():
+            buf[p - self.lo] = v
+        return buf
+
+    def _gathered_row(self, g: torch.Tensor, peer: int) -> torch.Tensor:
+        r = self.comm.owner(peer, self.N)
+        return g[r, peer - self.comm.peer_range(self.N, r).start]
+
+    # ------------------------------------------------------------------ the round
+    def run_round(self) -> RoundResult | None:
+        cfg, R, fsm, comm = self.cfg, self.R, self.fsm, self.comm
+        t_round = time.perf_counter()
+        tm = self.timer
+        with tm.phase("roles"):
+            live = self._live_mask()
+            plan = fsm.begin_round(live)
+            if plan.done:
+                return None
+            it = plan.iteration
+            latest_hash = fsm.chain.latest().hash
+            workers = [w for w in plan.workers if live[w]]
+            local_workers = [w for w in workers if w in self.local]
+            # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100)
+            seeds = [self.vrf_noise_seed[w] for w in local_workers]
+            outs = R.vrf_prove_batch(seeds, latest_hash, cfg.host_threads) if seeds else []
+            stake = dict(fsm.stake)
+            noisers = {w: R.select_noisers(stake, beta, w, cfg.num_noisers, self.N)
+                       for w, (beta, _) in zip(local_workers, outs)}
+            if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
+                R.vrf_prove_batch([self.vrf_roles_seed[p] for p in self.local if live[p]], latest_hash,
+                                  cfg.host_threads)
+        # ---------------------------------------------------------------- local step + commitments
+        with tm.phase("local_step"):
+            delta, qdelta = self.task.step(self.W, it, local_workers)
+        with tm.phase("commit"):
+            if self.gpu:
+                comm_dev = self.crypto.commitments_dev(qdelta)
+                commits_local = comm_dev.cpu().numpy()
+            else:
+                commits_local = self.crypto.commitments(qdelta)
+        with tm.phase("noise"):
+            if cfg.noising and self.sigma > 0 and local_workers:
+                nz = torch.tensor([noisers[w] for w in local_workers], dtype=torch.int32, device=self.dev)
+                sc = torch.tensor([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma)
+                                    for j in noisers[w]] for w in local_workers], dtype=torch.float32,
+                                  device=self.dev)
+                noised = K.dp_noise(delta, nz, sc, cfg.seed, it)
+            else:
+                noised = delta
+        # ---------------------------------------------------------------- verification
+        with tm.phase("verify"):
+            row_of = {w: i for i, w in enumerate(local_workers)}
+            cbuf = torch.zeros((self.maxlocal, 64), dtype=torch.uint8, device=self.dev)
+            if local_workers:
+                idx = torch.tensor([w - self.lo for w in local_workers], dtype=torch.long, device=self.dev)
+                cbuf[idx] = torch.from_numpy(commits_local).to(self.dev)
+            commits_all = comm.all_gather(cbuf).cpu().numpy()  # [world, maxlocal, 64]
+            commit_of = {w: bytes(self._gathered_row(commits_all, w)) for w in workers}
+            if cfg.colluders > 0:  # privacy experiment bookkeeping (isCollusionAttack, main.go:1026-1057)
+                thr = self.pc.collusion_thresh
+                if any(v >= thr for v in plan.verifiers):
+                    self.stats["unmasked_updates"] += sum(
+                        1 for w in local_workers if all(j >= thr for j in noisers[w]))
+            accepted_map: dict = {}
+            inbox = fsm.verifier_inbox(workers) if cfg.verification else []
+            online_verifiers = [v for v in plan.verifiers if live[v]]
+            local_verifiers = [v for v in online_verifiers if v in self.local]
+            if cfg.verification and inbox:
+                nbuf = torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev)
+                if local_workers:
+                    nbuf[idx] = noised
+                gathered = comm.all_gather(nbuf) if (local_verifiers or comm.world > 1) else None
+                acc_mask = torch.zeros((len(plan.verifiers), len(inbox)), dtype=torch.uint8, device=self.dev)
+                sig_buf = torch.zeros((len(plan.verifiers), len(inbox), 64), dtype=torch.uint8, device=self.dev)
+                if local_verifiers:
+                    X = torch.stack([self._gathered_row(gathered, w) for w in inbox]).contiguous()
+                    krum_cache = None
+                    for v in local_verifiers:
+                        if cfg.defense == "KRUM":  # identical inputs -> identical Krum result per rank
+                            krum_cache = krum_cache or self._verify(X, inbox, it, v)
+                            accept = krum_cache
+                        else:
+                            accept = self._verify(X, inbox, it, v)
+                        acc_ids = [w for w, a in zip(inbox, accept) if a]
+                        vi = plan.verifiers.index(v)
+                        msgs = [commit_of[w] for w in acc_ids]
+                        nonces = [_seed_bytes(cfg.seed, f"nonce-{it}-{v}", w) for w in acc_ids]
+                        sigs = R.schnorr_sign_batch(msgs, self.sk[v], nonces, cfg.host_threads)
+                        for w, s in zip(acc_ids, sigs):
+                            j = inbox.index(w)
+                            acc_mask[vi, j] = 1
+                            sig_buf[vi, j] = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(self.dev)
+                acc_all = comm.all_gather(acc_mask).cpu().numpy()
+                sig_all = comm.all_gather(sig_buf).cpu().numpy()
+                signatures: dict = {}
+                for vi, v in enumerate(plan.verifiers):
+                    if not live[v]:
+                        continue
+                    owner = comm.owner(v, self.N)
+                    ids = [inbox[j] for j in range(len(inbox)) if acc_all[owner, vi, j]]
+                    accepted_map[v] = ids
+                    for j in range(len(inbox)):
+                        if acc_all[owner, vi, j]:
+                            signatures.setdefault(inbox[j], []).append(bytes(sig_all[owner, vi, j]))
+                approved, _ = fsm.approve(accepted_map)
+            else:
+                signatures = {}
+                approved, _ = fsm.approve({})
+        # ---------------------------------------------------------------- aggregation + block
+        if cfg.secure_agg:
+            block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, row_of,
+                                             commit_of, signatures)
+        else:
+            block = self._plain_aggregation(plan, live, approved, delta, noised, local_workers, commit_of,
+                                            signatures)
+        with tm.phase("block"):
+            if block is None:
+                block = fsm.make_empty_block()
+            r = fsm.commit_block(block)
+            if r < 0:
+                raise RuntimeError("block refused by the ledger")
+            if cfg.chain_file and comm.rank == 0:
+                R.Blockchain.append_to_file(cfg.chain_file, block)
+            self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
+        with tm.phase("eval"):
+            ev = self.task.evaluate(self.W)
+        self.stats["total_updates"] += len(block.data.deltas)
+        res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=len(block.data.deltas) == 0,
+                          node_list=self._last_nodes, approved=list(approved), verifiers=list(plan.verifiers),
+                          miners=list(plan.miners), test_error=ev["test_error"], attack_rate=ev["attack_rate"],
+                          phases=tm.reset(), wall=time.perf_counter() - t_round)
+        self._log_round(res)
+        self.rounds_done += 1
+        return res
+
+    # ------------------------------------------------------------------ verification defences
+    def _verify(self, X: torch.Tensor, inbox: list, it: int, verifier: int) -> list[bool]:
+        cfg = self.cfg
+        n = len(inbox)
+        if cfg.defense == "RONI":
+            # VerifyUpdateRONI (main.go:191-233): accept iff the update raises the verifier's
+            # training error by at most 0.02 (always accept in the collusion experiment)
+            if cfg.colluders > 0:
+                return [True] * n
+            base = self.task.train_error(self.W, verifier, it)
+            return [self.task.train_error(self.W + X[i].double(), verifier, it) - base <= 0.02 for i in range(n)]
+        clip = self.fsm.krum_clip(n)
+        acc, _ = K.krum(X, n - clip, n - clip)
+        return [bool(a) for a in acc.cpu().tolist()]
+
+    # ------------------------------------------------------------------ secure aggregation path
+    def _secure_aggregation(self, plan, live, approved, delta, qdelta, local_workers, row_of, commit_of,
+                            signatures):
+        cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
+        self._last_nodes = []
+        with tm.phase("shares"):
+            routes = fsm.route_shares(approved)
+            lv = fsm.leader_view(routes)
+            local_approved = [w for w in approved if w in self.local]
+            if local_approved and routes:
+                sel = torch.tensor([row_of[w] for w in local_approved], dtype=torch.long, device=self.dev)
+                pts, ys = self.crypto.shares(qdelta[sel].contiguous())
+            else:
+                pts = ys = None
+            ap_row = {w: i for i, w in enumerate(local_approved)}
+        with tm.phase("share_exchange"):
+            S = cfg.poly_size  # unused name guard
+            spm = self.pc.shares_per_miner
+            pw = pts.shape[-1] if pts is not None else (24 if self.gpu else 64)
+            pdt = pts.dtype if pts is not None else (torch.int32 if self.gpu else torch.uint8)
+            # what each rank sends to each destination: for every (worker, miner, part) route whose
+            # worker is local and miner lives on that destination, the miner's share slice
+            send_p, send_y, manifest = [], [], []
+            for dst in range(comm.world):
+                dst_range = comm.peer_range(self.N, dst)
+                ps, yl, man = [], [], []
+                for m in sorted(routes):
+                    if m not in dst_range:
+                        continue
+                    for (w, part) in routes[m]:
+                        if w not in ap_row:
+                            continue
+                        i = ap_row[w]
+                        cols = list(range(spm * part, spm * part + spm)) + [self.T]
+                        ps.append(pts[i][:, cols].reshape(-1))
+                        yl.append(ys[i][:, spm * part: spm * part + spm].reshape(-1))
+                        man.append((m, w, part))
+                send_p.append(torch.cat(ps) if ps else torch.empty((0,), dtype=pdt, device=self.dev))
+                send_y.append(torch.cat(yl) if yl else torch.empty((0,), dtype=torch.int64, device=self.dev))
+                manifest.append(man)
+            recv_p = comm.all_to_all(send_p)
+            recv_y = comm.all_to_all(send_y)
+            # reconstruct the manifest of what this rank received, in sender order
+            inbox_parts: dict = {}
+            per_p = self.nchunks * (spm + 1) * pw
+            per_y = self.nchunks * spm
+            for src in range(comm.world):
+                src_range = comm.peer_range(self.N, src)
+                k = 0
+                for m in sorted(routes):
+                    if m not in self.local:
+                        continue
+                    for (w, part) in routes[m]:
+                        if w not in src_range:
+                            continue
+                        p_ = recv_p[src][k * per_p:(k + 1) * per_p].view(self.nchunks, spm + 1, pw)
+                        y_ = recv_y[src][k * per_y:(k + 1) * per_y].view(self.nchunks, spm)
+                        inbox_parts.setdefault(m, {})[w] = (part, p_, y_)
+                        k += 1
+        with tm.phase("miner_aggregate"):
+            # every online local miner aggregates the shares of the leader's node list
+            node_list = list(lv.node_list)
+            contributing = list(lv.contributing_miners)
+            nc = len(contributing)
+            agg_y_buf = torch.zeros((nc, self.nchunks, spm), dtype=torch.int64, device=self.dev)
+            part_buf = torch.zeros((nc,), dtype=torch.int64, device=self.dev)
+            if lv.leader_online and lv.quorum:
+                for ci, m in enumerate(contributing):
+                    if m not in self.local:
+                        continue
+                    got = inbox_parts.get(m, {})
+                    if cfg.verify_signatures:
+                        need = len(plan.verifiers) // 2
+                        ok_nodes = [w for w in node_list if sum(
+                            R.schnorr_verify(commit_of[w], self.pk[v], s) for s in signatures.get(w, [])
+                            for v in plan.verifiers) >= need]
+                    else:
+                        ok_nodes = node_list
+                    ps = torch.stack([got[w][1] for w in ok_nodes])     # [R, nchunks, spm+1, pw]
+                    yv = torch.stack([got[w][2] for w in ok_nodes])     # [R, nchunks, spm]
+                    _ = self.crypto.sum_rows(ps.reshape(len(ok_nodes), -1, pw))  # witnesses + commitments
+                    agg_y_buf[ci] = yv.sum(0)
+                    part_buf[ci] = got[ok_nodes[0]][0]
+        with tm.phase("recover"):
+            if not (lv.leader_online and lv.quorum):
+                return None
+            agg_y_all = comm.all_gather(agg_y_buf)      # [world, nc, nchunks, spm]
+            parts_all = comm.all_gather(part_buf)
+            leader_rank = comm.owner(plan.leader, self.N)
+            block_bytes = None
+            if comm.rank == leader_rank:
+                ys_cols, xs = [], []
+                for ci, m in enumerate(contributing):
+                    o = comm.owner(m, self.N)
+                    part = int(parts_all[o, ci])
+                    ys_cols.append(agg_y_all[o, ci])
+                    xs += [spm * part + s - 10 for s in range(spm)]
+                agg = torch.cat(ys_cols, dim=1).contiguous()      # [nchunks, npts]
+                xs_t = torch.tensor(xs, dtype=torch.int32, device=self.dev)
+                W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
+                st = status.cpu().numpy()
+                W_np = W_new.cpu().numpy()
+                if not st.all():  # inconsistent shares: the reference's float64 least squares
+                    aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()
+                    for k in np.nonzero(st == 0)[0]:
+                        c = R.recover_lstsq(xs, [int(v) for v in aggn[k]], cfg.poly_size - 1)
+                        for j, v in enumerate(c):
+                            i = k * cfg.poly_size + j
+                            if i < self.d:
+                                W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
+                    self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
+                comms = [commit_of[w] for w in node_list]
+                blk = fsm.make_secagg_block(W_np, node_list, comms, int(time.time()))
+                block_bytes = blk.serialize()
+            data = comm.broadcast_bytes(block_bytes, leader_rank)
+            block = R.Block.deserialize(data)
+            if block.compute_hash() != block.hash:
+                raise RuntimeError("received block with a bad hash")
+            self._last_nodes = node_list
+            return block
+
+    # ------------------------------------------------------------------ plain aggregation path
+    def _plain_aggregation(self, plan, live, approved, delta, noised, local_workers, commit_of, signatures):
+        cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
+        self._last_nodes = []
+        with tm.phase("aggregate"):
+            routes = fsm.route_updates(approved)
+            leader = plan.leader
+            if not live[leader] or not routes.get(leader):
+                return None
+            ups = routes[leader]
+            idx = {w: i for i, w in enumerate(local_workers)}
+            dbuf = self._rows_buffer({w: delta[idx[w]] for w in local_workers}, self.d, torch.float32)
+            nbuf = self._rows_buffer({w: noised[idx[w]] for w in local_workers}, self.d, torch.float32)
+            dall, nall = comm.all_gather(dbuf), comm.all_gather(nbuf)
+            leader_rank = comm.owner(leader, self.N)
+            block_bytes = None
+            if comm.rank == leader_rank:
+                upd = []
+                W = self.W.clone()
+                for w in ups:
+                    u = R.Update()
+                    dv = self._gathered_row(dall, w).double()
+                    nv = self._gathered_row(nall, w).double()
+                    W += dv
+                    u.source_id, u.iteration, u.accepted = w, plan.iteration, True
+                    u.delta = dv.cpu().tolist()
+                    u.noised_delta = nv.cpu().tolist()
+                    u.noise = (nv - dv).cpu().tolist()
+                    u.commitment = commit_of[w]
+                    u.signatures = signatures.get(w, [])
+                    upd.append(u)
+                blk = fsm.make_plain_block(W.cpu().numpy(), upd, int(time.time()))
+                block_bytes = blk.serialize()
+            data = comm.broadcast_bytes(block_bytes, leader_rank)
+            self._last_nodes = list(ups)
+            return R.Block.deserialize(data)
+
+    # ------------------------------------------------------------------ logging
+    def _log_round(self, r: RoundResult) -> None:
+        peers = list(self.local) if self.cfg.log_every_peer else [self.lo]
+        for p in peers:
+            self.log.info("%d:Train Error is %.5f in Iteration %d", p, r.test_error, r.iteration)
+            if self.cfg.dataset != "creditcard":
+                self.log.info("%d:Attack Rate is %.5f in Iteration %d", p, r.attack_rate, r.iteration)
+        self.trace.write({"iteration": r.iteration, "wall_s": r.wall, "empty": r.empty, "nodes": len(r.node_list),
+                          "approved": len(r.approved), "test_error": r.test_error, "attack_rate": r.attack_rate,
+                          "hash": r.block_hash.hex(), **{f"t_{k}": v for k, v in r.phases.items()}})
+
+    def print_chain(self) -> str:
+        return self.fsm.chain.print_chain()

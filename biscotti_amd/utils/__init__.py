@@ -1,0 +1,78 @@
+"""Logging in the reference's format and structured phase tracing.
+
+Reference logging (DistSys/main.go:136-137): ``log.New(os.Stderr, "[peer] ",
+log.Lshortfile|log.LUTC|log.Lmicroseconds)`` -> ``[peer] 21:03:12.123456 file.go:151: msg``.
+The eval parsers key on lines such as ``"<id>:Train Error is %.5f in Iteration %d"``
+(honest.go:151) and ``"<id>:Attack Rate is %.5f in Iteration %d"`` (:153); those are kept
+verbatim.  Phase timings go to JSON lines (one record per round) instead of being reconstructed
+from marker lines.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import sys
+import time
+from contextlib import contextmanager
+
+
+class _GoFormatter(logging.Formatter):
+    def __init__(self, prefix: str):
+        super().__init__()
+        self.prefix = prefix
+
+    def format(self, record: logging.LogRecord) -> str:
+        t = time.gmtime(record.created)
+        us = int((record.created % 1) * 1e6)
+        return (f"{self.prefix}{t.tm_hour:02d}:{t.tm_min:02d}:{t.tm_sec:02d}.{us:06d} "
+                f"{os.path.basename(record.pathname)}:{record.lineno}: {record.getMessage()}")
+
+
+def get_logger(name: str = "peer", path: str | None = None, level=logging.INFO) -> logging.Logger:
+    lg = logging.getLogger(f"biscotti.{name}.{path or 'stderr'}")
+    if not lg.handlers:
+        h = logging.FileHandler(path) if path else logging.StreamHandler(sys.stderr)
+        h.setFormatter(_GoFormatter(f"[{name}] "))
+        lg.addHandler(h)
+        lg.propagate = False
+    lg.setLevel(level)
+    return lg
+
+
+class PhaseTimer:
+    """Accumulates wall time per protocol phase; ``sync`` makes GPU work visible to the clock."""
+
+    def __init__(self, sync=None):
+        self.t: dict[str, float] = {}
+        self.sync = sync
+
+    @contextmanager
+    def phase(self, name: str):
+        if self.sync:
+            self.sync()
+        s = time.perf_counter()
+        try:
+            yield
+        finally:
+            if self.sync:
+                self.sync()
+            self.t[name] = self.t.get(name, 0.0) + time.perf_counter() - s
+
+    def reset(self) -> dict[str, float]:
+        out, self.t = self.t, {}
+        return out
+
+
+class JsonlWriter:
+    def __init__(self, path: str | None):
+        self.f = open(path, "a") if path else None
+
+    def write(self, rec: dict) -> None:
+        if self.f:
+            self.f.write(json.dumps(rec) + "\n")
+            self.f.flush()
+
+    def close(self) -> None:
+        if self.f:
+            self.f.close()
