@@ -1,0 +1,70 @@
+"""Peer entry point: ``python -m biscotti_amd.peer -i <k> -t <N> -d <dataset> [reference flags]``.
+
+Two launch modes share one engine:
+
+* per-peer processes, like DistSys/localTest.sh (``-i k -t N`` and no WORLD_SIZE in the env): the
+  process becomes rank k of an N-rank group (rendezvous at 127.0.0.1:8000 = basePort, or the first
+  line of the ``-f`` peers file), hosting exactly one peer;
+* SPMD under torchrun (WORLD_SIZE set): the N peers are packed as virtual peers onto the ranks,
+  one rank per GPU, collectives over RCCL/xGMI.
+
+At exit rank 0 prints the chain with PrintChain's format (blockchain.go:43-54) to stdout, which
+is what localTest.sh compares between peers.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+from .protocol.config import add_framework_flags, add_reference_flags, config_from_args
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="biscotti_amd.peer", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    add_reference_flags(ap)
+    add_framework_flags(ap)
+    ap.add_argument("--rounds", type=int, default=None, help="stop after this many rounds")
+    ap.add_argument("--print-chain", default="rank0", choices=["rank0", "all", "none"])
+    ns = ap.parse_args(argv)
+    cfg = config_from_args(ns)
+    if cfg.num_nodes <= 0 or not cfg.dataset:
+        ap.print_usage()
+        return 1
+    if "WORLD_SIZE" not in os.environ and cfg.node_index >= 0:
+        # one process per peer (reference deployment)
+        os.environ["WORLD_SIZE"] = str(cfg.num_nodes)
+        os.environ["RANK"] = str(cfg.node_index)
+        os.environ.setdefault("LOCAL_RANK", "0")
+        host, port = "127.0.0.1", "8000"
+        if cfg.peers_file:
+            with open(cfg.peers_file) as f:
+                first = f.readline().strip()
+            host, port = first.rsplit(":", 1)
+        os.environ.setdefault("MASTER_ADDR", host)
+        os.environ.setdefault("MASTER_PORT", port)
+    from .parallel.comm import Comm
+    from .protocol.engine import BiscottiEngine
+
+    comm = Comm.init(device=cfg.device)
+    eng = BiscottiEngine(cfg, comm)
+    n = 0
+    while ns.rounds is None or n < ns.rounds:
+        r = eng.run_round()
+        if r is None:
+            eng.log.info("Reached the max iterations!")
+            break
+        n += 1
+    if cfg.colluders > 0:
+        print(eng.stats["unmasked_updates"], eng.stats["total_updates"], cfg.colluders / 100.0, cfg.num_noisers)
+    if ns.print_chain == "all" or (ns.print_chain == "rank0" and comm.rank == 0):
+        sys.stdout.write(eng.print_chain())
+        sys.stdout.flush()
+    comm.barrier()
+    comm.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,124 @@
+"""gfx950 learning-side kernels vs the CPU reference path (same Philox streams, fp32/fp64 refs)."""
+import numpy as np
+import pytest
+import torch
+
+from biscotti_amd.ops import ml as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _fed(P=6, n=40, d_in=784, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn((P * n, d_in), generator=g)
+    y = torch.randint(0, 10, (P * n,), generator=g, dtype=torch.int32)
+    off = torch.arange(P, dtype=torch.int64) * n
+    nt = torch.full((P,), n, dtype=torch.int32)
+    pid = torch.arange(P, dtype=torch.int32) * 7 + 3
+    W = torch.randn(10 * d_in + 10, generator=g, dtype=torch.float64) * 0.05
+    return X, y, off, nt, pid, W
+
+
+def test_softmax_step_matches_reference():
+    X, y, off, nt, pid, W = _fed()
+    d_ref, q_ref, l_ref = K.softmax_step(X, y, off, nt, pid, W, 784, 10, 10, 1234, 5)
+    c = lambda t: t.cuda()
+    d_gpu, q_gpu, l_gpu = K.softmax_step(c(X), c(y), c(off), c(nt), c(pid), c(W), 784, 10, 10, 1234, 5)
+    torch.testing.assert_close(d_gpu.cpu(), d_ref, rtol=2e-4, atol=2e-6)
+    torch.testing.assert_close(l_gpu.cpu(), l_ref, rtol=1e-4, atol=1e-5)
+    assert (q_gpu.cpu() - q_ref).abs().max() <= 1
+
+
+def test_softmax_step_clips_large_gradients():
+    X, y, off, nt, pid, W = _fed(P=3)
+    X = X * 1e3  # huge activations -> gradient norm far above 100
+    d_gpu, _, _ = K.softmax_step(X.cuda(), y.cuda(), off.cuda(), nt.cuda(), pid.cuda(), W.cuda(), 784, 10, 10, 9, 0)
+    norms = d_gpu.double().norm(dim=1)
+    assert torch.all(norms <= 100.0 + 1e-3) and torch.all(norms > 99.0)
+
+
+def test_logreg_step_matches_reference():
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn((300, 25), generator=g, dtype=torch.float64)
+    y = torch.where(torch.rand(300, generator=g) > 0.5, 1.0, -1.0).double()
+    off = torch.tensor([0, 100, 200], dtype=torch.int64)
+    nr = torch.tensor([100, 100, 100], dtype=torch.int32)
+    pid = torch.tensor([0, 1, 2], dtype=torch.int32)
+    W = torch.randn(25, generator=g, dtype=torch.float64) * 0.1
+    calls = torch.tensor([1, 2, 3], dtype=torch.int32)
+    sigma = torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64)
+    ref = K.logreg_step(X, y, off, nr, pid, W, 10, 77, calls, 1e-2, 1e-2, sigma)
+    c = lambda t: t.cuda()
+    got = K.logreg_step(c(X), c(y), c(off), c(nr), c(pid), c(W), 10, 77, c(calls), 1e-2, 1e-2, c(sigma))
+    torch.testing.assert_close(got[0].cpu(), ref[0], rtol=1e-4, atol=1e-6)
+
+
+def test_dp_noise_matches_reference():
+    delta = torch.randn((5, 7850))
+    noisers = torch.tensor([[1, 2], [2, 3], [1, 4], [0, 9], [5, 6]], dtype=torch.int32)
+    scales = torch.full((5, 2), -0.77)
+    scales[3, 1] = 0.0  # colluding noiser
+    ref = K.dp_noise(delta, noisers, scales, 42, 13)
+    got = K.dp_noise(delta.cuda(), noisers.cuda(), scales.cuda(), 42, 13).cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+    # same noiser + iteration -> same noise vector for every worker (pre-sampled samples semantics)
+    n01 = got[0] - delta[0]
+    n21 = got[2] - delta[2]
+    assert not torch.allclose(n01, n21)
+
+
+def test_krum_matches_reference():
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn((70, 7850), generator=g) * 0.1
+    X[60:] += 3.0  # outliers
+    acc_ref, sc_ref = K.krum(X, 35, 35)
+    acc, sc = K.krum(X.cuda(), 35, 35)
+    torch.testing.assert_close(sc.cpu(), sc_ref, rtol=1e-9, atol=1e-6)
+    assert torch.equal(acc.cpu(), acc_ref)
+    assert not acc.cpu()[60:].any()
+
+
+def test_eval_error_matches_reference():
+    X, y, off, nt, pid, W = _fed(P=1, n=2000)
+    ref = K.eval_error(X, y, W, 784, 10)
+    got = K.eval_error(X.cuda(), y.cuda(), W.cuda(), 784, 10)
+    assert abs(ref - got) <= 1.0 / 2000
+
+
+def test_recover_exact(rt):
+    rng = np.random.default_rng(0)
+    nch, poly = 50, 10
+    coeffs = rng.integers(-10**7, 10**7, size=(nch, poly))
+    xs = np.arange(-10, 11)
+    ys = np.stack([[sum(int(c) * int(x) ** j for j, c in enumerate(row)) for x in xs] for row in coeffs])
+    W = torch.zeros(nch * poly - 3, dtype=torch.float64)
+    Wn, got, st = K.recover(torch.from_numpy(ys).cuda(), torch.from_numpy(xs.astype(np.int32)).cuda(), poly,
+                            W.numel(), W.cuda(), 1e4)
+    assert st.cpu().all()
+    np.testing.assert_array_equal(got.cpu().numpy(), coeffs)
+    np.testing.assert_allclose(Wn.cpu().numpy(), coeffs.reshape(-1)[: W.numel()] / 1e4)
+    bad = ys.copy()
+    bad[3, 5] += 1
+    _, _, st2 = K.recover(torch.from_numpy(bad).cuda(), torch.from_numpy(xs.astype(np.int32)).cuda(), poly,
+                          W.numel(), W.cuda(), 1e4)
+    assert st2.cpu()[3] == 0 and st2.cpu().sum() == nch - 1
+    # two miners only (x in -10..-4 and 4..10): still exact
+    sel = list(range(0, 7)) + list(range(14, 21))
+    _, got3, st3 = K.recover(torch.from_numpy(ys[:, sel].copy()).cuda(),
+                             torch.from_numpy(xs[sel].astype(np.int32)).cuda(), poly, W.numel(), W.cuda(), 1e4)
+    assert st3.cpu().all()
+    np.testing.assert_array_equal(got3.cpu().numpy(), coeffs)
+
+
+def test_engine_rounds_on_gpu():
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100)
+    eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
+    res = [eng.run_round() for _ in range(4)]
+    ok, why = eng.fsm.chain.verify()
+    assert ok, why
+    assert sum(not r.empty for r in res) >= 3
+    assert res[-1].test_error < res[0].test_error + 0.05
