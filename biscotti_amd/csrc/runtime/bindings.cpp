@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <thread>
 
 #include "bn256.hpp"
@@ -35,24 +36,82 @@ static py::int_ pyint_from_u256(const U256& v) {
   return py::int_(py::module_::import("builtins").attr("int").attr("from_bytes")(P(b), "big"));
 }
 
-// Parallel-for over host threads (VRF proofs, Schnorr signatures of many local peers).
+// Persistent worker pool for host crypto of many local peers (VRF proofs, Schnorr signatures):
+// threads are created once, each call hands out indices through an atomic counter.
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+class Pool {
+ public:
+  void run(size_t n, int threads, const std::function<void(size_t)>& f) {
+    if (threads <= 1 || n <= 1) {
+      for (size_t i = 0; i < n; ++i) f(i);
+      return;
+    }
+    ensure(threads - 1);
+    std::unique_lock<std::mutex> lk(m_);
+    job_ = &f;
+    n_ = n;
+    next_.store(0);
+    active_ = int(workers_.size());
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    work();
+    lk.lock();
+    done_cv_.wait(lk, [&] { return active_ == 0; });
+    job_ = nullptr;
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+ private:
+  void ensure(int k) {
+    while (int(workers_.size()) < k) workers_.emplace_back([this] { loop(); });
+  }
+  void work() {
+    for (;;) {
+      size_t i = next_.fetch_add(1);
+      if (i >= n_) break;
+      (*job_)(i);
+    }
+  }
+  void loop() {
+    size_t seen = 0;
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      lk.unlock();
+      work();
+      lk.lock();
+      if (--active_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  std::atomic<size_t> next_{0};
+  size_t n_ = 0, gen_ = 0;
+  int active_ = 0;
+  bool stop_ = false;
+};
+static Pool& pool() {
+  static Pool* p = new Pool();  // intentionally leaked: no join at interpreter teardown
+  return *p;
+}
 template <class F>
 static void parallel_for(size_t n, int threads, F f) {
-  if (threads <= 1 || n <= 1) {
-    for (size_t i = 0; i < n; ++i) f(i);
-    return;
-  }
-  std::vector<std::thread> ts;
-  std::atomic<size_t> next{0};
-  for (int t = 0; t < threads; ++t)
-    ts.emplace_back([&] {
-      for (;;) {
-        size_t i = next.fetch_add(1);
-        if (i >= n) break;
-        f(i);
-      }
-    });
-  for (auto& t : ts) t.join();
+  std::function<void(size_t)> fn = f;
+  pool().run(n, threads, fn);
 }
 
 struct CommitKey {

@@ -23,10 +23,20 @@ Fe fe_carry(Fe a) {
   }
   return a;
 }
+// one carry pass: inputs with limbs < 2^52 give limbs < 2^51 + 2^2 (limb 0 < 2^51 + 19*2^2)
+inline Fe fe_carry1(Fe a) {
+  u64 c;
+  c = a.v[0] >> 51; a.v[0] &= MASK51; a.v[1] += c;
+  c = a.v[1] >> 51; a.v[1] &= MASK51; a.v[2] += c;
+  c = a.v[2] >> 51; a.v[2] &= MASK51; a.v[3] += c;
+  c = a.v[3] >> 51; a.v[3] &= MASK51; a.v[4] += c;
+  c = a.v[4] >> 51; a.v[4] &= MASK51; a.v[0] += c * 19;
+  return a;
+}
 Fe fe_add(const Fe& a, const Fe& b) {
   Fe r;
   for (int i = 0; i < 5; ++i) r.v[i] = a.v[i] + b.v[i];
-  return fe_carry(r);
+  return fe_carry1(r);
 }
 Fe fe_sub(const Fe& a, const Fe& b) {
   // add 4p to keep limbs positive
@@ -34,7 +44,7 @@ Fe fe_sub(const Fe& a, const Fe& b) {
                             0x1FFFFFFFFFFFFCULL, 0x1FFFFFFFFFFFFCULL};
   Fe r;
   for (int i = 0; i < 5; ++i) r.v[i] = a.v[i] + p4[i] - b.v[i];
-  return fe_carry(r);
+  return fe_carry1(r);
 }
 Fe fe_neg(const Fe& a) { return fe_sub(fe_zero(), a); }
 Fe fe_mul(const Fe& a, const Fe& b) {
@@ -55,9 +65,31 @@ Fe fe_mul(const Fe& a, const Fe& b) {
     c = t[i] >> 51;
   }
   r.v[0] += u64(c) * 19;
-  return fe_carry(r);
+  return fe_carry1(r);
 }
-Fe fe_sq(const Fe& a) { return fe_mul(a, a); }
+Fe fe_sq(const Fe& a) {
+  const u64* x = a.v;
+  const u64 d0 = 2 * x[0], d1 = 2 * x[1], d2 = 2 * x[2], d3_19 = 2 * 19 * x[3], x4_19 = 19 * x[4], x3_19 = 19 * x[3];
+  u128 t[5];
+  t[0] = u128(x[0]) * x[0] + u128(d1) * x4_19 + u128(d2) * x3_19;
+  t[1] = u128(d0) * x[1] + u128(d2) * x4_19 + u128(x[3]) * x3_19;
+  t[2] = u128(d0) * x[2] + u128(x[1]) * x[1] + u128(d3_19) * x[4];
+  t[3] = u128(d0) * x[3] + u128(d1) * x[2] + u128(x[4]) * x4_19;
+  t[4] = u128(d0) * x[4] + u128(d1) * x[3] + u128(x[2]) * x[2];
+  Fe r;
+  u128 c = 0;
+  for (int i = 0; i < 5; ++i) {
+    t[i] += c;
+    r.v[i] = u64(t[i]) & MASK51;
+    c = t[i] >> 51;
+  }
+  r.v[0] += u64(c) * 19;
+  return fe_carry1(r);
+}
+Fe fe_sqn(Fe a, int n) {
+  for (int i = 0; i < n; ++i) a = fe_sq(a);
+  return a;
+}
 
 // canonical 32-byte little-endian encoding
 void fe_tobytes(u8 out[32], Fe a) {
@@ -116,19 +148,55 @@ Fe fe_pow(const Fe& a, const u8 e_le[32]) {
   }
   return r;
 }
-Fe fe_invert(const Fe& a) {
-  u8 e[32];
-  memset(e, 0xff, 32);
-  e[0] = 0xeb;  // p - 2 = 2^255 - 21
-  e[31] = 0x7f;
-  return fe_pow(a, e);
+// z^(p-2), addition chain: 254 squarings + 11 multiplications
+Fe fe_invert(const Fe& z) {
+  Fe t0 = fe_sq(z);
+  Fe t1 = fe_sqn(t0, 2);
+  t1 = fe_mul(z, t1);
+  t0 = fe_mul(t0, t1);
+  Fe t2 = fe_sq(t0);
+  t1 = fe_mul(t1, t2);
+  t2 = fe_sqn(t1, 5);
+  t1 = fe_mul(t2, t1);
+  t2 = fe_sqn(t1, 10);
+  t2 = fe_mul(t2, t1);
+  Fe t3 = fe_sqn(t2, 20);
+  t2 = fe_mul(t3, t2);
+  t2 = fe_sqn(t2, 10);
+  t1 = fe_mul(t2, t1);
+  t2 = fe_sqn(t1, 50);
+  t2 = fe_mul(t2, t1);
+  t3 = fe_sqn(t2, 100);
+  t2 = fe_mul(t3, t2);
+  t2 = fe_sqn(t2, 50);
+  t1 = fe_mul(t2, t1);
+  t1 = fe_sqn(t1, 5);
+  return fe_mul(t1, t0);
 }
-Fe fe_pow22523(const Fe& a) {
-  u8 e[32];  // (p-5)/8 = 2^252 - 3
-  memset(e, 0xff, 32);
-  e[0] = 0xfd;
-  e[31] = 0x0f;
-  return fe_pow(a, e);
+// z^((p-5)/8) = z^(2^252 - 3)
+Fe fe_pow22523(const Fe& z) {
+  Fe t0 = fe_sq(z);
+  Fe t1 = fe_sqn(t0, 2);
+  t1 = fe_mul(z, t1);
+  t0 = fe_mul(t0, t1);
+  t0 = fe_sq(t0);
+  t0 = fe_mul(t1, t0);
+  t1 = fe_sqn(t0, 5);
+  t0 = fe_mul(t1, t0);
+  t1 = fe_sqn(t0, 10);
+  t1 = fe_mul(t1, t0);
+  Fe t2 = fe_sqn(t1, 20);
+  t1 = fe_mul(t2, t1);
+  t1 = fe_sqn(t1, 10);
+  t0 = fe_mul(t1, t0);
+  t1 = fe_sqn(t0, 50);
+  t1 = fe_mul(t1, t0);
+  t2 = fe_sqn(t1, 100);
+  t1 = fe_mul(t2, t1);
+  t1 = fe_sqn(t1, 50);
+  t0 = fe_mul(t1, t0);
+  t0 = fe_sqn(t0, 2);
+  return fe_mul(t0, z);
 }
 Fe fe_from_dec(const char* s) {
   u64 w[4] = {0, 0, 0, 0};
@@ -161,12 +229,26 @@ Ge ge_add(const Ge& p, const Ge& q) {
   return Ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
 Ge ge_neg(const Ge& p) { return Ge{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
-// scalar as 32-byte little-endian
+// dbl-2008-hwcd for a = -1: 4M + 4S (vs 9M for the unified addition)
+Ge ge_dbl(const Ge& p) {
+  Fe A = fe_sq(p.X), Bv = fe_sq(p.Y);
+  Fe C = fe_add(fe_sq(p.Z), fe_sq(p.Z));
+  Fe Dd = fe_neg(A);
+  Fe E = fe_sub(fe_sub(fe_sq(fe_add(p.X, p.Y)), A), Bv);
+  Fe G = fe_add(Dd, Bv), F = fe_sub(G, C), H = fe_sub(Dd, Bv);
+  return Ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+// scalar as 32-byte little-endian; fixed 4-bit windows (256 doublings + 64 additions)
 Ge ge_mul(const Ge& p, const u8 k[32]) {
+  Ge tbl[16];
+  tbl[0] = ge_identity();
+  tbl[1] = p;
+  for (int i = 2; i < 16; ++i) tbl[i] = (i & 1) ? ge_add(tbl[i - 1], p) : ge_dbl(tbl[i / 2]);
   Ge r = ge_identity();
-  for (int i = 255; i >= 0; --i) {
-    r = ge_add(r, r);
-    if ((k[i >> 3] >> (i & 7)) & 1) r = ge_add(r, p);
+  for (int w = 63; w >= 0; --w) {
+    if (w != 63) { r = ge_dbl(r); r = ge_dbl(r); r = ge_dbl(r); r = ge_dbl(r); }
+    int d = (k[w >> 1] >> ((w & 1) * 4)) & 15;
+    if (d) r = ge_add(r, tbl[d]);
   }
   return r;
 }
@@ -187,7 +269,7 @@ struct BaseTable {
     for (int w = 0; w < 64; ++w) {
       t[w * 16] = ge_identity();
       for (int d = 1; d < 16; ++d) t[w * 16 + d] = ge_add(t[w * 16 + d - 1], base);
-      for (int i = 0; i < 4; ++i) base = ge_add(base, base);
+      for (int i = 0; i < 4; ++i) base = ge_dbl(base);
     }
   }
 };
@@ -322,18 +404,18 @@ Ge encode_to_curve(const Bytes& pk, const Bytes& alpha) {
     h.final(dig);
     Ge H;
     if (ge_frombytes(H, dig)) {
-      H = ge_add(H, H); H = ge_add(H, H); H = ge_add(H, H);  // cofactor 8
+      H = ge_dbl(ge_dbl(ge_dbl(H)));  // cofactor 8
       return H;
     }
   }
   fail("ecvrf: encode_to_curve failed");
 }
 
-Bytes challenge(const Ge& Y, const Ge& H, const Ge& G, const Ge& U, const Ge& V) {
+Bytes challenge_str(const Bytes& Y, const Bytes& H, const Bytes& G, const Bytes& U, const Bytes& V) {
   Sha512 h;
   u8 pre[2] = {SUITE, 0x02};
   h.update(pre, 2);
-  for (const Ge* p : {&Y, &H, &G, &U, &V}) h.update(ge_tobytes(*p));
+  for (const Bytes* p : {&Y, &H, &G, &U, &V}) h.update(*p);
   u8 z = 0;
   h.update(&z, 1);
   u8 dig[64];
@@ -361,11 +443,24 @@ Bytes vrf_proof_to_hash(const Bytes& pi) {
   if (pi.size() != 80) fail("ecvrf: bad proof length");
   Ge G;
   if (!ge_frombytes(G, pi.data())) fail("ecvrf: bad gamma");
-  G = ge_add(G, G); G = ge_add(G, G); G = ge_add(G, G);
+  G = ge_dbl(ge_dbl(ge_dbl(G)));
   Sha512 h;
   u8 pre[2] = {SUITE, 0x03};
   h.update(pre, 2);
   h.update(ge_tobytes(G));
+  u8 z = 0;
+  h.update(&z, 1);
+  Bytes out(64);
+  h.final(out.data());
+  return out;
+}
+
+static Bytes gamma_to_hash(const Ge& Gamma) {
+  Ge G8 = ge_dbl(ge_dbl(ge_dbl(Gamma)));
+  Sha512 h;
+  u8 pre[2] = {SUITE, 0x03};
+  h.update(pre, 2);
+  h.update(ge_tobytes(G8));
   u8 z = 0;
   h.update(&z, 1);
   Bytes out(64);
@@ -386,15 +481,14 @@ std::pair<Bytes, Bytes> vrf_prove(const VrfKey& key, const Bytes& alpha) {
   kh.final(kd);
   u8 k[32];
   sc_reduce(k, kd, 64);
-  Ge Y;
-  ge_frombytes(Y, key.pk.data());
-  Bytes c = challenge(Y, H, Gamma, ge_mul_base(k), ge_mul(H, k));
+  Bytes gstr = ge_tobytes(Gamma);
+  Bytes c = challenge_str(key.pk, hstr, gstr, ge_tobytes(ge_mul_base(k)), ge_tobytes(ge_mul(H, k)));
   u8 s[32];
   sc_muladd(s, k, c.data(), 16, x);
-  Bytes pi = ge_tobytes(Gamma);
+  Bytes pi = gstr;
   pi.insert(pi.end(), c.begin(), c.end());
   pi.insert(pi.end(), s, s + 32);
-  return {vrf_proof_to_hash(pi), pi};
+  return {gamma_to_hash(Gamma), pi};
 }
 
 bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* beta) {
@@ -411,7 +505,7 @@ bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* bet
   Ge H = encode_to_curve(pk, alpha);
   Ge U = ge_add(ge_mul_base(s), ge_neg(ge_mul(Y, c)));
   Ge V = ge_add(ge_mul(H, s), ge_neg(ge_mul(Gamma, c)));
-  Bytes c2 = challenge(Y, H, Gamma, U, V);
+  Bytes c2 = challenge_str(pk, ge_tobytes(H), Bytes(pi.begin(), pi.begin() + 32), ge_tobytes(U), ge_tobytes(V));
   if (memcmp(c2.data(), c, 16) != 0) return false;
   if (beta) *beta = vrf_proof_to_hash(pi);
   return true;

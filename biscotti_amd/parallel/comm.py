@@ -84,9 +84,10 @@ class Comm:
         t = t.contiguous()
         if self.world == 1:
             return t.unsqueeze(0)
-        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t)
-        return out
+        flat = t.reshape(-1)
+        out = torch.empty((self.world * flat.numel(),), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, flat)
+        return out.view(self.world, *t.shape)
 
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
         if self.world > 1:

@@ -49,6 +49,7 @@ class RunConfig:
     resume: bool = False
     device: str | None = None       # "cpu" forces the CPU path
     log_every_peer: bool = False    # one Train Error line per local peer (reference style)
+    deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
 
     def protocol(self, rt):
         pc = rt.ProtocolConfig()
@@ -118,6 +119,7 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--device", default=None)
     ap.add_argument("--log-every-peer", action="store_true")
+    ap.add_argument("--deterministic-time", action="store_true")
 
 
 def config_from_args(ns: argparse.Namespace) -> RunConfig:

@@ -125,6 +125,9 @@ class BiscottiEngine:
         self.local = self.comm.peer_range(self.N)
         self.lo = self.local.start
         self.maxlocal = self.comm.max_local(self.N)
+        # peer -> row in a [world * maxlocal] gathered buffer
+        self.flat = {p: r * self.maxlocal + (p - self.comm.peer_range(self.N, r).start)
+                     for r in range(self.comm.world) for p in self.comm.peer_range(self.N, r)}
         tag = f"{cfg.log_dir}/log_{self.comm.rank}_{self.N}.log" if cfg.log_dir else None
         self.log = get_logger("peer", tag)
         self.trace = JsonlWriter(cfg.trace_file if self.comm.rank == 0 else None)
@@ -150,6 +153,11 @@ class BiscottiEngine:
                 self.fsm.addresses = addrs[: self.N]
         if cfg.resume and cfg.chain_file:
             self._resume(cfg.chain_file)
+        if cfg.chain_file and self.comm.rank == 0:
+            import os
+
+            if not (cfg.resume and os.path.exists(cfg.chain_file)):
+                self.fsm.chain.save(cfg.chain_file)  # genesis (or the resumed prefix) first
         self.W = torch.from_numpy(np.array(self.fsm.chain.latest().data.global_w, dtype=np.float64)).to(self.dev)
         # ---- keys
         if cfg.commit_key:
@@ -176,6 +184,9 @@ class BiscottiEngine:
         self.rounds_done = 0
 
     # ------------------------------------------------------------------ helpers
+    def _now(self, iteration: int) -> int:
+        return iteration + 1 if self.cfg.deterministic_time else int(time.time())
+
     def _resume(self, path: str) -> None:
         import os
 
@@ -255,61 +266,70 @@ class BiscottiEngine:
         # ---------------------------------------------------------------- verification
         with tm.phase("verify"):
             row_of = {w: i for i, w in enumerate(local_workers)}
-            cbuf = torch.zeros((self.maxlocal, 64), dtype=torch.uint8, device=self.dev)
-            if local_workers:
-                idx = torch.tensor([w - self.lo for w in local_workers], dtype=torch.long, device=self.dev)
-                cbuf[idx] = torch.from_numpy(commits_local).to(self.dev)
-            commits_all = comm.all_gather(cbuf).cpu().numpy()  # [world, maxlocal, 64]
-            commit_of = {w: bytes(self._gathered_row(commits_all, w)) for w in workers}
+            single = comm.world == 1
+            if single:
+                commit_of = {w: commits_local[row_of[w]].tobytes() for w in local_workers}
+            else:
+                cbuf = torch.zeros((self.maxlocal, 64), dtype=torch.uint8, device=self.dev)
+                if local_workers:
+                    lidx = torch.tensor([w - self.lo for w in local_workers], dtype=torch.long, device=self.dev)
+                    cbuf.index_copy_(0, lidx, torch.from_numpy(commits_local).to(self.dev))
+                commits_all = comm.all_gather(cbuf).reshape(-1, 64).cpu().numpy()
+                commit_of = {w: commits_all[self.flat[w]].tobytes() for w in workers}
             if cfg.colluders > 0:  # privacy experiment bookkeeping (isCollusionAttack, main.go:1026-1057)
                 thr = self.pc.collusion_thresh
                 if any(v >= thr for v in plan.verifiers):
                     self.stats["unmasked_updates"] += sum(
                         1 for w in local_workers if all(j >= thr for j in noisers[w]))
             accepted_map: dict = {}
+            signatures: dict = {}
             inbox = fsm.verifier_inbox(workers) if cfg.verification else []
-            online_verifiers = [v for v in plan.verifiers if live[v]]
-            local_verifiers = [v for v in online_verifiers if v in self.local]
+            local_verifiers = [v for v in plan.verifiers if live[v] and v in self.local]
             if cfg.verification and inbox:
-                nbuf = torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev)
-                if local_workers:
-                    nbuf[idx] = noised
-                gathered = comm.all_gather(nbuf) if (local_verifiers or comm.world > 1) else None
-                acc_mask = torch.zeros((len(plan.verifiers), len(inbox)), dtype=torch.uint8, device=self.dev)
-                sig_buf = torch.zeros((len(plan.verifiers), len(inbox), 64), dtype=torch.uint8, device=self.dev)
-                if local_verifiers:
-                    X = torch.stack([self._gathered_row(gathered, w) for w in inbox]).contiguous()
-                    krum_cache = None
-                    for v in local_verifiers:
-                        if cfg.defense == "KRUM":  # identical inputs -> identical Krum result per rank
-                            krum_cache = krum_cache or self._verify(X, inbox, it, v)
-                            accept = krum_cache
-                        else:
-                            accept = self._verify(X, inbox, it, v)
-                        acc_ids = [w for w, a in zip(inbox, accept) if a]
-                        vi = plan.verifiers.index(v)
-                        msgs = [commit_of[w] for w in acc_ids]
-                        nonces = [_seed_bytes(cfg.seed, f"nonce-{it}-{v}", w) for w in acc_ids]
-                        sigs = R.schnorr_sign_batch(msgs, self.sk[v], nonces, cfg.host_threads)
-                        for w, s in zip(acc_ids, sigs):
-                            j = inbox.index(w)
-                            acc_mask[vi, j] = 1
-                            sig_buf[vi, j] = torch.frombuffer(bytearray(s), dtype=torch.uint8).to(self.dev)
-                acc_all = comm.all_gather(acc_mask).cpu().numpy()
-                sig_all = comm.all_gather(sig_buf).cpu().numpy()
-                signatures: dict = {}
+                nv, ni = len(plan.verifiers), len(inbox)
+                if single:
+                    X = noised.index_select(0, torch.tensor([row_of[w] for w in inbox], dtype=torch.long,
+                                                            device=self.dev)) if local_verifiers else None
+                else:
+                    nbuf = torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev)
+                    if local_workers:
+                        nbuf.index_copy_(0, lidx, noised)
+                    gathered = comm.all_gather(nbuf).reshape(-1, self.d)
+                    X = gathered.index_select(0, torch.tensor([self.flat[w] for w in inbox], dtype=torch.long,
+                                                              device=self.dev)) if local_verifiers else None
+                acc_np = np.zeros((nv, ni), np.uint8)
+                sig_np = np.zeros((nv, ni, 64), np.uint8)
+                krum_cache = None
+                pos = {w: j for j, w in enumerate(inbox)}
+                for v in local_verifiers:
+                    if cfg.defense == "KRUM":  # identical inputs -> identical Krum result per rank
+                        krum_cache = krum_cache or self._verify(X, inbox, it, v)
+                        accept = krum_cache
+                    else:
+                        accept = self._verify(X, inbox, it, v)
+                    acc_ids = [w for w, a_ in zip(inbox, accept) if a_]
+                    vi = plan.verifiers.index(v)
+                    nonces = [_seed_bytes(cfg.seed, f"nonce-{it}-{v}", w) for w in acc_ids]
+                    sigs = R.schnorr_sign_batch([commit_of[w] for w in acc_ids], self.sk[v], nonces,
+                                                cfg.host_threads)
+                    for w, sg in zip(acc_ids, sigs):
+                        acc_np[vi, pos[w]] = 1
+                        sig_np[vi, pos[w]] = np.frombuffer(sg, np.uint8)
+                if single:
+                    acc_all, sig_all = acc_np[None], sig_np[None]
+                else:
+                    acc_all = comm.all_gather(torch.from_numpy(acc_np).to(self.dev)).cpu().numpy()
+                    sig_all = comm.all_gather(torch.from_numpy(sig_np).to(self.dev)).cpu().numpy()
                 for vi, v in enumerate(plan.verifiers):
                     if not live[v]:
                         continue
-                    owner = comm.owner(v, self.N)
-                    ids = [inbox[j] for j in range(len(inbox)) if acc_all[owner, vi, j]]
-                    accepted_map[v] = ids
-                    for j in range(len(inbox)):
-                        if acc_all[owner, vi, j]:
-                            signatures.setdefault(inbox[j], []).append(bytes(sig_all[owner, vi, j]))
+                    o = 0 if single else comm.owner(v, self.N)
+                    js = np.nonzero(acc_all[o, vi])[0]
+                    accepted_map[v] = [inbox[j] for j in js]
+                    for j in js:
+                        signatures.setdefault(inbox[j], []).append(sig_all[o, vi, j].tobytes())
                 approved, _ = fsm.approve(accepted_map)
             else:
-                signatures = {}
                 approved, _ = fsm.approve({})
         # ---------------------------------------------------------------- aggregation + block
         if cfg.secure_agg:
@@ -358,99 +378,100 @@ class BiscottiEngine:
                             signatures):
         cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
         self._last_nodes = []
+        spm, T, nch = self.pc.shares_per_miner, self.T, self.nchunks
+        single = comm.world == 1
+        if cfg.verify_signatures and cfg.verification:
+            # miners reject shares without >= nv/2 valid verifier signatures (main.go:269-277, Q5)
+            need = len(plan.verifiers) // 2
+            approved = [w for w in approved
+                        if sum(any(R.schnorr_verify(commit_of[w], self.pk[v], sg) for v in plan.verifiers)
+                               for sg in signatures.get(w, [])) >= need]
         with tm.phase("shares"):
             routes = fsm.route_shares(approved)
             lv = fsm.leader_view(routes)
             local_approved = [w for w in approved if w in self.local]
-            if local_approved and routes:
+            pts = ys = None
+            if local_approved and routes:  # workers share as soon as any miner is reachable
                 sel = torch.tensor([row_of[w] for w in local_approved], dtype=torch.long, device=self.dev)
-                pts, ys = self.crypto.shares(qdelta[sel].contiguous())
-            else:
-                pts = ys = None
+                pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
             ap_row = {w: i for i, w in enumerate(local_approved)}
+        if not (lv.leader_online and lv.quorum):
+            return None
+        node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
+        part_of = {m: dict(routes[m])[node_list[0]] for m in contributing}
+        pw = 24 if self.gpu else 64
+        pdt = torch.int32 if self.gpu else torch.uint8
+        ar = torch.arange(nch, dtype=torch.long, device=self.dev)
+
+        def cols_of(part):  # the miner's witness slots + the chunk-commitment slot
+            return list(range(spm * part, spm * part + spm)) + [T]
+
         with tm.phase("share_exchange"):
-            S = cfg.poly_size  # unused name guard
-            spm = self.pc.shares_per_miner
-            pw = pts.shape[-1] if pts is not None else (24 if self.gpu else 64)
-            pdt = pts.dtype if pts is not None else (torch.int32 if self.gpu else torch.uint8)
-            # what each rank sends to each destination: for every (worker, miner, part) route whose
-            # worker is local and miner lives on that destination, the miner's share slice
-            send_p, send_y, manifest = [], [], []
-            for dst in range(comm.world):
-                dst_range = comm.peer_range(self.N, dst)
-                ps, yl, man = [], [], []
-                for m in sorted(routes):
-                    if m not in dst_range:
-                        continue
-                    for (w, part) in routes[m]:
-                        if w not in ap_row:
-                            continue
-                        i = ap_row[w]
-                        cols = list(range(spm * part, spm * part + spm)) + [self.T]
-                        ps.append(pts[i][:, cols].reshape(-1))
-                        yl.append(ys[i][:, spm * part: spm * part + spm].reshape(-1))
-                        man.append((m, w, part))
-                send_p.append(torch.cat(ps) if ps else torch.empty((0,), dtype=pdt, device=self.dev))
-                send_y.append(torch.cat(yl) if yl else torch.empty((0,), dtype=torch.int64, device=self.dev))
-                manifest.append(man)
-            recv_p = comm.all_to_all(send_p)
-            recv_y = comm.all_to_all(send_y)
-            # reconstruct the manifest of what this rank received, in sender order
-            inbox_parts: dict = {}
-            per_p = self.nchunks * (spm + 1) * pw
-            per_y = self.nchunks * spm
-            for src in range(comm.world):
-                src_range = comm.peer_range(self.N, src)
-                k = 0
-                for m in sorted(routes):
-                    if m not in self.local:
-                        continue
-                    for (w, part) in routes[m]:
-                        if w not in src_range:
-                            continue
-                        p_ = recv_p[src][k * per_p:(k + 1) * per_p].view(self.nchunks, spm + 1, pw)
-                        y_ = recv_y[src][k * per_y:(k + 1) * per_y].view(self.nchunks, spm)
-                        inbox_parts.setdefault(m, {})[w] = (part, p_, y_)
-                        k += 1
-        with tm.phase("miner_aggregate"):
-            # every online local miner aggregates the shares of the leader's node list
-            node_list = list(lv.node_list)
-            contributing = list(lv.contributing_miners)
-            nc = len(contributing)
-            agg_y_buf = torch.zeros((nc, self.nchunks, spm), dtype=torch.int64, device=self.dev)
-            part_buf = torch.zeros((nc,), dtype=torch.int64, device=self.dev)
-            if lv.leader_online and lv.quorum:
-                for ci, m in enumerate(contributing):
-                    if m not in self.local:
-                        continue
-                    got = inbox_parts.get(m, {})
-                    if cfg.verify_signatures:
-                        need = len(plan.verifiers) // 2
-                        ok_nodes = [w for w in node_list if sum(
-                            R.schnorr_verify(commit_of[w], self.pk[v], s) for s in signatures.get(w, [])
-                            for v in plan.verifiers) >= need]
+            recv: dict = {}  # miner -> (pts [E, nch, spm+1, pw] or None, ys [E, nch, spm], rows or None)
+            if single:
+                rows = torch.tensor([ap_row[w] for w in node_list], dtype=torch.long, device=self.dev)
+                for m in contributing:
+                    recv[m] = (None, None, rows)
+            else:
+                send_p, send_y = [], []
+                for dst in range(comm.world):
+                    ents = [(m, w) for m in contributing if comm.owner(m, self.N) == dst
+                            for w in node_list if w in ap_row]
+                    if ents:
+                        ir = torch.tensor([ap_row[w] for _, w in ents], dtype=torch.long, device=self.dev)
+                        ic = torch.tensor([cols_of(part_of[m]) for m, _ in ents], dtype=torch.long, device=self.dev)
+                        g = pts[ir[:, None, None], ar[None, :, None], ic[:, None, :]]
+                        gy = ys[ir[:, None, None], ar[None, :, None], ic[:, None, :spm]]
+                        send_p.append(g.reshape(-1))
+                        send_y.append(gy.reshape(-1))
                     else:
-                        ok_nodes = node_list
-                    ps = torch.stack([got[w][1] for w in ok_nodes])     # [R, nchunks, spm+1, pw]
-                    yv = torch.stack([got[w][2] for w in ok_nodes])     # [R, nchunks, spm]
-                    _ = self.crypto.sum_rows(ps.reshape(len(ok_nodes), -1, pw))  # witnesses + commitments
-                    agg_y_buf[ci] = yv.sum(0)
-                    part_buf[ci] = got[ok_nodes[0]][0]
+                        send_p.append(torch.empty((0,), dtype=pdt, device=self.dev))
+                        send_y.append(torch.empty((0,), dtype=torch.int64, device=self.dev))
+                rp, ry = comm.all_to_all(send_p), comm.all_to_all(send_y)
+                for m in contributing:
+                    if m not in self.local:
+                        continue
+                    ps_, ys_ = [], []
+                    for src in range(comm.world):
+                        src_ents = [(mm, w) for mm in contributing if comm.owner(mm, self.N) == self.comm.rank
+                                    for w in node_list if comm.owner(w, self.N) == src]
+                        per_p, per_y = nch * (spm + 1) * pw, nch * spm
+                        for k, (mm, w) in enumerate(src_ents):
+                            if mm == m:
+                                ps_.append(rp[src][k * per_p:(k + 1) * per_p].view(nch, spm + 1, pw))
+                                ys_.append(ry[src][k * per_y:(k + 1) * per_y].view(nch, spm))
+                    recv[m] = (torch.stack(ps_), torch.stack(ys_), None)
+        with tm.phase("miner_aggregate"):
+            nc = len(contributing)
+            agg_y = torch.zeros((nc, nch, spm), dtype=torch.int64, device=self.dev)
+            for ci, m in enumerate(contributing):
+                if m not in self.local:
+                    continue
+                p_, y_, rows = recv[m]
+                part = part_of[m]
+                if rows is not None:  # single rank: aggregate straight out of the share tensors
+                    cols = torch.tensor([k * (T + 1) + c for k in range(nch) for c in cols_of(part)],
+                                        dtype=torch.long, device=self.dev)
+                    flat = pts.view(pts.shape[0], nch * (T + 1), pw)
+                    if self.gpu:
+                        _ = B.sum_rows(flat, rows.int(), cols.int())  # aggregateSecret: witnesses + commitments
+                    else:
+                        _ = self.crypto.sum_rows(flat.index_select(0, rows).index_select(1, cols))
+                    agg_y[ci] = ys.index_select(0, rows)[:, :, spm * part: spm * part + spm].sum(0)
+                else:
+                    _ = self.crypto.sum_rows(p_.reshape(p_.shape[0], -1, pw))
+                    agg_y[ci] = y_.sum(0)
         with tm.phase("recover"):
-            if not (lv.leader_online and lv.quorum):
-                return None
-            agg_y_all = comm.all_gather(agg_y_buf)      # [world, nc, nchunks, spm]
-            parts_all = comm.all_gather(part_buf)
+            agg_all = agg_y[None] if single else comm.all_gather(agg_y)   # [world, nc, nch, spm]
             leader_rank = comm.owner(plan.leader, self.N)
-            block_bytes = None
+            block = block_bytes = None
             if comm.rank == leader_rank:
-                ys_cols, xs = [], []
+                cols, xs = [], []
                 for ci, m in enumerate(contributing):
-                    o = comm.owner(m, self.N)
-                    part = int(parts_all[o, ci])
-                    ys_cols.append(agg_y_all[o, ci])
-                    xs += [spm * part + s - 10 for s in range(spm)]
-                agg = torch.cat(ys_cols, dim=1).contiguous()      # [nchunks, npts]
+                    o = 0 if single else comm.owner(m, self.N)
+                    cols.append(agg_all[o, ci])
+                    xs += [spm * part_of[m] + s_ - 10 for s_ in range(spm)]
+                agg = torch.cat(cols, dim=1).contiguous()      # [nchunks, npts]
                 xs_t = torch.tensor(xs, dtype=torch.int32, device=self.dev)
                 W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
                 st = status.cpu().numpy()
@@ -464,13 +485,15 @@ class BiscottiEngine:
                             if i < self.d:
                                 W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
                     self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
-                comms = [commit_of[w] for w in node_list]
-                blk = fsm.make_secagg_block(W_np, node_list, comms, int(time.time()))
-                block_bytes = blk.serialize()
-            data = comm.broadcast_bytes(block_bytes, leader_rank)
-            block = R.Block.deserialize(data)
-            if block.compute_hash() != block.hash:
-                raise RuntimeError("received block with a bad hash")
+                block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], self._now(plan.iteration))
+                if not single:
+                    block_bytes = block.serialize()
+            if not single:
+                data = comm.broadcast_bytes(block_bytes, leader_rank)
+                if comm.rank != leader_rank:
+                    block = R.Block.deserialize(data)
+                    if block.compute_hash() != block.hash:
+                        raise RuntimeError("received block with a bad hash")
             self._last_nodes = node_list
             return block
 
@@ -505,7 +528,7 @@ class BiscottiEngine:
                     u.commitment = commit_of[w]
                     u.signatures = signatures.get(w, [])
                     upd.append(u)
-                blk = fsm.make_plain_block(W.cpu().numpy(), upd, int(time.time()))
+                blk = fsm.make_plain_block(W.cpu().numpy(), upd, self._now(plan.iteration))
                 block_bytes = blk.serialize()
             data = comm.broadcast_bytes(block_bytes, leader_rank)
             self._last_nodes = list(ups)

@@ -1,0 +1,100 @@
+"""Multi-process runs over gloo (CPU): every rank must hold the same chain, and it must equal the
+single-process chain byte for byte (deterministic timestamps) -- the localTest.sh oracle."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, kw, rounds, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    comm = Comm.init(device="cpu")
+    eng = BiscottiEngine(RunConfig(**kw), comm)
+    for _ in range(rounds):
+        eng.run_round()
+    q.put((rank, [bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))]))
+    comm.barrier()
+    comm.shutdown()
+
+
+def _run(world, kw, rounds):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kw, rounds, q)) for r in range(world)]
+    import queue
+    import time
+
+    for p in ps:
+        p.start()
+    out, deadline = {}, time.time() + 600
+    try:
+        while len(out) < world:
+            try:
+                r, hashes = q.get(timeout=1.0)
+                out[r] = hashes
+            except queue.Empty:
+                if any(p.exitcode not in (None, 0) for p in ps) or time.time() > deadline:
+                    raise AssertionError("a rank failed: " + str([p.exitcode for p in ps]))
+        for p in ps:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+KW = dict(num_nodes=6, dataset="creditcard", num_verifiers=2, num_miners=3, num_noisers=1, epsilon=1.0,
+          device="cpu", seed=11, deterministic_time=True)
+
+
+@pytest.mark.parametrize("secure_agg", [True, False])
+def test_two_ranks_match_single_process(secure_agg):
+    kw = dict(KW, secure_agg=secure_agg)
+    single = _run(1, kw, 4)[0]
+    multi = _run(2, kw, 4)
+    assert multi[0] == multi[1]
+    assert multi[0] == single
+
+
+def test_three_ranks_uneven_packing():
+    single = _run(1, KW, 3)[0]
+    multi = _run(3, dict(KW, num_nodes=7), 3)
+    assert multi[0] == multi[1] == multi[2]
+
+
+def test_peer_processes_localtest_oracle():
+    """DistSys/localTest.sh: N processes `peer -i k -t N -d creditcard`, identical chain dumps."""
+    n = 4
+    port = _free_port()
+    env = dict(os.environ, MASTER_PORT=str(port), PYTHONPATH=ROOT)
+    procs = [subprocess.Popen([sys.executable, "-m", "biscotti_amd.peer", f"-i={k}", f"-t={n}", "-d=creditcard",
+                               "-na=1", "-nv=1", "-nn=1", "-np=false", "--device", "cpu", "--rounds", "3",
+                               "--print-chain", "all", "--deterministic-time"],
+                              cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+             for k in range(n)]
+    outs = [b"\n".join(ln for ln in p.communicate(timeout=600)[0].split(b"\n") if not ln.startswith(b"[Gloo]"))
+            for p in procs]
+    assert all(p.returncode == 0 for p in procs)
+    assert all(o == outs[0] for o in outs) and outs[0].count(b"Hash: ") == 4
