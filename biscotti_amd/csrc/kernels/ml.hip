@@ -303,47 +303,50 @@ extern "C" __global__ void __launch_bounds__(64) k_gram_f64(const float* X, int 
   }
 }
 
-// K5b: reduce partials, distances, Krum scores and Multi-Krum selection; one block, n <= 256.
-// score_i = sum(sort(D_i)[1:groupsize-1]);  accept the n_accept lowest scores (index tiebreak).
+// K5b: reduce partials, distances, Krum scores and Multi-Krum selection; one block, n <= 128.
+// score_i = sum(sort(D_i)[1:groupsize-1]): computed without sorting -- every D_ij gets its rank in
+// row i by parallel counting (ties broken by column index) and rank in [1, groupsize-2] is summed.
+// Accept the n_accept lowest scores (index tiebreak).  Everything lives in LDS.
 extern "C" __global__ void __launch_bounds__(256) k_krum_select(const double* part, int nsplit, int n, int npad,
                                                                int groupsize, int n_accept, double* dist,
                                                                double* scores, int* accept) {
-  __shared__ double sq[256];
-  __shared__ double sc[256];
+  __shared__ double D[128 * 128];
+  __shared__ double sc[128];
+  __shared__ uint8_t keep[128 * 128];
   const int t = threadIdx.x;
   for (int idx = t; idx < n * n; idx += blockDim.x) {
     const int i = idx / n, j = idx % n;
     double g = 0.0;
     for (int s = 0; s < nsplit; ++s) g += part[((size_t)s * npad + i) * npad + j];
-    dist[idx] = g;  // temporarily the Gram matrix
+    D[idx] = g;  // Gram matrix for now
   }
-  __syncthreads();
-  if (t < n) sq[t] = dist[t * n + t];
   __syncthreads();
   for (int idx = t; idx < n * n; idx += blockDim.x) {
     const int i = idx / n, j = idx % n;
-    dist[idx] = sq[i] + sq[j] - 2.0 * dist[idx];
+    dist[idx] = D[i * n + i] + D[j * n + j] - 2.0 * D[idx];
   }
   __syncthreads();
-  if (t < n) {
-    // insertion sort of row t in place (global, row is private to this thread)
-    double* row = dist + (size_t)t * n;
-    for (int a = 1; a < n; ++a) {
-      const double v = row[a];
-      int b = a - 1;
-      while (b >= 0 && row[b] > v) {
-        row[b + 1] = row[b];
-        --b;
-      }
-      row[b + 1] = v;
+  for (int idx = t; idx < n * n; idx += blockDim.x) D[idx] = dist[idx];
+  __syncthreads();
+  for (int idx = t; idx < n * n; idx += blockDim.x) {
+    const int i = idx / n, j = idx % n;
+    const double v = D[idx];
+    int rank = 0;
+    for (int k = 0; k < n; ++k) {
+      const double u = D[i * n + k];
+      rank += (u < v) || (u == v && k < j);
     }
-    double s = 0.0;
-    for (int k = 1; k < groupsize - 1 && k < n; ++k) s += row[k];
-    sc[t] = s;
-    scores[t] = s;
+    keep[idx] = (rank >= 1 && rank < groupsize - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (t < n) {  // fixed summation order -> bit-reproducible scores
+    double a = 0.0;
+    for (int j = 0; j < n; ++j) a += keep[t * n + j] ? D[t * n + j] : 0.0;
+    sc[t] = a;
   }
   __syncthreads();
   if (t < n) {
+    scores[t] = sc[t];
     int rank = 0;
     for (int j = 0; j < n; ++j) rank += (sc[j] < sc[t]) || (sc[j] == sc[t] && j < t);
     accept[t] = rank < n_accept ? 1 : 0;
@@ -527,7 +530,7 @@ extern "C" int bsc_dp_noise(const float* delta, int P, int D, const int* noisers
 extern "C" int bsc_krum(const float* X, int n, int D, int ksplit, double* part, double* dist, double* scores,
                         int* accept, int groupsize, int n_accept, void* stream) {
   if (n <= 0) return 0;
-  if (n > 256) return -1;
+  if (n > 128) return -1;
   const int tiles = (n + 15) / 16;
   const int nsplit = (D + ksplit - 1) / ksplit;
   hipLaunchKernelGGL(k_gram_f64, dim3(tiles, tiles, nsplit), dim3(64), 0, (hipStream_t)stream, X, n, D, ksplit,

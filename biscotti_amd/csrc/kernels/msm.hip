@@ -239,6 +239,31 @@ extern "C" __global__ void __launch_bounds__(128) k_sum_rows(const uint32_t* pts
   st_jac(out + 24 * (size_t)i, acc);
 }
 
+// Two-level version: block = 32 columns x 8 row groups; each thread sums every 8th row of its
+// column, then an LDS tree over the 8 partials.  8x the parallelism of k_sum_rows, and the column
+// list may concatenate several miners' slots (one launch per rank).
+extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
+                                                             int nrows, const int* cols, int ncols, uint32_t* out) {
+  __shared__ uint32_t sh[8][32][24];
+  const int cx = threadIdx.x & 31, ry = threadIdx.x >> 5;
+  const int i = blockIdx.x * 32 + cx;
+  jac acc = jac_inf();
+  if (i < ncols) {
+    const int col = cols ? cols[i] : i;
+    for (int r = ry; r < nrows; r += 8) {
+      const int row = rows ? rows[r] : r;
+      acc = jac_add(acc, ld_jac(pts + 24 * ((size_t)row * ncols_in + col)));
+    }
+  }
+  st_jac(&sh[ry][cx][0], acc);
+  __syncthreads();
+  for (int s = 4; s > 0; s >>= 1) {
+    if (ry < s) st_jac(&sh[ry][cx][0], jac_add(ld_jac(&sh[ry][cx][0]), ld_jac(&sh[ry + s][cx][0])));
+    __syncthreads();
+  }
+  if (ry == 0 && i < ncols) st_jac(out + 24 * (size_t)i, ld_jac(&sh[0][cx][0]));
+}
+
 // Sum of a strided segment per group: out[g] = sum_{k<n} pts[(g*n + k)*stride + off], one block
 // per group, LDS tree.  Used for the full commitment = sum of chunk commitments.
 extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* pts, int n, int stride, int off,
@@ -340,6 +365,14 @@ extern "C" int bsc_sum_rows(const uint32_t* pts, int ncols_in, const int* rows, 
                             uint32_t* out, void* stream) {
   if (ncols <= 0) return 0;
   hipLaunchKernelGGL(k_sum_rows, dim3(blocks_for(ncols, 128)), dim3(128), 0, (hipStream_t)stream, pts, ncols_in,
+                     rows, nrows, cols, ncols, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
+                             int ncols, uint32_t* out, void* stream) {
+  if (ncols <= 0) return 0;
+  hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 32)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
                      rows, nrows, cols, ncols, out);
   return (int)hipGetLastError();
 }

@@ -48,6 +48,21 @@ class Pool {
       for (size_t i = 0; i < n; ++i) f(i);
       return;
     }
+    // a second Python thread may call in while the pool is busy (host crypto overlapped with
+    // GPU work): it gets short-lived threads of its own instead of clobbering the running job
+    std::unique_lock<std::mutex> busy(run_m_, std::try_to_lock);
+    if (!busy.owns_lock()) {
+      std::atomic<size_t> next{0};
+      auto body = [&] {
+        for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+      };
+      std::vector<std::thread> ts;
+      const int extra = std::min<int>(threads, int(n)) - 1;
+      for (int t = 0; t < extra; ++t) ts.emplace_back(body);
+      body();
+      for (auto& t : ts) t.join();
+      return;
+    }
     ensure(threads - 1);
     std::unique_lock<std::mutex> lk(m_);
     job_ = &f;
@@ -96,7 +111,7 @@ class Pool {
     }
   }
   std::vector<std::thread> workers_;
-  std::mutex m_;
+  std::mutex m_, run_m_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(size_t)>* job_ = nullptr;
   std::atomic<size_t> next_{0};
@@ -200,6 +215,37 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     for (py::ssize_t i = 0; i < jac.shape(0); ++i) out.append(P(g1_from_jac_u32(jac.data(i, 0)).marshal()));
     return out;
   });
+  m.def("g1_marshal_jac_batch", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> jac) {
+    // [n, 24] device Jacobian limbs -> uint8 [n, 64] marshals with ONE inversion (Montgomery's trick)
+    if (jac.ndim() != 2 || jac.shape(1) != 24) throw std::runtime_error("expected [n, 24] uint32");
+    const size_t n = size_t(jac.shape(0));
+    py::array_t<uint8_t> out({py::ssize_t(n), py::ssize_t(64)});
+    std::vector<G1> pts(n);
+    for (size_t i = 0; i < n; ++i) pts[i] = g1_from_jac_u32(jac.data(py::ssize_t(i), 0));
+    const MontField& F = Fp();
+    std::vector<U256> pre(n);
+    U256 acc = F.one;
+    for (size_t i = 0; i < n; ++i) {
+      pre[i] = acc;
+      if (!pts[i].is_inf()) F.mul(acc, acc, pts[i].z);
+    }
+    U256 inv;
+    F.inv_mont(inv, acc);
+    std::memset(out.mutable_data(), 0, n * 64);
+    for (size_t k = n; k-- > 0;) {
+      if (pts[k].is_inf()) continue;
+      U256 zi, zi2, zi3, ax, ay;
+      F.mul(zi, inv, pre[k]);
+      F.mul(inv, inv, pts[k].z);
+      F.sqr(zi2, zi);
+      F.mul(zi3, zi2, zi);
+      F.mul(ax, pts[k].x, zi2);
+      F.mul(ay, pts[k].y, zi3);
+      F.from_mont(ax).to_be(out.mutable_data(py::ssize_t(k), 0));
+      F.from_mont(ay).to_be(out.mutable_data(py::ssize_t(k), 32));
+    }
+    return out;
+  });
   m.def("g1_sum_jac_u32", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> jac) {
     G1 acc = G1::infinity();
     for (py::ssize_t i = 0; i < jac.shape(0); ++i) acc = acc.add(g1_from_jac_u32(jac.data(i, 0)));
@@ -261,7 +307,7 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   m.def("vrf_public_key", [](py::bytes seed) { return P(VrfKey::from_seed(B(seed)).pk); });
   m.def("ed25519_public_key", [](py::bytes seed) { return P(ed25519_public_from_seed(B(seed))); });
   m.def("vrf_prove", [](py::bytes seed, py::bytes alpha) {
-    auto r = vrf_prove(VrfKey::from_seed(B(seed)), B(alpha));
+    auto r = vrf_prove(VrfKey::cached(B(seed)), B(alpha));
     return py::make_tuple(P(r.first), P(r.second));
   });
   m.def("vrf_verify", [](py::bytes pk, py::bytes alpha, py::bytes pi) -> py::object {
@@ -276,7 +322,7 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     std::vector<std::pair<Bytes, Bytes>> out(ss.size());
     {
       py::gil_scoped_release rel;
-      parallel_for(ss.size(), threads, [&](size_t i) { out[i] = vrf_prove(VrfKey::from_seed(ss[i]), a); });
+      parallel_for(ss.size(), threads, [&](size_t i) { out[i] = vrf_prove(VrfKey::cached(ss[i]), a); });
     }
     py::list r;
     for (auto& o : out) r.append(py::make_tuple(P(o.first), P(o.second)));

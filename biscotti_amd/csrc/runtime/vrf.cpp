@@ -2,6 +2,11 @@
 
 #include "hash.hpp"
 
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
 namespace bsc {
 namespace {
 
@@ -238,17 +243,62 @@ Ge ge_dbl(const Ge& p) {
   Fe G = fe_add(Dd, Bv), F = fe_sub(G, C), H = fe_sub(Dd, Bv);
   return Ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
 }
-// scalar as 32-byte little-endian; fixed 4-bit windows (256 doublings + 64 additions)
+// doubling whose result feeds another doubling: T is never read, skip its multiplication
+Ge ge_dbl_noT(const Ge& p) {
+  Fe A = fe_sq(p.X), Bv = fe_sq(p.Y);
+  Fe zz = fe_sq(p.Z);
+  Fe C = fe_add(zz, zz);
+  Fe Dd = fe_neg(A);
+  Fe E = fe_sub(fe_sub(fe_sq(fe_add(p.X, p.Y)), A), Bv);
+  Fe G = fe_add(Dd, Bv), F = fe_sub(G, C), H = fe_sub(Dd, Bv);
+  return Ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_zero()};
+}
+// "cached" form of a table entry: (Y+X, Y-X, 2Z, 2dT) -> an addition costs 8M instead of 10M
+struct GeCached { Fe YpX, YmX, Z2, T2d; };
+GeCached ge_cache(const Ge& p) {
+  return GeCached{fe_add(p.Y, p.X), fe_sub(p.Y, p.X), fe_add(p.Z, p.Z), fe_mul(p.T, D2())};
+}
+GeCached ge_cached_neg(const GeCached& c) { return GeCached{c.YmX, c.YpX, c.Z2, fe_neg(c.T2d)}; }
+Ge ge_add_cached(const Ge& p, const GeCached& q) {
+  Fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
+  Fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
+  Fe C = fe_mul(p.T, q.T2d);
+  Fe Dd = fe_mul(p.Z, q.Z2);
+  Fe E = fe_sub(B, A), F = fe_sub(Dd, C), G = fe_add(Dd, C), H = fe_add(B, A);
+  return Ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+// scalar (32-byte LE, < 2^255) -> 64 signed radix-16 digits in [-8, 8)
+void signed_digits(int8_t e[64], const u8 k[32]) {
+  for (int i = 0; i < 32; ++i) {
+    e[2 * i] = int8_t(k[i] & 15);
+    e[2 * i + 1] = int8_t(k[i] >> 4);
+  }
+  int carry = 0;
+  for (int i = 0; i < 63; ++i) {
+    e[i] = int8_t(e[i] + carry);
+    carry = (e[i] + 8) >> 4;
+    e[i] = int8_t(e[i] - (carry << 4));
+  }
+  e[63] = int8_t(e[63] + carry);
+}
+// variable-base: table of 1P..8P in cached form, 4 doublings (3 without T) + 1 cached add per digit
 Ge ge_mul(const Ge& p, const u8 k[32]) {
-  Ge tbl[16];
-  tbl[0] = ge_identity();
-  tbl[1] = p;
-  for (int i = 2; i < 16; ++i) tbl[i] = (i & 1) ? ge_add(tbl[i - 1], p) : ge_dbl(tbl[i / 2]);
+  GeCached tbl[8];  // tbl[i] = (i+1) P
+  tbl[0] = ge_cache(p);
+  Ge acc = ge_dbl(p);
+  tbl[1] = ge_cache(acc);
+  for (int i = 2; i < 8; ++i) {
+    acc = ge_add_cached(acc, tbl[0]);
+    tbl[i] = ge_cache(acc);
+  }
+  int8_t e[64];
+  signed_digits(e, k);
   Ge r = ge_identity();
   for (int w = 63; w >= 0; --w) {
-    if (w != 63) { r = ge_dbl(r); r = ge_dbl(r); r = ge_dbl(r); r = ge_dbl(r); }
-    int d = (k[w >> 1] >> ((w & 1) * 4)) & 15;
-    if (d) r = ge_add(r, tbl[d]);
+    if (w != 63) { r = ge_dbl_noT(r); r = ge_dbl_noT(r); r = ge_dbl_noT(r); r = ge_dbl(r); }
+    const int d = e[w];
+    if (d > 0) r = ge_add_cached(r, tbl[d - 1]);
+    else if (d < 0) r = ge_add_cached(r, ge_cached_neg(tbl[-d - 1]));
   }
   return r;
 }
@@ -260,25 +310,32 @@ Ge ge_base() {
   }();
   return b;
 }
-// fixed-base table for B: 64 windows x 16 entries
+// fixed-base table for B: 64 signed radix-16 windows x 8 cached multiples (d * 16^w * B, d = 1..8)
 struct BaseTable {
-  std::vector<Ge> t;
+  std::vector<GeCached> t;
   BaseTable() {
-    t.resize(64 * 16);
+    t.resize(64 * 8);
     Ge base = ge_base();
     for (int w = 0; w < 64; ++w) {
-      t[w * 16] = ge_identity();
-      for (int d = 1; d < 16; ++d) t[w * 16 + d] = ge_add(t[w * 16 + d - 1], base);
+      Ge acc = base;
+      for (int d = 0; d < 8; ++d) {
+        t[w * 8 + d] = ge_cache(acc);
+        acc = ge_add_cached(acc, t[w * 8]);
+      }
       for (int i = 0; i < 4; ++i) base = ge_dbl(base);
     }
   }
 };
+// no doublings at all: one cached addition per non-zero digit
 Ge ge_mul_base(const u8 k[32]) {
   static const BaseTable bt;
+  int8_t e[64];
+  signed_digits(e, k);
   Ge r = ge_identity();
   for (int w = 0; w < 64; ++w) {
-    int d = (k[w >> 1] >> ((w & 1) * 4)) & 15;
-    if (d) r = ge_add(r, bt.t[w * 16 + d]);
+    const int d = e[w];
+    if (d > 0) r = ge_add_cached(r, bt.t[w * 8 + d - 1]);
+    else if (d < 0) r = ge_add_cached(r, ge_cached_neg(bt.t[w * 8 - d - 1]));
   }
   return r;
 }
@@ -289,6 +346,21 @@ Bytes ge_tobytes(const Ge& p) {
   fe_tobytes(out.data(), y);
   if (fe_isneg(x)) out[31] |= 0x80;
   return out;
+}
+// encode several points with ONE field inversion (Montgomery's trick)
+void ge_tobytes_batch(const Ge* const* pts, int n, Bytes* out) {
+  Fe pre[8];
+  Fe acc = fe_one();
+  for (int i = 0; i < n; ++i) { pre[i] = acc; acc = fe_mul(acc, pts[i]->Z); }
+  Fe inv = fe_invert(acc);
+  for (int i = n - 1; i >= 0; --i) {
+    Fe zi = fe_mul(inv, pre[i]);
+    inv = fe_mul(inv, pts[i]->Z);
+    Fe x = fe_mul(pts[i]->X, zi), y = fe_mul(pts[i]->Y, zi);
+    out[i].assign(32, 0);
+    fe_tobytes(out[i].data(), y);
+    if (fe_isneg(x)) out[i][31] |= 0x80;
+  }
 }
 bool ge_frombytes(Ge& out, const u8 in[32]) {
   // RFC 8032 5.1.3: reject non-canonical y
@@ -433,10 +505,28 @@ Bytes ed25519_public_from_seed(const Bytes& seed32) {
 }
 
 VrfKey VrfKey::from_seed(const Bytes& seed32) {
+  if (seed32.size() != 32) fail("ed25519: seed must be 32 bytes");
   VrfKey k;
   k.seed = seed32;
-  k.pk = ed25519_public_from_seed(seed32);
+  clamp_secret(seed32, k.x, k.prefix);
+  k.pk = ge_tobytes(ge_mul_base(k.x));
   return k;
+}
+
+const VrfKey& VrfKey::cached(const Bytes& seed32) {
+  static std::mutex mu;
+  static std::unordered_map<std::string, std::unique_ptr<VrfKey>> cache;
+  std::string key(seed32.begin(), seed32.end());
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return *it->second;
+  }
+  auto k = std::make_unique<VrfKey>(from_seed(seed32));
+  std::lock_guard<std::mutex> lk(mu);
+  auto& slot = cache[key];
+  if (!slot) slot = std::move(k);
+  return *slot;
 }
 
 Bytes vrf_proof_to_hash(const Bytes& pi) {
@@ -455,7 +545,7 @@ Bytes vrf_proof_to_hash(const Bytes& pi) {
   return out;
 }
 
-static Bytes gamma_to_hash(const Ge& Gamma) {
+[[maybe_unused]] static Bytes gamma_to_hash(const Ge& Gamma) {
   Ge G8 = ge_dbl(ge_dbl(ge_dbl(Gamma)));
   Sha512 h;
   u8 pre[2] = {SUITE, 0x03};
@@ -469,26 +559,38 @@ static Bytes gamma_to_hash(const Ge& Gamma) {
 }
 
 std::pair<Bytes, Bytes> vrf_prove(const VrfKey& key, const Bytes& alpha) {
-  u8 x[32], prefix[32];
-  clamp_secret(key.seed, x, prefix);
+  const u8* x = key.x;
   Ge H = encode_to_curve(key.pk, alpha);
   Bytes hstr = ge_tobytes(H);
   Ge Gamma = ge_mul(H, x);
   Sha512 kh;
-  kh.update(prefix, 32);
+  kh.update(key.prefix, 32);
   kh.update(hstr);
   u8 kd[64];
   kh.final(kd);
   u8 k[32];
   sc_reduce(k, kd, 64);
-  Bytes gstr = ge_tobytes(Gamma);
-  Bytes c = challenge_str(key.pk, hstr, gstr, ge_tobytes(ge_mul_base(k)), ge_tobytes(ge_mul(H, k)));
+  // Gamma, k*B, k*H and 8*Gamma (for beta) share one inversion
+  Ge U = ge_mul_base(k), V = ge_mul(H, k);
+  Ge G8 = ge_dbl(ge_dbl(ge_dbl(Gamma)));
+  const Ge* pts[4] = {&Gamma, &U, &V, &G8};
+  Bytes enc[4];
+  ge_tobytes_batch(pts, 4, enc);
+  Bytes c = challenge_str(key.pk, hstr, enc[0], enc[1], enc[2]);
   u8 s[32];
   sc_muladd(s, k, c.data(), 16, x);
-  Bytes pi = gstr;
+  Bytes pi = enc[0];
   pi.insert(pi.end(), c.begin(), c.end());
   pi.insert(pi.end(), s, s + 32);
-  return {gamma_to_hash(Gamma), pi};
+  Sha512 bh;
+  u8 pre[2] = {SUITE, 0x03};
+  bh.update(pre, 2);
+  bh.update(enc[3]);
+  u8 z = 0;
+  bh.update(&z, 1);
+  Bytes beta(64);
+  bh.final(beta.data());
+  return {beta, pi};
 }
 
 bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* beta) {

@@ -13,9 +13,13 @@
 namespace bsc {
 
 struct VrfKey {
-  Bytes seed;  // 32-byte secret seed
-  Bytes pk;    // 32-byte encoded public key
+  Bytes seed;        // 32-byte secret seed
+  Bytes pk;          // 32-byte encoded public key
+  uint8_t x[32];     // clamped secret scalar (SHA-512(seed)[0:32])
+  uint8_t prefix[32];  // nonce prefix (SHA-512(seed)[32:64])
   static VrfKey from_seed(const Bytes& seed32);
+  // process-wide cache: keys are derived once per seed (peers prove every round)
+  static const VrfKey& cached(const Bytes& seed32);
 };
 
 // Returns (beta = 64-byte output, pi = 80-byte proof).

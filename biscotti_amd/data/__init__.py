@@ -26,6 +26,10 @@ import numpy as np
 
 FILES = Path(__file__).resolve().parent / "files"
 TRAIN_CUT = 0.8
+# Augmentation strength, calibrated so a multinomial logistic regression (sklearn, full batch)
+# reaches ~92% test accuracy, like real MNIST (measured 92.7% on 30% of the synthetic train set).
+ROT_DEG = 6.0
+SHIFT_PX = 1.25
 
 
 def standardize_cols(X, mu=None, sigma=None):
@@ -65,16 +69,16 @@ def synthetic_mnist(n_train: int = 60000, n_test: int = 10000, seed: int = 1234)
         img = F.interpolate(img, size=(20, 20), mode="bilinear", align_corners=False)
         canvas = torch.zeros((m, 1, 28, 28))
         canvas[:, :, 4:24, 4:24] = img
-        ang = (torch.rand(m, generator=g) - 0.5) * (2 * math.pi * 12 / 360)
+        ang = (torch.rand(m, generator=g) - 0.5) * (2 * math.pi * ROT_DEG / 360)
         scl = 1.0 + (torch.rand(m, generator=g) - 0.5) * 0.2
-        shift = (torch.rand(m, 2, generator=g) - 0.5) * (4.0 / 14.0)
+        shift = (torch.rand(m, 2, generator=g) - 0.5) * (2 * SHIFT_PX / 14.0)
         cos, sin = torch.cos(ang) / scl, torch.sin(ang) / scl
         theta = torch.stack([torch.stack([cos, -sin, shift[:, 0]], 1), torch.stack([sin, cos, shift[:, 1]], 1)], 1)
         grid = F.affine_grid(theta, (m, 1, 28, 28), align_corners=False)
         warped = F.grid_sample(canvas, grid, mode="bilinear", padding_mode="zeros", align_corners=False)
-        thick = 0.8 + 0.6 * torch.rand(m, 1, 1, 1, generator=g)
+        thick = 0.9 + 0.3 * torch.rand(m, 1, 1, 1, generator=g)
         warped = torch.clamp(warped * thick, 0, 1)
-        noise = torch.rand(warped.shape, generator=g) * 0.08
+        noise = torch.rand(warped.shape, generator=g) * 0.04
         warped = torch.clamp(warped + noise * (warped > 0.05), 0, 1)
         out[s:s + m] = (warped * 255.0).reshape(m, -1)
     y = labels[pick].numpy()

@@ -19,6 +19,7 @@ SIGNATURES = {
     "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, P, P, P],
     "bsc_sum_rows": [P, I, P, I, P, I, P, P],
     "bsc_segment_sum": [P, I, I, I, I, P, P],
+    "bsc_sum_rows2": [P, I, P, I, P, I, P, P],
     "bsc_marshal": [P, I, P, P],
     "bsc_to_affine": [P, I, P, P],
     # ml.hip

@@ -123,9 +123,16 @@ def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | 
     if cols is not None:
         assert cols.dtype == torch.int32 and (ncols == 0 or int(cols.max()) < Cn)
     out = torch.empty((ncols, 24), dtype=torch.int32, device=pts.device)
-    _check(hip().bsc_sum_rows(_ptr(pts), Cn, _ptr(rows), nrows, _ptr(cols), ncols, _ptr(out), _stream()),
-           "sum_rows")
+    _check(hip().bsc_sum_rows2(_ptr(pts), Cn, _ptr(rows), nrows, _ptr(cols), ncols, _ptr(out), _stream()),
+           "sum_rows2")
     return out
+
+
+def marshal_host(pts: torch.Tensor) -> "np.ndarray":
+    """Jacobian [..., 24] on device -> kyber marshals uint8 [N, 64] on host, normalised with a single
+    field inversion (Montgomery's batch trick) instead of one latency-bound inversion per point."""
+    flat = pts.reshape(-1, 24).contiguous().cpu().numpy().view(np.uint32)
+    return rt().g1_marshal_jac_batch(flat)
 
 
 def marshal(pts: torch.Tensor) -> torch.Tensor:

@@ -194,7 +194,7 @@ def krum(X, groupsize: int, n_accept: int, ksplit: int = 512):
     if n == 0:
         return torch.zeros(0, dtype=torch.bool), torch.zeros(0, dtype=torch.float64)
     if X.device.type == "cuda":
-        assert n <= 256, "krum kernel handles up to 256 updates per verifier"
+        assert n <= 128, "krum kernel handles up to 128 updates per verifier"
         tiles = (n + 15) // 16
         nsplit = (D + ksplit - 1) // ksplit
         part = torch.empty((nsplit, tiles * 16, tiles * 16), dtype=torch.float64, device=X.device)

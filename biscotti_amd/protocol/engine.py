@@ -24,6 +24,7 @@ the native :class:`RoundFSM`, replicated identically on every rank.
 from __future__ import annotations
 
 import hashlib
+from concurrent.futures import ThreadPoolExecutor
 import time
 from dataclasses import dataclass, field
 
@@ -96,13 +97,14 @@ class DeviceCrypto:
         self.eng = B.DeviceCommitEngine(key, poly, T, device)
         self.d, self.poly, self.T, self.nchunks = self.eng.d, poly, T, self.eng.nchunks
 
-    def commitments_dev(self, qdelta: torch.Tensor) -> torch.Tensor:
+    def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
+        """Fixed-base MSM on device, one batch-normalised marshal on host -> uint8 [n, 64]."""
         n = qdelta.shape[0]
         if n == 0:
-            return torch.zeros((0, 64), dtype=torch.uint8, device=qdelta.device)
+            return np.zeros((0, 64), np.uint8)
         rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
         pts, _ = self.eng.shares(qdelta, rows, commit_only=True)
-        return B.marshal(self.eng.commitments(pts))
+        return B.marshal_host(self.eng.commitments(pts))
 
     def shares(self, qdelta: torch.Tensor):
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
@@ -182,6 +184,7 @@ class BiscottiEngine:
         self.sigma = self.task.noise_sigma(cfg.epsilon)
         self.stats = {"unmasked_updates": 0, "total_updates": 0}
         self.rounds_done = 0
+        self._host = ThreadPoolExecutor(max_workers=1, thread_name_prefix="bsc-host")
 
     # ------------------------------------------------------------------ helpers
     def _now(self, iteration: int) -> int:
@@ -236,24 +239,26 @@ class BiscottiEngine:
             latest_hash = fsm.chain.latest().hash
             workers = [w for w in plan.workers if live[w]]
             local_workers = [w for w in workers if w in self.local]
-            # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100)
+            # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  The host
+            # proofs run on a side thread (the native prover drops the GIL) while the GPU does the
+            # local step and the commitments; the noise phase joins them.
             seeds = [self.vrf_noise_seed[w] for w in local_workers]
-            outs = R.vrf_prove_batch(seeds, latest_hash, cfg.host_threads) if seeds else []
             stake = dict(fsm.stake)
-            noisers = {w: R.select_noisers(stake, beta, w, cfg.num_noisers, self.N)
-                       for w, (beta, _) in zip(local_workers, outs)}
+            fut_noise = self._host.submit(R.vrf_prove_batch, seeds, latest_hash, cfg.host_threads) \
+                if seeds else None
+            fut_roles = None
             if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
-                R.vrf_prove_batch([self.vrf_roles_seed[p] for p in self.local if live[p]], latest_hash,
-                                  cfg.host_threads)
+                fut_roles = self._host.submit(R.vrf_prove_batch, [self.vrf_roles_seed[p] for p in self.local
+                                                                  if live[p]], latest_hash, cfg.host_threads)
         # ---------------------------------------------------------------- local step + commitments
         with tm.phase("local_step"):
             delta, qdelta = self.task.step(self.W, it, local_workers)
         with tm.phase("commit"):
-            if self.gpu:
-                comm_dev = self.crypto.commitments_dev(qdelta)
-                commits_local = comm_dev.cpu().numpy()
-            else:
-                commits_local = self.crypto.commitments(qdelta)
+            commits_local = self.crypto.commitments(qdelta)
+        with tm.phase("vrf_join"):
+            outs = fut_noise.result() if fut_noise is not None else []
+            noisers = {w: R.select_noisers(stake, beta, w, cfg.num_noisers, self.N)
+                       for w, (beta, _) in zip(local_workers, outs)}
         with tm.phase("noise"):
             if cfg.noising and self.sigma > 0 and local_workers:
                 nz = torch.tensor([noisers[w] for w in local_workers], dtype=torch.int32, device=self.dev)
@@ -349,6 +354,8 @@ class BiscottiEngine:
             self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
         with tm.phase("eval"):
             ev = self.task.evaluate(self.W)
+            if fut_roles is not None:
+                fut_roles.result()
         self.stats["total_updates"] += len(block.data.deltas)
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=len(block.data.deltas) == 0,
                           node_list=self._last_nodes, approved=list(approved), verifiers=list(plan.verifiers),
@@ -444,23 +451,33 @@ class BiscottiEngine:
         with tm.phase("miner_aggregate"):
             nc = len(contributing)
             agg_y = torch.zeros((nc, nch, spm), dtype=torch.int64, device=self.dev)
-            for ci, m in enumerate(contributing):
-                if m not in self.local:
-                    continue
-                p_, y_, rows = recv[m]
-                part = part_of[m]
-                if rows is not None:  # single rank: aggregate straight out of the share tensors
-                    cols = torch.tensor([k * (T + 1) + c for k in range(nch) for c in cols_of(part)],
-                                        dtype=torch.long, device=self.dev)
-                    flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-                    if self.gpu:
-                        _ = B.sum_rows(flat, rows.int(), cols.int())  # aggregateSecret: witnesses + commitments
-                    else:
+            if single and self.gpu and contributing:
+                # aggregateSecret for every miner in ONE launch: the rows (contributing workers) are
+                # shared, the column list concatenates each miner's witness + commitment slots
+                rows = recv[contributing[0]][2]
+                base = np.arange(nch)[:, None] * (T + 1)
+                cols = np.concatenate([(base + np.asarray(cols_of(part_of[m]))[None, :]).reshape(-1)
+                                       for m in contributing])
+                flat = pts.view(pts.shape[0], nch * (T + 1), pw)
+                _ = B.sum_rows(flat, rows.int(), torch.from_numpy(cols.astype(np.int32)).to(self.dev))
+                ysum = ys.index_select(0, rows).sum(0)   # [nch, T]
+                for ci, m in enumerate(contributing):
+                    agg_y[ci] = ysum[:, spm * part_of[m]: spm * part_of[m] + spm]
+            else:
+                for ci, m in enumerate(contributing):
+                    if m not in self.local:
+                        continue
+                    p_, y_, rows = recv[m]
+                    part = part_of[m]
+                    if rows is not None:  # single rank (CPU): aggregate straight out of the share tensors
+                        cols = torch.tensor([k * (T + 1) + c for k in range(nch) for c in cols_of(part)],
+                                            dtype=torch.long, device=self.dev)
+                        flat = pts.view(pts.shape[0], nch * (T + 1), pw)
                         _ = self.crypto.sum_rows(flat.index_select(0, rows).index_select(1, cols))
-                    agg_y[ci] = ys.index_select(0, rows)[:, :, spm * part: spm * part + spm].sum(0)
-                else:
-                    _ = self.crypto.sum_rows(p_.reshape(p_.shape[0], -1, pw))
-                    agg_y[ci] = y_.sum(0)
+                        agg_y[ci] = ys.index_select(0, rows)[:, :, spm * part: spm * part + spm].sum(0)
+                    else:
+                        _ = self.crypto.sum_rows(p_.reshape(p_.shape[0], -1, pw))
+                        agg_y[ci] = y_.sum(0)
         with tm.phase("recover"):
             agg_all = agg_y[None] if single else comm.all_gather(agg_y)   # [world, nc, nch, spm]
             leader_rank = comm.owner(plan.leader, self.N)

@@ -179,3 +179,47 @@ def test_vrf_properties(rt):
     assert other != beta
     batch = rt.vrf_prove_batch([seed, bytes(32)], b"block-hash", 2)
     assert batch[0] == (beta, pi) and batch[1][0] == other
+
+
+def test_marshal_jac_batch_matches_single(rt):
+    """Batch normalisation (one inversion via Montgomery's trick) == per-point marshal, incl. infinity."""
+    import random
+
+    import numpy as np
+
+    p = 65000549695646603732796438742359905742825358107623003571877145026864184071783
+    R = 1 << 256
+    rng = random.Random(5)
+    rows, want = [], []
+    for k in [3, 17, 1 << 40, 99991, 5]:
+        m = rt.g1_base_mul(k)
+        aff = np.asarray(rt.g1_affine_mont_u32(m), dtype=np.uint32).reshape(-1)
+        to_int = lambda a: sum(int(v) << (32 * i) for i, v in enumerate(a))
+        xm, ym = to_int(aff[:8]), to_int(aff[8:16])
+        z = rng.randrange(1, p)
+        x, y = xm * pow(R, -1, p) % p, ym * pow(R, -1, p) % p
+        X, Y = x * z * z % p, y * z * z * z % p
+        limbs = lambda v: [(v * R % p >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
+        rows.append(limbs(X) + limbs(Y) + limbs(z))
+        want.append(m)
+    rows.insert(2, [0] * 24)  # point at infinity (z == 0)
+    want.insert(2, rt.g1_infinity())
+    got = rt.g1_marshal_jac_batch(np.asarray(rows, dtype=np.uint32))
+    assert got.shape == (6, 64)
+    for g, w in zip(got, want):
+        assert bytes(g) == (w if len(w) == 64 else bytes(64))
+    single = rt.g1_marshal_jac_u32(np.asarray(rows, dtype=np.uint32))
+    assert [bytes(g) for g in got] == [s if len(s) == 64 else bytes(64) for s in single]
+
+
+def test_ecvrf_rfc9381_vector(rt):
+    """RFC 9381 ECVRF-EDWARDS25519-SHA512-TAI example (SK = RFC 8032 test 1, alpha = empty)."""
+    seed = bytes.fromhex("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60")
+    beta, pi = rt.vrf_prove(seed, b"")
+    assert pi.hex() == ("8657106690b5526245a92b003bb079ccd1a92130477671f6fc01ad16f26f723f26f8a57ccaed74ee1b190b"
+                        "ed1f479d9727d2d0f9b005a6e456a35d4fb0daab1268a1b0db10836d9826a528ca76567805")
+    assert beta.hex() == ("90cf1df3b703cce59e2a35b925d411164068269d7b2d29f3301c03dd757876ff66b71dda49d2de59d0345"
+                          "0451af026798e8f81cd2e333de5cdf4f3e140fdd8ae")
+    assert rt.vrf_verify(rt.vrf_public_key(seed), b"", pi) == beta
+    # batched prover (thread pool + key cache) agrees
+    assert rt.vrf_prove_batch([seed] * 3, b"", 3) == [(beta, pi)] * 3
