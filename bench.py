@@ -43,6 +43,10 @@ def main() -> int:
     from biscotti_amd.protocol.engine import BiscottiEngine
 
     comm = Comm.init()
+    if comm.device.type == "cuda":
+        # the GPU path does little CPU tensor work; idle-spinning OpenMP workers would only steal the
+        # cgroup CPU quota from the native crypto pool
+        torch.set_num_threads(min(4, torch.get_num_threads()))
     cfg = RunConfig(num_nodes=a.peers, dataset=a.dataset, seed=a.seed, max_iterations=10**9,
                     trace_file=a.trace, host_threads=16)
     eng = BiscottiEngine(cfg, comm)

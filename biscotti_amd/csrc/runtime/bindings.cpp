@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <future>
 #include <thread>
 
 #include "bn256.hpp"
@@ -128,6 +129,21 @@ static void parallel_for(size_t n, int threads, F f) {
   std::function<void(size_t)> fn = f;
   pool().run(n, threads, fn);
 }
+
+struct VrfJob {
+  std::vector<Bytes> seeds;
+  Bytes alpha;
+  std::vector<std::pair<Bytes, Bytes>> out;
+  std::string error;
+  std::atomic<bool> finished{false};
+  std::promise<void> done_p;
+  std::shared_future<void> done = done_p.get_future().share();
+  std::shared_ptr<VrfJob> after;  // run only once this job has finished (keeps the pool to one job)
+  std::thread th;
+  ~VrfJob() {
+    if (th.joinable()) th.join();
+  }
+};
 
 struct CommitKey {
   std::vector<G1> pk;
@@ -328,6 +344,42 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     for (auto& o : out) r.append(py::make_tuple(P(o.first), P(o.second)));
     return r;
   });
+  // Asynchronous batch: proving starts on a native thread immediately (no GIL hand-off, so it
+  // overlaps with the caller's GPU work from the first microsecond); result() joins.
+  py::class_<VrfJob, std::shared_ptr<VrfJob>>(m, "VrfJob")
+      .def("done", [](VrfJob& j) { return j.finished.load(); })
+      .def("result", [](VrfJob& j) {
+        {
+          py::gil_scoped_release rel;
+          j.done.wait();
+        }
+        if (!j.error.empty()) throw std::runtime_error(j.error);
+        py::list r;
+        for (auto& o : j.out) r.append(py::make_tuple(P(o.first), P(o.second)));
+        return r;
+      });
+  m.def("vrf_prove_batch_async", [](std::vector<py::bytes> seeds, py::bytes alpha, int threads,
+                                    std::shared_ptr<VrfJob> after) {
+    auto job = std::make_shared<VrfJob>();
+    job->after = std::move(after);
+    for (auto& s : seeds) job->seeds.push_back(B(s));
+    job->alpha = B(alpha);
+    job->out.resize(job->seeds.size());
+    VrfJob* jp = job.get();
+    job->th = std::thread([jp, threads] {
+      if (jp->after) jp->after->done.wait();
+      try {
+        parallel_for(jp->seeds.size(), threads,
+                     [&](size_t i) { jp->out[i] = vrf_prove(VrfKey::cached(jp->seeds[i]), jp->alpha); });
+      } catch (const std::exception& e) {
+        jp->error = e.what();
+      }
+      jp->finished.store(true);
+      jp->after.reset();
+      jp->done_p.set_value();
+    });
+    return job;
+  }, py::arg("seeds"), py::arg("alpha"), py::arg("threads"), py::arg("after") = nullptr);
 
   // ---------------------------------------------------------------- keys
   py::class_<CommitKey>(m, "CommitKey")

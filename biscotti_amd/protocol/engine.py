@@ -24,7 +24,6 @@ the native :class:`RoundFSM`, replicated identically on every rank.
 from __future__ import annotations
 
 import hashlib
-from concurrent.futures import ThreadPoolExecutor
 import time
 from dataclasses import dataclass, field
 
@@ -184,7 +183,6 @@ class BiscottiEngine:
         self.sigma = self.task.noise_sigma(cfg.epsilon)
         self.stats = {"unmasked_updates": 0, "total_updates": 0}
         self.rounds_done = 0
-        self._host = ThreadPoolExecutor(max_workers=1, thread_name_prefix="bsc-host")
 
     # ------------------------------------------------------------------ helpers
     def _now(self, iteration: int) -> int:
@@ -244,12 +242,11 @@ class BiscottiEngine:
             # local step and the commitments; the noise phase joins them.
             seeds = [self.vrf_noise_seed[w] for w in local_workers]
             stake = dict(fsm.stake)
-            fut_noise = self._host.submit(R.vrf_prove_batch, seeds, latest_hash, cfg.host_threads) \
-                if seeds else None
+            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads) if seeds else None
             fut_roles = None
             if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
-                fut_roles = self._host.submit(R.vrf_prove_batch, [self.vrf_roles_seed[p] for p in self.local
-                                                                  if live[p]], latest_hash, cfg.host_threads)
+                fut_roles = R.vrf_prove_batch_async([self.vrf_roles_seed[p] for p in self.local if live[p]],
+                                                    latest_hash, cfg.host_threads, fut_noise)
         # ---------------------------------------------------------------- local step + commitments
         with tm.phase("local_step"):
             delta, qdelta = self.task.step(self.W, it, local_workers)

@@ -223,3 +223,14 @@ def test_ecvrf_rfc9381_vector(rt):
     assert rt.vrf_verify(rt.vrf_public_key(seed), b"", pi) == beta
     # batched prover (thread pool + key cache) agrees
     assert rt.vrf_prove_batch([seed] * 3, b"", 3) == [(beta, pi)] * 3
+
+
+def test_vrf_async_jobs_match_sync(rt):
+    import os
+
+    seeds = [os.urandom(32) for _ in range(20)]
+    j1 = rt.vrf_prove_batch_async(seeds, b"alpha", 4)
+    j2 = rt.vrf_prove_batch_async(seeds[:5], b"beta", 4, j1)  # chained: starts after j1
+    assert j2.result() == rt.vrf_prove_batch(seeds[:5], b"beta", 1)
+    assert j1.done() and j1.result() == rt.vrf_prove_batch(seeds, b"alpha", 3)
+    assert rt.vrf_prove_batch_async([], b"x", 4).result() == []
