@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <chrono>
 #include <future>
 #include <thread>
 
@@ -140,6 +141,7 @@ struct VrfJob {
   std::shared_future<void> done = done_p.get_future().share();
   std::shared_ptr<VrfJob> after;  // run only once this job has finished (keeps the pool to one job)
   std::thread th;
+  std::chrono::steady_clock::time_point t_submit, t_start, t_end;
   ~VrfJob() {
     if (th.joinable()) th.join();
   }
@@ -348,6 +350,10 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   // overlaps with the caller's GPU work from the first microsecond); result() joins.
   py::class_<VrfJob, std::shared_ptr<VrfJob>>(m, "VrfJob")
       .def("done", [](VrfJob& j) { return j.finished.load(); })
+      .def("timing_us", [](VrfJob& j) {  // (submit -> start, start -> end), valid after result()
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        return py::make_tuple(us(j.t_submit, j.t_start), us(j.t_start, j.t_end));
+      })
       .def("result", [](VrfJob& j) {
         {
           py::gil_scoped_release rel;
@@ -366,14 +372,17 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     job->alpha = B(alpha);
     job->out.resize(job->seeds.size());
     VrfJob* jp = job.get();
+    job->t_submit = std::chrono::steady_clock::now();
     job->th = std::thread([jp, threads] {
       if (jp->after) jp->after->done.wait();
+      jp->t_start = std::chrono::steady_clock::now();
       try {
         parallel_for(jp->seeds.size(), threads,
                      [&](size_t i) { jp->out[i] = vrf_prove(VrfKey::cached(jp->seeds[i]), jp->alpha); });
       } catch (const std::exception& e) {
         jp->error = e.what();
       }
+      jp->t_end = std::chrono::steady_clock::now();
       jp->finished.store(true);
       jp->after.reset();
       jp->done_p.set_value();
@@ -605,6 +614,14 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   });
   m.def("select_noisers", [](const std::map<i64, i64>& stake, py::bytes out, i64 self, i64 nn, i64 n) {
     return select_noisers(stake, B(out), self, nn, n);
+  });
+  m.def("select_noisers_batch", [](const std::map<i64, i64>& stake, std::vector<py::bytes> outs,
+                                   std::vector<i64> selfs, i64 nn, i64 n) {
+    if (outs.size() != selfs.size()) throw std::runtime_error("outs/selfs length mismatch");
+    std::vector<std::vector<i64>> r;
+    r.reserve(outs.size());
+    for (size_t k = 0; k < outs.size(); ++k) r.push_back(select_noisers(stake, B(outs[k]), selfs[k], nn, n));
+    return r;
   });
   m.def("krum_scores", [](py::array_t<double, py::array::c_style | py::array::forcecast> X, i64 groupsize) {
     if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");

@@ -21,27 +21,31 @@ void ProtocolConfig::derive() {
 
 // ------------------------------------------------------------------ lottery
 Lottery::Lottery(const std::map<i64, i64>& stake, i64 total, const Bytes& in) : input(in) {
+  i64 acc = 0;
   for (i64 id = 0; id < total; ++id) {
     auto it = stake.find(id);
-    i64 s = it == stake.end() ? 0 : it->second;
-    for (i64 k = 0; k < s; ++k) tickets.push_back(id);
+    const i64 s = it == stake.end() ? 0 : it->second;
+    if (s <= 0) continue;
+    acc += s;
+    ids.push_back(id);
+    cum.push_back(acc);
   }
-  if (tickets.empty()) fail("lottery: no stake");
+  if (ids.empty()) fail("lottery: no stake");
+}
+i64 Lottery::ticket(i64 idx) const {
+  return ids[size_t(std::upper_bound(cum.begin(), cum.end(), idx) - cum.begin())];
 }
 i64 Lottery::draw() {
   if (i + 1 >= input.size()) {
     input = Sha256::digest(input);
     i = 0;
   }
-  size_t idx = (size_t(input[i]) * 256 + size_t(input[i + 1])) % tickets.size();
+  const i64 idx = i64((size_t(input[i]) * 256 + size_t(input[i + 1])) % size_t(total()));
   ++i;
-  return tickets[idx];
+  return ticket(idx);
 }
 
-static size_t distinct_holders(const Lottery& l) {
-  std::set<i64> s(l.tickets.begin(), l.tickets.end());
-  return s.size();
-}
+static size_t distinct_holders(const Lottery& l) { return l.ids.size(); }
 
 void select_roles(const std::map<i64, i64>& stake, const Bytes& hash, i64 nv, i64 na, i64 n,
                   std::vector<i64>* verifiers, std::vector<i64>* miners) {
@@ -62,9 +66,8 @@ void select_roles(const std::map<i64, i64>& stake, const Bytes& hash, i64 nv, i6
 
 std::vector<i64> select_noisers(const std::map<i64, i64>& stake, const Bytes& out, i64 self, i64 nn, i64 n) {
   Lottery l(stake, n, out);
-  std::set<i64> holders(l.tickets.begin(), l.tickets.end());
-  holders.erase(self);
-  if (i64(holders.size()) < nn) fail("lottery: not enough peers for noisers");
+  const i64 others = i64(l.ids.size()) - (std::binary_search(l.ids.begin(), l.ids.end(), self) ? 1 : 0);
+  if (others < nn) fail("lottery: not enough peers for noisers");
   std::set<i64> seen;
   std::vector<i64> res;
   while (i64(res.size()) < nn) {

@@ -52,11 +52,15 @@ struct ProtocolConfig {
 };
 
 // Stake lottery over 2-byte windows of `input`, SHA-256 re-hash when exhausted (vrf.go).
+// The reference materialises one ticket per stake unit (its list grows by 5 per contribution
+// every round); the same draw is an upper_bound over stake prefix sums: O(n) memory, O(log n).
 struct Lottery {
-  std::vector<i64> tickets;
+  std::vector<i64> ids, cum;  // holders with stake > 0 (ascending id) and inclusive prefix sums
   Bytes input;
   size_t i = 0;
   Lottery(const std::map<i64, i64>& stake, i64 total_nodes, const Bytes& in);
+  i64 total() const { return cum.empty() ? 0 : cum.back(); }
+  i64 ticket(i64 idx) const;  // owner of ticket #idx in the reference's list order
   i64 draw();
 };
 void select_roles(const std::map<i64, i64>& stake, const Bytes& block_hash, i64 nv, i64 na, i64 n,

@@ -254,8 +254,9 @@ class BiscottiEngine:
             commits_local = self.crypto.commitments(qdelta)
         with tm.phase("vrf_join"):
             outs = fut_noise.result() if fut_noise is not None else []
-            noisers = {w: R.select_noisers(stake, beta, w, cfg.num_noisers, self.N)
-                       for w, (beta, _) in zip(local_workers, outs)}
+            sel = R.select_noisers_batch(stake, [beta for beta, _ in outs], local_workers, cfg.num_noisers,
+                                         self.N) if outs else []
+            noisers = dict(zip(local_workers, sel))
         with tm.phase("noise"):
             if cfg.noising and self.sigma > 0 and local_workers:
                 nz = torch.tensor([noisers[w] for w in local_workers], dtype=torch.int32, device=self.dev)
