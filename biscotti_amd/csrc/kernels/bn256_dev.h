@@ -173,7 +173,7 @@ __device__ inline jac jac_dbl(const jac& p) {
 }
 
 // add-2007-bl, complete for the special cases (P==Q, P==-Q, infinities)
-__device__ inline jac jac_add(const jac& p, const jac& q) {
+__device__ __forceinline__ jac jac_add(const jac& p, const jac& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   fp z1z1 = fp_sqr(p.z);

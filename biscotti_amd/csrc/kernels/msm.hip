@@ -23,7 +23,28 @@ using namespace bn;
 
 namespace {
 
-constexpr int TBL_ENTRIES = 128;  // signed 8-bit digits
+constexpr int TBL_ENTRIES = 128;  // entries of an 8-bit signed window
+
+// Window plan of every fixed-base table: window 0 is B0 bits wide (2^(B0-1) entries: signed digits
+// |d| <= 2^(B0-1)), windows 1..NW-1 are 8 bits (128 entries).  Per base the entries are laid out
+// window 0 first, then 128 per further window; entry (w, |d|) of a base is entry index
+//   w == 0 ? |d| - 1 : E0 + (w - 1) * 128 + |d| - 1,   E0 = 2^(B0-1).
+// A wide first window turns the typical quantised update coefficient (|q| < 2^13) into ONE mixed
+// addition instead of two: HBM is spent (tens of GB of tables) to halve the MSM arithmetic.
+__device__ __forceinline__ int win_bits(int w, int B0) { return w ? 8 : B0; }
+__device__ __forceinline__ int win_entry(int w, int ad, int E0) { return (w ? E0 + (w - 1) * TBL_ENTRIES : 0) + ad - 1; }
+// next signed digit of width `bits` from (m, carry); digits lie in (-2^(bits-1), 2^(bits-1)]
+__device__ __forceinline__ int recode(unsigned long long& m, int& carry, int bits) {
+  int dg = (int)(m & ((1ull << bits) - 1)) + carry;
+  m >>= bits;
+  if (dg > (1 << (bits - 1))) {
+    dg -= 1 << bits;
+    carry = 1;
+  } else {
+    carry = 0;
+  }
+  return dg;
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   // bijective: blocks that share an XCD (bid % 8) get a contiguous logical range
@@ -98,16 +119,26 @@ extern "C" __global__ void __launch_bounds__(128) k_witness_bases(const uint32_t
 }
 
 // ------------------------------------------------------------------ fixed-base tables
-// Thread per (base b, window w).  base index b = outer * inner + in; entry (b, w, k) is stored at
-//   table + 16 * (outer * s_outer + w * s_w + (k-1) * s_k + in * s_in)
-// scratch: per thread 128 x 32 u32 (Jacobian + running Z product), in the caller's chunk.
-extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb, int inner, int NW,
-                                      long long s_outer, long long s_w, long long s_k, long long s_in,
-                                      uint32_t* table, uint32_t* scratch) {
-  int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nb * NW) return;
-  const int bl = g / NW, w = g % NW;
+// Thread per (base b, run): a run is 128 consecutive entries of one window -- window 0 has
+// E0/128 runs, every 8-bit window one.  Run r of window w holds (128 r + k) * 2^shift_w * base,
+// k = 1..128, shift_0 = 0, shift_w = B0 + 8 (w - 1).  Base index b = outer * inner + in; entry e
+// of base b is stored at table + 16 * (outer * s_outer + e * s_e + in * s_in).
+// scratch: per thread 128 x 32 u32 (Jacobian + exclusive prefix product of the Z's).
+extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb,
+                                                           int inner, int B0, int NW, long long s_outer,
+                                                           long long s_e, long long s_in, uint32_t* table,
+                                                           uint32_t* scratch) {
+  const int E0 = 1 << (B0 - 1);
+  const int R0 = E0 / TBL_ENTRIES;
+  const int runs = R0 + NW - 1;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long long)nb * runs) return;
+  const int bl = (int)(g / runs), run = (int)(g % runs);
   const int b = b0 + bl;
+  const int w = run < R0 ? 0 : run - R0 + 1;
+  const int r = run < R0 ? run : 0;
+  const int shift = w ? B0 + 8 * (w - 1) : 0;
+  const int e0 = w ? E0 + (w - 1) * TBL_ENTRIES : r * TBL_ENTRIES;
   jac P;
   if (bases_are_jac) {
     P = ld_jac(bases + 24 * (size_t)b);
@@ -115,9 +146,9 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
     aff a = ld_aff(bases + 16 * (size_t)b);
     P = jac_add_aff(jac_inf(), a);
   }
-  for (int i = 0; i < 8 * w; ++i) P = jac_dbl(P);
+  for (int i = 0; i < shift; ++i) P = jac_dbl(P);
   uint32_t* sc = scratch + (size_t)g * TBL_ENTRIES * 32;
-  jac acc = P;
+  jac acc = r ? jac_mul_small(P, r * TBL_ENTRIES + 1) : P;
   fp prod = fp_one();
   for (int k = 0; k < TBL_ENTRIES; ++k) {
     st_jac(sc + 32 * k, acc);
@@ -125,9 +156,9 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
     if (!jac_is_inf(acc)) prod = fp_mul(prod, acc.z);
     acc = jac_add(acc, P);
   }
-  fp inv = fp_inv(prod);  // Montgomery's trick: one inversion per (base, window)
+  fp inv = fp_inv(prod);  // Montgomery's trick: one inversion per run
   const int outer = b / inner, in = b % inner;
-  uint32_t* dst0 = table + 16 * (outer * s_outer + w * s_w + in * s_in);
+  uint32_t* dst0 = table + 16 * ((long long)outer * s_outer + (long long)e0 * s_e + (long long)in * s_in);
   for (int k = TBL_ENTRIES - 1; k >= 0; --k) {
     jac pt = ld_jac(sc + 32 * k);
     aff o;
@@ -141,18 +172,18 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
       o.x = fp_mul(pt.x, zi2);
       o.y = fp_mul(pt.y, fp_mul(zi2, zi));
     }
-    st_aff(dst0 + 16 * (k * s_k), o);
+    st_aff(dst0 + 16 * ((long long)k * s_e), o);
   }
 }
 
 // ------------------------------------------------------------------ fused shares + commitments
 // coeffs: int64 [*, d] (row stride d); rows: worker rows to process.
-// tbl_pk: [d][NW][128][16]; tbl_wb: [nchunks][J][NW][128][T][16].
+// tbl_pk: [d][PB][16]; tbl_wb: [nchunks][J][PB][T][16]; PB = E0 + (NW-1)*128 entries per base.
 // out_pts: Jacobian [nrows][nchunks][S][24] with S = T+1 (slots 0..T-1 witnesses, slot T the chunk
 // commitment) or S = 1 (commit_only: chunk commitments only).  out_y: int64 [nrows][nchunks][T].
 extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
-    int poly, int T, int NW, int commit_only, uint32_t* out_pts, long long* out_y) {
+    int poly, int T, int B0, int NW, int commit_only, uint32_t* out_pts, long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
   const long long total = (long long)nrows * nchunks * S;
@@ -171,9 +202,10 @@ extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
   const int J = poly - 1;
   const long long* c = coeffs + (size_t)row * d + prev;
 
-  const size_t pk_base_stride = (size_t)NW * TBL_ENTRIES * 16;
-  const size_t wb_w_stride = (size_t)TBL_ENTRIES * T * 16;
-  const size_t wb_j_stride = (size_t)NW * wb_w_stride;
+  const int E0 = 1 << (B0 - 1);
+  const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
+  const size_t pk_base_stride = PB * 16;
+  const size_t wb_j_stride = PB * T * 16;
   const uint32_t* wb_chunk = tbl_wb + (size_t)k * J * wb_j_stride;
 
   jac acc = jac_inf();
@@ -184,30 +216,20 @@ extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     const bool neg = cj < 0;
     unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
     const uint32_t* tb;
-    size_t kstride;
-    size_t wstride;
+    size_t estride;
     if (is_commit) {
       tb = tbl_pk + (size_t)(prev + j) * pk_base_stride;
-      kstride = 16;
-      wstride = (size_t)TBL_ENTRIES * 16;
+      estride = 16;
     } else {
       tb = wb_chunk + (size_t)(j - 1) * wb_j_stride + (size_t)slot * 16;
-      kstride = (size_t)T * 16;
-      wstride = wb_w_stride;
+      estride = (size_t)T * 16;
     }
     int carry = 0;
     for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
-      int dg = (int)(m & 0xFFull) + carry;
-      m >>= 8;
-      if (dg > 128) {
-        dg -= 256;
-        carry = 1;
-      } else {
-        carry = 0;
-      }
+      const int dg = recode(m, carry, win_bits(w, B0));
       if (dg == 0) continue;
       const int ad = dg < 0 ? -dg : dg;
-      aff q = ld_aff(tb + (size_t)w * wstride + (size_t)(ad - 1) * kstride);
+      aff q = ld_aff(tb + (size_t)win_entry(w, ad, E0) * estride);
       if ((dg < 0) != neg) q = aff_neg(q);
       acc = jac_add_aff(acc, q);
     }
@@ -221,6 +243,73 @@ extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     for (int j = L - 1; j >= 0; --j) y = y * (unsigned long long)x + (unsigned long long)c[j];
     out_y[((size_t)r * nchunks + k) * T + slot] = (long long)y;
   }
+}
+
+// ------------------------------------------------------------------ full-vector commitments
+// C_row = sum_i c_i PK[i] for whole rows (the commit phase: commitUpdate, kyber.go:533-559).
+// One 256-thread block per (row, 1024-coefficient slab):
+//   1. signed 8-bit digit decomposition of the slab into an LDS work list of NONZERO digits
+//      (table entry index | sign bit) -- lanes holding different coefficients would otherwise
+//      diverge on their different digit counts;
+//   2. every lane consumes the list round-robin (uniform mixed additions, no divergence);
+//   3. LDS tree over the 256 partial sums (the list's LDS is reused).
+// out_partial: Jacobian [nrows][nslab][24]; bsc_commit_rows finishes with a per-row segment sum.
+#define COMMIT_CB 1024
+extern "C" __global__ void __launch_bounds__(256) k_commit_rows(const long long* coeffs, int d, const int* rows,
+                                                               int nrows, const uint32_t* tbl_pk, int B0, int NW,
+                                                               uint32_t* out_partial) {
+  __shared__ uint32_t lds[9 * COMMIT_CB];  // >= 256 * 24 for the reduction
+  __shared__ int cnt;
+  const int nslab = (d + COMMIT_CB - 1) / COMMIT_CB;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int r = b / nslab, slab = b % nslab;
+  if (r >= nrows) return;  // uniform per block
+  const long long* c = coeffs + (size_t)rows[r] * d;
+  const int c0 = slab * COMMIT_CB, c1 = min(d, c0 + COMMIT_CB);
+  const int E0 = 1 << (B0 - 1);
+  const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  for (int i = c0 + (int)threadIdx.x; i < c1; i += 256) {
+    const long long cj = c[i];
+    if (cj == 0) continue;
+    const bool neg = cj < 0;
+    unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
+    int carry = 0;
+    for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
+      const int dg = recode(m, carry, win_bits(w, B0));
+      if (dg == 0) continue;
+      const int ad = dg < 0 ? -dg : dg;
+      uint32_t e = (uint32_t)((size_t)i * PB + win_entry(w, ad, E0));
+      if ((dg < 0) != neg) e |= 0x80000000u;
+      lds[atomicAdd(&cnt, 1)] = e;
+    }
+  }
+  __syncthreads();
+  const int n = cnt;
+  jac acc = jac_inf();
+  // software pipeline: the next table point is in flight while the current one is added
+  int k = threadIdx.x;
+  uint32_t e = k < n ? lds[k] : 0u;
+  aff q = ld_aff(tbl_pk + (size_t)(e & 0x7FFFFFFFu) * 16);
+  while (k < n) {
+    const int kn = k + 256;
+    const uint32_t en = kn < n ? lds[kn] : 0u;
+    const aff qn = ld_aff(tbl_pk + (size_t)(en & 0x7FFFFFFFu) * 16);
+    acc = jac_add_aff(acc, (e >> 31) ? aff_neg(q) : q);
+    k = kn;
+    e = en;
+    q = qn;
+  }
+  __syncthreads();
+  st_jac(lds + threadIdx.x * 24, acc);
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      st_jac(lds + threadIdx.x * 24, jac_add(ld_jac(lds + threadIdx.x * 24), ld_jac(lds + (threadIdx.x + s) * 24)));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) st_jac(out_partial + 24 * (size_t)b, ld_jac(lds));
 }
 
 // ------------------------------------------------------------------ reductions
@@ -248,11 +337,15 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
   const int cx = threadIdx.x & 31, ry = threadIdx.x >> 5;
   const int i = blockIdx.x * 32 + cx;
   jac acc = jac_inf();
-  if (i < ncols) {
+  if (i < ncols && ry < nrows) {
     const int col = cols ? cols[i] : i;
+    // software pipeline: load row r + 8 while adding row r
+    jac cur = ld_jac(pts + 24 * ((size_t)(rows ? rows[ry] : ry) * ncols_in + col));
     for (int r = ry; r < nrows; r += 8) {
-      const int row = rows ? rows[r] : r;
-      acc = jac_add(acc, ld_jac(pts + 24 * ((size_t)row * ncols_in + col)));
+      const int rn = r + 8 < nrows ? r + 8 : r;
+      const jac nxt = ld_jac(pts + 24 * ((size_t)(rows ? rows[rn] : rn) * ncols_in + col));
+      acc = jac_add(acc, cur);
+      cur = nxt;
     }
   }
   st_jac(&sh[ry][cx][0], acc);
@@ -339,25 +432,28 @@ extern "C" int bsc_witness_bases(const uint32_t* pk_aff, int d, int poly, int T,
   return (int)hipGetLastError();
 }
 
-extern "C" int bsc_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb, int inner, int NW,
-                            long long s_outer, long long s_w, long long s_k, long long s_in, uint32_t* table,
-                            uint32_t* scratch, void* stream) {
-  const long long n = (long long)nb * NW;
+extern "C" int bsc_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb, int inner, int B0, int NW,
+                            long long s_outer, long long s_e, long long s_in, uint32_t* table, uint32_t* scratch,
+                            void* stream) {
+  if (B0 < 8 || B0 > 20 || NW < 1) return -1;
+  const long long runs = (1ll << (B0 - 1)) / TBL_ENTRIES + NW - 1;
+  const long long n = (long long)nb * runs;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_fb_table, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, bases, bases_are_jac, b0,
-                     nb, inner, NW, s_outer, s_w, s_k, s_in, table, scratch);
+                     nb, inner, B0, NW, s_outer, s_e, s_in, table, scratch);
   return (int)hipGetLastError();
 }
 
 extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
-                              const uint32_t* tbl_wb, int poly, int T, int NW, int commit_only, uint32_t* out_pts,
-                              long long* out_y, void* stream) {
+                              const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
+                              uint32_t* out_pts, long long* out_y, void* stream) {
+  if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;  // every int64 scalar must be covered
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
   const long long n = (long long)nrows * nchunks * S;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_shares_msm, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows,
-                     nrows, tbl_pk, tbl_wb, poly, T, NW, commit_only, out_pts, out_y);
+                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, out_pts, out_y);
   return (int)hipGetLastError();
 }
 
@@ -374,6 +470,19 @@ extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
   if (ncols <= 0) return 0;
   hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 32)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
                      rows, nrows, cols, ncols, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
+                               int B0, int NW, uint32_t* partial, uint32_t* out, void* stream) {
+  if (nrows <= 0) return 0;
+  if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65 || NW > 9) return -1;
+  const long long PB = (1ll << (B0 - 1)) + (long long)(NW - 1) * TBL_ENTRIES;
+  if ((long long)d * PB >= (1ll << 31)) return -1;
+  const int nslab = (d + COMMIT_CB - 1) / COMMIT_CB;
+  hipLaunchKernelGGL(k_commit_rows, dim3(nrows * nslab), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows, nrows,
+                     tbl_pk, B0, NW, partial);
+  hipLaunchKernelGGL(k_segment_sum, dim3(nrows), dim3(256), 0, (hipStream_t)stream, partial, nslab, 1, 0, out);
   return (int)hipGetLastError();
 }
 

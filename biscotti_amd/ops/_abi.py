@@ -15,11 +15,12 @@ SIGNATURES = {
     "bsc_fp_op": [P, P, P, I, I, P],
     "bsc_point_op": [P, P, P, P, I, I, P],
     "bsc_witness_bases": [P, I, I, I, P, P],
-    "bsc_fb_table": [P, I, I, I, I, I, L, L, L, L, P, P, P],
-    "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, P, P, P],
+    "bsc_fb_table": [P, I, I, I, I, I, I, L, L, L, P, P, P],
+    "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, I, P, P, P],
     "bsc_sum_rows": [P, I, P, I, P, I, P, P],
     "bsc_segment_sum": [P, I, I, I, I, P, P],
     "bsc_sum_rows2": [P, I, P, I, P, I, P, P],
+    "bsc_commit_rows": [P, I, P, I, P, I, I, P, P, P],
     "bsc_marshal": [P, I, P, P],
     "bsc_to_affine": [P, I, P, P],
     # ml.hip

@@ -15,9 +15,37 @@ import torch
 
 from ..native import hip, rt
 
-NW_DEFAULT = 9       # 9 signed 8-bit windows cover any |scalar| < 2^64
-TBL_ENTRIES = 128
+TBL_ENTRIES = 128    # entries of an 8-bit signed window
+B0_CHOICES = (14, 13, 12, 11, 10, 9, 8)   # first-window widths, widest that fits in HBM wins
 _SCRATCH_BYTES = 1 << 31
+
+
+def windows_for(b0: int) -> tuple[int, int]:
+    """(NW, entries per base) for a B0-bit first window followed by 8-bit windows covering int64."""
+    nw = 1 + -(-(65 - b0) // 8)
+    return nw, (1 << (b0 - 1)) + (nw - 1) * TBL_ENTRIES
+
+
+def table_bytes_for(d: int, poly: int, total_shares: int, b0: int) -> int:
+    nchunks = (d + poly - 1) // poly
+    return (d + nchunks * (poly - 1) * total_shares) * windows_for(b0)[1] * 64
+
+
+def choose_b0(d: int, poly: int, total_shares: int, device, fraction: float = 0.6) -> int:
+    """Widest first window whose tables fit in `fraction` of the free device memory.
+
+    BSC_TABLE_B0 overrides.  On a 288 GB MI355X the MNIST key (d = 7850) gets B0 = 14: ~91 GB of
+    tables and one mixed addition for every |coefficient| <= 8192."""
+    import os
+    env = os.environ.get("BSC_TABLE_B0")
+    if env:
+        return int(env)
+    free, _ = torch.cuda.mem_get_info(device)
+    budget = fraction * free - _SCRATCH_BYTES
+    for b0 in B0_CHOICES:
+        if table_bytes_for(d, poly, total_shares, b0) <= budget:
+            return b0
+    return 8
 
 
 def _stream() -> int:
@@ -46,13 +74,14 @@ class DeviceCommitEngine:
     poly: POLY_SIZE (10); total_shares: TOTAL_SHARES (21) -- x = i - 10 (kyber.go:588).
     """
 
-    def __init__(self, commit_key, poly: int, total_shares: int, device="cuda", nw: int = NW_DEFAULT):
+    def __init__(self, commit_key, poly: int, total_shares: int, device="cuda", b0: int | None = None):
         self.device = torch.device(device)
         self.d = len(commit_key)
         self.poly = int(poly)
         self.T = int(total_shares)
         self.J = self.poly - 1
-        self.nw = int(nw)
+        self.b0 = int(b0) if b0 is not None else choose_b0(self.d, self.poly, self.T, self.device)
+        self.nw, self.pb = windows_for(self.b0)
         self.nchunks = (self.d + self.poly - 1) // self.poly
         lib = hip()
         self.pk_aff = u32_tensor(commit_key.affine_mont_u32(), self.device)  # [d, 16]
@@ -60,12 +89,11 @@ class DeviceCommitEngine:
         self.wbases = torch.empty((self.nchunks, self.J, self.T, 24), dtype=torch.int32, device=self.device)
         _check(lib.bsc_witness_bases(_ptr(self.pk_aff), self.d, self.poly, self.T, _ptr(self.wbases), _stream()),
                "witness_bases")
-        self.tbl_pk = torch.empty((self.d, self.nw, TBL_ENTRIES, 16), dtype=torch.int32, device=self.device)
-        self.tbl_wb = torch.empty((self.nchunks, self.J, self.nw, TBL_ENTRIES, self.T, 16), dtype=torch.int32,
-                                  device=self.device)
-        nw, E, T = self.nw, TBL_ENTRIES, self.T
-        self._build_table(self.pk_aff, False, self.d, 1, (nw * E, E, 1, 0), self.tbl_pk)
-        self._build_table(self.wbases, True, self.nchunks * self.J * self.T, T, (nw * E * T, E * T, T, 1), self.tbl_wb)
+        PB, T = self.pb, self.T
+        self.tbl_pk = torch.empty((self.d, PB, 16), dtype=torch.int32, device=self.device)
+        self.tbl_wb = torch.empty((self.nchunks, self.J, PB, T, 16), dtype=torch.int32, device=self.device)
+        self._build_table(self.pk_aff, False, self.d, 1, (PB, 1, 0), self.tbl_pk)
+        self._build_table(self.wbases, True, self.nchunks * self.J * T, T, (PB * T, T, 1), self.tbl_wb)
         del self.wbases
         torch.cuda.synchronize(self.device)
 
@@ -74,13 +102,13 @@ class DeviceCommitEngine:
 
     def _build_table(self, bases, jac: bool, nbases: int, inner: int, strides, table) -> None:
         lib = hip()
-        per_thread = TBL_ENTRIES * 32 * 4
-        batch = max(inner, (_SCRATCH_BYTES // (per_thread * self.nw)) // inner * inner)
-        scratch = torch.empty((min(batch, nbases) * self.nw * TBL_ENTRIES * 32,), dtype=torch.int32,
-                              device=self.device)
-        for b0 in range(0, nbases, batch):
-            nb = min(batch, nbases - b0)
-            _check(lib.bsc_fb_table(_ptr(bases), int(jac), b0, nb, inner, self.nw, *strides, _ptr(table),
+        runs = (1 << (self.b0 - 1)) // TBL_ENTRIES + self.nw - 1   # 128-entry runs per base
+        per_base = TBL_ENTRIES * 32 * 4 * runs
+        batch = max(inner, (_SCRATCH_BYTES // per_base) // inner * inner)
+        scratch = torch.empty((min(batch, nbases) * runs * TBL_ENTRIES * 32,), dtype=torch.int32, device=self.device)
+        for s0 in range(0, nbases, batch):
+            nb = min(batch, nbases - s0)
+            _check(lib.bsc_fb_table(_ptr(bases), int(jac), s0, nb, inner, self.b0, self.nw, *strides, _ptr(table),
                                     _ptr(scratch), _stream()), "fb_table")
         del scratch
 
@@ -100,9 +128,25 @@ class DeviceCommitEngine:
         pts = torch.empty((n, self.nchunks, S, 24), dtype=torch.int32, device=self.device)
         ys = None if commit_only else torch.empty((n, self.nchunks, self.T), dtype=torch.int64, device=self.device)
         _check(hip().bsc_shares_msm(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), _ptr(self.tbl_wb),
-                                    self.poly, self.T, self.nw, int(commit_only), _ptr(pts), _ptr(ys), _stream()),
+                                    self.poly, self.T, self.b0, self.nw, int(commit_only), _ptr(pts), _ptr(ys),
+                                    _stream()),
                "shares_msm")
         return pts, ys
+
+    def commit_rows(self, coeffs: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+        """Full-vector commitments sum_i c_i PK[i] of the given rows, Jacobian [n, 24] (commit phase)."""
+        assert coeffs.dtype == torch.int64 and coeffs.dim() == 2 and coeffs.shape[1] == self.d
+        assert rows.dtype == torch.int32 and rows.dim() == 1
+        n = rows.numel()
+        out = torch.empty((n, 24), dtype=torch.int32, device=self.device)
+        if n == 0:
+            return out
+        assert int(rows.min()) >= 0 and int(rows.max()) < coeffs.shape[0], "row index out of range"
+        nslab = (self.d + 1023) // 1024
+        partial = torch.empty((n * nslab, 24), dtype=torch.int32, device=self.device)
+        _check(hip().bsc_commit_rows(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), self.b0, self.nw,
+                                     _ptr(partial), _ptr(out), _stream()), "commit_rows")
+        return out
 
     def commitments(self, pts: torch.Tensor) -> torch.Tensor:
         """Full-vector commitment per row = sum of its chunk commitments. Returns Jacobian [n, 24]."""

@@ -102,8 +102,7 @@ class DeviceCrypto:
         if n == 0:
             return np.zeros((0, 64), np.uint8)
         rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
-        pts, _ = self.eng.shares(qdelta, rows, commit_only=True)
-        return B.marshal_host(self.eng.commitments(pts))
+        return B.marshal_host(self.eng.commit_rows(qdelta.contiguous(), rows))
 
     def shares(self, qdelta: torch.Tensor):
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)

@@ -22,22 +22,30 @@ def main():
     ap.add_argument("--d", type=int, default=7850)
     ap.add_argument("--rows", type=int, default=35)
     ap.add_argument("--workers", type=int, default=94)
-    ap.add_argument("--scale", type=int, default=30000)
+    ap.add_argument("--scale", type=int, default=30000, help="uniform coefficient range (--dist uniform)")
+    ap.add_argument("--dist", default="real", choices=["real", "uniform"],
+                    help="real: N(0, 1500^2) integers, the measured spread of quantised MNIST updates")
+    ap.add_argument("--b0", type=int, default=None)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
     t0 = time.time()
     key = rt().CommitKey.generate(a.d, 2)
     t1 = time.time()
-    eng = B.DeviceCommitEngine(key, 10, 21)
+    eng = B.DeviceCommitEngine(key, 10, 21, b0=a.b0)
     torch.cuda.synchronize()
     t2 = time.time()
     rng = np.random.default_rng(0)
-    coeffs = torch.from_numpy(rng.integers(-a.scale, a.scale, size=(a.workers, a.d), dtype=np.int64)).cuda()
+    if a.dist == "real":
+        c = np.rint(rng.normal(0.0, 1500.0, size=(a.workers, a.d))).astype(np.int64)
+    else:
+        c = rng.integers(-a.scale, a.scale, size=(a.workers, a.d), dtype=np.int64)
+    coeffs = torch.from_numpy(c).cuda()
     allrows = torch.arange(a.workers, dtype=torch.int32, device="cuda")
     rows = allrows[: a.rows].contiguous()
-    res = {"d": a.d, "key_gen_s": t1 - t0, "table_build_s": t2 - t1, "table_gb": eng.table_bytes() / 1e9}
+    res = {"d": a.d, "dist": a.dist, "b0": eng.b0, "key_gen_s": t1 - t0, "table_build_s": t2 - t1,
+           "table_gb": eng.table_bytes() / 1e9}
     for name, fn in [
-        ("commit_only_all_workers", lambda: eng.commitments(eng.shares(coeffs, allrows, commit_only=True)[0])),
+        ("commit_rows_all_workers", lambda: eng.commit_rows(coeffs, allrows)),
         ("shares_approved", lambda: eng.shares(coeffs, rows)),
     ]:
         fn()

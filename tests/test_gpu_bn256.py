@@ -74,12 +74,12 @@ def test_point_ops_match_host(rt):
             assert bytes(out[i]) == rt.g1_mul(g, k % order), (op, i)
 
 
-@pytest.mark.parametrize("d,secret,scale", [(25, 2, 10**4), (57, 2, 10**6), (33, 987654321123, 10**12),
-                                             (40, 2, 2**62)])
-def test_shares_msm_matches_host(rt, d, secret, scale):
+@pytest.mark.parametrize("d,secret,scale,b0", [(25, 2, 10**4, 8), (57, 2, 10**6, 14), (33, 987654321123, 10**12, 11),
+                                                (40, 2, 2**62, 14), (40, 2, 2**62, 8), (31, 7, 9000, 14)])
+def test_shares_msm_matches_host(rt, d, secret, scale, b0):
     from biscotti_amd.ops import bn256 as B
     key = rt.CommitKey.generate(d, secret)
-    eng = B.DeviceCommitEngine(key, poly=10, total_shares=21)
+    eng = B.DeviceCommitEngine(key, poly=10, total_shares=21, b0=b0)
     rng = np.random.default_rng(d)
     P_ = 3
     coeffs = rng.integers(-scale, scale, size=(P_, d), dtype=np.int64)
@@ -104,6 +104,26 @@ def test_shares_msm_matches_host(rt, d, secret, scale):
     # commit-only pass gives the same chunk commitments
     pts_c, _ = eng.shares(ct, rows, commit_only=True)
     np.testing.assert_array_equal(B.marshal(pts_c).cpu().numpy().reshape(3, eng.nchunks, 64), allb[:, :, 21])
+    # compacted full-vector commitment kernel == sum of chunk commitments
+    np.testing.assert_array_equal(B.marshal_host(eng.commit_rows(ct, rows)), comm)
+
+
+@pytest.mark.parametrize("scale,b0", [(3000, 14), (2**40, 14), (2**40, 8), (8193, 14)])
+def test_commit_rows_multi_slab(rt, scale, b0):
+    """d spanning several 1024-coefficient slabs, zero rows, sparse rows and wide scalars."""
+    from biscotti_amd.ops import bn256 as B
+    d = 2600
+    key = rt.CommitKey.generate(d, 5)
+    eng = B.DeviceCommitEngine(key, poly=10, total_shares=21, b0=b0)
+    rng = np.random.default_rng(scale % 97)
+    coeffs = rng.integers(-scale, scale, size=(4, d), dtype=np.int64)
+    coeffs[1] = 0
+    coeffs[2, ::7] = 0
+    coeffs[3, 1500:] = 0
+    rows = torch.tensor([3, 1, 0, 2], dtype=torch.int32, device="cuda")
+    got = B.marshal_host(eng.commit_rows(torch.from_numpy(coeffs).cuda(), rows))
+    for i, r in enumerate([3, 1, 0, 2]):
+        assert bytes(got[i]) == key.commit(coeffs[r], 0), r
 
 
 def test_sum_rows_is_aggregate(rt):
