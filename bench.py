@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--dataset", default="mnist")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--trace", default=None)
+    ap.add_argument("--phase-sync", action="store_true",
+                    help="synchronise the GPU at every phase boundary (per-phase GPU attribution, slower)")
     a = ap.parse_args()
 
     from biscotti_amd.parallel.comm import Comm
@@ -48,7 +50,7 @@ def main() -> int:
         # cgroup CPU quota from the native crypto pool
         torch.set_num_threads(min(4, torch.get_num_threads()))
     cfg = RunConfig(num_nodes=a.peers, dataset=a.dataset, seed=a.seed, max_iterations=10**9,
-                    trace_file=a.trace, host_threads=16)
+                    trace_file=a.trace, host_threads=16, phase_sync=a.phase_sync)
     eng = BiscottiEngine(cfg, comm)
     sync = (lambda: torch.cuda.synchronize()) if eng.gpu else (lambda: None)
     for _ in range(a.warmup):
@@ -99,6 +101,7 @@ def main() -> int:
                        "verifiers": cfg.num_verifiers, "aggregators": cfg.num_miners, "noisers": cfg.num_noisers,
                        "epsilon": cfg.epsilon, "ns_percent": cfg.perc_samples},
             "phase_ms_per_round": {k: 1e3 * v / max(a.steps, 1) for k, v in sorted(phases.items())},
+            "phase_sync": bool(a.phase_sync),
             "chain_valid": bool(ok),
         }
         print(json.dumps(out), flush=True)

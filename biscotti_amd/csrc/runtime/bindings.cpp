@@ -310,7 +310,52 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     (void)gen_table();
     {
       py::gil_scoped_release rel;
-      parallel_for(ms.size(), threads, [&](size_t i) { out[i] = schnorr_sign(ms[i], s, ns[i]); });
+      // nonce points in parallel, ONE inversion for all their marshals, responses in parallel
+      if (ms.size() != ns.size()) throw std::runtime_error("messages / nonces length mismatch");
+      std::vector<Scalar> vs(ms.size());
+      std::vector<G1> ts(ms.size());
+      parallel_for(ms.size(), threads, [&](size_t i) {
+        auto vt = schnorr_nonce(ns[i]);
+        vs[i] = vt.first;
+        ts[i] = vt.second;
+      });
+      const std::vector<Bytes> tm = g1_marshal_batch(ts);
+      parallel_for(ms.size(), threads, [&](size_t i) { out[i] = schnorr_finish(ms[i], s, vs[i], tm[i]); });
+    }
+    std::vector<py::bytes> r;
+    for (auto& o : out) r.push_back(P(o));
+    return r;
+  });
+  // All signatures of a round in one call: message i signed with sks[key_of[i]], nonce entropy
+  // nonce_base[key_of[i]] || le32(nonce_ids[i]).
+  m.def("schnorr_sign_multi", [](std::vector<py::bytes> msgs, std::vector<py::bytes> sks, std::vector<int> key_of,
+                                 std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads) {
+    const size_t n = msgs.size();
+    if (key_of.size() != n || nonce_ids.size() != n || nonce_base.size() != sks.size())
+      throw std::runtime_error("schnorr_sign_multi: length mismatch");
+    std::vector<Bytes> ms, bases;
+    std::vector<Scalar> keys;
+    for (auto& x : msgs) ms.push_back(B(x));
+    for (auto& x : sks) keys.push_back(Scalar::from_be(B(x)));
+    for (auto& x : nonce_base) bases.push_back(B(x));
+    for (int k : key_of)
+      if (k < 0 || size_t(k) >= keys.size()) throw std::runtime_error("schnorr_sign_multi: bad key index");
+    (void)gen_table();
+    std::vector<Bytes> out(n);
+    {
+      py::gil_scoped_release rel;
+      std::vector<Scalar> vs(n);
+      std::vector<G1> ts(n);
+      parallel_for(n, threads, [&](size_t i) {
+        Bytes ent = bases[size_t(key_of[i])];
+        const uint32_t id = uint32_t(nonce_ids[i]);
+        for (int b = 0; b < 4; ++b) ent.push_back(u8(id >> (8 * b)));
+        auto vt = schnorr_nonce(ent);
+        vs[i] = vt.first;
+        ts[i] = vt.second;
+      });
+      const std::vector<Bytes> tm = g1_marshal_batch(ts);
+      parallel_for(n, threads, [&](size_t i) { out[i] = schnorr_finish(ms[i], keys[size_t(key_of[i])], vs[i], tm[i]); });
     }
     std::vector<py::bytes> r;
     for (auto& o : out) r.push_back(P(o));

@@ -284,6 +284,61 @@ G1 G1::add(const G1& o) const {
   return out;
 }
 
+// madd-2007-bl (a = 0) with the exceptional cases handled: P == Q doubles, P == -Q -> infinity
+G1 G1::add_affine(const U256& ax, const U256& ay) const {
+  const MontField& F = Fp();
+  if (is_inf()) return from_affine_mont(ax, ay);
+  U256 z1z1, u2, s2, h, hh, i, j, r, v, t;
+  F.sqr(z1z1, z);
+  F.mul(u2, ax, z1z1);
+  F.mul(t, z, z1z1); F.mul(s2, ay, t);
+  F.sub(h, u2, x);
+  F.sub(r, s2, y);
+  if (h.is_zero()) {
+    if (r.is_zero()) return dbl();
+    return infinity();
+  }
+  F.sqr(hh, h);
+  F.add(i, hh, hh); F.add(i, i, i);
+  F.mul(j, h, i);
+  F.add(r, r, r);
+  F.mul(v, x, i);
+  G1 out;
+  F.sqr(out.x, r); F.sub(out.x, out.x, j); F.sub(out.x, out.x, v); F.sub(out.x, out.x, v);
+  F.sub(t, v, out.x); F.mul(t, r, t);
+  U256 yj; F.mul(yj, y, j); F.add(yj, yj, yj);
+  F.sub(out.y, t, yj);
+  F.add(t, z, h); F.sqr(t, t); F.sub(t, t, z1z1); F.sub(out.z, t, hh);
+  return out;
+}
+
+std::vector<Bytes> g1_marshal_batch(const std::vector<G1>& pts) {
+  const MontField& F = Fp();
+  const size_t n = pts.size();
+  std::vector<U256> pre(n);
+  U256 acc = F.one;
+  for (size_t i = 0; i < n; ++i) {
+    pre[i] = acc;
+    if (!pts[i].is_inf()) F.mul(acc, acc, pts[i].z);
+  }
+  U256 inv;
+  F.inv_mont(inv, acc);
+  std::vector<Bytes> out(n, Bytes(64, 0));
+  for (size_t k = n; k-- > 0;) {
+    if (pts[k].is_inf()) continue;
+    U256 zi, zi2, zi3, ax, ay;
+    F.mul(zi, inv, pre[k]);
+    F.mul(inv, inv, pts[k].z);
+    F.sqr(zi2, zi);
+    F.mul(zi3, zi2, zi);
+    F.mul(ax, pts[k].x, zi2);
+    F.mul(ay, pts[k].y, zi3);
+    F.from_mont(ax).to_be(out[k].data());
+    F.from_mont(ay).to_be(out[k].data() + 32);
+  }
+  return out;
+}
+
 G1 G1::neg() const {
   G1 r = *this;
   Fp().neg(r.y, y);
@@ -349,24 +404,50 @@ G1 G1::unmarshal(const Bytes& b) {
 bool G1::equals(const G1& o) const { return marshal() == o.marshal(); }
 
 G1GenTable::G1GenTable() {
-  t.resize(64 * 16);
+  constexpr int NWIN = 33, E = 128;
+  tx.resize(NWIN * E);
+  ty.resize(NWIN * E);
+  const MontField& F = Fp();
   G1 base = G1::generator();
-  for (int w = 0; w < 64; ++w) {
-    t[w * 16] = G1::infinity();
-    for (int d = 1; d < 16; ++d) t[w * 16 + d] = t[w * 16 + d - 1].add(base);
-    for (int d = 1; d < 16; ++d) {  // normalise so later additions are cheaper to reason about
-      U256 ax, ay;
-      t[w * 16 + d].to_affine(ax, ay);
-      t[w * 16 + d] = G1::from_affine_mont(ax, ay);
+  std::vector<G1> row(E);
+  for (int w = 0; w < NWIN; ++w) {
+    row[0] = base;
+    for (int d = 1; d < E; ++d) row[d] = row[d - 1].add(base);
+    // one inversion per window (Montgomery's trick); multiples of G are never infinity here
+    std::vector<U256> pre(E);
+    U256 acc = F.one;
+    for (int d = 0; d < E; ++d) { pre[d] = acc; F.mul(acc, acc, row[d].z); }
+    U256 inv;
+    F.inv_mont(inv, acc);
+    for (int d = E - 1; d >= 0; --d) {
+      U256 zi, zi2, zi3;
+      F.mul(zi, inv, pre[d]);
+      F.mul(inv, inv, row[d].z);
+      F.sqr(zi2, zi);
+      F.mul(zi3, zi2, zi);
+      F.mul(tx[w * E + d], row[d].x, zi2);
+      F.mul(ty[w * E + d], row[d].y, zi3);
     }
-    for (int i = 0; i < 4; ++i) base = base.dbl();
+    for (int i = 0; i < 8; ++i) base = base.dbl();
   }
 }
 G1 G1GenTable::mul(const U256& k) const {
+  // signed radix-256 digits in [-127, 128]
   G1 acc = G1::infinity();
-  for (int w = 0; w < 64; ++w) {
-    int d = int((k.w[w / 16] >> ((w % 16) * 4)) & 15);
-    if (d) acc = acc.add(t[w * 16 + d]);
+  int carry = 0;
+  for (int w = 0; w < 33; ++w) {
+    int d = carry + (w < 32 ? int((k.w[w / 8] >> ((w % 8) * 8)) & 0xFF) : 0);
+    if (d > 128) { d -= 256; carry = 1; } else { carry = 0; }
+    if (d == 0) continue;
+    const int ad = d < 0 ? -d : d;
+    const U256& x = tx[w * 128 + ad - 1];
+    if (d > 0) {
+      acc = acc.add_affine(x, ty[w * 128 + ad - 1]);
+    } else {
+      U256 ny;
+      Fp().neg(ny, ty[w * 128 + ad - 1]);
+      acc = acc.add_affine(x, ny);
+    }
   }
   return acc;
 }
@@ -529,6 +610,23 @@ Scalar hash_schnorr(const Bytes& message, const G1& T) {
   Blake2Xb xof(T.marshal());
   xof.write(message);
   return pick_scalar_from_xof(xof);
+}
+
+std::pair<Scalar, G1> schnorr_nonce(const Bytes& nonce_entropy) {
+  Blake2Xb nx(nonce_entropy);
+  Scalar v = pick_scalar_from_xof(nx);
+  return {v, gen_table().mul(v.v)};
+}
+
+Bytes schnorr_finish(const Bytes& message, const Scalar& sk, const Scalar& v, const Bytes& t_marshal) {
+  Blake2Xb xof(t_marshal);
+  xof.write(message);
+  Scalar c = pick_scalar_from_xof(xof);
+  Scalar r = v.sub(sk.mul(c));
+  Bytes out = c.to_be();
+  Bytes rb = r.to_be();
+  out.insert(out.end(), rb.begin(), rb.end());
+  return out;
 }
 
 Bytes schnorr_sign(const Bytes& message, const Scalar& sk, const Bytes& nonce_entropy) {

@@ -86,6 +86,7 @@ struct G1 {
   bool is_inf() const { return z.is_zero(); }
   G1 dbl() const;
   G1 add(const G1& o) const;
+  G1 add_affine(const U256& ax, const U256& ay) const;  // mixed addition, (ax, ay) != infinity
   G1 neg() const;
   G1 mul(const U256& k) const;       // k taken as an integer (any 256-bit value)
   G1 mul_i64(i64 k) const;            // signed small scalar: |k|*P, negated if k<0
@@ -96,13 +97,16 @@ struct G1 {
   bool equals(const G1& o) const;
 };
 
-// Fixed-base comb for the generator (Schnorr nonces, key generation): 64 windows x 16.
+// Fixed-base table for the generator (Schnorr nonces, key generation): 33 signed 8-bit windows x
+// 128 affine multiples, so k*G costs <= 33 mixed additions and no doublings.
 struct G1GenTable {
-  std::vector<G1> t;  // t[win*16 + d] = d * 16^win * G, affine-normalised (z = R)
+  std::vector<U256> tx, ty;  // entry w*128 + (d-1) = d * 256^w * G, affine Montgomery
   G1GenTable();
   G1 mul(const U256& k) const;
 };
 const G1GenTable& gen_table();
+// Kyber marshals of many points with ONE field inversion (Montgomery's trick).
+std::vector<Bytes> g1_marshal_batch(const std::vector<G1>& pts);
 
 // ------------------------------------------------------------------ Fp2 / G2
 struct Fp2 {
@@ -140,6 +144,9 @@ const Fp2& twist_b();
 // ------------------------------------------------------------------ Schnorr (kyber.go:873-933)
 // Signature bytes = marshal(c) || marshal(r), 64 B. nonce: 32 B of entropy (the reference draws
 // it from crypto/rand); pass deterministic bytes for reproducible runs.
+// Batched signing pieces: nonce scalar + commitment point, then the response from T's marshal.
+std::pair<Scalar, G1> schnorr_nonce(const Bytes& nonce_entropy);
+Bytes schnorr_finish(const Bytes& message, const Scalar& sk, const Scalar& v, const Bytes& t_marshal);
 Bytes schnorr_sign(const Bytes& message, const Scalar& sk, const Bytes& nonce_entropy);
 bool schnorr_verify(const Bytes& message, const G1& pk, const Bytes& sig);
 Scalar hash_schnorr(const Bytes& message, const G1& T);

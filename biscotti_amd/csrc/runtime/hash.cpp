@@ -1,5 +1,7 @@
 #include "hash.hpp"
 
+#include <immintrin.h>
+
 namespace bsc {
 
 // ---------------------------------------------------------------- SHA-256
@@ -21,7 +23,55 @@ Sha256::Sha256() {
   memcpy(h, iv, sizeof(h));
 }
 
+// ---- SHA-NI (x86 SHA extensions): the ledger hashes ~75 KB of gob per block, 5-8x faster than
+// the portable rounds.  Runtime-dispatched, so the portable path stays the fallback.
+__attribute__((target("sha,sse4.1,ssse3"))) static void sha256_ni_blocks(u32 state[8], const u8* data, size_t nblocks) {
+  const __m128i MASK = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+  __m128i tmp = _mm_loadu_si128(reinterpret_cast<const __m128i*>(&state[0]));
+  __m128i st1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(&state[4]));
+  tmp = _mm_shuffle_epi32(tmp, 0xB1);          // CDAB
+  st1 = _mm_shuffle_epi32(st1, 0x1B);          // EFGH
+  __m128i st0 = _mm_alignr_epi8(tmp, st1, 8);  // ABEF
+  st1 = _mm_blend_epi16(st1, tmp, 0xF0);       // CDGH
+  for (; nblocks > 0; --nblocks, data += 64) {
+    const __m128i abef = st0, cdgh = st1;
+    __m128i w[16];
+    for (int g = 0; g < 16; ++g) {
+      if (g < 4) {
+        w[g] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(data + 16 * g)), MASK);
+      } else {
+        __m128i t = _mm_add_epi32(_mm_sha256msg1_epu32(w[g - 4], w[g - 3]), _mm_alignr_epi8(w[g - 1], w[g - 2], 4));
+        w[g] = _mm_sha256msg2_epu32(t, w[g - 1]);
+      }
+      __m128i msg = _mm_add_epi32(w[g], _mm_loadu_si128(reinterpret_cast<const __m128i*>(&K256[4 * g])));
+      st1 = _mm_sha256rnds2_epu32(st1, st0, msg);
+      msg = _mm_shuffle_epi32(msg, 0x0E);
+      st0 = _mm_sha256rnds2_epu32(st0, st1, msg);
+    }
+    st0 = _mm_add_epi32(st0, abef);
+    st1 = _mm_add_epi32(st1, cdgh);
+  }
+  tmp = _mm_shuffle_epi32(st0, 0x1B);        // FEBA
+  st1 = _mm_shuffle_epi32(st1, 0xB1);        // DCHG
+  st0 = _mm_blend_epi16(tmp, st1, 0xF0);     // DCBA
+  st1 = _mm_alignr_epi8(st1, tmp, 8);        // HGFE
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(&state[0]), st0);
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(&state[4]), st1);
+}
+
+static bool have_sha_ni() {
+  static const bool ok = [] {
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
+  }();
+  return ok;
+}
+
 void Sha256::block(const u8* p) {
+  if (have_sha_ni()) {
+    sha256_ni_blocks(h, p, 1);
+    return;
+  }
   u32 w[64];
   for (int i = 0; i < 16; ++i)
     w[i] = (u32(p[4 * i]) << 24) | (u32(p[4 * i + 1]) << 16) | (u32(p[4 * i + 2]) << 8) | p[4 * i + 3];
@@ -45,6 +95,12 @@ void Sha256::block(const u8* p) {
 
 void Sha256::update(const u8* p, size_t n) {
   total += n;
+  if (blen == 0 && n >= 64 && have_sha_ni()) {  // whole blocks straight from the input
+    const size_t nb = n / 64;
+    sha256_ni_blocks(h, p, nb);
+    p += nb * 64;
+    n -= nb * 64;
+  }
   while (n > 0) {
     size_t take = std::min(n, size_t(64) - blen);
     memcpy(buf + blen, p, take);

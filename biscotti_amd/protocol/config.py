@@ -43,6 +43,7 @@ class RunConfig:
     roles_vrf_proof: bool = True    # getVRFRoles computes (and discards) a proof; keep the work
     verify_signatures: bool = False  # miners check verifier signatures (commented out in reference, Q5)
     host_threads: int = 16
+    roles_vrf_threads: int = 4      # the discarded roles proof (Q7) runs in the background on few threads
     log_dir: str | None = None
     trace_file: str | None = None
     chain_file: str | None = None   # append-only chain persistence (checkpoint / resume)
@@ -50,6 +51,7 @@ class RunConfig:
     device: str | None = None       # "cpu" forces the CPU path
     log_every_peer: bool = False    # one Train Error line per local peer (reference style)
     deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
+    phase_sync: bool = True         # device sync at phase boundaries (accurate per-phase GPU times)
 
     def protocol(self, rt):
         pc = rt.ProtocolConfig()
@@ -120,6 +122,7 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--device", default=None)
     ap.add_argument("--log-every-peer", action="store_true")
     ap.add_argument("--deterministic-time", action="store_true")
+    ap.add_argument("--no-phase-sync", dest="phase_sync", action="store_false")
 
 
 def config_from_args(ns: argparse.Namespace) -> RunConfig:

@@ -234,3 +234,22 @@ def test_vrf_async_jobs_match_sync(rt):
     assert j2.result() == rt.vrf_prove_batch(seeds[:5], b"beta", 1)
     assert j1.done() and j1.result() == rt.vrf_prove_batch(seeds, b"alpha", 3)
     assert rt.vrf_prove_batch_async([], b"x", 4).result() == []
+
+
+def test_schnorr_sign_multi_batch(rt):
+    """Round-wide batched signing: per-message keys, derived nonces, one shared inversion."""
+    import os
+
+    keys = [rt.client_key_from_entropy(os.urandom(32)) for _ in range(3)]
+    msgs = [os.urandom(64) for _ in range(25)]
+    key_of = [i % 3 for i in range(25)]
+    bases = [os.urandom(32) for _ in range(3)]
+    ids = list(range(100, 125))
+    sigs = rt.schnorr_sign_multi(msgs, [k[0] for k in keys], key_of, bases, ids, 4)
+    for m, k, s in zip(msgs, key_of, sigs):
+        assert rt.schnorr_verify(m, keys[k][1], s)
+        assert not rt.schnorr_verify(m, keys[(k + 1) % 3][1], s)
+    # deterministic, and equal to the single-signature path with the same nonce entropy
+    assert rt.schnorr_sign_multi(msgs, [k[0] for k in keys], key_of, bases, ids, 1) == sigs
+    ent = bases[key_of[7]] + (107).to_bytes(4, "little")
+    assert rt.schnorr_sign(msgs[7], keys[key_of[7]][0], ent) == sigs[7]
