@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <future>
@@ -44,81 +45,73 @@ static py::int_ pyint_from_u256(const U256& v) {
 #include <functional>
 #include <mutex>
 class Pool {
+  // Several jobs may run at once (background VRF proofs, round-wide Schnorr batches, the main
+  // thread's calls): every run() registers its job, works on it itself, and the persistent
+  // workers help whichever registered job still has items and is below its thread cap.
+  struct Job {
+    const std::function<void(size_t)>* f;
+    size_t n;
+    int cap;                          // pool workers allowed on this job (threads - 1)
+    std::atomic<size_t> next{0};
+    int active = 0;                   // workers inside the job (guarded by m_)
+  };
+
  public:
   void run(size_t n, int threads, const std::function<void(size_t)>& f) {
     if (threads <= 1 || n <= 1) {
       for (size_t i = 0; i < n; ++i) f(i);
       return;
     }
-    // a second Python thread may call in while the pool is busy (host crypto overlapped with
-    // GPU work): it gets short-lived threads of its own instead of clobbering the running job
-    std::unique_lock<std::mutex> busy(run_m_, std::try_to_lock);
-    if (!busy.owns_lock()) {
-      std::atomic<size_t> next{0};
-      auto body = [&] {
-        for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
-      };
-      std::vector<std::thread> ts;
-      const int extra = std::min<int>(threads, int(n)) - 1;
-      for (int t = 0; t < extra; ++t) ts.emplace_back(body);
-      body();
-      for (auto& t : ts) t.join();
-      return;
+    Job job;
+    job.f = &f;
+    job.n = n;
+    job.cap = std::min<int>(threads, int(n)) - 1;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      ensure(threads - 1);
+      jobs_.push_back(&job);
     }
-    ensure(threads - 1);
-    std::unique_lock<std::mutex> lk(m_);
-    job_ = &f;
-    n_ = n;
-    next_.store(0);
-    active_ = int(workers_.size());
-    ++gen_;
     cv_.notify_all();
-    lk.unlock();
-    work();
-    lk.lock();
-    done_cv_.wait(lk, [&] { return active_ == 0; });
-    job_ = nullptr;
+    for (size_t i; (i = job.next.fetch_add(1)) < n;) f(i);
+    std::unique_lock<std::mutex> lk(m_);
+    jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));  // no new helper can join
+    done_cv_.wait(lk, [&] { return job.active == 0; });       // helpers still inside finish
   }
   ~Pool() {
     {
       std::lock_guard<std::mutex> lk(m_);
       stop_ = true;
-      ++gen_;
     }
     cv_.notify_all();
     for (auto& t : workers_) t.join();
   }
+
  private:
-  void ensure(int k) {
+  void ensure(int k) {  // caller holds m_
     while (int(workers_.size()) < k) workers_.emplace_back([this] { loop(); });
   }
-  void work() {
-    for (;;) {
-      size_t i = next_.fetch_add(1);
-      if (i >= n_) break;
-      (*job_)(i);
-    }
+  Job* pick() {  // caller holds m_
+    for (Job* j : jobs_)
+      if (j->active < j->cap && j->next.load() < j->n) return j;
+    return nullptr;
   }
   void loop() {
-    size_t seen = 0;
     std::unique_lock<std::mutex> lk(m_);
     for (;;) {
-      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      Job* j = nullptr;
+      cv_.wait(lk, [&] { return stop_ || (j = pick()) != nullptr; });
       if (stop_) return;
-      seen = gen_;
+      ++j->active;
       lk.unlock();
-      work();
+      for (size_t i; (i = j->next.fetch_add(1)) < j->n;) (*j->f)(i);
       lk.lock();
-      if (--active_ == 0) done_cv_.notify_all();
+      if (--j->active == 0) done_cv_.notify_all();
     }
   }
   std::vector<std::thread> workers_;
-  std::mutex m_, run_m_;
+  std::vector<Job*> jobs_;
+  std::mutex m_;
   std::condition_variable cv_, done_cv_;
-  const std::function<void(size_t)>* job_ = nullptr;
-  std::atomic<size_t> next_{0};
-  size_t n_ = 0, gen_ = 0;
-  int active_ = 0;
   bool stop_ = false;
 };
 static Pool& pool() {
@@ -146,6 +139,59 @@ struct VrfJob {
     if (th.joinable()) th.join();
   }
 };
+
+struct SignJob {
+  std::vector<Bytes> msgs, bases, out;
+  std::vector<Scalar> keys;
+  std::vector<int> key_of, ids;
+  int threads = 1;
+  std::string error;
+  std::promise<void> done_p;
+  std::shared_future<void> done = done_p.get_future().share();
+  std::thread th;
+  ~SignJob() {
+    if (th.joinable()) th.join();
+  }
+};
+
+static std::shared_ptr<SignJob> make_sign_job(std::vector<py::bytes>& msgs, std::vector<py::bytes>& sks,
+                                              std::vector<int>& key_of, std::vector<py::bytes>& nonce_base,
+                                              std::vector<int>& nonce_ids, int threads) {
+  const size_t n = msgs.size();
+  if (key_of.size() != n || nonce_ids.size() != n || nonce_base.size() != sks.size())
+    throw std::runtime_error("schnorr_sign_multi: length mismatch");
+  auto job = std::make_shared<SignJob>();
+  for (auto& x : msgs) job->msgs.push_back(B(x));
+  for (auto& x : sks) job->keys.push_back(Scalar::from_be(B(x)));
+  for (auto& x : nonce_base) job->bases.push_back(B(x));
+  for (int k : key_of)
+    if (k < 0 || size_t(k) >= job->keys.size()) throw std::runtime_error("schnorr_sign_multi: bad key index");
+  job->key_of = key_of;
+  job->ids = nonce_ids;
+  job->threads = threads;
+  job->out.resize(n);
+  (void)gen_table();
+  return job;
+}
+
+static void run_sign_job(SignJob& j) {
+  // nonce points in parallel, ONE inversion for all their marshals, responses in parallel
+  const size_t n = j.msgs.size();
+  std::vector<Scalar> vs(n);
+  std::vector<G1> ts(n);
+  parallel_for(n, j.threads, [&](size_t i) {
+    Bytes ent = j.bases[size_t(j.key_of[i])];
+    const uint32_t id = uint32_t(j.ids[i]);
+    for (int b = 0; b < 4; ++b) ent.push_back(u8(id >> (8 * b)));
+    auto vt = schnorr_nonce(ent);
+    vs[i] = vt.first;
+    ts[i] = vt.second;
+  });
+  const std::vector<Bytes> tm = g1_marshal_batch(ts);
+  parallel_for(n, j.threads, [&](size_t i) {
+    j.out[i] = schnorr_finish(j.msgs[i], j.keys[size_t(j.key_of[i])], vs[i], tm[i]);
+  });
+}
 
 struct CommitKey {
   std::vector<G1> pk;
@@ -327,39 +373,43 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     return r;
   });
   // All signatures of a round in one call: message i signed with sks[key_of[i]], nonce entropy
-  // nonce_base[key_of[i]] || le32(nonce_ids[i]).
-  m.def("schnorr_sign_multi", [](std::vector<py::bytes> msgs, std::vector<py::bytes> sks, std::vector<int> key_of,
-                                 std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads) {
-    const size_t n = msgs.size();
-    if (key_of.size() != n || nonce_ids.size() != n || nonce_base.size() != sks.size())
-      throw std::runtime_error("schnorr_sign_multi: length mismatch");
-    std::vector<Bytes> ms, bases;
-    std::vector<Scalar> keys;
-    for (auto& x : msgs) ms.push_back(B(x));
-    for (auto& x : sks) keys.push_back(Scalar::from_be(B(x)));
-    for (auto& x : nonce_base) bases.push_back(B(x));
-    for (int k : key_of)
-      if (k < 0 || size_t(k) >= keys.size()) throw std::runtime_error("schnorr_sign_multi: bad key index");
-    (void)gen_table();
-    std::vector<Bytes> out(n);
+  // nonce_base[key_of[i]] || le32(nonce_ids[i]).  _async returns a job that signs on native
+  // threads right away (result() joins) so the work overlaps the GPU share computation.
+  py::class_<SignJob, std::shared_ptr<SignJob>>(m, "SignJob").def("result", [](SignJob& j) {
     {
       py::gil_scoped_release rel;
-      std::vector<Scalar> vs(n);
-      std::vector<G1> ts(n);
-      parallel_for(n, threads, [&](size_t i) {
-        Bytes ent = bases[size_t(key_of[i])];
-        const uint32_t id = uint32_t(nonce_ids[i]);
-        for (int b = 0; b < 4; ++b) ent.push_back(u8(id >> (8 * b)));
-        auto vt = schnorr_nonce(ent);
-        vs[i] = vt.first;
-        ts[i] = vt.second;
-      });
-      const std::vector<Bytes> tm = g1_marshal_batch(ts);
-      parallel_for(n, threads, [&](size_t i) { out[i] = schnorr_finish(ms[i], keys[size_t(key_of[i])], vs[i], tm[i]); });
+      j.done.wait();
+    }
+    if (!j.error.empty()) throw std::runtime_error(j.error);
+    std::vector<py::bytes> r;
+    for (auto& o : j.out) r.push_back(P(o));
+    return r;
+  });
+  m.def("schnorr_sign_multi", [](std::vector<py::bytes> msgs, std::vector<py::bytes> sks, std::vector<int> key_of,
+                                 std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads) {
+    auto job = make_sign_job(msgs, sks, key_of, nonce_base, nonce_ids, threads);
+    {
+      py::gil_scoped_release rel;
+      run_sign_job(*job);
     }
     std::vector<py::bytes> r;
-    for (auto& o : out) r.push_back(P(o));
+    for (auto& o : job->out) r.push_back(P(o));
     return r;
+  });
+  m.def("schnorr_sign_multi_async", [](std::vector<py::bytes> msgs, std::vector<py::bytes> sks,
+                                       std::vector<int> key_of, std::vector<py::bytes> nonce_base,
+                                       std::vector<int> nonce_ids, int threads) {
+    auto job = make_sign_job(msgs, sks, key_of, nonce_base, nonce_ids, threads);
+    SignJob* jp = job.get();
+    jp->th = std::thread([jp] {
+      try {
+        run_sign_job(*jp);
+      } catch (const std::exception& e) {
+        jp->error = e.what();
+      }
+      jp->done_p.set_value();
+    });
+    return job;
   });
   m.def("client_key_from_entropy", [](py::bytes e) {
     auto kp = client_key_from_entropy(B(e));

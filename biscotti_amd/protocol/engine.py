@@ -288,6 +288,7 @@ class BiscottiEngine:
                         1 for w in local_workers if all(j >= thr for j in noisers[w]))
             accepted_map: dict = {}
             signatures: dict = {}
+            pending_signatures = None
             inbox = fsm.verifier_inbox(workers) if cfg.verification else []
             local_verifiers = [v for v in plan.verifiers if live[v] and v in self.local]
             if cfg.verification and inbox:
@@ -324,24 +325,39 @@ class BiscottiEngine:
                             key_of.append(len(sks) - 1)
                             ids.append(w)
                             slots.append((vi, pos[w]))
-                with tm.phase("verify.sign"):
-                    sigs = R.schnorr_sign_multi(msgs, sks, key_of, bases, ids, cfg.host_threads) if msgs else []
-                for (vi, j), sg in zip(slots, sigs):
+                # verifier signatures (main.go:1120-1140) sign on native threads while the GPU
+                # computes shares; they are joined where first needed (plain blocks carry them,
+                # --verify-signatures checks them) or at the end of the round
+                sign_job = R.schnorr_sign_multi_async(msgs, sks, key_of, bases, ids, cfg.host_threads) \
+                    if msgs else None
+                for vi, j in slots:
                     acc_np[vi, j] = 1
-                    sig_np[vi, j] = np.frombuffer(sg, np.uint8)
-                if single:
-                    acc_all, sig_all = acc_np[None], sig_np[None]
-                else:
-                    acc_all = comm.all_gather(torch.from_numpy(acc_np).to(self.dev)).cpu().numpy()
-                    sig_all = comm.all_gather(torch.from_numpy(sig_np).to(self.dev)).cpu().numpy()
+                acc_all = acc_np[None] if single else \
+                    comm.all_gather(torch.from_numpy(acc_np).to(self.dev)).cpu().numpy()
                 for vi, v in enumerate(plan.verifiers):
                     if not live[v]:
                         continue
                     o = 0 if single else comm.owner(v, self.N)
-                    js = np.nonzero(acc_all[o, vi])[0]
-                    accepted_map[v] = [inbox[j] for j in js]
-                    for j in js:
-                        signatures.setdefault(inbox[j], []).append(sig_all[o, vi, j].tobytes())
+                    accepted_map[v] = [inbox[j] for j in np.nonzero(acc_all[o, vi])[0]]
+
+                def _join_signatures(sign_job=sign_job, slots=slots, sig_np=sig_np, acc_all=acc_all,
+                                     inbox=inbox, live=live, plan=plan):
+                    with tm.phase("verify.sign_join"):
+                        sigs = sign_job.result() if sign_job is not None else []
+                        for (vi, j), sg in zip(slots, sigs):
+                            sig_np[vi, j] = np.frombuffer(sg, np.uint8)
+                        sig_all = sig_np[None] if single else \
+                            comm.all_gather(torch.from_numpy(sig_np).to(self.dev)).cpu().numpy()
+                        for vi, v in enumerate(plan.verifiers):
+                            if not live[v]:
+                                continue
+                            o = 0 if single else comm.owner(v, self.N)
+                            for j in np.nonzero(acc_all[o, vi])[0]:
+                                signatures.setdefault(inbox[j], []).append(sig_all[o, vi, j].tobytes())
+                pending_signatures = _join_signatures
+                if not cfg.secure_agg or cfg.verify_signatures:
+                    pending_signatures()
+                    pending_signatures = None
                 approved, _ = fsm.approve(accepted_map)
             else:
                 approved, _ = fsm.approve({})
@@ -361,6 +377,8 @@ class BiscottiEngine:
             if cfg.chain_file and comm.rank == 0:
                 R.Blockchain.append_to_file(cfg.chain_file, block)
             self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
+        if pending_signatures is not None:  # every rank, same point: the collective stays aligned
+            pending_signatures()
         with tm.phase("eval"):
             ev = self.task.evaluate(self.W)
             if fut_roles is not None:

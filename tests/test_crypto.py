@@ -253,3 +253,21 @@ def test_schnorr_sign_multi_batch(rt):
     assert rt.schnorr_sign_multi(msgs, [k[0] for k in keys], key_of, bases, ids, 1) == sigs
     ent = bases[key_of[7]] + (107).to_bytes(4, "little")
     assert rt.schnorr_sign(msgs[7], keys[key_of[7]][0], ent) == sigs[7]
+
+
+def test_concurrent_native_jobs_share_the_pool(rt):
+    """VRF and signing jobs running at once (and a foreground batch) give the serial results."""
+    import os
+
+    seeds = [os.urandom(32) for _ in range(40)]
+    keys = [rt.client_key_from_entropy(os.urandom(32)) for _ in range(2)]
+    msgs = [os.urandom(64) for _ in range(60)]
+    key_of = [i % 2 for i in range(60)]
+    bases = [os.urandom(32), os.urandom(32)]
+    ids = list(range(60))
+    v = rt.vrf_prove_batch_async(seeds, b"h", 3)
+    s = rt.schnorr_sign_multi_async(msgs, [k[0] for k in keys], key_of, bases, ids, 8)
+    fg = rt.vrf_prove_batch(seeds[:10], b"g", 8)
+    assert s.result() == rt.schnorr_sign_multi(msgs, [k[0] for k in keys], key_of, bases, ids, 1)
+    assert v.result() == rt.vrf_prove_batch(seeds, b"h", 1)
+    assert fg == rt.vrf_prove_batch(seeds[:10], b"g", 1)
