@@ -15,6 +15,7 @@ import torch
 
 from .. import data as D
 from ..ops import ml as K
+from ..utils import h2d
 
 
 class SoftmaxTask:
@@ -41,8 +42,8 @@ class SoftmaxTask:
             o += X.shape[0]
         self.X = torch.from_numpy(np.concatenate(Xs).astype(np.float32)).to(self.device)
         self.y = torch.from_numpy(np.concatenate(ys).astype(np.int32)).to(self.device)
-        self.off = torch.tensor(offs, dtype=torch.int64, device=self.device)
-        self.ntrain = torch.tensor(ns, dtype=torch.int32, device=self.device)
+        self.off = h2d(offs, torch.int64, self.device)
+        self.ntrain = h2d(ns, torch.int32, self.device)
         self.test_X = torch.from_numpy(fed.test_X).to(self.device)
         self.test_y = torch.from_numpy(fed.test_y.astype(np.int32)).to(self.device)
         self.att_X = torch.from_numpy(fed.attack_X).to(self.device)
@@ -62,8 +63,8 @@ class SoftmaxTask:
         if not peers:
             z = torch.empty((0, self.nparam), device=self.device)
             return z.float(), z.long()
-        sel = torch.tensor([self._local_index[p] for p in peers], dtype=torch.long, device=self.device)
-        pid = torch.tensor(peers, dtype=torch.int32, device=self.device)
+        sel = h2d([self._local_index[p] for p in peers], torch.long, self.device)
+        pid = h2d(peers, torch.int32, self.device)
         delta, qdelta, loss = K.softmax_step(self.X, self.y, self.off[sel].contiguous(),
                                              self.ntrain[sel].contiguous(), pid, W, self.d_in, self.d_out,
                                              self.batch, self.seed, iteration, 100.0, 1e4)
@@ -80,7 +81,7 @@ class SoftmaxTask:
         i = self._local_index[peer]
         o, n = int(self.off[i]), int(self.ntrain[i])
         rows = K.minibatch_indices(peer, iteration, n, self.batch, self.seed ^ 0xB0B)
-        sel = torch.tensor([o + r for r in rows], dtype=torch.long, device=self.device)
+        sel = h2d([o + r for r in rows], torch.long, self.device)
         return K.eval_error(self.X[sel].contiguous(), self.y[sel].contiguous(), W, self.d_in, self.d_out, True)
 
 
@@ -113,8 +114,8 @@ class LogisticTask:
             ns.append(n)
         self.X = torch.from_numpy(np.concatenate(Xs)).to(self.device)
         self.y = torch.from_numpy(np.concatenate(ys)).to(self.device)
-        self.off = torch.tensor(offs, dtype=torch.int64, device=self.device)
-        self.nrows = torch.tensor(ns, dtype=torch.int32, device=self.device)
+        self.off = h2d(offs, torch.int64, self.device)
+        self.nrows = h2d(ns, torch.int32, self.device)
         # diffPriv16 noise at source: sigma = sqrt(2 ln 1.25)/epsilon (logistic_model.py:81)
         s = math.sqrt(2 * math.log(1.25)) / epsilon if epsilon > 0 else 0.0
         colluders = colluders or set()
@@ -135,10 +136,10 @@ class LogisticTask:
 
     def step(self, W: torch.Tensor, iteration: int, peers: list[int]):
         idx = [self._local_index[p] for p in peers]
-        sel = torch.tensor(idx, dtype=torch.long, device=self.device)
+        sel = h2d(idx, torch.long, self.device)
         off, nr = self.off[sel].contiguous(), self.nrows[sel].contiguous()
         sig, calls = self.sigma[sel].contiguous(), self.calls[sel].contiguous()
-        pid = torch.tensor(peers, dtype=torch.int32, device=self.device)
+        pid = h2d(peers, torch.int32, self.device)
         delta, qdelta = K.logreg_step(self.X, self.y, off, nr, pid, W, self.batch, self.seed, calls, self.alpha,
                                       self.lammy, sig, 1e4)
         self.calls[sel] += 1

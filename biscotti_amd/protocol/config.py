@@ -43,7 +43,7 @@ class RunConfig:
     roles_vrf_proof: bool = True    # getVRFRoles computes (and discards) a proof; keep the work
     verify_signatures: bool = False  # miners check verifier signatures (commented out in reference, Q5)
     host_threads: int = 16
-    roles_vrf_threads: int = 4      # the discarded roles proof (Q7) runs in the background on few threads
+    roles_vrf_threads: int = 8      # the discarded roles proof (Q7) runs in the background on fewer threads
     log_dir: str | None = None
     trace_file: str | None = None
     chain_file: str | None = None   # append-only chain persistence (checkpoint / resume)

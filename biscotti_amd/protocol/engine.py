@@ -34,7 +34,7 @@ from ..native import rt
 from ..ops import bn256 as B
 from ..ops import ml as K
 from ..parallel.comm import Comm
-from ..utils import JsonlWriter, PhaseTimer, get_logger
+from ..utils import JsonlWriter, PhaseTimer, get_logger, h2d
 from .config import RunConfig
 
 
@@ -57,6 +57,25 @@ class RoundResult:
     wall: float = 0.0
 
 
+class _Ready:
+    def __init__(self, value):
+        self.value = value
+
+    def result(self):
+        return self.value
+
+
+class _PendingCommitments:
+    def __init__(self, host: torch.Tensor, event):
+        self.host, self.event, self.value = host, event, None
+
+    def result(self) -> np.ndarray:
+        if self.value is None:
+            self.event.synchronize()
+            self.value = rt().g1_marshal_jac_batch(self.host.numpy().view(np.uint32))
+        return self.value
+
+
 class HostCrypto:
     """CPU crypto backend (native host BN256): points travel as 64-byte marshals."""
 
@@ -65,6 +84,9 @@ class HostCrypto:
         self.d = len(key)
         self.nchunks = (self.d + poly - 1) // poly
         self.threads = threads
+
+    def commitments_async(self, qdelta: torch.Tensor):
+        return _Ready(self.commitments(qdelta))
 
     def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
         q = qdelta.cpu().numpy()
@@ -96,13 +118,23 @@ class DeviceCrypto:
         self.eng = B.DeviceCommitEngine(key, poly, T, device)
         self.d, self.poly, self.T, self.nchunks = self.eng.d, poly, T, self.eng.nchunks
 
-    def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
-        """Fixed-base MSM on device, one batch-normalised marshal on host -> uint8 [n, 64]."""
+    def commitments_async(self, qdelta: torch.Tensor):
+        """Fixed-base MSM on device, queued download into pinned memory; result() waits for it and
+        marshals on host with one batch inversion -> uint8 [n, 64].  The noise and Krum kernels
+        queue behind the copy instead of waiting for the host to finish with the commitments."""
         n = qdelta.shape[0]
         if n == 0:
-            return np.zeros((0, 64), np.uint8)
+            return _Ready(np.zeros((0, 64), np.uint8))
         rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
-        return B.marshal_host(self.eng.commit_rows(qdelta.contiguous(), rows))
+        jac = self.eng.commit_rows(qdelta.contiguous(), rows)
+        host = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
+        host.copy_(jac, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return _PendingCommitments(host, ev)
+
+    def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
+        return self.commitments_async(qdelta).result()
 
     def shares(self, qdelta: torch.Tensor):
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
@@ -253,7 +285,7 @@ class BiscottiEngine:
         with tm.phase("local_step"):
             delta, qdelta = self.task.step(self.W, it, local_workers)
         with tm.phase("commit"):
-            commits_local = self.crypto.commitments(qdelta)
+            pending_commits = self.crypto.commitments_async(qdelta)
         with tm.phase("vrf_join"):
             outs = fut_noise.result() if fut_noise is not None else []
             sel = R.select_noisers_batch(stake, [beta for beta, _ in outs], local_workers, cfg.num_noisers,
@@ -261,10 +293,9 @@ class BiscottiEngine:
             noisers = dict(zip(local_workers, sel))
         with tm.phase("noise"):
             if cfg.noising and self.sigma > 0 and local_workers:
-                nz = torch.tensor([noisers[w] for w in local_workers], dtype=torch.int32, device=self.dev)
-                sc = torch.tensor([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma)
-                                    for j in noisers[w]] for w in local_workers], dtype=torch.float32,
-                                  device=self.dev)
+                nz = h2d([noisers[w] for w in local_workers], torch.int32, self.dev)
+                sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma)
+                           for j in noisers[w]] for w in local_workers], torch.float32, self.dev)
                 noised = K.dp_noise(delta, nz, sc, cfg.seed, it)
             else:
                 noised = delta
@@ -272,12 +303,17 @@ class BiscottiEngine:
         with tm.phase("verify"):
             row_of = {w: i for i, w in enumerate(local_workers)}
             single = comm.world == 1
-            if single:
-                commit_of = {w: commits_local[row_of[w]].tobytes() for w in local_workers}
-            else:
+            commit_of: dict = {}
+
+            def _materialize_commits():  # single rank: first use, after the Krum kernels are queued
+                if not commit_of and local_workers:
+                    cl = pending_commits.result()
+                    commit_of.update({w: cl[row_of[w]].tobytes() for w in local_workers})
+            if not single:
+                commits_local = pending_commits.result()
                 cbuf = torch.zeros((self.maxlocal, 64), dtype=torch.uint8, device=self.dev)
                 if local_workers:
-                    lidx = torch.tensor([w - self.lo for w in local_workers], dtype=torch.long, device=self.dev)
+                    lidx = h2d([w - self.lo for w in local_workers], torch.long, self.dev)
                     cbuf.index_copy_(0, lidx, torch.from_numpy(commits_local).to(self.dev))
                 commits_all = comm.all_gather(cbuf).reshape(-1, 64).cpu().numpy()
                 commit_of = {w: commits_all[self.flat[w]].tobytes() for w in workers}
@@ -294,15 +330,15 @@ class BiscottiEngine:
             if cfg.verification and inbox:
                 nv, ni = len(plan.verifiers), len(inbox)
                 if single:
-                    X = noised.index_select(0, torch.tensor([row_of[w] for w in inbox], dtype=torch.long,
-                                                            device=self.dev)) if local_verifiers else None
+                    X = noised.index_select(0, h2d([row_of[w] for w in inbox], torch.long, self.dev)) \
+                        if local_verifiers else None
                 else:
                     nbuf = torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev)
                     if local_workers:
                         nbuf.index_copy_(0, lidx, noised)
                     gathered = comm.all_gather(nbuf).reshape(-1, self.d)
-                    X = gathered.index_select(0, torch.tensor([self.flat[w] for w in inbox], dtype=torch.long,
-                                                              device=self.dev)) if local_verifiers else None
+                    X = gathered.index_select(0, h2d([self.flat[w] for w in inbox], torch.long, self.dev)) \
+                        if local_verifiers else None
                 acc_np = np.zeros((nv, ni), np.uint8)
                 sig_np = np.zeros((nv, ni, 64), np.uint8)
                 krum_cache = None
@@ -317,6 +353,7 @@ class BiscottiEngine:
                         else:
                             accept = self._verify(X, inbox, it, v)
                     vi = plan.verifiers.index(v)
+                    _materialize_commits()
                     sks.append(self.sk[v])
                     bases.append(_seed_bytes(cfg.seed, f"nonce-{it}", v))
                     for w, a_ in zip(inbox, accept):
@@ -361,6 +398,7 @@ class BiscottiEngine:
                 approved, _ = fsm.approve(accepted_map)
             else:
                 approved, _ = fsm.approve({})
+            _materialize_commits()
         # ---------------------------------------------------------------- aggregation + block
         if cfg.secure_agg:
             block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, row_of,
@@ -426,7 +464,7 @@ class BiscottiEngine:
             local_approved = [w for w in approved if w in self.local]
             pts = ys = None
             if local_approved and routes:  # workers share as soon as any miner is reachable
-                sel = torch.tensor([row_of[w] for w in local_approved], dtype=torch.long, device=self.dev)
+                sel = h2d([row_of[w] for w in local_approved], torch.long, self.dev)
                 pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
             ap_row = {w: i for i, w in enumerate(local_approved)}
         if not (lv.leader_online and lv.quorum):
@@ -443,7 +481,7 @@ class BiscottiEngine:
         with tm.phase("share_exchange"):
             recv: dict = {}  # miner -> (pts [E, nch, spm+1, pw] or None, ys [E, nch, spm], rows or None)
             if single:
-                rows = torch.tensor([ap_row[w] for w in node_list], dtype=torch.long, device=self.dev)
+                rows = h2d([ap_row[w] for w in node_list], torch.long, self.dev)
                 for m in contributing:
                     recv[m] = (None, None, rows)
             else:
@@ -452,8 +490,8 @@ class BiscottiEngine:
                     ents = [(m, w) for m in contributing if comm.owner(m, self.N) == dst
                             for w in node_list if w in ap_row]
                     if ents:
-                        ir = torch.tensor([ap_row[w] for _, w in ents], dtype=torch.long, device=self.dev)
-                        ic = torch.tensor([cols_of(part_of[m]) for m, _ in ents], dtype=torch.long, device=self.dev)
+                        ir = h2d([ap_row[w] for _, w in ents], torch.long, self.dev)
+                        ic = h2d([cols_of(part_of[m]) for m, _ in ents], torch.long, self.dev)
                         g = pts[ir[:, None, None], ar[None, :, None], ic[:, None, :]]
                         gy = ys[ir[:, None, None], ar[None, :, None], ic[:, None, :spm]]
                         send_p.append(g.reshape(-1))
@@ -486,7 +524,7 @@ class BiscottiEngine:
                 cols = np.concatenate([(base + np.asarray(cols_of(part_of[m]))[None, :]).reshape(-1)
                                        for m in contributing])
                 flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-                _ = B.sum_rows(flat, rows.int(), torch.from_numpy(cols.astype(np.int32)).to(self.dev))
+                _ = B.sum_rows(flat, rows.int(), h2d(cols.astype(np.int32), torch.int32, self.dev))
                 ysum = ys.index_select(0, rows).sum(0)   # [nch, T]
                 for ci, m in enumerate(contributing):
                     agg_y[ci] = ysum[:, spm * part_of[m]: spm * part_of[m] + spm]
@@ -497,8 +535,8 @@ class BiscottiEngine:
                     p_, y_, rows = recv[m]
                     part = part_of[m]
                     if rows is not None:  # single rank (CPU): aggregate straight out of the share tensors
-                        cols = torch.tensor([k * (T + 1) + c for k in range(nch) for c in cols_of(part)],
-                                            dtype=torch.long, device=self.dev)
+                        cols = h2d([k * (T + 1) + c for k in range(nch) for c in cols_of(part)], torch.long,
+                                   self.dev)
                         flat = pts.view(pts.shape[0], nch * (T + 1), pw)
                         _ = self.crypto.sum_rows(flat.index_select(0, rows).index_select(1, cols))
                         agg_y[ci] = ys.index_select(0, rows)[:, :, spm * part: spm * part + spm].sum(0)
@@ -516,7 +554,7 @@ class BiscottiEngine:
                     cols.append(agg_all[o, ci])
                     xs += [spm * part_of[m] + s_ - 10 for s_ in range(spm)]
                 agg = torch.cat(cols, dim=1).contiguous()      # [nchunks, npts]
-                xs_t = torch.tensor(xs, dtype=torch.int32, device=self.dev)
+                xs_t = h2d(xs, torch.int32, self.dev)
                 with tm.phase("recover.kernel"):
                     W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
                     st = status.cpu().numpy()
