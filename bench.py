@@ -106,6 +106,7 @@ def main() -> int:
         }
         print(json.dumps(out), flush=True)
     comm.barrier()
+    eng.close()
     comm.shutdown()
     return 0
 

@@ -17,6 +17,10 @@
 //    kernel.  Full-vector commitment = sum of chunk commitments (PK slices are consecutive).
 //  * Blocks are remapped XCD-contiguously (chunk-major order), so one chunk's table lines are
 //    pulled into a single XCD's L2.
+#include <hip/hip_ext.h>
+
+#include <vector>
+
 #include "bn256_dev.h"
 
 using namespace bn;
@@ -504,3 +508,29 @@ extern "C" int bsc_to_affine(const uint32_t* pts, int n, uint32_t* out, void* st
   hipLaunchKernelGGL(k_to_affine, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, pts, n, out);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------ streams
+// A stream restricted to a subset of the CUs: the speculative share/commitment MSMs run there so
+// the protocol's critical-path kernels (noise, Krum, aggregation) always find idle CUs -- HIP
+// stream priorities only order dispatch, they do not preempt the MSM's long-lived waves.
+// `skip_every` = 4 leaves every 4th CU (spread over all XCDs / shader engines) out of the mask.
+extern "C" void* bsc_stream_create_cumask(int skip_every, int* ncu_used) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return nullptr;
+  const int ncu = prop.multiProcessorCount;
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  int used = 0;
+  for (int c = 0; c < ncu; ++c) {
+    if (skip_every > 0 && c % skip_every == skip_every - 1) continue;
+    mask[c / 32] |= 1u << (c % 32);
+    ++used;
+  }
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+  if (ncu_used) *ncu_used = used;
+  return (void*)st;
+}
+
+extern "C" int bsc_stream_destroy(void* st) { return (int)hipStreamDestroy((hipStream_t)st); }

@@ -42,8 +42,8 @@ class SoftmaxTask:
             o += X.shape[0]
         self.X = torch.from_numpy(np.concatenate(Xs).astype(np.float32)).to(self.device)
         self.y = torch.from_numpy(np.concatenate(ys).astype(np.int32)).to(self.device)
-        self.off = h2d(offs, torch.int64, self.device)
-        self.ntrain = h2d(ns, torch.int32, self.device)
+        self.off = torch.tensor(offs, dtype=torch.int64, device=self.device)
+        self.ntrain = torch.tensor(ns, dtype=torch.int32, device=self.device)
         self.test_X = torch.from_numpy(fed.test_X).to(self.device)
         self.test_y = torch.from_numpy(fed.test_y.astype(np.int32)).to(self.device)
         self.att_X = torch.from_numpy(fed.attack_X).to(self.device)
@@ -114,8 +114,8 @@ class LogisticTask:
             ns.append(n)
         self.X = torch.from_numpy(np.concatenate(Xs)).to(self.device)
         self.y = torch.from_numpy(np.concatenate(ys)).to(self.device)
-        self.off = h2d(offs, torch.int64, self.device)
-        self.nrows = h2d(ns, torch.int32, self.device)
+        self.off = torch.tensor(offs, dtype=torch.int64, device=self.device)
+        self.nrows = torch.tensor(ns, dtype=torch.int32, device=self.device)
         # diffPriv16 noise at source: sigma = sqrt(2 ln 1.25)/epsilon (logistic_model.py:81)
         s = math.sqrt(2 * math.log(1.25)) / epsilon if epsilon > 0 else 0.0
         colluders = colluders or set()

@@ -21,6 +21,8 @@ SIGNATURES = {
     "bsc_segment_sum": [P, I, I, I, I, P, P],
     "bsc_sum_rows2": [P, I, P, I, P, I, P, P],
     "bsc_commit_rows": [P, I, P, I, P, I, I, P, P, P],
+    "bsc_stream_create_cumask": [I, P],
+    "bsc_stream_destroy": [P],
     "bsc_marshal": [P, I, P, P],
     "bsc_to_affine": [P, I, P, P],
     # ml.hip
@@ -34,10 +36,13 @@ SIGNATURES = {
 }
 
 
+RESTYPES = {"bsc_stream_create_cumask": C.c_void_p}
+
+
 def declare(lib) -> None:
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name, None)
         if fn is None:
             continue
         fn.argtypes = args
-        fn.restype = C.c_int
+        fn.restype = RESTYPES.get(name, C.c_int)

@@ -113,7 +113,7 @@ class DeviceCommitEngine:
         del scratch
 
     # ---------------------------------------------------------------- per-round kernels
-    def shares(self, coeffs: torch.Tensor, rows: torch.Tensor, commit_only: bool = False):
+    def shares(self, coeffs: torch.Tensor, rows: torch.Tensor, commit_only: bool = False, check_rows: bool = True):
         """Fused chunk commitments (+ witnesses and share values unless commit_only).
 
         coeffs: int64 [P, d] quantized deltas; rows: int32 [n] rows of `coeffs` to process.
@@ -122,7 +122,7 @@ class DeviceCommitEngine:
         assert coeffs.dtype == torch.int64 and coeffs.dim() == 2 and coeffs.shape[1] == self.d
         assert rows.dtype == torch.int32 and rows.dim() == 1
         n = rows.numel()
-        if n:
+        if n and check_rows:  # .item() synchronises the stream: callers passing arange skip it
             assert int(rows.min()) >= 0 and int(rows.max()) < coeffs.shape[0], "row index out of range"
         S = 1 if commit_only else self.T + 1
         pts = torch.empty((n, self.nchunks, S, 24), dtype=torch.int32, device=self.device)
@@ -133,7 +133,7 @@ class DeviceCommitEngine:
                "shares_msm")
         return pts, ys
 
-    def commit_rows(self, coeffs: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    def commit_rows(self, coeffs: torch.Tensor, rows: torch.Tensor, check_rows: bool = True) -> torch.Tensor:
         """Full-vector commitments sum_i c_i PK[i] of the given rows, Jacobian [n, 24] (commit phase)."""
         assert coeffs.dtype == torch.int64 and coeffs.dim() == 2 and coeffs.shape[1] == self.d
         assert rows.dtype == torch.int32 and rows.dim() == 1
@@ -141,7 +141,8 @@ class DeviceCommitEngine:
         out = torch.empty((n, 24), dtype=torch.int32, device=self.device)
         if n == 0:
             return out
-        assert int(rows.min()) >= 0 and int(rows.max()) < coeffs.shape[0], "row index out of range"
+        if check_rows:
+            assert int(rows.min()) >= 0 and int(rows.max()) < coeffs.shape[0], "row index out of range"
         nslab = (self.d + 1023) // 1024
         partial = torch.empty((n * nslab, 24), dtype=torch.int32, device=self.device)
         _check(hip().bsc_commit_rows(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), self.b0, self.nw,
@@ -212,3 +213,18 @@ def point_op(a_aff: torch.Tensor, b_aff: torch.Tensor, ks: torch.Tensor, op: int
 def host_commit_key(d: int, secret: int = 2):
     """Reference commitment key PK[i] = secret^i * G1 (DistSys/publicKey.go:26-61)."""
     return rt().CommitKey.generate(d, secret)
+
+
+def cu_masked_stream(device, skip_every: int = 4):
+    """A torch stream bound to (1 - 1/skip_every) of the device's CUs (hipExtStreamCreateWithCUMask).
+
+    Long-running speculative MSMs go there so the protocol's critical-path kernels keep a quarter
+    of the CUs to themselves.  Returns (stream, cus_used); the HIP stream lives for the process."""
+    import ctypes
+
+    used = ctypes.c_int(0)
+    with torch.cuda.device(device):
+        ptr = hip().bsc_stream_create_cumask(int(skip_every), ctypes.byref(used))
+    if not ptr:
+        raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+    return torch.cuda.ExternalStream(ptr, device=device), used.value

@@ -62,6 +62,7 @@ def main(argv=None) -> int:
         sys.stdout.write(eng.print_chain())
         sys.stdout.flush()
     comm.barrier()
+    eng.close()
     comm.shutdown()
     return 0
 

@@ -52,6 +52,7 @@ class RunConfig:
     log_every_peer: bool = False    # one Train Error line per local peer (reference style)
     deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
     phase_sync: bool = True         # device sync at phase boundaries (accurate per-phase GPU times)
+    side_stream_skip_every: int = 4  # speculative-MSM stream leaves every Nth CU free (0: no CU mask)
 
     def protocol(self, rt):
         pc = rt.ProtocolConfig()

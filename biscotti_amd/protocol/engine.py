@@ -85,7 +85,7 @@ class HostCrypto:
         self.nchunks = (self.d + poly - 1) // poly
         self.threads = threads
 
-    def commitments_async(self, qdelta: torch.Tensor):
+    def commitments_async(self, qdelta: torch.Tensor, stream=None):
         return _Ready(self.commitments(qdelta))
 
     def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
@@ -118,19 +118,24 @@ class DeviceCrypto:
         self.eng = B.DeviceCommitEngine(key, poly, T, device)
         self.d, self.poly, self.T, self.nchunks = self.eng.d, poly, T, self.eng.nchunks
 
-    def commitments_async(self, qdelta: torch.Tensor):
+    def commitments_async(self, qdelta: torch.Tensor, stream=None):
         """Fixed-base MSM on device, queued download into pinned memory; result() waits for it and
         marshals on host with one batch inversion -> uint8 [n, 64].  The noise and Krum kernels
         queue behind the copy instead of waiting for the host to finish with the commitments."""
         n = qdelta.shape[0]
         if n == 0:
             return _Ready(np.zeros((0, 64), np.uint8))
-        rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
-        jac = self.eng.commit_rows(qdelta.contiguous(), rows)
-        host = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
-        host.copy_(jac, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        main = torch.cuda.current_stream()
+        stream = stream or main
+        stream.wait_stream(main)
+        with torch.cuda.stream(stream):
+            rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
+            jac = self.eng.commit_rows(qdelta.contiguous(), rows, check_rows=False)
+            host = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
+            host.copy_(jac, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        qdelta.record_stream(stream)
         return _PendingCommitments(host, ev)
 
     def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
@@ -139,6 +144,21 @@ class DeviceCrypto:
     def shares(self, qdelta: torch.Tensor):
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
         return self.eng.shares(qdelta, rows)
+
+    def shares_async(self, qdelta: torch.Tensor, rows: list, stream):
+        """Shares + witnesses of qdelta[rows] on `stream` (the caller's work keeps flowing on its own
+        stream); returns (pts, ys, event).  Consumers wait on the event before touching them."""
+        main = torch.cuda.current_stream()
+        stream.wait_stream(main)                       # qdelta is produced on the main stream
+        with torch.cuda.stream(stream):
+            rows_t = h2d(rows, torch.int32, qdelta.device)
+            pts, ys = self.eng.shares(qdelta, rows_t, check_rows=False)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        qdelta.record_stream(stream)
+        for t in (pts, ys):                            # allocated on `stream`, consumed on main
+            t.record_stream(main)
+        return pts, ys, ev
 
     def sum_rows(self, pts: torch.Tensor) -> torch.Tensor:
         """[R, C, 24] -> [C, 24]"""
@@ -200,6 +220,16 @@ class BiscottiEngine:
         else:
             key = self.R.CommitKey.generate(self.d, 2)  # publicKey.go: s = 2
         self.T = self.pc.total_shares
+        if self.gpu:
+            # protocol critical path on a high-priority stream; speculative share MSMs on a
+            # low-priority one so they fill the GPU while the host waits for VRF proofs / Krum
+            lo, hi = torch.cuda.Stream.priority_range()
+            self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
+            # speculative MSMs: a stream masked to 3/4 of the CUs (critical path keeps the rest)
+            self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, cfg.side_stream_skip_every) \
+                if cfg.side_stream_skip_every > 0 else (torch.cuda.Stream(device=self.dev, priority=lo), 0)
+            torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
+            torch.cuda.set_stream(self.main_stream)
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
             HostCrypto(key, cfg.poly_size, self.T, cfg.host_threads)
         self.nchunks = self.crypto.nchunks
@@ -217,6 +247,28 @@ class BiscottiEngine:
         self.sigma = self.task.noise_sigma(cfg.epsilon)
         self.stats = {"unmasked_updates": 0, "total_updates": 0}
         self.rounds_done = 0
+        self._head = None
+        import atexit
+        import weakref
+        ref = weakref.ref(self)
+        atexit.register(lambda: ref() is not None and ref().close())
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self) -> None:
+        """Join the pre-opened round's native VRF jobs, drain the device and release the CU-masked
+        stream.  Idempotent; also registered with atexit so interpreter teardown never races
+        native threads or a live HIP stream."""
+        head, self._head = self._head, None
+        if head:
+            for k in ("fut_noise", "fut_roles"):
+                if head.get(k) is not None:
+                    head[k].result()
+        if self.gpu and getattr(self, "side_stream", None) is not None:
+            torch.cuda.synchronize(self.dev)
+            torch.cuda.set_stream(torch.cuda.default_stream(self.dev))
+            if getattr(self, "side_cus", 0):
+                B.hip().bsc_stream_destroy(self.side_stream.cuda_stream)
+            self.side_stream = None
 
     # ------------------------------------------------------------------ helpers
     def _now(self, iteration: int) -> int:
@@ -258,34 +310,63 @@ class BiscottiEngine:
         return g[r, peer - self.comm.peer_range(self.N, r).start]
 
     # ------------------------------------------------------------------ the round
+    def _open_round(self) -> dict:
+        """Round head: live set, committee plan and the asynchronous noiser / roles VRF proofs.
+
+        It depends only on the latest block, so it is opened as soon as that block is committed
+        (overlapping the previous round's evaluation and logging) and consumed by run_round."""
+        cfg, R, fsm = self.cfg, self.R, self.fsm
+        live = self._live_mask()
+        plan = fsm.begin_round(live)
+        head = {"live": live, "plan": plan}
+        if plan.done:
+            return head
+        latest_hash = fsm.chain.latest().hash
+        workers = [w for w in plan.workers if live[w]]
+        local_workers = [w for w in workers if w in self.local]
+        # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  The host
+        # proofs run on native threads while the GPU does the local step and the commitments; the
+        # noise phase joins them.
+        seeds = [self.vrf_noise_seed[w] for w in local_workers]
+        fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads) if seeds else None
+        fut_roles = None
+        if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
+            fut_roles = R.vrf_prove_batch_async([self.vrf_roles_seed[p] for p in self.local if live[p]],
+                                                latest_hash, cfg.roles_vrf_threads, fut_noise)
+        head.update(workers=workers, local_workers=local_workers, stake=dict(fsm.stake), fut_noise=fut_noise,
+                    fut_roles=fut_roles)
+        return head
+
     def run_round(self) -> RoundResult | None:
         cfg, R, fsm, comm = self.cfg, self.R, self.fsm, self.comm
         t_round = time.perf_counter()
         tm = self.timer
         with tm.phase("roles"):
-            live = self._live_mask()
-            plan = fsm.begin_round(live)
+            head, self._head = self._head or self._open_round(), None
+            live, plan = head["live"], head["plan"]
             if plan.done:
                 return None
             it = plan.iteration
-            latest_hash = fsm.chain.latest().hash
-            workers = [w for w in plan.workers if live[w]]
-            local_workers = [w for w in workers if w in self.local]
-            # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  The host
-            # proofs run on a side thread (the native prover drops the GIL) while the GPU does the
-            # local step and the commitments; the noise phase joins them.
-            seeds = [self.vrf_noise_seed[w] for w in local_workers]
-            stake = dict(fsm.stake)
-            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads) if seeds else None
-            fut_roles = None
-            if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
-                fut_roles = R.vrf_prove_batch_async([self.vrf_roles_seed[p] for p in self.local if live[p]],
-                                                    latest_hash, cfg.roles_vrf_threads, fut_noise)
+            workers, local_workers, stake = head["workers"], head["local_workers"], head["stake"]
+            fut_noise, fut_roles = head["fut_noise"], head["fut_roles"]
         # ---------------------------------------------------------------- local step + commitments
         with tm.phase("local_step"):
             delta, qdelta = self.task.step(self.W, it, local_workers)
         with tm.phase("commit"):
-            pending_commits = self.crypto.commitments_async(qdelta)
+            side = self.side_stream if self.gpu else None
+            pending_commits = self.crypto.commitments_async(qdelta, side)
+            # only the first krum_thresh arrivals reach the verifiers (verifier_inbox), so only they
+            # can be approved: they secret-share while verification runs (kyber.go:533-646), the MSM
+            # on the side stream; shares of workers the verifiers reject are simply never routed
+            inbox = fsm.verifier_inbox(workers) if cfg.verification else []
+            row_of = {w: i for i, w in enumerate(local_workers)}
+            spec = None
+            if self.gpu and cfg.secure_agg and local_workers:
+                cand = set(inbox) if cfg.verification else set(workers)
+                spec_workers = [w for w in local_workers if w in cand]
+                if spec_workers:
+                    spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
+                                                                   side))
         with tm.phase("vrf_join"):
             outs = fut_noise.result() if fut_noise is not None else []
             sel = R.select_noisers_batch(stake, [beta for beta, _ in outs], local_workers, cfg.num_noisers,
@@ -301,7 +382,6 @@ class BiscottiEngine:
                 noised = delta
         # ---------------------------------------------------------------- verification
         with tm.phase("verify"):
-            row_of = {w: i for i, w in enumerate(local_workers)}
             single = comm.world == 1
             commit_of: dict = {}
 
@@ -325,7 +405,6 @@ class BiscottiEngine:
             accepted_map: dict = {}
             signatures: dict = {}
             pending_signatures = None
-            inbox = fsm.verifier_inbox(workers) if cfg.verification else []
             local_verifiers = [v for v in plan.verifiers if live[v] and v in self.local]
             if cfg.verification and inbox:
                 nv, ni = len(plan.verifiers), len(inbox)
@@ -402,7 +481,7 @@ class BiscottiEngine:
         # ---------------------------------------------------------------- aggregation + block
         if cfg.secure_agg:
             block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, row_of,
-                                             commit_of, signatures)
+                                             commit_of, signatures, spec)
         else:
             block = self._plain_aggregation(plan, live, approved, delta, noised, local_workers, commit_of,
                                             signatures)
@@ -415,6 +494,8 @@ class BiscottiEngine:
             if cfg.chain_file and comm.rank == 0:
                 R.Blockchain.append_to_file(cfg.chain_file, block)
             self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
+        with tm.phase("next_head"):
+            self._head = self._open_round()   # next round's committee + VRF proofs start now
         if pending_signatures is not None:  # every rank, same point: the collective stays aligned
             pending_signatures()
         with tm.phase("eval"):
@@ -447,7 +528,7 @@ class BiscottiEngine:
 
     # ------------------------------------------------------------------ secure aggregation path
     def _secure_aggregation(self, plan, live, approved, delta, qdelta, local_workers, row_of, commit_of,
-                            signatures):
+                            signatures, spec=None):
         cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
         self._last_nodes = []
         spm, T, nch = self.pc.shares_per_miner, self.T, self.nchunks
@@ -463,10 +544,16 @@ class BiscottiEngine:
             lv = fsm.leader_view(routes)
             local_approved = [w for w in approved if w in self.local]
             pts = ys = None
-            if local_approved and routes:  # workers share as soon as any miner is reachable
-                sel = h2d([row_of[w] for w in local_approved], torch.long, self.dev)
-                pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
             ap_row = {w: i for i, w in enumerate(local_approved)}
+            if local_approved and routes:  # workers share as soon as any miner is reachable
+                spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
+                if spec is not None and all(w in spec_row for w in local_approved):
+                    pts, ys, ev = spec[1]
+                    torch.cuda.current_stream().wait_event(ev)
+                    ap_row = {w: spec_row[w] for w in local_approved}   # rows of the speculative tensors
+                else:
+                    sel = h2d([row_of[w] for w in local_approved], torch.long, self.dev)
+                    pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
         if not (lv.leader_online and lv.quorum):
             return None
         node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
