@@ -60,8 +60,10 @@ def main() -> int:
     t0 = time.perf_counter()
     last = None
     phases: dict = {}
+    accs = []
     for _ in range(a.steps):
         last = eng.run_round()
+        accs.append(1.0 - last.test_error)
         for k, v in last.phases.items():
             phases[k] = phases.get(k, 0.0) + v
     sync()
@@ -90,6 +92,7 @@ def main() -> int:
             "vs_baseline": s_per_round / BASELINE_S_PER_ROUND,
             "speedup_vs_baseline": BASELINE_S_PER_ROUND / s_per_round,
             "final_test_acc": acc,
+            "test_acc_last10_mean": sum(accs[-10:]) / max(1, len(accs[-10:])),
             "baseline_test_acc": BASELINE_ACC,
             "rounds_total": eng.rounds_done,
             "dtype": "fp32 model / fp64 ledger / exact BN256",

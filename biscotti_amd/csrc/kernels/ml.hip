@@ -303,50 +303,54 @@ extern "C" __global__ void __launch_bounds__(64) k_gram_f64(const float* X, int 
   }
 }
 
-// K5b: reduce partials, distances, Krum scores and Multi-Krum selection; one block, n <= 128.
-// score_i = sum(sort(D_i)[1:groupsize-1]): computed without sorting -- every D_ij gets its rank in
-// row i by parallel counting (ties broken by column index) and rank in [1, groupsize-2] is summed.
-// Accept the n_accept lowest scores (index tiebreak).  Everything lives in LDS.
-extern "C" __global__ void __launch_bounds__(256) k_krum_select(const double* part, int nsplit, int n, int npad,
-                                                               int groupsize, int n_accept, double* dist,
-                                                               double* scores, int* accept) {
-  __shared__ double D[128 * 128];
-  __shared__ double sc[128];
-  __shared__ uint8_t keep[128 * 128];
-  const int t = threadIdx.x;
-  for (int idx = t; idx < n * n; idx += blockDim.x) {
-    const int i = idx / n, j = idx % n;
-    double g = 0.0;
-    for (int s = 0; s < nsplit; ++s) g += part[((size_t)s * npad + i) * npad + j];
-    D[idx] = g;  // Gram matrix for now
+// K5b: Krum scores, one wave per row i (n blocks): reduce the split-K Gram partials of row i and of
+// the diagonal, D_ij = G_ii + G_jj - 2 G_ij, then score_i = sum of D_ij whose rank in row i lies in
+// [1, groupsize-2] -- the sum of the groupsize-2 nearest neighbours after the zero self-distance
+// (sort(D_i)[1:groupsize-1], client_obj.py:114-143).  Ranks by parallel counting, ties broken by
+// column index; the kept distances are summed in column order (bit-reproducible).  n <= 128.
+extern "C" __global__ void __launch_bounds__(64) k_krum_scores(const double* part, int nsplit, int n, int npad,
+                                                              int groupsize, double* dist, double* scores) {
+  __shared__ double row[128];
+  __shared__ double kept[128];
+  const int i = blockIdx.x, lane = threadIdx.x;
+  double gii = 0.0;
+  for (int s = 0; s < nsplit; ++s) gii += part[((size_t)s * npad + i) * npad + i];
+  for (int j = lane; j < n; j += 64) {
+    double gij = 0.0, gjj = 0.0;
+    for (int s = 0; s < nsplit; ++s) {
+      gij += part[((size_t)s * npad + i) * npad + j];
+      gjj += part[((size_t)s * npad + j) * npad + j];
+    }
+    const double d = gii + gjj - 2.0 * gij;
+    row[j] = d;
+    dist[(size_t)i * n + j] = d;
   }
   __syncthreads();
-  for (int idx = t; idx < n * n; idx += blockDim.x) {
-    const int i = idx / n, j = idx % n;
-    dist[idx] = D[i * n + i] + D[j * n + j] - 2.0 * D[idx];
-  }
-  __syncthreads();
-  for (int idx = t; idx < n * n; idx += blockDim.x) D[idx] = dist[idx];
-  __syncthreads();
-  for (int idx = t; idx < n * n; idx += blockDim.x) {
-    const int i = idx / n, j = idx % n;
-    const double v = D[idx];
+  for (int j = lane; j < n; j += 64) {
+    const double v = row[j];
     int rank = 0;
     for (int k = 0; k < n; ++k) {
-      const double u = D[i * n + k];
+      const double u = row[k];
       rank += (u < v) || (u == v && k < j);
     }
-    keep[idx] = (rank >= 1 && rank < groupsize - 1) ? 1 : 0;
+    kept[j] = (rank >= 1 && rank < groupsize - 1) ? v : 0.0;
   }
   __syncthreads();
-  if (t < n) {  // fixed summation order -> bit-reproducible scores
+  if (lane == 0) {
     double a = 0.0;
-    for (int j = 0; j < n; ++j) a += keep[t * n + j] ? D[t * n + j] : 0.0;
-    sc[t] = a;
+    for (int j = 0; j < n; ++j) a += kept[j];
+    scores[i] = a;
   }
+}
+
+// K5c: Multi-Krum selection: accept the n_accept lowest scores (index tiebreak).  One block.
+extern "C" __global__ void __launch_bounds__(128) k_krum_accept(const double* scores, int n, int n_accept,
+                                                               int* accept) {
+  __shared__ double sc[128];
+  const int t = threadIdx.x;
+  if (t < n) sc[t] = scores[t];
   __syncthreads();
   if (t < n) {
-    scores[t] = sc[t];
     int rank = 0;
     for (int j = 0; j < n; ++j) rank += (sc[j] < sc[t]) || (sc[j] == sc[t] && j < t);
     accept[t] = rank < n_accept ? 1 : 0;
@@ -535,8 +539,9 @@ extern "C" int bsc_krum(const float* X, int n, int D, int ksplit, double* part, 
   const int nsplit = (D + ksplit - 1) / ksplit;
   hipLaunchKernelGGL(k_gram_f64, dim3(tiles, tiles, nsplit), dim3(64), 0, (hipStream_t)stream, X, n, D, ksplit,
                      part);
-  hipLaunchKernelGGL(k_krum_select, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nsplit, n, tiles * 16,
-                     groupsize, n_accept, dist, scores, accept);
+  hipLaunchKernelGGL(k_krum_scores, dim3(n), dim3(64), 0, (hipStream_t)stream, part, nsplit, n, tiles * 16,
+                     groupsize, dist, scores);
+  hipLaunchKernelGGL(k_krum_accept, dim3(1), dim3(128), 0, (hipStream_t)stream, scores, n, n_accept, accept);
   return (int)hipGetLastError();
 }
 

@@ -335,6 +335,27 @@ class BiscottiEngine:
                                                 latest_hash, cfg.roles_vrf_threads, fut_noise)
         head.update(workers=workers, local_workers=local_workers, stake=dict(fsm.stake), fut_noise=fut_noise,
                     fut_roles=fut_roles)
+        # the local step, the commitments and the speculative shares depend only on the new global
+        # model too: queue them now, behind nothing but the block that produced it
+        tm, it = self.timer, plan.iteration
+        with tm.phase("local_step"):
+            delta, qdelta = self.task.step(self.W, it, local_workers)
+        with tm.phase("commit"):
+            pending_commits = self.crypto.commitments_async(qdelta)
+            # only the first krum_thresh arrivals reach the verifiers (verifier_inbox), so only they
+            # can be approved: they secret-share while verification runs (kyber.go:533-646), the MSM
+            # on the CU-masked side stream; shares of workers the verifiers reject are never routed
+            inbox = fsm.verifier_inbox(workers) if cfg.verification else []
+            row_of = {w: i for i, w in enumerate(local_workers)}
+            spec = None
+            if self.gpu and cfg.secure_agg and local_workers:
+                cand = set(inbox) if cfg.verification else set(workers)
+                spec_workers = [w for w in local_workers if w in cand]
+                if spec_workers:
+                    spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
+                                                                   self.side_stream))
+        head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inbox=inbox, row_of=row_of,
+                    spec=spec)
         return head
 
     def run_round(self) -> RoundResult | None:
@@ -349,24 +370,8 @@ class BiscottiEngine:
             it = plan.iteration
             workers, local_workers, stake = head["workers"], head["local_workers"], head["stake"]
             fut_noise, fut_roles = head["fut_noise"], head["fut_roles"]
-        # ---------------------------------------------------------------- local step + commitments
-        with tm.phase("local_step"):
-            delta, qdelta = self.task.step(self.W, it, local_workers)
-        with tm.phase("commit"):
-            side = self.side_stream if self.gpu else None
-            pending_commits = self.crypto.commitments_async(qdelta, side)
-            # only the first krum_thresh arrivals reach the verifiers (verifier_inbox), so only they
-            # can be approved: they secret-share while verification runs (kyber.go:533-646), the MSM
-            # on the side stream; shares of workers the verifiers reject are simply never routed
-            inbox = fsm.verifier_inbox(workers) if cfg.verification else []
-            row_of = {w: i for i, w in enumerate(local_workers)}
-            spec = None
-            if self.gpu and cfg.secure_agg and local_workers:
-                cand = set(inbox) if cfg.verification else set(workers)
-                spec_workers = [w for w in local_workers if w in cand]
-                if spec_workers:
-                    spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
-                                                                   side))
+            delta, qdelta, pending_commits = head["delta"], head["qdelta"], head["pending_commits"]
+            inbox, row_of, spec = head["inbox"], head["row_of"], head["spec"]
         with tm.phase("vrf_join"):
             outs = fut_noise.result() if fut_noise is not None else []
             sel = R.select_noisers_batch(stake, [beta for beta, _ in outs], local_workers, cfg.num_noisers,
