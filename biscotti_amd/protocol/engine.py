@@ -255,18 +255,25 @@ class BiscottiEngine:
 
     # ------------------------------------------------------------------ lifecycle
     def close(self) -> None:
-        """Join the pre-opened round's native VRF jobs, drain the device and release the CU-masked
-        stream.  Idempotent; also registered with atexit so interpreter teardown never races
-        native threads or a live HIP stream."""
+        """Join the pre-opened round's native VRF jobs and drain the device.  Idempotent; also
+        registered with atexit so interpreter teardown never races native threads."""
         head, self._head = self._head, None
         if head:
             for k in ("fut_noise", "fut_roles"):
                 if head.get(k) is not None:
                     head[k].result()
+        head = None  # drop the round's tensors while their streams are all still alive
         if self.gpu and getattr(self, "side_stream", None) is not None:
             torch.cuda.synchronize(self.dev)
             torch.cuda.set_stream(torch.cuda.default_stream(self.dev))
             if getattr(self, "side_cus", 0):
+                # every tensor used on the CU-masked stream is gone (round locals, the head above):
+                # flush the allocator's stream-use events, then release the stream before
+                # interpreter teardown (the HIP runtime must not be left to destroy it at exit)
+                import gc
+                gc.collect()
+                torch.cuda.synchronize(self.dev)
+                torch.cuda.empty_cache()
                 B.hip().bsc_stream_destroy(self.side_stream.cuda_stream)
             self.side_stream = None
 
