@@ -72,9 +72,13 @@ class SoftmaxTask:
         return delta, qdelta
 
     def evaluate(self, W: torch.Tensor) -> dict:
-        err = K.eval_error(self.test_X, self.test_y, W, self.d_in, self.d_out, transform=True)
-        att = K.eval_error(self.att_X, self.att_y, W, self.d_in, self.d_out, transform=True)
-        return {"test_error": err, "attack_rate": att}
+        return self.evaluate_async(W)()
+
+    def evaluate_async(self, W: torch.Tensor):
+        """Queue the test / attack evaluations now; the returned callable reads them back."""
+        err = K.eval_error_async(self.test_X, self.test_y, W, self.d_in, self.d_out, transform=True)
+        att = K.eval_error_async(self.att_X, self.att_y, W, self.d_in, self.d_out, transform=True)
+        return lambda: {"test_error": err(), "attack_rate": att()}
 
     def train_error(self, W: torch.Tensor, peer: int, iteration: int) -> float:
         """RONI's getTrainErr: error on a (random) minibatch of the verifier's own shard."""
@@ -148,6 +152,10 @@ class LogisticTask:
     def _err(self, X, y, W) -> float:
         yhat = torch.sign(X @ W)
         return float((yhat != y).sum()) / y.numel()
+
+    def evaluate_async(self, W: torch.Tensor):
+        v = self.evaluate(W)
+        return lambda: v
 
     def evaluate(self, W: torch.Tensor) -> dict:
         # logistic_model_test.py: train_error on credittrain, test_error on credittest

@@ -217,16 +217,25 @@ def krum(X, groupsize: int, n_accept: int, ksplit: int = 512):
 
 
 # ---------------------------------------------------------------------------- K2 evaluation
+def eval_error_async(X, y, W, d_in, d_out, transform=True):
+    """Queue the evaluation kernel; returns a zero-argument callable giving the error rate."""
+    N = X.shape[0]
+    if N == 0 or X.device.type != "cuda":
+        v = eval_error(X, y, W, d_in, d_out, transform)
+        return lambda: v
+    err = torch.zeros((1,), dtype=torch.int32, device=X.device)
+    _check(hip().bsc_eval_error(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), _p(err), _stream()),
+           "eval_error")
+    return lambda: float(err.item()) / N
+
+
 def eval_error(X, y, W, d_in, d_out, transform=True) -> float:
     """1 - accuracy of the softmax model W on (X, y) (client.getTestErr / get17AttackRate)."""
     N = X.shape[0]
     if N == 0:
         return 0.0
     if X.device.type == "cuda":
-        err = torch.zeros((1,), dtype=torch.int32, device=X.device)
-        _check(hip().bsc_eval_error(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), _p(err), _stream()),
-               "eval_error")
-        return float(err.item()) / N
+        return eval_error_async(X, y, W, d_in, d_out, transform)()
     Wm = W.to(torch.float32)
     xb = (X - 0.5) / 0.5 if transform else X
     logits = xb @ Wm[: d_out * d_in].view(d_out, d_in).T + Wm[d_out * d_in:]

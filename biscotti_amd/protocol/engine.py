@@ -506,12 +506,13 @@ class BiscottiEngine:
             if cfg.chain_file and comm.rank == 0:
                 R.Blockchain.append_to_file(cfg.chain_file, block)
             self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
+            eval_pending = self.task.evaluate_async(self.W)   # queued ahead of the next round's MSMs
         with tm.phase("next_head"):
             self._head = self._open_round()   # next round's committee + VRF proofs start now
         if pending_signatures is not None:  # every rank, same point: the collective stays aligned
             pending_signatures()
         with tm.phase("eval"):
-            ev = self.task.evaluate(self.W)
+            ev = eval_pending()
             if fut_roles is not None:
                 fut_roles.result()
         self.stats["total_updates"] += len(block.data.deltas)
