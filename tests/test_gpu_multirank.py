@@ -1,0 +1,72 @@
+"""Multi-rank engine on the GPU: 2 ranks share cuda:0 over the gloo backend (RCCL cannot put two
+ranks on one device), which runs every device-side multi-rank path -- all_gather of noised
+deltas, all_to_all of share tensors, leader gather, block broadcast -- and must reproduce the
+single-process GPU chain byte for byte (deterministic timestamps)."""
+import os
+import queue
+import sys
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+from test_distributed_cpu import ROOT, _free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, kw, rounds, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", BSC_TABLE_B0="10")
+    sys.path.insert(0, ROOT)
+    import torch
+
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    comm = Comm.init(backend="gloo") if world > 1 else Comm(device=torch.device("cuda", 0))
+    assert comm.device.type == "cuda"
+    eng = BiscottiEngine(RunConfig(**kw), comm)
+    for _ in range(rounds):
+        eng.run_round()
+    q.put((rank, [bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))]))
+    comm.barrier()
+    eng.close()
+    comm.shutdown()
+
+
+def _run(world, kw, rounds):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kw, rounds, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out, deadline = {}, time.time() + 400
+    try:
+        while len(out) < world:
+            try:
+                r, hashes = q.get(timeout=1.0)
+                out[r] = hashes
+            except queue.Empty:
+                if any(p.exitcode not in (None, 0) for p in ps) or time.time() > deadline:
+                    raise AssertionError("a rank failed: " + str([p.exitcode for p in ps]))
+        for p in ps:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+@pytest.mark.parametrize("secure_agg", [True, False])
+def test_gpu_two_ranks_match_single_process(secure_agg):
+    kw = dict(num_nodes=12, dataset="mnist", seed=5, deterministic_time=True, secure_agg=secure_agg,
+              max_iterations=100)
+    single = _run(1, kw, 3)[0]
+    multi = _run(2, kw, 3)
+    assert multi[0] == multi[1]
+    assert multi[0] == single
