@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--dataset", default="mnist")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--trace", default=None)
+    ap.add_argument("--fedsys", action="store_true",
+                    help="time the FedSys baseline (central server, -ns 35) instead of Biscotti")
     ap.add_argument("--phase-sync", action="store_true",
                     help="synchronise the GPU at every phase boundary (per-phase GPU attribution, slower)")
     a = ap.parse_args()
@@ -51,7 +53,13 @@ def main() -> int:
         torch.set_num_threads(min(4, torch.get_num_threads()))
     cfg = RunConfig(num_nodes=a.peers, dataset=a.dataset, seed=a.seed, max_iterations=10**9,
                     trace_file=a.trace, host_threads=16, phase_sync=a.phase_sync)
-    eng = BiscottiEngine(cfg, comm)
+    if a.fedsys:
+        from biscotti_amd.protocol.fedsys import FedSysEngine
+
+        cfg.perc_samples, cfg.epsilon = 35, 5.0      # FedSys/main.go:42,212 defaults
+        eng = FedSysEngine(cfg, comm)
+    else:
+        eng = BiscottiEngine(cfg, comm)
     sync = (lambda: torch.cuda.synchronize()) if eng.gpu else (lambda: None)
     for _ in range(a.warmup):
         eng.run_round()
@@ -77,10 +85,11 @@ def main() -> int:
     elapsed = float(t.item())
     s_per_round = elapsed / max(a.steps, 1)
     acc = 1.0 - last.test_error if last is not None else float("nan")
-    ok, why = eng.fsm.chain.verify()
+    ok, why = eng.fsm.chain.verify() if not a.fedsys else (True, "")
     if comm.rank == 0:
         out = {
-            "metric": "sec/round (block commit) + final test acc, MNIST 100 peers",
+            "metric": ("sec/round (FedSys baseline) + final test acc, MNIST 100 peers" if a.fedsys else
+                       "sec/round (block commit) + final test acc, MNIST 100 peers"),
             "value": s_per_round,
             "unit": "s/round",
             "n_gpus": comm.world if eng.gpu else 0,
@@ -94,7 +103,7 @@ def main() -> int:
             "final_test_acc": acc,
             "test_acc_last10_mean": sum(accs[-10:]) / max(1, len(accs[-10:])),
             "baseline_test_acc": BASELINE_ACC,
-            "rounds_total": eng.rounds_done,
+            "rounds_total": eng.rounds_done if not a.fedsys else eng.iteration,
             "dtype": "fp32 model / fp64 ledger / exact BN256",
             "data": f"synthetic ({eng.task.source if hasattr(eng.task, 'source') else a.dataset}: MNIST-shaped "
                     f"digits from sklearn 8x8 real digits, augmented)",
@@ -109,7 +118,8 @@ def main() -> int:
         }
         print(json.dumps(out), flush=True)
     comm.barrier()
-    eng.close()
+    if not a.fedsys:
+        eng.close()
     comm.shutdown()
     return 0
 
