@@ -1,7 +1,7 @@
 """Headline benchmark: Biscotti seconds per round (block commit) + final test accuracy,
 MNIST softmax regression, 100 peers (BASELINE.json; reference 29.83 s/round at 87.7%).
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W [--config NAME]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -10,14 +10,17 @@ Each step is one full protocol round with the reference defaults (3 verifiers, 3
 workers, BN256 commitments, noise, Krum + Schnorr signatures, Shamir shares with KZG-style
 witnesses, miner aggregation, exact recovery, gob+SHA-256 block, evaluation.  Peers are packed as
 virtual peers onto the N GPUs (strong scaling: 100 peers regardless of N).  Data: synthetic
-MNIST-shaped digits (see biscotti_amd/data), random/zero-init model as in the reference.
+MNIST-shaped digits (see biscotti_amd/data), zero-init model as in the reference.
+
+``--config`` selects the other BASELINE.md rows (each compared with its own reference number):
+fedsys, poison30, poison50_5v, churn10, scale40/60/80, secagg_off/verification_off/noising_off
+(100-peer increments), mnist10_dp1 and credit4 (no published number).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import math
-import os
 import sys
 import time
 
@@ -26,21 +29,46 @@ import torch
 BASELINE_S_PER_ROUND = 29.83   # nsdi-eval/scaleup/bis_baseline_100
 BASELINE_ACC = 0.877
 
+# name -> (RunConfig overrides, reference s/round or None, reference accuracy or None, extra refs, source)
+PRESETS = {
+    "headline": ({}, 29.83, 0.877, {}, "nsdi-eval/scaleup/bis_baseline_100"),
+    "fedsys": ({"fedsys": True, "perc_samples": 35, "epsilon": 5.0}, 3.42, 0.9365, {},
+               "nsdi-eval/scaleup/fed_baseline_100"),
+    "poison30": ({"num_nodes": 50, "poisoning": 0.3}, 1.98, 0.940, {"attack_rate": 0.052},
+                 "nsdi-eval/credit/bis_3v_30p:102"),
+    "poison50_5v": ({"num_nodes": 50, "poisoning": 0.5, "num_verifiers": 5}, None, 0.923, {"attack_rate": 0.075},
+                    "nsdi-eval/credit/bis_5v_50p:102"),
+    "churn10": ({"churn": 0.1}, None, None, {}, "BASELINE.json config 5 (reference churn runs: 25-31 s/round)"),
+    "scale40": ({"num_nodes": 40}, 23.87, None, {}, "nsdi-eval/increments/results.log:2"),
+    "scale60": ({"num_nodes": 60}, 34.05, None, {}, "nsdi-eval/increments/results.log:3"),
+    "scale80": ({"num_nodes": 80}, 48.07, None, {}, "nsdi-eval/increments/results.log:4"),
+    "secagg_off": ({"secure_agg": False}, 50.63, None, {}, "nsdi-eval/increments/results.log:10"),
+    "verification_off": ({"verification": False}, 19.95, None, {}, "nsdi-eval/increments/results.log:15"),
+    "noising_off": ({"noising": False}, 53.10, None, {}, "nsdi-eval/increments/results.log:20"),
+    "mnist10_dp1": ({"num_nodes": 10, "epsilon": 1.0}, None, None, {}, "BASELINE.json config 2"),
+    "credit4": ({"num_nodes": 4, "dataset": "creditcard", "noising": False, "num_verifiers": 1,
+                 "num_miners": 2, "num_noisers": 1, "epsilon": 0.0}, None, None, {}, "BASELINE.json config 1"),
+}
+
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--peers", type=int, default=100)
-    ap.add_argument("--dataset", default="mnist")
+    ap.add_argument("--config", default="headline", choices=sorted(PRESETS))
+    ap.add_argument("--peers", type=int, default=None, help="override the preset's peer count")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--trace", default=None)
-    ap.add_argument("--fedsys", action="store_true",
-                    help="time the FedSys baseline (central server, -ns 35) instead of Biscotti")
+    ap.add_argument("--fedsys", action="store_true", help="same as --config fedsys")
     ap.add_argument("--phase-sync", action="store_true",
                     help="synchronise the GPU at every phase boundary (per-phase GPU attribution, slower)")
     a = ap.parse_args()
+    if a.fedsys:
+        a.config = "fedsys"
+    over, ref_s, ref_acc, ref_extra, ref_src = PRESETS[a.config]
+    over = dict(over)
+    fedsys = over.pop("fedsys", False)
 
     from biscotti_amd.parallel.comm import Comm
     from biscotti_amd.protocol.config import RunConfig
@@ -51,12 +79,15 @@ def main() -> int:
         # the GPU path does little CPU tensor work; idle-spinning OpenMP workers would only steal the
         # cgroup CPU quota from the native crypto pool
         torch.set_num_threads(min(4, torch.get_num_threads()))
-    cfg = RunConfig(num_nodes=a.peers, dataset=a.dataset, seed=a.seed, max_iterations=10**9,
-                    trace_file=a.trace, host_threads=16, phase_sync=a.phase_sync)
-    if a.fedsys:
+    kw = dict(num_nodes=100, dataset="mnist", seed=a.seed, max_iterations=10**9, trace_file=a.trace,
+              host_threads=16, phase_sync=a.phase_sync)
+    kw.update(over)
+    if a.peers:
+        kw["num_nodes"] = a.peers
+    cfg = RunConfig(**kw)
+    if fedsys:
         from biscotti_amd.protocol.fedsys import FedSysEngine
 
-        cfg.perc_samples, cfg.epsilon = 35, 5.0      # FedSys/main.go:42,212 defaults
         eng = FedSysEngine(cfg, comm)
     else:
         eng = BiscottiEngine(cfg, comm)
@@ -68,10 +99,11 @@ def main() -> int:
     t0 = time.perf_counter()
     last = None
     phases: dict = {}
-    accs = []
+    accs, attacks = [], []
     for _ in range(a.steps):
         last = eng.run_round()
         accs.append(1.0 - last.test_error)
+        attacks.append(last.attack_rate)
         for k, v in last.phases.items():
             phases[k] = phases.get(k, 0.0) + v
     sync()
@@ -85,11 +117,12 @@ def main() -> int:
     elapsed = float(t.item())
     s_per_round = elapsed / max(a.steps, 1)
     acc = 1.0 - last.test_error if last is not None else float("nan")
-    ok, why = eng.fsm.chain.verify() if not a.fedsys else (True, "")
+    ok, why = eng.fsm.chain.verify() if not fedsys else (True, "")
     if comm.rank == 0:
+        headline = a.config == "headline"
         out = {
-            "metric": ("sec/round (FedSys baseline) + final test acc, MNIST 100 peers" if a.fedsys else
-                       "sec/round (block commit) + final test acc, MNIST 100 peers"),
+            "metric": ("sec/round (block commit) + final test acc, MNIST 100 peers" if headline else
+                       f"sec/round + final test acc, {a.config}"),
             "value": s_per_round,
             "unit": "s/round",
             "n_gpus": comm.world if eng.gpu else 0,
@@ -98,27 +131,36 @@ def main() -> int:
             "ms_per_step": 1e3 * s_per_round,
             "higher_is_better": False,
             "scaling": "strong",
-            "vs_baseline": s_per_round / BASELINE_S_PER_ROUND,
-            "speedup_vs_baseline": BASELINE_S_PER_ROUND / s_per_round,
+            "vs_baseline": s_per_round / ref_s if ref_s else None,
+            "speedup_vs_baseline": ref_s / s_per_round if ref_s else None,
             "final_test_acc": acc,
             "test_acc_last10_mean": sum(accs[-10:]) / max(1, len(accs[-10:])),
-            "baseline_test_acc": BASELINE_ACC,
-            "rounds_total": eng.rounds_done if not a.fedsys else eng.iteration,
+            "baseline_test_acc": ref_acc,
+            "baseline_source": ref_src,
+            "rounds_total": eng.rounds_done if not fedsys else eng.iteration,
             "dtype": "fp32 model / fp64 ledger / exact BN256",
-            "data": f"synthetic ({eng.task.source if hasattr(eng.task, 'source') else a.dataset}: MNIST-shaped "
-                    f"digits from sklearn 8x8 real digits, augmented)",
-            "config": {"model": "softmax regression 784x10 (7850 params, SoftmaxModel)", "peers": a.peers,
-                       "global_batch": a.peers * cfg.batch_size, "seq_len": 1,
-                       "parallelism": f"dp{comm.world} (virtual peers: {math.ceil(a.peers / comm.world)}/GPU)",
+            "data": ("synthetic: MNIST-shaped digits from sklearn's 8x8 real digits, augmented; zero-init model"
+                     if cfg.dataset == "mnist" else "creditcard.csv shipped with the reference"),
+            "config": {"name": a.config, "model": ("softmax regression 784x10 (7850 params, SoftmaxModel)"
+                                                   if cfg.dataset == "mnist" else "logistic regression (25)"),
+                       "peers": cfg.num_nodes, "global_batch": cfg.num_nodes * cfg.batch_size, "seq_len": 1,
+                       "parallelism": f"dp{comm.world} (virtual peers: {math.ceil(cfg.num_nodes / comm.world)}/GPU)",
                        "verifiers": cfg.num_verifiers, "aggregators": cfg.num_miners, "noisers": cfg.num_noisers,
-                       "epsilon": cfg.epsilon, "ns_percent": cfg.perc_samples},
+                       "epsilon": cfg.epsilon, "ns_percent": cfg.perc_samples, "poisoning": cfg.poisoning,
+                       "churn": cfg.churn, "secure_agg": cfg.secure_agg, "verification": cfg.verification,
+                       "noising": cfg.noising, "fedsys": fedsys},
             "phase_ms_per_round": {k: 1e3 * v / max(a.steps, 1) for k, v in sorted(phases.items())},
             "phase_sync": bool(a.phase_sync),
             "chain_valid": bool(ok),
         }
+        if cfg.dataset == "mnist":
+            out["final_attack_rate"] = attacks[-1] if attacks else None
+            out["attack_rate_last10_mean"] = sum(attacks[-10:]) / max(1, len(attacks[-10:]))
+        for k, v in ref_extra.items():
+            out[f"baseline_{k}"] = v
         print(json.dumps(out), flush=True)
     comm.barrier()
-    if not a.fedsys:
+    if not fedsys:
         eng.close()
     comm.shutdown()
     return 0
