@@ -13,6 +13,7 @@
 #include "hash.hpp"
 #include "keys.hpp"
 #include "ledger.hpp"
+#include "pairing.hpp"
 #include "protocol.hpp"
 #include "shares.hpp"
 #include "vrf.hpp"
@@ -415,6 +416,66 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     auto kp = client_key_from_entropy(B(e));
     return py::make_tuple(P(kp.first.to_be()), P(kp.second.marshal()));
   });
+
+  // ---------------------------------------------------------------- pairing (kyber.go:650-673)
+  auto gt_bytes = [](const Fp12& g) {
+    Bytes out;
+    for (int k = 0; k < 6; ++k)
+      for (const U256* v : {&g.c[k].x, &g.c[k].y}) {
+        u8 b[32];
+        Fp().from_mont(*v).to_be(b);
+        out.insert(out.end(), b, b + 32);
+      }
+    return out;
+  };
+  m.def("pairing_digest", [gt_bytes](py::bytes g1, py::bytes g2, py::int_ k) {
+    // e(P, Q)^k as 384 canonical bytes (GT equality tests; kyber's GT marshal is not reproduced)
+    Fp12 g;
+    {
+      G1 P = G1::unmarshal(B(g1));
+      G2 Q = G2::unmarshal(B(g2));
+      U256 e = u256_from_pyint(k);
+      py::gil_scoped_release rel;
+      g = pairing(P, Q).pow(e);
+    }
+    return P(gt_bytes(g));
+  }, py::arg("g1"), py::arg("g2"), py::arg("k") = 1);
+  m.def("pairing_product_is_one", [](std::vector<py::bytes> g1s, std::vector<py::bytes> g2s) {
+    std::vector<G1> Ps;
+    std::vector<G2> Qs;
+    for (auto& b : g1s) Ps.push_back(G1::unmarshal(B(b)));
+    for (auto& b : g2s) Qs.push_back(G2::unmarshal(B(b)));
+    py::gil_scoped_release rel;
+    return multi_pairing(Ps, Qs).is_one();
+  });
+  m.def("verify_secret", [](py::bytes commitment, py::bytes witness, py::bytes g2_0, py::bytes g2_1, i64 x, i64 y,
+                            py::object y_base) {
+    G1 C = G1::unmarshal(B(commitment)), W = G1::unmarshal(B(witness));
+    G2 A = G2::unmarshal(B(g2_0)), S = G2::unmarshal(B(g2_1));
+    G1 Yb = y_base.is_none() ? G1::generator() : G1::unmarshal(B(y_base.cast<py::bytes>()));
+    py::gil_scoped_release rel;
+    return verify_secret(C, W, A, S, x, y, Yb);
+  }, py::arg("commitment"), py::arg("witness"), py::arg("g2_0"), py::arg("g2_1"), py::arg("x"), py::arg("y"),
+     py::arg("y_base") = py::none());
+  m.def("verify_secrets_batch", [](std::vector<py::bytes> commits, std::vector<py::bytes> witnesses, py::bytes g2_0,
+                                   py::bytes g2_1, std::vector<i64> xs, std::vector<i64> ys, int threads,
+                                   py::object y_base) {
+    const size_t n = commits.size();
+    if (witnesses.size() != n || xs.size() != n || ys.size() != n) throw std::runtime_error("length mismatch");
+    std::vector<G1> C, W;
+    for (auto& b : commits) C.push_back(G1::unmarshal(B(b)));
+    for (auto& b : witnesses) W.push_back(G1::unmarshal(B(b)));
+    G2 A = G2::unmarshal(B(g2_0)), S = G2::unmarshal(B(g2_1));
+    G1 Yb = y_base.is_none() ? G1::generator() : G1::unmarshal(B(y_base.cast<py::bytes>()));
+    std::vector<uint8_t> ok(n, 0);
+    {
+      py::gil_scoped_release rel;
+      parallel_for(n, threads, [&](size_t i) { ok[i] = verify_secret(C[i], W[i], A, S, xs[i], ys[i], Yb) ? 1 : 0; });
+    }
+    std::vector<bool> r(ok.begin(), ok.end());
+    return r;
+  }, py::arg("commits"), py::arg("witnesses"), py::arg("g2_0"), py::arg("g2_1"), py::arg("xs"), py::arg("ys"),
+     py::arg("threads") = 1, py::arg("y_base") = py::none());
 
   // ---------------------------------------------------------------- VRF
   m.def("vrf_public_key", [](py::bytes seed) { return P(VrfKey::from_seed(B(seed)).pk); });

@@ -271,3 +271,37 @@ def test_concurrent_native_jobs_share_the_pool(rt):
     assert s.result() == rt.schnorr_sign_multi(msgs, [k[0] for k in keys], key_of, bases, ids, 1)
     assert v.result() == rt.vrf_prove_batch(seeds, b"h", 1)
     assert fg == rt.vrf_prove_batch(seeds[:10], b"g", 1)
+
+
+def test_pairing_bilinear_and_kzg_witnesses(rt):
+    """Optimal ate pairing (K13) + verifySecret (kyber.go:650-673) on our Shamir witnesses."""
+    import random
+
+    import numpy as np
+
+    n = 65000549695646603732796438742359905742570406053903786389881062969044166799969
+    g1, g2 = rt.g1_generator(), rt.g2_generator()
+    one = rt.pairing_digest(g1, g2, 0)
+    assert rt.pairing_digest(g1, g2) != one and rt.pairing_digest(g1, g2, n) == one
+    rnd = random.Random(3)
+    a, b = rnd.randrange(1, n), rnd.randrange(1, n)
+    assert rt.pairing_digest(rt.g1_mul(g1, a), rt.g2_mul(g2, b)) == rt.pairing_digest(g1, g2, a * b % n)
+    # KZG evaluation proofs of the secret shares
+    s = 2
+    key = rt.CommitKey.generate(25, s)
+    coeffs = np.random.default_rng(0).integers(-10**6, 10**6, size=25)
+    _, chunk_commits, ys, wits = key.make_shares(coeffs, 10, 21)
+    g2s = rt.g2_mul(g2, s)
+    for k, t in [(0, 0), (1, 10), (2, 20), (2, 3)]:
+        x, y = t - 10, int(ys[k, t])
+        yb = rt.g1_mul(g1, s ** (10 * k))          # PK_G1[10k]: chunk k is committed on PK[10k..]
+        assert rt.verify_secret(chunk_commits[k], wits[k * 21 + t], g2, g2s, x, y, yb)
+        assert not rt.verify_secret(chunk_commits[k], wits[k * 21 + t], g2, g2s, x, y + 1, yb)
+        assert not rt.verify_secret(chunk_commits[k], wits[k * 21 + (t + 1) % 21], g2, g2s, x, y, yb)
+    # the reference's literal check (y base = G1) holds for chunk 0 only (quirk Q9)
+    assert rt.verify_secret(chunk_commits[0], wits[4], g2, g2s, -6, int(ys[0, 4]))
+    assert not rt.verify_secret(chunk_commits[1], wits[21 + 4], g2, g2s, -6, int(ys[1, 4]))
+    xs = [t - 10 for t in range(21)]
+    ok = rt.verify_secrets_batch([chunk_commits[1]] * 21, wits[21:42], g2, g2s, xs, [int(v) for v in ys[1]], 4,
+                                 rt.g1_mul(g1, s ** 10))
+    assert all(ok)
