@@ -58,6 +58,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="headline", choices=sorted(PRESETS))
     ap.add_argument("--peers", type=int, default=None, help="override the preset's peer count")
+    ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
+                    help="override any RunConfig field (sweeps), e.g. --set num_verifiers=5")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--trace", default=None)
     ap.add_argument("--fedsys", action="store_true", help="same as --config fedsys")
@@ -84,6 +86,16 @@ def main() -> int:
     kw.update(over)
     if a.peers:
         kw["num_nodes"] = a.peers
+    import dataclasses
+
+    types = {f.name: f.type for f in dataclasses.fields(RunConfig)}
+    for item in a.set:
+        k, v = item.split("=", 1)
+        if k not in types:
+            raise SystemExit(f"unknown RunConfig field {k!r}")
+        cur = kw.get(k, getattr(RunConfig, k, None))
+        kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v) if cur is not None \
+            else v
     cfg = RunConfig(**kw)
     if fedsys:
         from biscotti_amd.protocol.fedsys import FedSysEngine

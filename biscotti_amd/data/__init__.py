@@ -180,6 +180,23 @@ def credit_poisoned(cd: CreditData) -> CreditData:
     return CreditData(cd.X.copy(), -cd.y, cd.Xvalid, cd.yvalid)
 
 
+def synthetic_images(n: int, shape: tuple, n_classes: int, seed: int = 0, noise: float = 0.6):
+    """Class-conditional synthetic images for the LFW / CIFAR sandboxes (their files are not in the
+    reference either): each class is a smooth random prototype; samples are the prototype under a
+    random brightness change plus pixel noise.  Returns float32 [n, prod(shape)] and int64 labels."""
+    import torch
+    import torch.nn.functional as F
+
+    g = torch.Generator().manual_seed(seed)
+    c, h, w = shape
+    coarse = torch.rand((n_classes, c, max(2, h // 8), max(2, w // 8)), generator=g)
+    protos = F.interpolate(coarse, size=(h, w), mode="bilinear", align_corners=False)
+    y = torch.randint(0, n_classes, (n,), generator=g)
+    gain = 0.8 + 0.4 * torch.rand((n, 1, 1, 1), generator=g)
+    X = protos[y] * gain + noise * torch.randn((n, c, h, w), generator=g)
+    return X.reshape(n, -1).numpy().astype(np.float32), y.numpy()
+
+
 def dataset_dims(name: str) -> tuple[int, int, int]:
     """(num_params, num_features, num_classes) -- ML/Pytorch/datasets.py:22-52."""
     return {"mnist": (7850, 784, 10), "lfw": (18254, 8742, 12), "creditcard": (25, 25, 2)}[name]
