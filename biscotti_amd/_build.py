@@ -79,6 +79,20 @@ def build_runtime(force: bool = False) -> Path:
     return target
 
 
+def build_selftest(sanitize: bool = True) -> Path:
+    """Native self-test of the host runtime (csrc/selftest), with ASan + UBSan on the host code."""
+    rt_dir = CSRC / "runtime"
+    out = BUILD / ("selftest_asan" if sanitize else "selftest")
+    out.parent.mkdir(parents=True, exist_ok=True)
+    srcs = [s for s in sorted(rt_dir.glob("*.cpp")) if s.name != "bindings.cpp"]
+    srcs.append(CSRC / "selftest" / "selftest.cpp")
+    flags = ["-O1", "-g", "-std=c++17", "-pthread", f"-I{rt_dir}", "-fno-omit-frame-pointer"]
+    if sanitize:
+        flags += ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+    _run(["g++", *flags, *map(str, srcs), "-o", str(out)])
+    return out
+
+
 def build_kernels(force: bool = False) -> Path:
     if not Path(HIPCC).exists() and shutil.which("hipcc") is None:
         raise RuntimeError("hipcc not found; cannot build the gfx950 kernels")
@@ -106,7 +120,14 @@ def main(argv=None) -> None:
     ap.add_argument("--runtime", action="store_true")
     ap.add_argument("--kernels", action="store_true")
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--sanitize", action="store_true",
+                    help="build and run the host-runtime self-test under ASan + UBSan")
     a = ap.parse_args(argv)
+    if a.sanitize:
+        exe = build_selftest(True)
+        print("built", exe)
+        r = subprocess.run([str(exe)], env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
+        raise SystemExit(r.returncode)
     both = not (a.runtime or a.kernels)
     if a.runtime or both:
         print("built", build_runtime(a.force))

@@ -64,3 +64,11 @@ def test_sandbox_models_train_on_cpu():
         r = run(model, ds, clients=2, iters=60, eval_every=30, lr=5e-3, device="cpu", verbose=False)
         assert r["final_test_error"] <= r["history"][0]["test_error"] + 0.05
         assert len(r["history"]) == 3
+
+
+def test_native_selftest_under_asan_ubsan():
+    """Host runtime under AddressSanitizer + UBSan, 6 threads (race/sanitizer coverage)."""
+    r = subprocess.run([sys.executable, "-m", "biscotti_amd._build", "--sanitize"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "selftest: ok" in r.stdout
