@@ -758,6 +758,48 @@ PYBIND11_MODULE(_biscotti_rt, m) {
                                   const std::vector<Update>& ups, i64 now) {
         return f.make_plain_block(std::vector<double>(w.data(), w.data() + w.size()), ups, now);
       })
+      .def("make_plain_block_arrays",
+           [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w0, std::vector<i64> ids,
+              py::array_t<double, py::array::c_style | py::array::forcecast> deltas,
+              py::array_t<double, py::array::c_style | py::array::forcecast> noised, std::vector<py::bytes> commits,
+              std::vector<std::vector<py::bytes>> sigs, i64 now) {
+             // plain-path block (honest.go:346-388) straight from [n, d] arrays: W = W0 + sum of the
+             // deltas in `ids` order (float64), Update{delta, noise = noised - delta, noised_delta}
+             const size_t n = ids.size(), d = size_t(w0.size());
+             if (deltas.ndim() != 2 || size_t(deltas.shape(0)) != n || size_t(deltas.shape(1)) != d ||
+                 noised.ndim() != 2 || size_t(noised.shape(0)) != n || size_t(noised.shape(1)) != d ||
+                 commits.size() != n || sigs.size() != n)
+               throw std::runtime_error("make_plain_block_arrays: shape mismatch");
+             std::vector<double> W(w0.data(), w0.data() + d);
+             std::vector<Update> ups(n);
+             std::vector<Bytes> cm(n);
+             std::vector<std::vector<Bytes>> sg(n);
+             for (size_t k = 0; k < n; ++k) {
+               cm[k] = B(commits[k]);
+               for (auto& x : sigs[k]) sg[k].push_back(B(x));
+             }
+             {
+               py::gil_scoped_release rel;
+               for (size_t k = 0; k < n; ++k) {
+                 const double* dv = deltas.data(py::ssize_t(k), 0);
+                 const double* nv = noised.data(py::ssize_t(k), 0);
+                 Update& u = ups[k];
+                 u.source_id = ids[k];
+                 u.iteration = f.iteration;
+                 u.accepted = true;
+                 u.delta.assign(dv, dv + d);
+                 u.noised_delta.assign(nv, nv + d);
+                 u.noise.resize(d);
+                 for (size_t j = 0; j < d; ++j) {
+                   u.noise[j] = nv[j] - dv[j];
+                   W[j] += dv[j];
+                 }
+                 u.commitment = std::move(cm[k]);
+                 u.signatures = std::move(sg[k]);
+               }
+             }
+             return f.make_plain_block(W, ups, now);
+           })
       .def("make_empty_block", &RoundFSM::make_empty_block)
       .def("commit_block", &RoundFSM::commit_block)
       .def("is_poisoner", &RoundFSM::is_poisoner, py::arg("id"), py::arg("fedsys") = false)

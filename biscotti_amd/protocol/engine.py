@@ -699,21 +699,16 @@ class BiscottiEngine:
             leader_rank = comm.owner(leader, self.N)
             block_bytes = None
             if comm.rank == leader_rank:
-                upd = []
-                W = self.W.clone()
-                for w in ups:
-                    u = R.Update()
-                    dv = self._gathered_row(dall, w).double()
-                    nv = self._gathered_row(nall, w).double()
-                    W += dv
-                    u.source_id, u.iteration, u.accepted = w, plan.iteration, True
-                    u.delta = dv.cpu().tolist()
-                    u.noised_delta = nv.cpu().tolist()
-                    u.noise = (nv - dv).cpu().tolist()
-                    u.commitment = commit_of[w]
-                    u.signatures = signatures.get(w, [])
-                    upd.append(u)
-                blk = fsm.make_plain_block(W.cpu().numpy(), upd, self._now(plan.iteration))
+                rows = h2d([comm.owner(w, self.N) * self.maxlocal + (w - comm.peer_range(self.N, comm.owner(w, self.N)).start)
+                            for w in ups], torch.long, self.dev)
+                dv = dall.reshape(-1, self.d).index_select(0, rows).double().cpu().numpy()
+                nv = nall.reshape(-1, self.d).index_select(0, rows).double().cpu().numpy()
+                blk = fsm.make_plain_block_arrays(self.W.cpu().numpy(), list(ups), dv, nv,
+                                                  [commit_of[w] for w in ups],
+                                                  [signatures.get(w, []) for w in ups], self._now(plan.iteration))
+                if comm.world == 1:
+                    self._last_nodes = list(ups)
+                    return blk
                 block_bytes = blk.serialize()
             data = comm.broadcast_bytes(block_bytes, leader_rank)
             self._last_nodes = list(ups)
