@@ -72,3 +72,18 @@ def test_native_selftest_under_asan_ubsan():
                        text=True, timeout=900)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "selftest: ok" in r.stdout
+
+
+def test_centralblock_prototype():
+    import numpy as np
+
+    from biscotti_amd.centralblock import CentralBlock, invert
+
+    cb = CentralBlock(n_branches=2, poisoners=2, batch=20, device="cpu")
+    e0 = cb.evaluate()["best_test_error"]
+    for _ in range(30):
+        cb.step()
+    assert all(sum(h) == len(cb.clients) for h in cb.history)      # every client submits once per step
+    assert cb.evaluate()["best_test_error"] < e0
+    img = invert(np.arange(7840, dtype=np.float64))
+    assert img.shape == (784,) and abs(img.max() - 2.55 * 1567 / 7839) < 1e-12
