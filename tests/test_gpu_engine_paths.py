@@ -17,13 +17,21 @@ def _engine(**kw):
 
 
 def _run_exact(eng, rounds=4):
+    seen = {}
+    step = eng.task.step
+
+    def spy(W, it, peers):  # record every peer's quantised update as the engine computes it
+        d, q = step(W, it, peers)
+        seen.update({(it, p): q[i].clone() for i, p in enumerate(peers)})
+        return d, q
+    eng.task.step = spy
     res = []
     for _ in range(rounds):
         W0 = eng.W.clone()
         r = eng.run_round()
         res.append(r)
         if not r.empty and eng.cfg.secure_agg:
-            _, q = eng.task.step(W0, r.iteration, sorted(r.node_list))
+            q = torch.stack([seen[(r.iteration, p)] for p in r.node_list])
             torch.testing.assert_close(eng.W, W0 + q.sum(0).double() / 10.0 ** eng.cfg.precision, rtol=0,
                                        atol=1e-12)
     ok, why = eng.fsm.chain.verify()
