@@ -44,6 +44,11 @@ class Comm:
             dev = torch.device("cpu")
         if world > 1 and not dist.is_initialized():
             be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+            if be == "nccl" and torch.cuda.device_count() < local_world:
+                # several ranks share one device (rehearsals on a 1-GPU box): RCCL refuses
+                # duplicate devices, gloo moves the same device tensors through host memory
+                be = "gloo"
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {"device_id": dev} if be == "nccl" else {}
             try:
