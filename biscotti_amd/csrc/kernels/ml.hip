@@ -277,6 +277,35 @@ extern "C" __global__ void k_dp_noise(const float* delta, int P, int D, const in
   noised[g] = delta[g] + (nn > 0 ? acc / (float)nn : 0.f);
 }
 
+// K4, resident form.  The reference pre-samples each peer's 100 noise vectors at init
+// (samples[it % 100], client_obj.py:61-63); here the whole federation's table [N][100][D]
+// (314 MB for MNIST, 100 peers) is built once in HBM with the same Philox counters, and the
+// per-round kernel becomes a gather + average (memory-bound) instead of ~2 Philox + Box-Muller
+// evaluations per element on the critical path.  Values and float operations are those of
+// k_dp_noise, so both forms give identical bits.
+extern "C" __global__ void k_noise_table(int nnoisers, int D, unsigned long long seed, float* tbl) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long long)nnoisers * 100 * D) return;
+  const int i = (int)(g % D);
+  const long long nm = g / D;
+  const int m = (int)(nm % 100), nid = (int)(nm / 100);
+  u4 r = philox(u4{(uint32_t)i, (uint32_t)m, (uint32_t)nid, 0xA11CEu}, (uint32_t)seed, (uint32_t)(seed >> 32));
+  tbl[g] = gauss(r.x, r.y);
+}
+
+extern "C" __global__ void k_dp_noise_tbl(const float* delta, int P, int D, const int* noisers, int nn,
+                                          const float* noiser_scale, const float* tbl, int iter_mod, float* noised) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long long)P * D) return;
+  const int p = (int)(g / D), i = (int)(g % D);
+  float acc = 0.f;
+  for (int j = 0; j < nn; ++j) {
+    const int nid = noisers[p * nn + j];
+    acc += noiser_scale[p * nn + j] * tbl[((size_t)nid * 100 + iter_mod) * D + i];
+  }
+  noised[g] = delta[g] + (nn > 0 ? acc / (float)nn : 0.f);
+}
+
 // =====================================================================================
 // K5a: Gram partials G_part[split][i][j] = sum_{k in split} X[i][k] X[j][k] in f64 via
 // v_mfma_f64_16x16x4f64.  Grid (tiles_i, tiles_j, splits), one wave per block.
@@ -288,13 +317,34 @@ extern "C" __global__ void __launch_bounds__(64) k_gram_f64(const float* X, int 
   const int lane = threadIdx.x;
   const int i = ti * 16 + (lane & 15), j = tj * 16 + (lane & 15), kk = lane >> 4;
   const int k0 = sp * ksplit, k1 = min(D, k0 + ksplit);
-  f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k = k0; k < k1; k += 4) {
-    const int kx = k + kk;
-    const double a = (i < n && kx < k1) ? (double)X[(size_t)i * D + kx] : 0.0;
-    const double b = (j < n && kx < k1) ? (double)X[(size_t)j * D + kx] : 0.0;
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  const float* xa = X + (size_t)min(i, n - 1) * D;
+  const float* xb = X + (size_t)min(j, n - 1) * D;
+  const bool va = i < n, vb = j < n;
+  // loads issued 8 k-steps ahead of the MFMAs, two accumulators (one wave per block, so the
+  // memory latency is otherwise fully exposed at every step)
+  f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  int k = k0;
+  for (; k + 32 <= k1; k += 32) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = xa[k + 4 * u + kk];
+      b[u] = xb[k + 4 * u + kk];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a[u] : 0.0, vb ? (double)b[u] : 0.0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a[u + 1] : 0.0, vb ? (double)b[u + 1] : 0.0, acc1,
+                                                  0, 0, 0);
+    }
   }
+  for (; k < k1; k += 4) {
+    const int kx = k + kk;
+    const double a = (va && kx < k1) ? (double)xa[kx] : 0.0;
+    const double b = (vb && kx < k1) ? (double)xb[kx] : 0.0;
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc0, 0, 0, 0);
+  }
+  const f64x4 acc = acc0 + acc1;
   const int npad = gridDim.x * 16;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -314,9 +364,11 @@ extern "C" __global__ void __launch_bounds__(64) k_krum_scores(const double* par
   __shared__ double kept[128];
   const int i = blockIdx.x, lane = threadIdx.x;
   double gii = 0.0;
+#pragma unroll 8
   for (int s = 0; s < nsplit; ++s) gii += part[((size_t)s * npad + i) * npad + i];
   for (int j = lane; j < n; j += 64) {
     double gij = 0.0, gjj = 0.0;
+#pragma unroll 8
     for (int s = 0; s < nsplit; ++s) {
       gij += part[((size_t)s * npad + i) * npad + j];
       gjj += part[((size_t)s * npad + j) * npad + j];
@@ -358,39 +410,72 @@ extern "C" __global__ void __launch_bounds__(128) k_krum_accept(const double* sc
 }
 
 // =====================================================================================
-// K2: classification error of a softmax model: err[0] += #(argmax != label) over N rows.
-// One wave per row (grid-stride), W staged in LDS.
+// K2: classification error of a softmax model over up to two row sets in ONE launch (test rows
+// [0, split), attack rows [split, N)): err[row >= split] += #(argmax != label).
+// One wave per 16-row tile: logits = X_tile[16 x D_IN] . W^T on v_mfma_f32_16x16x4f32 (lane l
+// holds A[row l&15][k l>>4] with the (x-0.5)/0.5 transform fused and B[k][class l&15]; two
+// accumulators hide the 40-cycle dependent latency, loads are issued 8 k-steps ahead), then the
+// argmax across the 16 class lanes by xor-shuffles (first maximum, like np.argmax) and one atomic
+// per (wave, set).  Replaces a wave-per-row kernel that re-staged W into 64 KB of LDS per block.
 // =====================================================================================
 extern "C" __global__ void __launch_bounds__(256) k_eval_error(const float* X, const int* y, int N, int D_IN,
-                                                              int D_OUT, const double* W, int transform,
+                                                              int D_OUT, const double* W, int transform, int split,
                                                               unsigned int* err) {
-  __shared__ float w[16 * SM_MAXK];
-  __shared__ float bsh[16];
-  for (int i = threadIdx.x; i < D_OUT * D_IN; i += blockDim.x) w[i] = (float)W[i];
-  if (threadIdx.x < D_OUT) bsh[threadIdx.x] = (float)W[D_OUT * D_IN + threadIdx.x];
-  __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int waves = blockDim.x >> 6;
-  for (int r = blockIdx.x * waves + wid; r < N; r += gridDim.x * waves) {
-    float acc[16];
-    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
-    const float* xr = X + (size_t)r * D_IN;
-    for (int k = lane; k < D_IN; k += 64) {
-      float v = xr[k];
-      if (transform) v = (v - 0.5f) * 2.0f;
-      for (int c = 0; c < D_OUT; ++c) acc[c] += v * w[c * D_IN + k];
+  const int row0 = (blockIdx.x * 4 + wid) * 16;
+  if (row0 >= N) return;  // uniform per wave
+  const int i = lane & 15, kk = lane >> 4;
+  const float* xr = X + (size_t)min(row0 + i, N - 1) * D_IN;
+  const bool cval = i < D_OUT;
+  const double* wr = W + (size_t)(cval ? i : 0) * D_IN;
+  const float tsub = transform ? 0.5f : 0.f, tmul = transform ? 2.f : 1.f;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  int k0 = 0;
+  for (; k0 + 32 <= D_IN; k0 += 32) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + 4 * u + kk;
+      a[u] = xr[k];
+      b[u] = cval ? (float)wr[k] : 0.f;
     }
-    for (int c = 0; c < D_OUT; ++c)
-      for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
-    if (lane == 0) {
-      int best = 0;
-      float bv = acc[0] + bsh[0];
-      for (int c = 1; c < D_OUT; ++c) {
-        const float v = acc[c] + bsh[c];
-        if (v > bv) { bv = v; best = c; }  // np.argmax: first maximum
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32((a[u] - tsub) * tmul, b[u], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32((a[u + 1] - tsub) * tmul, b[u + 1], acc1, 0, 0, 0);
+    }
+  }
+  for (; k0 < D_IN; k0 += 4) {
+    const int k = k0 + kk;
+    const float a = k < D_IN ? (xr[k] - tsub) * tmul : 0.f;
+    const float b = (k < D_IN && cval) ? (float)wr[k] : 0.f;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
+  }
+  const float bias = cval ? (float)W[(size_t)D_OUT * D_IN + i] : 0.f;
+  unsigned int cnt0 = 0, cnt1 = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    // D layout of 16x16x4 f32: lane l holds D[row (l>>4)*4 + r][class l&15]
+    float bv = cval ? (acc0[r] + acc1[r]) + bias : -__builtin_huge_valf();
+    int bc = i;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 16);
+      const int oc = __shfl_xor(bc, o, 16);
+      if (ov > bv || (ov == bv && oc < bc)) {
+        bv = ov;
+        bc = oc;
       }
-      if (best != y[r]) atomicAdd(err, 1u);
     }
+    const int row = row0 + kk * 4 + r;
+    if (i == 0 && row < N && bc != y[row]) {
+      if (row < split) ++cnt0;
+      else ++cnt1;
+    }
+  }
+  if (i == 0) {
+    if (cnt0) atomicAdd(err, cnt0);
+    if (cnt1) atomicAdd(err + 1, cnt1);
   }
 }
 
@@ -546,12 +631,28 @@ extern "C" int bsc_krum(const float* X, int n, int D, int ksplit, double* part, 
 }
 
 extern "C" int bsc_eval_error(const float* X, const int* y, int N, int D_IN, int D_OUT, const double* W,
-                              int transform, unsigned int* err, void* stream) {
-  if (D_IN > SM_MAXK || D_OUT > 16) return -1;
+                              int transform, int split, unsigned int* err, void* stream) {
+  if (D_OUT > 16 || D_IN <= 0) return -1;
   if (N <= 0) return 0;
-  const int blocks = min(1024, nblk(N, 4));
-  hipLaunchKernelGGL(k_eval_error, dim3(blocks), dim3(256), 0, (hipStream_t)stream, X, y, N, D_IN, D_OUT, W,
-                     transform, err);
+  const int tiles = (N + 15) / 16;
+  hipLaunchKernelGGL(k_eval_error, dim3((tiles + 3) / 4), dim3(256), 0, (hipStream_t)stream, X, y, N, D_IN, D_OUT,
+                     W, transform, split, err);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_noise_table(int nnoisers, int D, unsigned long long seed, float* tbl, void* stream) {
+  const long long n = (long long)nnoisers * 100 * D;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_noise_table, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, nnoisers, D, seed, tbl);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_dp_noise_tbl(const float* delta, int P, int D, const int* noisers, int nn, const float* scale,
+                                const float* tbl, int iter_mod, float* noised, void* stream) {
+  const long long n = (long long)P * D;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_dp_noise_tbl, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, delta, P, D, noisers,
+                     nn, scale, tbl, iter_mod, noised);
   return (int)hipGetLastError();
 }
 

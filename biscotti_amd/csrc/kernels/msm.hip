@@ -316,6 +316,56 @@ extern "C" __global__ void __launch_bounds__(256) k_commit_rows(const long long*
   if (threadIdx.x == 0) st_jac(out_partial + 24 * (size_t)b, ld_jac(lds));
 }
 
+// ------------------------------------------------------------------ aggregate commitment audit
+// verifyCommitment (kyber.go:564-577) applied to the secure aggregate: by additive homomorphism
+// the miners' summed chunk commitments sum_w C_k(q_w) must equal the commitment of the recovered
+// chunk C_k(sum_w q_w).  One 64-lane block per chunk: lane j < L adds c_j * PK[prev + j] from the
+// fixed-base tables, an LDS tree sums the lanes, then lane m compares the result projectively
+// (X1 Z2^2 == X2 Z1^2, Y1 Z2^3 == Y2 Z1^3: no inversion) with miner m's sum.
+// coeffs: int64 [nch][poly] (recovered); csum: Jacobian [nm][nch][24]; ok: int32 [nm][nch].
+__device__ __forceinline__ bool jac_equal(const jac& p, const jac& q) {
+  const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  const fp z1s = fp_sqr(p.z), z2s = fp_sqr(q.z);
+  if (!fp_eq(fp_mul(p.x, z2s), fp_mul(q.x, z1s))) return false;
+  return fp_eq(fp_mul(p.y, fp_mul(z2s, q.z)), fp_mul(q.y, fp_mul(z1s, p.z)));
+}
+
+extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* coeffs, int d, int poly,
+                                                              const uint32_t* tbl_pk, int B0, int NW,
+                                                              const uint32_t* csum, int nm, int nch, int* ok) {
+  __shared__ uint32_t sh[64 * 24];
+  const int k = blockIdx.x, t = threadIdx.x;
+  const int prev = k * poly, L = min(poly, d - prev);
+  const int E0 = 1 << (B0 - 1);
+  const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
+  jac acc = jac_inf();
+  if (t < L) {
+    const long long cj = coeffs[(size_t)k * poly + t];
+    const bool neg = cj < 0;
+    unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
+    const uint32_t* tb = tbl_pk + (size_t)(prev + t) * PB * 16;
+    int carry = 0;
+    for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
+      const int dg = recode(m, carry, win_bits(w, B0));
+      if (dg == 0) continue;
+      const int ad = dg < 0 ? -dg : dg;
+      aff q = ld_aff(tb + (size_t)win_entry(w, ad, E0) * 16);
+      if ((dg < 0) != neg) q = aff_neg(q);
+      acc = jac_add_aff(acc, q);
+    }
+  }
+  st_jac(sh + t * 24, acc);
+  __syncthreads();
+  int top = 1;
+  while (top < L) top <<= 1;
+  for (int s = top >> 1; s > 0; s >>= 1) {
+    if (t < s) st_jac(sh + t * 24, jac_add(ld_jac(sh + t * 24), ld_jac(sh + (t + s) * 24)));
+    __syncthreads();
+  }
+  if (t < nm) ok[(size_t)t * nch + k] = jac_equal(ld_jac(sh), ld_jac(csum + 24 * ((size_t)t * nch + k))) ? 1 : 0;
+}
+
 // ------------------------------------------------------------------ reductions
 // out[i] = sum_{r < nrows} pts[(rows[r] * ncols_in + cols[i]) * 24]   (cols == nullptr: cols[i] = i)
 // One thread per output column; used for miner-side share aggregation (aggregateSecret).
@@ -494,6 +544,16 @@ extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stri
                                void* stream) {
   if (ngroups <= 0) return 0;
   hipLaunchKernelGGL(k_segment_sum, dim3(ngroups), dim3(256), 0, (hipStream_t)stream, pts, n, stride, off, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
+                               const uint32_t* csum, int nm, int nch, int* ok, void* stream) {
+  if (nch <= 0 || nm <= 0) return 0;
+  if (poly < 1 || poly > 64 || nm > 64 || B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;
+  if ((long long)nch * poly < d || (long long)(nch - 1) * poly >= d) return -1;
+  hipLaunchKernelGGL(k_chunk_check, dim3(nch), dim3(64), 0, (hipStream_t)stream, coeffs, d, poly, tbl_pk, B0, NW,
+                     csum, nm, nch, ok);
   return (int)hipGetLastError();
 }
 

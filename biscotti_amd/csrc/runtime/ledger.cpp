@@ -446,6 +446,10 @@ Blockchain Blockchain::load(const std::string& path) {
   Blockchain c;
   size_t o = 8;
   while (o < all.size()) {
+    // a process killed mid-append leaves a torn final record (length prefix or body cut short):
+    // the chain up to it is intact, resume from there (the next save/append rewrites the tail)
+    const size_t rest = all.size() - o;
+    if (rest < 8 || load_le64(all.data() + o) > rest - 8) break;
     size_t used = 0;
     c.blocks.push_back(deserialize_block(all.data() + o, all.size() - o, &used));
     o += used;

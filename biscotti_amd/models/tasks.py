@@ -48,6 +48,10 @@ class SoftmaxTask:
         self.test_y = torch.from_numpy(fed.test_y.astype(np.int32)).to(self.device)
         self.att_X = torch.from_numpy(fed.attack_X).to(self.device)
         self.att_y = torch.from_numpy(fed.attack_y.astype(np.int32)).to(self.device)
+        # test | attack rows back to back: both metrics come from one kernel launch + one read-back
+        self.eval_X = torch.cat([self.test_X, self.att_X]).contiguous()
+        self.eval_y = torch.cat([self.test_y, self.att_y]).contiguous()
+        self.eval_split = int(self.test_X.shape[0])
         self._local_index = {p: i for i, p in enumerate(self.peers)}
 
     def noise_sigma(self, epsilon: float, delta: float = 1e-5) -> float:
@@ -76,9 +80,13 @@ class SoftmaxTask:
 
     def evaluate_async(self, W: torch.Tensor):
         """Queue the test / attack evaluations now; the returned callable reads them back."""
-        err = K.eval_error_async(self.test_X, self.test_y, W, self.d_in, self.d_out, transform=True)
-        att = K.eval_error_async(self.att_X, self.att_y, W, self.d_in, self.d_out, transform=True)
-        return lambda: {"test_error": err(), "attack_rate": att()}
+        both = K.eval_errors_async(self.eval_X, self.eval_y, self.eval_split, W, self.d_in, self.d_out,
+                                   transform=True)
+
+        def result():
+            err, att = both()
+            return {"test_error": err, "attack_rate": att}
+        return result
 
     def train_error(self, W: torch.Tensor, peer: int, iteration: int) -> float:
         """RONI's getTrainErr: error on a (random) minibatch of the verifier's own shard."""

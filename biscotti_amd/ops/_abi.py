@@ -25,12 +25,15 @@ SIGNATURES = {
     "bsc_stream_destroy": [P],
     "bsc_marshal": [P, I, P, P],
     "bsc_to_affine": [P, I, P, P],
+    "bsc_chunk_check": [P, I, I, P, I, I, P, I, I, P, P],
     # ml.hip
     "bsc_softmax_step": [P, P, P, P, P, P, I, I, I, I, U64, I, F, D, P, P, P, P],
     "bsc_logreg_step": [P, P, P, P, P, P, I, I, I, U64, P, D, D, P, D, P, P, P],
     "bsc_dp_noise": [P, I, I, P, I, P, U64, I, P, P],
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],
-    "bsc_eval_error": [P, P, I, I, I, P, I, P, P],
+    "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
+    "bsc_noise_table": [I, I, U64, P, P],
+    "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P],
     "bsc_recover": [P, I, I, P, I, I, P, D, P, P, P, P],
     "bsc_add_rows": [P, I, P, I, P, P, P],
 }

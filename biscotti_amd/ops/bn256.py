@@ -149,6 +149,19 @@ class DeviceCommitEngine:
                                      _ptr(partial), _ptr(out), _stream()), "commit_rows")
         return out
 
+    def check_chunks(self, coeffs: torch.Tensor, csum: torch.Tensor) -> torch.Tensor:
+        """Aggregate audit: ok[m, k] = 1 iff the chunk commitment of the recovered coefficients
+        coeffs[k] (int64 [nchunks, poly]) equals miner m's summed chunk commitment csum[m, k]
+        (Jacobian int32 [nm, nchunks, 24]) -- verifyCommitment (kyber.go:564-577) on the aggregate."""
+        assert coeffs.dtype == torch.int64 and tuple(coeffs.shape) == (self.nchunks, self.poly)
+        assert csum.dtype == torch.int32 and csum.dim() == 3 and tuple(csum.shape[1:]) == (self.nchunks, 24)
+        coeffs, csum = coeffs.contiguous(), csum.contiguous()
+        nm = csum.shape[0]
+        ok = torch.empty((nm, self.nchunks), dtype=torch.int32, device=self.device)
+        _check(hip().bsc_chunk_check(_ptr(coeffs), self.d, self.poly, _ptr(self.tbl_pk), self.b0, self.nw, _ptr(csum),
+                                     nm, self.nchunks, _ptr(ok), _stream()), "chunk_check")
+        return ok
+
     def commitments(self, pts: torch.Tensor) -> torch.Tensor:
         """Full-vector commitment per row = sum of its chunk commitments. Returns Jacobian [n, 24]."""
         n, nch, S, _ = pts.shape

@@ -160,12 +160,33 @@ def logreg_step(X, y, off, nrows, pid, W, B, seed, calls, alpha, lammy, sigma, q
 
 
 # ---------------------------------------------------------------------------- K4 DP noise
-def dp_noise(delta, noisers, scales, seed, iteration):
-    """noised = delta + mean_j scales[p, j] * N(0, 1; noiser_j, iteration % 100)."""
+def noise_table(num_noisers: int, D: int, seed: int, device) -> torch.Tensor:
+    """Every noiser's 100 pre-sampled N(0,1) vectors, resident on the device: fp32
+    [num_noisers, 100, D] (client_obj.py:61-63 pre-samples samples[100][D] per peer at init).
+    Entry [j, m] equals the vector dp_noise draws for noiser j at iterations = m (mod 100)."""
+    tbl = torch.empty((num_noisers, 100, D), dtype=torch.float32, device=device)
+    _check(hip().bsc_noise_table(num_noisers, D, seed & (2**64 - 1), _p(tbl), _stream()), "noise_table")
+    return tbl
+
+
+def dp_noise(delta, noisers, scales, seed, iteration, table=None):
+    """noised = delta + mean_j scales[p, j] * N(0, 1; noiser_j, iteration % 100).
+
+    `table` (GPU): the resident noise_table of the same seed -- the kernel then gathers the
+    noisers' vectors instead of regenerating them (identical values)."""
     P, D = delta.shape
     nn_ = noisers.shape[1] if noisers.dim() == 2 else 0
     out = torch.empty_like(delta)
     if delta.device.type == "cuda":
+        if table is not None:
+            assert table.shape[1:] == (100, D) and table.dtype == torch.float32
+            if nn_ and P and noisers.device.type == "cpu":
+                assert int(noisers.min()) >= 0 and int(noisers.max()) < table.shape[0], "noiser id out of range"
+            # device-resident ids: the caller range-checks them on the host (reading them back here
+            # would stall the stream)
+            _check(hip().bsc_dp_noise_tbl(_p(delta), P, D, _p(noisers), nn_, _p(scales), _p(table), iteration % 100,
+                                          _p(out), _stream()), "dp_noise_tbl")
+            return out
         _check(hip().bsc_dp_noise(_p(delta), P, D, _p(noisers), nn_, _p(scales), seed & (2**64 - 1), iteration % 100,
                                   _p(out), _stream()), "dp_noise")
         return out
@@ -188,7 +209,7 @@ def noise_vector(noiser: int, iteration: int, D: int, seed: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------- K5 Multi-Krum
-def krum(X, groupsize: int, n_accept: int, ksplit: int = 512):
+def krum(X, groupsize: int, n_accept: int, ksplit: int = 256):
     """Multi-Krum over the rows of X (fp32 [n, d]): returns (accept bool [n], scores fp64 [n])."""
     n, D = X.shape
     if n == 0:
@@ -217,16 +238,29 @@ def krum(X, groupsize: int, n_accept: int, ksplit: int = 512):
 
 
 # ---------------------------------------------------------------------------- K2 evaluation
+def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
+    """Error rates of W on rows [0, split) and [split, N) of X from ONE kernel launch and one
+    read-back (test error + 1->7 attack rate).  Returns a callable giving (err_a, err_b)."""
+    N = X.shape[0]
+    na, nb = split, N - split
+    if N == 0 or X.device.type != "cuda":
+        a = eval_error(X[:split], y[:split], W, d_in, d_out, transform) if na else 0.0
+        b = eval_error(X[split:], y[split:], W, d_in, d_out, transform) if nb else 0.0
+        return lambda: (a, b)
+    err = torch.zeros((2,), dtype=torch.int32, device=X.device)
+    _check(hip().bsc_eval_error(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), int(split), _p(err), _stream()),
+           "eval_error")
+
+    def result():
+        e = err.tolist()
+        return (e[0] / na if na else 0.0, e[1] / nb if nb else 0.0)
+    return result
+
+
 def eval_error_async(X, y, W, d_in, d_out, transform=True):
     """Queue the evaluation kernel; returns a zero-argument callable giving the error rate."""
-    N = X.shape[0]
-    if N == 0 or X.device.type != "cuda":
-        v = eval_error(X, y, W, d_in, d_out, transform)
-        return lambda: v
-    err = torch.zeros((1,), dtype=torch.int32, device=X.device)
-    _check(hip().bsc_eval_error(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), _p(err), _stream()),
-           "eval_error")
-    return lambda: float(err.item()) / N
+    f = eval_errors_async(X, y, X.shape[0], W, d_in, d_out, transform)
+    return lambda: f()[0]
 
 
 def eval_error(X, y, W, d_in, d_out, transform=True) -> float:

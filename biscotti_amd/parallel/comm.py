@@ -31,8 +31,12 @@ class Comm:
 
     # ------------------------------------------------------------------ setup
     @staticmethod
-    def init(device: str | None = None, backend: str | None = None) -> "Comm":
-        """Initialise from torchrun-style env vars (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
+    def init(device: str | None = None, backend: str | None = None, timeout_s: float | None = None) -> "Comm":
+        """Initialise from torchrun-style env vars (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT).
+
+        `timeout_s` bounds every collective: a rank that dies (the reference's crashed peer) makes
+        the survivors' next collective fail within that time instead of hanging, the job exits and
+        an elastic launcher (torchrun --max-restarts) restarts it from the persisted chain."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -51,6 +55,10 @@ class Comm:
                 be = "gloo"
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {"device_id": dev} if be == "nccl" else {}
+            if timeout_s:
+                import datetime
+
+                kw["timeout"] = datetime.timedelta(seconds=float(timeout_s))
             try:
                 dist.init_process_group(be, rank=rank, world_size=world, **kw)
             except TypeError:
@@ -94,6 +102,22 @@ class Comm:
         dist.all_gather_into_tensor(out, flat)
         return out.view(self.world, *t.shape)
 
+    def all_gather_packed(self, parts: list[torch.Tensor]) -> list[torch.Tensor]:
+        """ONE all_gather for several tensors of any dtypes (a round's small messages share a
+        launch instead of paying one xGMI latency each).  parts[i] has shape [L, ...] with the
+        same L everywhere; returns [world, L, ...] per part, bytes reinterpreted back to its dtype."""
+        L = parts[0].shape[0]
+        raw = [p.contiguous().reshape(L, -1).view(torch.uint8) for p in parts]
+        if self.world == 1:
+            return [p.unsqueeze(0) for p in parts]
+        g = self.all_gather(torch.cat(raw, dim=1))            # [world, L, total bytes]
+        out, o = [], 0
+        for p, r in zip(parts, raw):
+            nb = r.shape[1]
+            out.append(g[:, :, o:o + nb].contiguous().view(p.dtype).view(self.world, *p.shape))
+            o += nb
+        return out
+
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
         if self.world > 1:
             dist.broadcast(t, src)
@@ -113,17 +137,21 @@ class Comm:
         dist.broadcast(buf, src)
         return data if self.rank == src else bytes(buf.cpu().numpy())
 
-    def all_to_all(self, send: list[torch.Tensor]) -> list[torch.Tensor]:
+    def all_to_all(self, send: list[torch.Tensor], recv_sizes: list[int] | None = None) -> list[torch.Tensor]:
         """Personalised exchange of 1-D tensors of one dtype; send[r] goes to rank r.
 
-        Receive sizes are exchanged first (one tiny all_gather), then one all_to_all_single."""
+        When the caller already knows what it will receive (the round's routing is replicated on
+        every rank) it passes `recv_sizes` and the exchange is ONE all_to_all_single; otherwise the
+        sizes travel first in a tiny all_gather."""
         assert len(send) == self.world
         if self.world == 1:
             return [send[0]]
         dtype = send[0].dtype
-        sizes = torch.tensor([s.numel() for s in send], dtype=torch.int64, device=self.device)
-        allsizes = self.all_gather(sizes)  # [src, dst]
-        recv_sizes = [int(v) for v in allsizes[:, self.rank].tolist()]
+        allsizes = None
+        if recv_sizes is None:
+            sizes = torch.tensor([s.numel() for s in send], dtype=torch.int64, device=self.device)
+            allsizes = self.all_gather(sizes)  # [src, dst]
+            recv_sizes = [int(v) for v in allsizes[:, self.rank].tolist()]
         inp = torch.cat([s.reshape(-1) for s in send]) if any(s.numel() for s in send) else \
             torch.empty((0,), dtype=dtype, device=self.device)
         out = torch.empty((sum(recv_sizes),), dtype=dtype, device=self.device)
@@ -131,6 +159,9 @@ class Comm:
             dist.all_to_all_single(out, inp, recv_sizes, [s.numel() for s in send])
         except (RuntimeError, NotImplementedError):
             # backends without alltoall: padded all_gather
+            if allsizes is None:
+                sizes = torch.tensor([s.numel() for s in send], dtype=torch.int64, device=self.device)
+                allsizes = self.all_gather(sizes)
             m = max(int(allsizes.max()), 1)
             pad = torch.zeros((self.world, m), dtype=dtype, device=self.device)
             for r, s in enumerate(send):

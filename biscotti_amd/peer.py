@@ -8,6 +8,12 @@ Two launch modes share one engine:
 * SPMD under torchrun (WORLD_SIZE set): the N peers are packed as virtual peers onto the ranks,
   one rank per GPU, collectives over RCCL/xGMI.
 
+Rank failure (the reference's crashed peer, FAIL_PROB / failAndRestartLocal.sh): every collective
+has a timeout (``--comm-timeout``), so the survivors of a dead rank fail instead of hanging; run
+under ``torchrun --max-restarts K`` with ``--chain-file F --resume`` and the restarted job resumes
+from the last block on disk (a torn final record is dropped).  ``--fail-at IT --fail-rank R``
+injects such a crash deterministically.
+
 At exit rank 0 prints the chain with PrintChain's format (blockchain.go:43-54) to stdout, which
 is what localTest.sh compares between peers.
 """
@@ -47,7 +53,7 @@ def main(argv=None) -> int:
     from .parallel.comm import Comm
     from .protocol.engine import BiscottiEngine
 
-    comm = Comm.init(device=cfg.device)
+    comm = Comm.init(device=cfg.device, timeout_s=cfg.comm_timeout_s)
     eng = BiscottiEngine(cfg, comm)
     n = 0
     while ns.rounds is None or n < ns.rounds:

@@ -53,6 +53,13 @@ class RunConfig:
     deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
     phase_sync: bool = True         # device sync at phase boundaries (accurate per-phase GPU times)
     side_stream_skip_every: int = 4  # speculative-MSM stream leaves every Nth CU free (0: no CU mask)
+    audit_aggregate: bool = True    # check the recovered aggregate against the miners' summed chunk
+    #                                 commitments (verifyCommitment on the aggregate; not in the reference)
+    noise_table: bool = True        # GPU: every noiser's 100 noise vectors resident in HBM (pre-sampled
+    #                                 like client_obj.py:61-63) instead of regenerated each round
+    comm_timeout_s: float = 300.0   # collective timeout: a dead rank fails the job instead of hanging it
+    fail_at: int = -1               # fault injection: rank `fail_rank` dies right after committing this
+    fail_rank: int = 0              #   iteration (the reference's FAIL_PROB crash, made deterministic)
 
     def protocol(self, rt):
         pc = rt.ProtocolConfig()
@@ -124,6 +131,11 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--log-every-peer", action="store_true")
     ap.add_argument("--deterministic-time", action="store_true")
     ap.add_argument("--no-phase-sync", dest="phase_sync", action="store_false")
+    ap.add_argument("--no-audit-aggregate", dest="audit_aggregate", action="store_false")
+    ap.add_argument("--no-noise-table", dest="noise_table", action="store_false")
+    ap.add_argument("--comm-timeout", dest="comm_timeout_s", type=float, default=300.0)
+    ap.add_argument("--fail-at", type=int, default=-1, help="fault injection: die after committing this iteration")
+    ap.add_argument("--fail-rank", type=int, default=0)
 
 
 def config_from_args(ns: argparse.Namespace) -> RunConfig:

@@ -42,6 +42,15 @@ def _seed_bytes(seed: int, tag: str, i: int) -> bytes:
     return hashlib.sha256(f"{seed}:{tag}:{i}".encode()).digest()
 
 
+def _bytes_as(b: torch.Tensor, dtype) -> torch.Tensor:
+    """Reinterpret a 1-D uint8 slice of a received buffer as `dtype` (copying only if the slice is
+    not aligned for it)."""
+    isz = torch.empty((), dtype=dtype).element_size()
+    if b.storage_offset() % isz:
+        b = b.clone()
+    return b.view(dtype)
+
+
 @dataclass
 class RoundResult:
     iteration: int
@@ -66,8 +75,9 @@ class _Ready:
 
 
 class _PendingCommitments:
-    def __init__(self, host: torch.Tensor, event):
+    def __init__(self, host: torch.Tensor, event, jac: torch.Tensor | None = None):
         self.host, self.event, self.value = host, event, None
+        self.jac = jac   # device Jacobian rows (multi-rank rounds gather these, not host marshals)
 
     def result(self) -> np.ndarray:
         if self.value is None:
@@ -110,6 +120,25 @@ class HostCrypto:
         """[R, C, 64] -> [C, 64]"""
         return torch.from_numpy(rt().g1_sum_marshaled(pts.numpy()))
 
+    # points travel as 64-byte kyber marshals on this backend
+    point_width, point_dtype = 64, torch.uint8
+
+    def commit_rows_tensor(self, pending) -> torch.Tensor:
+        return torch.from_numpy(np.ascontiguousarray(pending.result()))
+
+    def marshal_rows(self, t: torch.Tensor) -> np.ndarray:
+        return t.contiguous().numpy()
+
+    def check_aggregate(self, coeffs: torch.Tensor, csum: torch.Tensor) -> np.ndarray:
+        """ok[m, k]: commitment of recovered chunk k == miner m's summed chunk commitment (host)."""
+        c, s = coeffs.numpy(), csum.numpy()
+        ok = np.zeros((s.shape[0], self.nchunks), np.int32)
+        for k in range(self.nchunks):
+            L = min(self.poly, self.d - k * self.poly)
+            ref = np.frombuffer(self.key.commit(np.ascontiguousarray(c[k, :L]), k * self.poly), np.uint8)
+            ok[:, k] = [int(np.array_equal(ref, s[m, k])) for m in range(s.shape[0])]
+        return ok
+
 
 class DeviceCrypto:
     """GPU crypto backend: HBM-resident tables, Jacobian points [.., 24] int32."""
@@ -136,7 +165,9 @@ class DeviceCrypto:
             ev = torch.cuda.Event()
             ev.record(stream)
         qdelta.record_stream(stream)
-        return _PendingCommitments(host, ev)
+        if stream is not main:
+            jac.record_stream(main)
+        return _PendingCommitments(host, ev, jac)
 
     def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
         return self.commitments_async(qdelta).result()
@@ -163,6 +194,18 @@ class DeviceCrypto:
     def sum_rows(self, pts: torch.Tensor) -> torch.Tensor:
         """[R, C, 24] -> [C, 24]"""
         return B.sum_rows(pts.contiguous(), None, None)
+
+    # points travel as Jacobian limbs [24] int32 on this backend
+    point_width, point_dtype = 24, torch.int32
+
+    def commit_rows_tensor(self, pending) -> torch.Tensor:
+        return pending.jac
+
+    def marshal_rows(self, t: torch.Tensor) -> np.ndarray:
+        return rt().g1_marshal_jac_batch(t.contiguous().cpu().numpy().view(np.uint32))
+
+    def check_aggregate(self, coeffs: torch.Tensor, csum: torch.Tensor) -> torch.Tensor:
+        return self.eng.check_chunks(coeffs, csum)
 
 
 class BiscottiEngine:
@@ -208,11 +251,12 @@ class BiscottiEngine:
                 self.fsm.addresses = addrs[: self.N]
         if cfg.resume and cfg.chain_file:
             self._resume(cfg.chain_file)
-        if cfg.chain_file and self.comm.rank == 0:
-            import os
-
-            if not (cfg.resume and os.path.exists(cfg.chain_file)):
-                self.fsm.chain.save(cfg.chain_file)  # genesis (or the resumed prefix) first
+        if cfg.chain_file:
+            # every rank has read the file before rank 0 rewrites it: genesis, or the verified
+            # prefix of a resumed chain (a torn final record left by a crash is dropped here)
+            self.comm.barrier()
+            if self.comm.rank == 0:
+                self.fsm.chain.save(cfg.chain_file)
         self.W = torch.from_numpy(np.array(self.fsm.chain.latest().data.global_w, dtype=np.float64)).to(self.dev)
         # ---- keys
         if cfg.commit_key:
@@ -228,6 +272,8 @@ class BiscottiEngine:
             # speculative MSMs: a stream masked to 3/4 of the CUs (critical path keeps the rest)
             self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, cfg.side_stream_skip_every) \
                 if cfg.side_stream_skip_every > 0 else (torch.cuda.Stream(device=self.dev, priority=lo), 0)
+            # work no consumer in the round waits for (the miners' witness sums) runs here
+            self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
             torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
             torch.cuda.set_stream(self.main_stream)
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
@@ -245,7 +291,12 @@ class BiscottiEngine:
         self.vrf_noise_seed = {i: _seed_bytes(cfg.seed, "vrf-noise", i) for i in self.local}
         self.vrf_roles_seed = {i: _seed_bytes(cfg.seed, "vrf-roles", i) for i in self.local}
         self.sigma = self.task.noise_sigma(cfg.epsilon)
-        self.stats = {"unmasked_updates": 0, "total_updates": 0}
+        # every noiser's 100 pre-sampled noise vectors resident in HBM (314 MB for MNIST x 100 peers)
+        self.noise_tbl = None
+        if self.gpu and cfg.noising and cfg.noise_table and self.sigma > 0 and self.N * 100 * self.d * 4 <= (8 << 30):
+            self.noise_tbl = K.noise_table(self.N, self.d, cfg.seed, self.dev)
+        self._side_work: list = []   # (event, tensors) of off-critical-path device work of this round
+        self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         self.rounds_done = 0
         self._head = None
         import atexit
@@ -263,6 +314,7 @@ class BiscottiEngine:
                 if head.get(k) is not None:
                     head[k].result()
         head = None  # drop the round's tensors while their streams are all still alive
+        self._side_work = []
         if self.gpu and getattr(self, "side_stream", None) is not None:
             torch.cuda.synchronize(self.dev)
             torch.cuda.set_stream(torch.cuda.default_stream(self.dev))
@@ -386,29 +438,55 @@ class BiscottiEngine:
             noisers = dict(zip(local_workers, sel))
         with tm.phase("noise"):
             if cfg.noising and self.sigma > 0 and local_workers:
-                nz = h2d([noisers[w] for w in local_workers], torch.int32, self.dev)
+                ids = [noisers[w] for w in local_workers]
+                assert all(0 <= j < self.N for row in ids for j in row), "noiser id out of range"
+                nz = h2d(ids, torch.int32, self.dev)
                 sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma)
                            for j in noisers[w]] for w in local_workers], torch.float32, self.dev)
-                noised = K.dp_noise(delta, nz, sc, cfg.seed, it)
+                noised = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl)
             else:
                 noised = delta
         # ---------------------------------------------------------------- verification
         with tm.phase("verify"):
             single = comm.world == 1
             commit_of: dict = {}
+            g_commit = g_noised = g_delta = g_ts = None
+            need_X = cfg.verification and bool(inbox)
 
-            def _materialize_commits():  # single rank: first use, after the Krum kernels are queued
-                if not commit_of and local_workers:
-                    cl = pending_commits.result()
-                    commit_of.update({w: cl[row_of[w]].tobytes() for w in local_workers})
+            def _materialize_commits():  # first use comes after the Krum kernels are queued
+                if commit_of:
+                    return
+                if single:
+                    if local_workers:
+                        cl = pending_commits.result()
+                        commit_of.update({w: cl[row_of[w]].tobytes() for w in local_workers})
+                elif workers:   # every worker's commitment: one batched marshal of the gathered rows
+                    sel = h2d([self.flat[w] for w in workers], torch.long, self.dev)
+                    cl = self.crypto.marshal_rows(g_commit.index_select(0, sel))
+                    commit_of.update({w: cl[i].tobytes() for i, w in enumerate(workers)})
             if not single:
-                commits_local = pending_commits.result()
-                cbuf = torch.zeros((self.maxlocal, 64), dtype=torch.uint8, device=self.dev)
+                # ONE all_gather carries every rank's commitments (device Jacobian rows), noised
+                # deltas (the verifiers' input) and, on the plain path, deltas (the block payload)
+                cr = self.crypto
+                parts = [torch.zeros((self.maxlocal, cr.point_width), dtype=cr.point_dtype, device=self.dev)]
+                if need_X or not cfg.secure_agg:
+                    parts.append(torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev))
+                if not cfg.secure_agg:
+                    parts.append(torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev))
+                    # + each rank's clock: every rank builds the plain block with the leader's timestamp
+                    parts.append(torch.full((self.maxlocal, 1), self._now(it), dtype=torch.int64, device=self.dev))
                 if local_workers:
                     lidx = h2d([w - self.lo for w in local_workers], torch.long, self.dev)
-                    cbuf.index_copy_(0, lidx, torch.from_numpy(commits_local).to(self.dev))
-                commits_all = comm.all_gather(cbuf).reshape(-1, 64).cpu().numpy()
-                commit_of = {w: commits_all[self.flat[w]].tobytes() for w in workers}
+                    parts[0].index_copy_(0, lidx, cr.commit_rows_tensor(pending_commits).to(self.dev))
+                    if len(parts) > 1:
+                        parts[1].index_copy_(0, lidx, noised)
+                    if len(parts) > 2:
+                        parts[2].index_copy_(0, lidx, delta)
+                got = comm.all_gather_packed(parts)
+                g_commit = got[0].reshape(-1, cr.point_width)
+                g_noised = got[1].reshape(-1, self.d) if len(got) > 1 else None
+                g_delta = got[2].reshape(-1, self.d) if len(got) > 2 else None
+                g_ts = got[3][:, 0, 0] if len(got) > 3 else None
             if cfg.colluders > 0:  # privacy experiment bookkeeping (isCollusionAttack, main.go:1026-1057)
                 thr = self.pc.collusion_thresh
                 if any(v >= thr for v in plan.verifiers):
@@ -418,32 +496,38 @@ class BiscottiEngine:
             signatures: dict = {}
             pending_signatures = None
             local_verifiers = [v for v in plan.verifiers if live[v] and v in self.local]
-            if cfg.verification and inbox:
+            # Multi-Krum is a pure function of the gathered inbox, so on several ranks EVERY rank
+            # evaluates it (identical inputs, deterministic kernel) instead of all_gathering the
+            # verifiers' accept masks; RONI depends on each verifier's own data and still gathers
+            replicated = not single and cfg.defense == "KRUM"
+            judges = [v for v in plan.verifiers if live[v]] if replicated else local_verifiers
+            if need_X:
                 nv, ni = len(plan.verifiers), len(inbox)
                 if single:
                     X = noised.index_select(0, h2d([row_of[w] for w in inbox], torch.long, self.dev)) \
-                        if local_verifiers else None
+                        if judges else None
                 else:
-                    nbuf = torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev)
-                    if local_workers:
-                        nbuf.index_copy_(0, lidx, noised)
-                    gathered = comm.all_gather(nbuf).reshape(-1, self.d)
-                    X = gathered.index_select(0, h2d([self.flat[w] for w in inbox], torch.long, self.dev)) \
-                        if local_verifiers else None
+                    X = g_noised.index_select(0, h2d([self.flat[w] for w in inbox], torch.long, self.dev)) \
+                        if judges else None
                 acc_np = np.zeros((nv, ni), np.uint8)
                 sig_np = np.zeros((nv, ni, 64), np.uint8)
                 krum_cache = None
                 pos = {w: j for j, w in enumerate(inbox)}
-                # every local verifier's accept list first, then ONE native call signs them all
+                # every verifier's accept list first, then ONE native call signs the local ones' lists
                 msgs, key_of, ids, slots, sks, bases = [], [], [], [], [], []
-                for v in local_verifiers:
+                for v in judges:
                     with tm.phase("verify.defense"):
-                        if cfg.defense == "KRUM":  # identical inputs -> identical Krum result per rank
+                        if cfg.defense == "KRUM":  # identical inputs -> identical Krum result
                             krum_cache = krum_cache or self._verify(X, inbox, it, v)
                             accept = krum_cache
                         else:
                             accept = self._verify(X, inbox, it, v)
                     vi = plan.verifiers.index(v)
+                    for j, a_ in enumerate(accept):
+                        if a_:
+                            acc_np[vi, j] = 1
+                    if v not in self.local:
+                        continue   # the verifier's own rank signs its approvals
                     _materialize_commits()
                     sks.append(self.sk[v])
                     bases.append(_seed_bytes(cfg.seed, f"nonce-{it}", v))
@@ -458,18 +542,16 @@ class BiscottiEngine:
                 # --verify-signatures checks them) or at the end of the round
                 sign_job = R.schnorr_sign_multi_async(msgs, sks, key_of, bases, ids, cfg.host_threads) \
                     if msgs else None
-                for vi, j in slots:
-                    acc_np[vi, j] = 1
-                acc_all = acc_np[None] if single else \
+                acc_all = acc_np[None] if (single or replicated) else \
                     comm.all_gather(torch.from_numpy(acc_np).to(self.dev)).cpu().numpy()
+                acc_row = {v: 0 if (single or replicated) else comm.owner(v, self.N) for v in plan.verifiers}
                 for vi, v in enumerate(plan.verifiers):
                     if not live[v]:
                         continue
-                    o = 0 if single else comm.owner(v, self.N)
-                    accepted_map[v] = [inbox[j] for j in np.nonzero(acc_all[o, vi])[0]]
+                    accepted_map[v] = [inbox[j] for j in np.nonzero(acc_all[acc_row[v], vi])[0]]
 
                 def _join_signatures(sign_job=sign_job, slots=slots, sig_np=sig_np, acc_all=acc_all,
-                                     inbox=inbox, live=live, plan=plan):
+                                     acc_row=acc_row, inbox=inbox, live=live, plan=plan):
                     with tm.phase("verify.sign_join"):
                         sigs = sign_job.result() if sign_job is not None else []
                         for (vi, j), sg in zip(slots, sigs):
@@ -480,7 +562,7 @@ class BiscottiEngine:
                             if not live[v]:
                                 continue
                             o = 0 if single else comm.owner(v, self.N)
-                            for j in np.nonzero(acc_all[o, vi])[0]:
+                            for j in np.nonzero(acc_all[acc_row[v], vi])[0]:
                                 signatures.setdefault(inbox[j], []).append(sig_all[o, vi, j].tobytes())
                 pending_signatures = _join_signatures
                 if not cfg.secure_agg or cfg.verify_signatures:
@@ -496,7 +578,7 @@ class BiscottiEngine:
                                              commit_of, signatures, spec)
         else:
             block = self._plain_aggregation(plan, live, approved, delta, noised, local_workers, commit_of,
-                                            signatures)
+                                            signatures, (g_delta, g_noised, g_ts))
         with tm.phase("block"):
             if block is None:
                 block = fsm.make_empty_block()
@@ -515,6 +597,7 @@ class BiscottiEngine:
             ev = eval_pending()
             if fut_roles is not None:
                 fut_roles.result()
+            self._join_side_work()
         self.stats["total_updates"] += len(block.data.deltas)
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=len(block.data.deltas) == 0,
                           node_list=self._last_nodes, approved=list(approved), verifiers=list(plan.verifiers),
@@ -522,7 +605,68 @@ class BiscottiEngine:
                           phases=tm.reset(), wall=time.perf_counter() - t_round)
         self._log_round(res)
         self.rounds_done += 1
+        if it == cfg.fail_at and comm.rank == cfg.fail_rank:
+            # fault injection: this rank's process dies abruptly after committing block `it`
+            # (the reference's FAIL_PROB crash / failAndRestartLocal.sh kill); the surviving ranks'
+            # next collective fails and an elastic launcher restarts the job from the chain file
+            self.log.info("fault injection: rank %d exits after iteration %d", comm.rank, it)
+            import os
+            import sys
+
+            sys.stderr.flush()
+            os._exit(17)
         return res
+
+    # ------------------------------------------------------------------ off-critical-path work
+    def _background(self, fn, *inputs):
+        """Run `fn` on the background stream behind everything queued so far on the main stream.
+        Nothing on the round's critical path reads the result; the main stream joins it
+        (stream-ordered, no host wait) at the end of the round.  Without a GPU it runs inline."""
+        if not self.gpu:
+            return fn()
+        main = torch.cuda.current_stream()
+        bg = self.bg_stream
+        bg.wait_stream(main)
+        with torch.cuda.stream(bg):
+            out = fn()
+            ev = torch.cuda.Event()
+            ev.record(bg)
+        for t in inputs:
+            if isinstance(t, torch.Tensor):
+                t.record_stream(bg)
+        self._side_work.append((ev, out))
+        return out
+
+    def _audit(self, coeffs: torch.Tensor, csum: torch.Tensor):
+        """Queue the aggregate audit (recovered chunks vs the miners' summed chunk commitments);
+        returns a callable giving ok int32 [n_miners, nchunks].  On the GPU the check runs on the
+        side stream while the host builds the block (gob + SHA-256)."""
+        if not self.gpu:
+            ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
+            return lambda: ok
+        main = torch.cuda.current_stream()
+        st = self.side_stream
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            ok = self.crypto.check_aggregate(coeffs, csum)
+            host = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
+            host.copy_(ok, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        coeffs.record_stream(st)
+        csum.record_stream(st)
+
+        def result():
+            ev.synchronize()
+            return host.numpy()
+        return result
+
+    def _join_side_work(self) -> None:
+        if self._side_work:
+            main = torch.cuda.current_stream()
+            for ev, _ in self._side_work:
+                main.wait_event(ev)
+            self._side_work.clear()
 
     # ------------------------------------------------------------------ verification defences
     def _verify(self, X: torch.Tensor, inbox: list, it: int, verifier: int) -> list[bool]:
@@ -571,9 +715,11 @@ class BiscottiEngine:
             return None
         node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
         part_of = {m: dict(routes[m])[node_list[0]] for m in contributing}
-        pw = 24 if self.gpu else 64
-        pdt = torch.int32 if self.gpu else torch.uint8
+        pw, pdt = self.crypto.point_width, self.crypto.point_dtype
+        esz = torch.empty((), dtype=pdt).element_size()
         ar = torch.arange(nch, dtype=torch.long, device=self.dev)
+        nc = len(contributing)
+        audit = cfg.audit_aggregate
 
         def cols_of(part):  # the miner's witness slots + the chunk-commitment slot
             return list(range(spm * part, spm * part + spm)) + [T]
@@ -585,46 +731,59 @@ class BiscottiEngine:
                 for m in contributing:
                     recv[m] = (None, None, rows)
             else:
-                send_p, send_y = [], []
+                # ONE all_to_all: per (miner, worker) entry the miner's witness + chunk-commitment
+                # points, then its share values, as raw bytes.  Every rank derives what it receives
+                # from the replicated routing, so no size exchange precedes it.
+                per_p, per_y = nch * (spm + 1) * pw, nch * spm
+                pbytes = per_p * esz
+                ent_bytes = pbytes + per_y * 8
+                send = []
                 for dst in range(comm.world):
                     ents = [(m, w) for m in contributing if comm.owner(m, self.N) == dst
                             for w in node_list if w in ap_row]
                     if ents:
                         ir = h2d([ap_row[w] for _, w in ents], torch.long, self.dev)
                         ic = h2d([cols_of(part_of[m]) for m, _ in ents], torch.long, self.dev)
-                        g = pts[ir[:, None, None], ar[None, :, None], ic[:, None, :]]
-                        gy = ys[ir[:, None, None], ar[None, :, None], ic[:, None, :spm]]
-                        send_p.append(g.reshape(-1))
-                        send_y.append(gy.reshape(-1))
+                        g = pts[ir[:, None, None], ar[None, :, None], ic[:, None, :]]       # [E, nch, spm+1, pw]
+                        gy = ys[ir[:, None, None], ar[None, :, None], ic[:, None, :spm]]  # [E, nch, spm]
+                        send.append(torch.cat([g.reshape(len(ents), -1).view(torch.uint8),
+                                               gy.reshape(len(ents), -1).view(torch.uint8)], dim=1).reshape(-1))
                     else:
-                        send_p.append(torch.empty((0,), dtype=pdt, device=self.dev))
-                        send_y.append(torch.empty((0,), dtype=torch.int64, device=self.dev))
-                rp, ry = comm.all_to_all(send_p), comm.all_to_all(send_y)
+                        send.append(torch.empty((0,), dtype=torch.uint8, device=self.dev))
+                src_ents = {src: [(mm, w) for mm in contributing if comm.owner(mm, self.N) == comm.rank
+                                  for w in node_list if comm.owner(w, self.N) == src] for src in range(comm.world)}
+                rb = comm.all_to_all(send, [len(src_ents[s]) * ent_bytes for s in range(comm.world)])
                 for m in contributing:
                     if m not in self.local:
                         continue
                     ps_, ys_ = [], []
                     for src in range(comm.world):
-                        src_ents = [(mm, w) for mm in contributing if comm.owner(mm, self.N) == self.comm.rank
-                                    for w in node_list if comm.owner(w, self.N) == src]
-                        per_p, per_y = nch * (spm + 1) * pw, nch * spm
-                        for k, (mm, w) in enumerate(src_ents):
+                        for k, (mm, w) in enumerate(src_ents[src]):
                             if mm == m:
-                                ps_.append(rp[src][k * per_p:(k + 1) * per_p].view(nch, spm + 1, pw))
-                                ys_.append(ry[src][k * per_y:(k + 1) * per_y].view(nch, spm))
+                                e = rb[src][k * ent_bytes:(k + 1) * ent_bytes]
+                                ps_.append(_bytes_as(e[:pbytes], pdt).view(nch, spm + 1, pw))
+                                ys_.append(_bytes_as(e[pbytes:], torch.int64).view(nch, spm))
                     recv[m] = (torch.stack(ps_), torch.stack(ys_), None)
         with tm.phase("miner_aggregate"):
-            nc = len(contributing)
             agg_y = torch.zeros((nc, nch, spm), dtype=torch.int64, device=self.dev)
+            # every miner's summed chunk commitments (aggregateSecret, kyber.go:251-253): the audit
+            # checks the recovered aggregate against them
+            csum = torch.zeros((nc, nch, pw), dtype=pdt, device=self.dev)
             if single and self.gpu and contributing:
-                # aggregateSecret for every miner in ONE launch: the rows (contributing workers) are
-                # shared, the column list concatenates each miner's witness + commitment slots
+                # aggregateSecret for every miner: the rows (contributing workers) are shared.  The
+                # chunk-commitment sums run first (the audit reads them); the 7 witness sums per
+                # chunk and miner -- which nothing in a round reads: the reference's leader never
+                # checks aggregated witnesses -- run on the background stream, off the critical path
                 rows = recv[contributing[0]][2]
-                base = np.arange(nch)[:, None] * (T + 1)
-                cols = np.concatenate([(base + np.asarray(cols_of(part_of[m]))[None, :]).reshape(-1)
-                                       for m in contributing])
+                rows_i = rows.int()
+                base = np.arange(nch) * (T + 1)
                 flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-                _ = B.sum_rows(flat, rows.int(), h2d(cols.astype(np.int32), torch.int32, self.dev))
+                ccols = h2d(np.concatenate([base + T for _ in contributing]).astype(np.int32), torch.int32,
+                            self.dev)
+                csum = B.sum_rows(flat, rows_i, ccols).view(nc, nch, pw)
+                wcols = h2d(np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
+                                            for m in contributing]).astype(np.int32), torch.int32, self.dev)
+                self._background(lambda: B.sum_rows(flat, rows_i, wcols), flat, rows_i, wcols)
                 ysum = ys.index_select(0, rows).sum(0)   # [nch, T]
                 for ci, m in enumerate(contributing):
                     agg_y[ci] = ysum[:, spm * part_of[m]: spm * part_of[m] + spm]
@@ -638,52 +797,80 @@ class BiscottiEngine:
                         cols = h2d([k * (T + 1) + c for k in range(nch) for c in cols_of(part)], torch.long,
                                    self.dev)
                         flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-                        _ = self.crypto.sum_rows(flat.index_select(0, rows).index_select(1, cols))
+                        s = self.crypto.sum_rows(flat.index_select(0, rows).index_select(1, cols))
+                        csum[ci] = s.view(nch, spm + 1, pw)[:, spm]
                         agg_y[ci] = ys.index_select(0, rows)[:, :, spm * part: spm * part + spm].sum(0)
+                    elif self.gpu:
+                        flatm = p_.reshape(p_.shape[0], nch * (spm + 1), pw)
+                        cc = h2d(np.arange(nch, dtype=np.int32) * (spm + 1) + spm, torch.int32, self.dev)
+                        csum[ci] = B.sum_rows(flatm, None, cc)
+                        wc = h2d((np.arange(nch)[:, None] * (spm + 1) + np.arange(spm)[None, :]).reshape(-1)
+                                 .astype(np.int32), torch.int32, self.dev)
+                        self._background(lambda f=flatm, c=wc: B.sum_rows(f, None, c), flatm, wc)
+                        agg_y[ci] = y_.sum(0)
                     else:
-                        _ = self.crypto.sum_rows(p_.reshape(p_.shape[0], -1, pw))
+                        s = self.crypto.sum_rows(p_.reshape(p_.shape[0], -1, pw))
+                        csum[ci] = s.view(nch, spm + 1, pw)[:, spm]
                         agg_y[ci] = y_.sum(0)
         with tm.phase("recover"):
-            agg_all = agg_y[None] if single else comm.all_gather(agg_y)   # [world, nc, nch, spm]
+            now = self._now(plan.iteration)
+            if single:
+                agg_all, cs_all, ts_all = agg_y[None], csum[None], None
+            else:
+                # ONE all_gather: every miner's share sums (+ its chunk-commitment sums for the audit)
+                # and every rank's clock.  Each rank then recovers the aggregate itself -- exact
+                # integer recovery on identical inputs, so every rank builds the leader's block bit
+                # for bit -- instead of waiting for a block broadcast.
+                parts = [agg_y.reshape(1, -1), torch.full((1, 1), now, dtype=torch.int64, device=self.dev)]
+                if audit:
+                    parts.append(csum.reshape(1, -1))
+                got = comm.all_gather_packed(parts)
+                agg_all = got[0].view(comm.world, nc, nch, spm)
+                ts_all = got[1]
+                cs_all = got[2].view(comm.world, nc, nch, pw) if audit else None
             leader_rank = comm.owner(plan.leader, self.N)
-            block = block_bytes = None
-            if comm.rank == leader_rank:
-                cols, xs = [], []
-                for ci, m in enumerate(contributing):
-                    o = 0 if single else comm.owner(m, self.N)
-                    cols.append(agg_all[o, ci])
-                    xs += [spm * part_of[m] + s_ - 10 for s_ in range(spm)]
-                agg = torch.cat(cols, dim=1).contiguous()      # [nchunks, npts]
-                xs_t = h2d(xs, torch.int32, self.dev)
-                with tm.phase("recover.kernel"):
-                    W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
-                    st = status.cpu().numpy()
-                    W_np = W_new.cpu().numpy()
-                if not st.all():  # inconsistent shares: the reference's float64 least squares
-                    aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()
-                    for k in np.nonzero(st == 0)[0]:
-                        c = R.recover_lstsq(xs, [int(v) for v in aggn[k]], cfg.poly_size - 1)
-                        for j, v in enumerate(c):
-                            i = k * cfg.poly_size + j
-                            if i < self.d:
-                                W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
-                    self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
-                with tm.phase("recover.block"):
-                    block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list],
-                                                  self._now(plan.iteration))
-                if not single:
-                    block_bytes = block.serialize()
-            if not single:
-                data = comm.broadcast_bytes(block_bytes, leader_rank)
-                if comm.rank != leader_rank:
-                    block = R.Block.deserialize(data)
-                    if block.compute_hash() != block.hash:
-                        raise RuntimeError("received block with a bad hash")
+            own = [0 if single else comm.owner(m, self.N) for m in contributing]
+            xs = [spm * part_of[m] + s_ - 10 for m in contributing for s_ in range(spm)]
+            agg = torch.cat([agg_all[own[ci], ci] for ci in range(nc)], dim=1).contiguous()   # [nchunks, npts]
+            xs_t = h2d(xs, torch.int32, self.dev)
+            with tm.phase("recover.kernel"):
+                W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
+                audit_ok = self._audit(coeffs, torch.stack([cs_all[own[ci], ci] for ci in range(nc)])) \
+                    if audit else None
+                st = status.cpu().numpy()
+                W_np = W_new.cpu().numpy()
+                if ts_all is not None:
+                    now = int(ts_all[leader_rank].reshape(-1)[0])   # the leader's clock stamps the block
+            if not st.all():  # inconsistent shares: the reference's float64 least squares
+                aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()
+                for k in np.nonzero(st == 0)[0]:
+                    c = R.recover_lstsq(xs, [int(v) for v in aggn[k]], cfg.poly_size - 1)
+                    for j, v in enumerate(c):
+                        i = k * cfg.poly_size + j
+                        if i < self.d:
+                            W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
+                self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
+            with tm.phase("recover.block"):
+                block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
+            if audit_ok is not None:
+                with tm.phase("recover.audit"):
+                    ok = audit_ok()
+                if not ok.all():
+                    # a miner's sums do not commit to the recovered update: refuse it (the round
+                    # ends like the reference's missing-quorum path, with an empty block)
+                    self.stats["audit_failures"] += 1
+                    self.log.info("aggregate audit failed for %d (miner, chunk) pairs in iteration %d: empty block",
+                                  int((ok == 0).sum()), plan.iteration)
+                    return None
             self._last_nodes = node_list
             return block
 
     # ------------------------------------------------------------------ plain aggregation path
-    def _plain_aggregation(self, plan, live, approved, delta, noised, local_workers, commit_of, signatures):
+    def _plain_aggregation(self, plan, live, approved, delta, noised, local_workers, commit_of, signatures,
+                           gathered=(None, None, None)):
+        """RegisterUpdate path (-sa=false): the leader miner's block carries every routed update in
+        full.  With several ranks the deltas, noised deltas and clocks already travelled in the
+        verification all_gather, so every rank builds the leader's block itself (no broadcast)."""
         cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
         self._last_nodes = []
         with tm.phase("aggregate"):
@@ -691,28 +878,22 @@ class BiscottiEngine:
             leader = plan.leader
             if not live[leader] or not routes.get(leader):
                 return None
-            ups = routes[leader]
-            idx = {w: i for i, w in enumerate(local_workers)}
-            dbuf = self._rows_buffer({w: delta[idx[w]] for w in local_workers}, self.d, torch.float32)
-            nbuf = self._rows_buffer({w: noised[idx[w]] for w in local_workers}, self.d, torch.float32)
-            dall, nall = comm.all_gather(dbuf), comm.all_gather(nbuf)
-            leader_rank = comm.owner(leader, self.N)
-            block_bytes = None
-            if comm.rank == leader_rank:
-                rows = h2d([comm.owner(w, self.N) * self.maxlocal + (w - comm.peer_range(self.N, comm.owner(w, self.N)).start)
-                            for w in ups], torch.long, self.dev)
-                dv = dall.reshape(-1, self.d).index_select(0, rows).double().cpu().numpy()
-                nv = nall.reshape(-1, self.d).index_select(0, rows).double().cpu().numpy()
-                blk = fsm.make_plain_block_arrays(self.W.cpu().numpy(), list(ups), dv, nv,
-                                                  [commit_of[w] for w in ups],
-                                                  [signatures.get(w, []) for w in ups], self._now(plan.iteration))
-                if comm.world == 1:
-                    self._last_nodes = list(ups)
-                    return blk
-                block_bytes = blk.serialize()
-            data = comm.broadcast_bytes(block_bytes, leader_rank)
-            self._last_nodes = list(ups)
-            return R.Block.deserialize(data)
+            ups = list(routes[leader])
+            now = self._now(plan.iteration)
+            if comm.world == 1:
+                idx = {w: i for i, w in enumerate(local_workers)}
+                sel = h2d([idx[w] for w in ups], torch.long, self.dev)
+                dsrc, nsrc = delta, noised
+            else:
+                dsrc, nsrc, ts = gathered
+                sel = h2d([self.flat[w] for w in ups], torch.long, self.dev)
+                now = int(ts[comm.owner(leader, self.N)])
+            dv = dsrc.index_select(0, sel).double().cpu().numpy()
+            nv = nsrc.index_select(0, sel).double().cpu().numpy()
+            blk = fsm.make_plain_block_arrays(self.W.cpu().numpy(), ups, dv, nv, [commit_of[w] for w in ups],
+                                              [signatures.get(w, []) for w in ups], now)
+            self._last_nodes = ups
+            return blk
 
     # ------------------------------------------------------------------ logging
     def _log_round(self, r: RoundResult) -> None:

@@ -142,3 +142,36 @@ def test_sum_rows_is_aggregate(rt):
         assert bytes(agg[k, 21]) == chunk_commits[k]
         for s in range(21):
             assert bytes(agg[k, s]) == wits[k * 21 + s]
+
+
+@pytest.mark.parametrize("d,b0", [(57, 11), (7850, 12)])
+def test_chunk_check_audits_aggregate(rt, d, b0):
+    """k_chunk_check: the recovered aggregate's chunk commitments against the miners' sums of the
+    workers' chunk commitments (homomorphism), incl. a short last chunk, wide recovered sums and
+    a tampered miner."""
+    from biscotti_amd.ops import bn256 as B
+    key = rt.CommitKey.generate(d, 3)
+    eng = B.DeviceCommitEngine(key, 10, 21, b0=b0)
+    rng = np.random.default_rng(d)
+    q = rng.integers(-5000, 5000, size=(6, d), dtype=np.int64)
+    q[0, :13] = 0
+    qt = torch.from_numpy(q).cuda()
+    pts, _ = eng.shares(qt, torch.arange(6, dtype=torch.int32, device="cuda"), commit_only=True)   # [6, nch, 1, 24]
+    csum = B.sum_rows(pts.reshape(6, eng.nchunks, 24), None, None).view(1, eng.nchunks, 24)
+    total = q.sum(0)
+    coeffs = np.zeros((eng.nchunks, 10), np.int64)
+    coeffs.reshape(-1)[:d] = total
+    bad = csum.clone()
+    bad[0, 1] = csum[0, 2]                   # miner 1 reports a wrong chunk-1 sum
+    both = torch.cat([csum, bad])
+    ok = eng.check_chunks(torch.from_numpy(coeffs).cuda(), both).cpu().numpy()
+    assert ok[0].all()
+    assert ok[1, 1] == 0 and ok[1].sum() == eng.nchunks - 1
+    wrong = coeffs.copy()
+    wrong[eng.nchunks - 1, 0] += 1
+    ok2 = eng.check_chunks(torch.from_numpy(wrong).cuda(), csum).cpu().numpy()
+    assert ok2[0, eng.nchunks - 1] == 0 and ok2[0, :-1].all()
+    # the device check agrees with the host commitments
+    hb = np.stack([np.frombuffer(key.commit(coeffs[k, :min(10, d - 10 * k)], 10 * k), np.uint8)
+                   for k in range(eng.nchunks)])
+    np.testing.assert_array_equal(B.marshal(csum.view(-1, 24)).cpu().numpy(), hb)

@@ -136,3 +136,32 @@ def test_engine_rounds_on_gpu():
     assert sum(not r.empty for r in res) >= 3
     assert min(r.test_error for r in res) < 0.8
     eng.close()
+
+
+def test_eval_errors_two_sets_one_launch():
+    """Test error and attack rate from one MFMA kernel launch, against the fp32 torch reference."""
+    X, y, off, nt, pid, W = _fed(P=1, n=2347)
+    split = 2000
+    ref_a = K.eval_error(X[:split], y[:split], W, 784, 10)
+    ref_b = K.eval_error(X[split:], y[split:], W, 784, 10)
+    a, b = K.eval_errors_async(X.cuda(), y.cuda(), split, W.cuda(), 784, 10)()
+    assert abs(a - ref_a) <= 1.0 / split and abs(b - ref_b) <= 1.0 / (2347 - split)
+    # rows not a multiple of the 16-row tile, no transform
+    Xs, ys_ = X[:37], y[:37]
+    assert abs(K.eval_error(Xs.cuda(), ys_.cuda(), W.cuda(), 784, 10, transform=False)
+               - K.eval_error(Xs, ys_, W, 784, 10, transform=False)) <= 1.0 / 37
+
+
+def test_noise_table_matches_on_the_fly():
+    """The resident noise table gives bit-identical noised deltas to per-round generation."""
+    delta = torch.randn((7, 7850)).cuda()
+    noisers = torch.tensor([[1, 2], [2, 3], [1, 4], [0, 9], [5, 6], [11, 3], [0, 0]], dtype=torch.int32).cuda()
+    scales = torch.full((7, 2), -0.77).cuda()
+    scales[3, 1] = 0.0
+    tbl = K.noise_table(12, 7850, 42, "cuda")
+    for it in (0, 13, 113):
+        a = K.dp_noise(delta, noisers, scales, 42, it)
+        b = K.dp_noise(delta, noisers, scales, 42, it, table=tbl)
+        assert torch.equal(a, b), it
+    ref = K.noise_vector(5, 13, 7850, 42)
+    np.testing.assert_allclose(tbl[5, 13].cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
