@@ -170,16 +170,20 @@ class DeviceCommitEngine:
         return out
 
 
-def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | None) -> torch.Tensor:
-    """out[i] = sum_r pts[rows[r], cols[i]] for a [R, C, 24] Jacobian tensor."""
+def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | None,
+             check: bool = True) -> torch.Tensor:
+    """out[i] = sum_r pts[rows[r], cols[i]] for a [R, C, 24] Jacobian tensor.
+
+    check=False: the caller validated the index lists on the host before uploading them (the
+    device-side max() would stall the host behind everything queued on the stream)."""
     assert pts.dim() == 3 and pts.shape[2] == 24
     R, Cn, _ = pts.shape
     nrows = R if rows is None else rows.numel()
     ncols = Cn if cols is None else cols.numel()
     if rows is not None:
-        assert rows.dtype == torch.int32 and (nrows == 0 or int(rows.max()) < R)
+        assert rows.dtype == torch.int32 and (not check or nrows == 0 or int(rows.max()) < R)
     if cols is not None:
-        assert cols.dtype == torch.int32 and (ncols == 0 or int(cols.max()) < Cn)
+        assert cols.dtype == torch.int32 and (not check or ncols == 0 or int(cols.max()) < Cn)
     out = torch.empty((ncols, 24), dtype=torch.int32, device=pts.device)
     _check(hip().bsc_sum_rows2(_ptr(pts), Cn, _ptr(rows), nrows, _ptr(cols), ncols, _ptr(out), _stream()),
            "sum_rows2")

@@ -250,9 +250,16 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
     err = torch.zeros((2,), dtype=torch.int32, device=X.device)
     _check(hip().bsc_eval_error(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), int(split), _p(err), _stream()),
            "eval_error")
+    # download queued right behind the kernel: the read-back waits for the evaluation only, not for
+    # whatever the caller queues on the stream afterwards (the next round's head)
+    host = torch.empty((2,), dtype=torch.int32, pin_memory=True)
+    host.copy_(err, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
 
     def result():
-        e = err.tolist()
+        ev.synchronize()
+        e = host.tolist()
         return (e[0] / na if na else 0.0, e[1] / nb if nb else 0.0)
     return result
 

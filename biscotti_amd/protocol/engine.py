@@ -199,6 +199,7 @@ class DeviceCrypto:
     point_width, point_dtype = 24, torch.int32
 
     def commit_rows_tensor(self, pending) -> torch.Tensor:
+        torch.cuda.current_stream().wait_event(pending.event)   # produced on the background stream
         return pending.jac
 
     def marshal_rows(self, t: torch.Tensor) -> np.ndarray:
@@ -400,7 +401,9 @@ class BiscottiEngine:
         with tm.phase("local_step"):
             delta, qdelta = self.task.step(self.W, it, local_workers)
         with tm.phase("commit"):
-            pending_commits = self.crypto.commitments_async(qdelta)
+            # full-vector commitments on the background stream: their first consumer is the signing
+            # after Krum, so noise + Krum on the main stream do not queue behind them
+            pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
             # only the first krum_thresh arrivals reach the verifiers (verifier_inbox), so only they
             # can be approved: they secret-share while verification runs (kyber.go:533-646), the MSM
             # on the CU-masked side stream; shares of workers the verifiers reject are never routed
@@ -775,15 +778,19 @@ class BiscottiEngine:
                 # chunk and miner -- which nothing in a round reads: the reference's leader never
                 # checks aggregated witnesses -- run on the background stream, off the critical path
                 rows = recv[contributing[0]][2]
-                rows_i = rows.int()
+                row_list = [ap_row[w] for w in node_list]
+                assert max(row_list) < pts.shape[0]        # index lists are validated on the host
+                rows_i = h2d(row_list, torch.int32, self.dev)
                 base = np.arange(nch) * (T + 1)
                 flat = pts.view(pts.shape[0], nch * (T + 1), pw)
                 ccols = h2d(np.concatenate([base + T for _ in contributing]).astype(np.int32), torch.int32,
                             self.dev)
-                csum = B.sum_rows(flat, rows_i, ccols).view(nc, nch, pw)
-                wcols = h2d(np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
-                                            for m in contributing]).astype(np.int32), torch.int32, self.dev)
-                self._background(lambda: B.sum_rows(flat, rows_i, wcols), flat, rows_i, wcols)
+                csum = B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)
+                wc = np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
+                                     for m in contributing]).astype(np.int32)
+                assert wc.max() < nch * (T + 1)
+                wcols = h2d(wc, torch.int32, self.dev)
+                self._background(lambda: B.sum_rows(flat, rows_i, wcols, check=False), flat, rows_i, wcols)
                 ysum = ys.index_select(0, rows).sum(0)   # [nch, T]
                 for ci, m in enumerate(contributing):
                     agg_y[ci] = ysum[:, spm * part_of[m]: spm * part_of[m] + spm]
@@ -803,10 +810,10 @@ class BiscottiEngine:
                     elif self.gpu:
                         flatm = p_.reshape(p_.shape[0], nch * (spm + 1), pw)
                         cc = h2d(np.arange(nch, dtype=np.int32) * (spm + 1) + spm, torch.int32, self.dev)
-                        csum[ci] = B.sum_rows(flatm, None, cc)
+                        csum[ci] = B.sum_rows(flatm, None, cc, check=False)
                         wc = h2d((np.arange(nch)[:, None] * (spm + 1) + np.arange(spm)[None, :]).reshape(-1)
                                  .astype(np.int32), torch.int32, self.dev)
-                        self._background(lambda f=flatm, c=wc: B.sum_rows(f, None, c), flatm, wc)
+                        self._background(lambda f=flatm, c=wc: B.sum_rows(f, None, c, check=False), flatm, wc)
                         agg_y[ci] = y_.sum(0)
                     else:
                         s = self.crypto.sum_rows(p_.reshape(p_.shape[0], -1, pw))
