@@ -55,10 +55,19 @@ class Comm:
                 be = "gloo"
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {"device_id": dev} if be == "nccl" else {}
-            if timeout_s:
-                import datetime
+            import datetime
 
+            if timeout_s:
                 kw["timeout"] = datetime.timedelta(seconds=float(timeout_s))
+            attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+            if attempt is not None:
+                # a restarted job (torchrun --max-restarts) must not read the previous attempt's
+                # rendezvous keys: a dead rank's stale address makes the new mesh dial a closed port
+                agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+                base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                     is_master=(rank == 0 and not agent),
+                                     timeout=datetime.timedelta(seconds=float(timeout_s or 300)))
+                kw["store"] = dist.PrefixStore(f"biscotti/attempt{attempt}", base)
             try:
                 dist.init_process_group(be, rank=rank, world_size=world, **kw)
             except TypeError:

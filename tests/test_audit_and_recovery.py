@@ -102,7 +102,7 @@ def test_rank_failure_restarts_from_chain_file(tmp_path):
            "--deterministic-time", "--comm-timeout", "60", "--print-chain", "rank0"]
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 0, "\n".join(l for l in p.stderr.splitlines() if "Train Error" not in l)[-6000:]
     assert "fault injection: rank 1 exits after iteration 2" in p.stderr
     assert "Resumed chain" in p.stderr
     from biscotti_amd.native import rt
