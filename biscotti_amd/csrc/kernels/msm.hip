@@ -420,10 +420,12 @@ extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* 
   jac acc = jac_inf();
   for (int k = threadIdx.x; k < n; k += blockDim.x)
     acc = jac_add(acc, ld_jac(pts + 24 * ((size_t)(g * (size_t)n + k) * stride + off)));
-  for (int t = 0; t < 24; ++t) sh[threadIdx.x * 24 + t] = 0;
   st_jac(sh + threadIdx.x * 24, acc);
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+  // tree only over the lanes that hold partial sums (n is typically 8 slabs: 3 levels, not 8)
+  int top = 1;
+  while (top < n && top < (int)blockDim.x) top <<= 1;
+  for (int s = top / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) {
       jac a = ld_jac(sh + threadIdx.x * 24), b = ld_jac(sh + (threadIdx.x + s) * 24);
       st_jac(sh + threadIdx.x * 24, jac_add(a, b));

@@ -640,17 +640,21 @@ class BiscottiEngine:
         self._side_work.append((ev, out))
         return out
 
-    def _audit(self, coeffs: torch.Tensor, csum: torch.Tensor):
+    def _audit(self, coeffs: torch.Tensor, csum):
         """Queue the aggregate audit (recovered chunks vs the miners' summed chunk commitments);
-        returns a callable giving ok int32 [n_miners, nchunks].  On the GPU the check runs on the
-        side stream while the host builds the block (gob + SHA-256)."""
+        returns a callable giving ok int32 [n_miners, nchunks].  On the GPU the check -- and, when
+        `csum` is a callable, the miners' commitment sums themselves -- run on the side stream
+        while the host builds the block (gob + SHA-256)."""
         if not self.gpu:
-            ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
+            cs = csum() if callable(csum) else csum
+            ok = self.crypto.check_aggregate(coeffs.cpu(), cs.cpu())
             return lambda: ok
         main = torch.cuda.current_stream()
         st = self.side_stream
         st.wait_stream(main)
         with torch.cuda.stream(st):
+            if callable(csum):
+                csum = csum()
             ok = self.crypto.check_aggregate(coeffs, csum)
             host = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
             host.copy_(ok, non_blocking=True)
@@ -785,7 +789,11 @@ class BiscottiEngine:
                 flat = pts.view(pts.shape[0], nch * (T + 1), pw)
                 ccols = h2d(np.concatenate([base + T for _ in contributing]).astype(np.int32), torch.int32,
                             self.dev)
-                csum = B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)
+                # the sums feed only the audit, which runs on the side stream next to the recovery
+                csum = (lambda: B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)) if audit else None
+                if audit:
+                    for t in (pts, rows_i, ccols):   # main-stream tensors read on the side stream
+                        t.record_stream(self.side_stream)
                 wc = np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
                                      for m in contributing]).astype(np.int32)
                 assert wc.max() < nch * (T + 1)
@@ -822,7 +830,8 @@ class BiscottiEngine:
         with tm.phase("recover"):
             now = self._now(plan.iteration)
             if single:
-                agg_all, cs_all, ts_all = agg_y[None], csum[None], None
+                agg_all, ts_all = agg_y[None], None
+                cs_all = csum if callable(csum) or csum is None else csum[None]
             else:
                 # ONE all_gather: every miner's share sums (+ its chunk-commitment sums for the audit)
                 # and every rank's clock.  Each rank then recovers the aggregate itself -- exact
@@ -842,8 +851,10 @@ class BiscottiEngine:
             xs_t = h2d(xs, torch.int32, self.dev)
             with tm.phase("recover.kernel"):
                 W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
-                audit_ok = self._audit(coeffs, torch.stack([cs_all[own[ci], ci] for ci in range(nc)])) \
-                    if audit else None
+                audit_ok = None
+                if audit:
+                    audit_ok = self._audit(coeffs, cs_all if callable(cs_all) else
+                                           torch.stack([cs_all[own[ci], ci] for ci in range(nc)]))
                 st = status.cpu().numpy()
                 W_np = W_new.cpu().numpy()
                 if ts_all is not None:
