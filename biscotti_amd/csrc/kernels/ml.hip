@@ -293,17 +293,21 @@ extern "C" __global__ void k_noise_table(int nnoisers, int D, unsigned long long
   tbl[g] = gauss(r.x, r.y);
 }
 
+// rows (optional): output row p is worker rows[p] -- the verifiers' inbox gathered in arrival order
+// straight out of the noise kernel (no separate index_select pass over [n, D])
 extern "C" __global__ void k_dp_noise_tbl(const float* delta, int P, int D, const int* noisers, int nn,
-                                          const float* noiser_scale, const float* tbl, int iter_mod, float* noised) {
+                                          const float* noiser_scale, const float* tbl, int iter_mod,
+                                          const int* rows, float* noised) {
   const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (long long)P * D) return;
   const int p = (int)(g / D), i = (int)(g % D);
+  const int src = rows ? rows[p] : p;
   float acc = 0.f;
   for (int j = 0; j < nn; ++j) {
-    const int nid = noisers[p * nn + j];
-    acc += noiser_scale[p * nn + j] * tbl[((size_t)nid * 100 + iter_mod) * D + i];
+    const int nid = noisers[src * nn + j];
+    acc += noiser_scale[src * nn + j] * tbl[((size_t)nid * 100 + iter_mod) * D + i];
   }
-  noised[g] = delta[g] + (nn > 0 ? acc / (float)nn : 0.f);
+  noised[g] = delta[(size_t)src * D + i] + (nn > 0 ? acc / (float)nn : 0.f);
 }
 
 // =====================================================================================
@@ -648,11 +652,11 @@ extern "C" int bsc_noise_table(int nnoisers, int D, unsigned long long seed, flo
 }
 
 extern "C" int bsc_dp_noise_tbl(const float* delta, int P, int D, const int* noisers, int nn, const float* scale,
-                                const float* tbl, int iter_mod, float* noised, void* stream) {
+                                const float* tbl, int iter_mod, const int* rows, float* noised, void* stream) {
   const long long n = (long long)P * D;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_dp_noise_tbl, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, delta, P, D, noisers,
-                     nn, scale, tbl, iter_mod, noised);
+                     nn, scale, tbl, iter_mod, rows, noised);
   return (int)hipGetLastError();
 }
 

@@ -33,7 +33,7 @@ SIGNATURES = {
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_noise_table": [I, I, U64, P, P],
-    "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P],
+    "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P, P],
     "bsc_recover": [P, I, I, P, I, I, P, D, P, P, P, P],
     "bsc_add_rows": [P, I, P, I, P, P, P],
 }

@@ -169,14 +169,14 @@ def noise_table(num_noisers: int, D: int, seed: int, device) -> torch.Tensor:
     return tbl
 
 
-def dp_noise(delta, noisers, scales, seed, iteration, table=None):
+def dp_noise(delta, noisers, scales, seed, iteration, table=None, rows=None):
     """noised = delta + mean_j scales[p, j] * N(0, 1; noiser_j, iteration % 100).
 
     `table` (GPU): the resident noise_table of the same seed -- the kernel then gathers the
-    noisers' vectors instead of regenerating them (identical values)."""
+    noisers' vectors instead of regenerating them (identical values).  `rows` (int32, GPU, needs
+    `table`): return only those rows, in that order (fused gather); the caller validated them."""
     P, D = delta.shape
     nn_ = noisers.shape[1] if noisers.dim() == 2 else 0
-    out = torch.empty_like(delta)
     if delta.device.type == "cuda":
         if table is not None:
             assert table.shape[1:] == (100, D) and table.dtype == torch.float32
@@ -184,9 +184,13 @@ def dp_noise(delta, noisers, scales, seed, iteration, table=None):
                 assert int(noisers.min()) >= 0 and int(noisers.max()) < table.shape[0], "noiser id out of range"
             # device-resident ids: the caller range-checks them on the host (reading them back here
             # would stall the stream)
-            _check(hip().bsc_dp_noise_tbl(_p(delta), P, D, _p(noisers), nn_, _p(scales), _p(table), iteration % 100,
-                                          _p(out), _stream()), "dp_noise_tbl")
+            assert rows is None or rows.dtype == torch.int32
+            n_out = P if rows is None else rows.numel()
+            out = torch.empty((n_out, D), dtype=delta.dtype, device=delta.device)
+            _check(hip().bsc_dp_noise_tbl(_p(delta), n_out, D, _p(noisers), nn_, _p(scales), _p(table),
+                                          iteration % 100, _p(rows), _p(out), _stream()), "dp_noise_tbl")
             return out
+        out = torch.empty_like(delta)
         _check(hip().bsc_dp_noise(_p(delta), P, D, _p(noisers), nn_, _p(scales), seed & (2**64 - 1), iteration % 100,
                                   _p(out), _stream()), "dp_noise")
         return out

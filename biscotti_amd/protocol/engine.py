@@ -440,13 +440,23 @@ class BiscottiEngine:
                                          self.N) if outs else []
             noisers = dict(zip(local_workers, sel))
         with tm.phase("noise"):
+            X_fused = None
             if cfg.noising and self.sigma > 0 and local_workers:
                 ids = [noisers[w] for w in local_workers]
                 assert all(0 <= j < self.N for row in ids for j in row), "noiser id out of range"
                 nz = h2d(ids, torch.int32, self.dev)
                 sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma)
                            for j in noisers[w]] for w in local_workers], torch.float32, self.dev)
-                noised = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl)
+                if comm.world == 1 and cfg.secure_agg and cfg.verification and inbox and self.noise_tbl is not None:
+                    # secure path on one rank: the noised deltas only feed Krum, so the noise kernel
+                    # writes the verifiers' inbox directly, in arrival order
+                    rr = [row_of[w] for w in inbox]
+                    assert max(rr) < delta.shape[0]
+                    X_fused = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl,
+                                         rows=h2d(rr, torch.int32, self.dev))
+                    noised = None
+                else:
+                    noised = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl)
             else:
                 noised = delta
         # ---------------------------------------------------------------- verification
@@ -507,8 +517,8 @@ class BiscottiEngine:
             if need_X:
                 nv, ni = len(plan.verifiers), len(inbox)
                 if single:
-                    X = noised.index_select(0, h2d([row_of[w] for w in inbox], torch.long, self.dev)) \
-                        if judges else None
+                    X = None if not judges else X_fused if X_fused is not None else \
+                        noised.index_select(0, h2d([row_of[w] for w in inbox], torch.long, self.dev))
                 else:
                     X = g_noised.index_select(0, h2d([self.flat[w] for w in inbox], torch.long, self.dev)) \
                         if judges else None
@@ -640,21 +650,17 @@ class BiscottiEngine:
         self._side_work.append((ev, out))
         return out
 
-    def _audit(self, coeffs: torch.Tensor, csum):
+    def _audit(self, coeffs: torch.Tensor, csum: torch.Tensor):
         """Queue the aggregate audit (recovered chunks vs the miners' summed chunk commitments);
-        returns a callable giving ok int32 [n_miners, nchunks].  On the GPU the check -- and, when
-        `csum` is a callable, the miners' commitment sums themselves -- run on the side stream
-        while the host builds the block (gob + SHA-256)."""
+        returns a callable giving ok int32 [n_miners, nchunks].  On the GPU the check runs on the
+        side stream while the host builds the block (gob + SHA-256)."""
         if not self.gpu:
-            cs = csum() if callable(csum) else csum
-            ok = self.crypto.check_aggregate(coeffs.cpu(), cs.cpu())
+            ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
             return lambda: ok
         main = torch.cuda.current_stream()
         st = self.side_stream
         st.wait_stream(main)
         with torch.cuda.stream(st):
-            if callable(csum):
-                csum = csum()
             ok = self.crypto.check_aggregate(coeffs, csum)
             host = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
             host.copy_(ok, non_blocking=True)
@@ -789,11 +795,15 @@ class BiscottiEngine:
                 flat = pts.view(pts.shape[0], nch * (T + 1), pw)
                 ccols = h2d(np.concatenate([base + T for _ in contributing]).astype(np.int32), torch.int32,
                             self.dev)
-                # the sums feed only the audit, which runs on the side stream next to the recovery
-                csum = (lambda: B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)) if audit else None
+                # the sums feed only the audit: they run on the side stream from now on, next to the
+                # share-value sums and the recovery on the main stream
                 if audit:
+                    st = self.side_stream
+                    st.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(st):
+                        csum = B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)
                     for t in (pts, rows_i, ccols):   # main-stream tensors read on the side stream
-                        t.record_stream(self.side_stream)
+                        t.record_stream(st)
                 wc = np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
                                      for m in contributing]).astype(np.int32)
                 assert wc.max() < nch * (T + 1)
@@ -830,8 +840,7 @@ class BiscottiEngine:
         with tm.phase("recover"):
             now = self._now(plan.iteration)
             if single:
-                agg_all, ts_all = agg_y[None], None
-                cs_all = csum if callable(csum) or csum is None else csum[None]
+                agg_all, cs_all, ts_all = agg_y[None], csum[None], None
             else:
                 # ONE all_gather: every miner's share sums (+ its chunk-commitment sums for the audit)
                 # and every rank's clock.  Each rank then recovers the aggregate itself -- exact
@@ -853,7 +862,7 @@ class BiscottiEngine:
                 W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
                 audit_ok = None
                 if audit:
-                    audit_ok = self._audit(coeffs, cs_all if callable(cs_all) else
+                    audit_ok = self._audit(coeffs, cs_all[0] if single else
                                            torch.stack([cs_all[own[ci], ci] for ci in range(nc)]))
                 st = status.cpu().numpy()
                 W_np = W_new.cpu().numpy()

@@ -165,3 +165,15 @@ def test_noise_table_matches_on_the_fly():
         assert torch.equal(a, b), it
     ref = K.noise_vector(5, 13, 7850, 42)
     np.testing.assert_allclose(tbl[5, 13].cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_noise_table_fused_row_gather():
+    """rows= gathers the verifiers' inbox straight out of the noise kernel."""
+    delta = torch.randn((6, 300)).cuda()
+    noisers = torch.tensor([[1, 2], [2, 3], [1, 4], [0, 5], [5, 3], [4, 0]], dtype=torch.int32).cuda()
+    scales = torch.full((6, 2), 0.5).cuda()
+    tbl = K.noise_table(6, 300, 7, "cuda")
+    full = K.dp_noise(delta, noisers, scales, 7, 4, table=tbl)
+    rows = torch.tensor([4, 0, 5, 2], dtype=torch.int32).cuda()
+    got = K.dp_noise(delta, noisers, scales, 7, 4, table=tbl, rows=rows)
+    assert torch.equal(got, full[rows.long()])
