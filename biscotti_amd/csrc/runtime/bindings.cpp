@@ -129,8 +129,11 @@ struct VrfJob {
   std::vector<Bytes> seeds;
   Bytes alpha;
   std::vector<std::pair<Bytes, Bytes>> out;
-  std::string error;
+  std::vector<VrfStage> stages;
+  std::string error, beta_error;  // beta_error: set before beta_ready (read by betas())
   std::atomic<bool> finished{false};
+  std::promise<void> beta_p;  // every output known (the proofs may still be in progress)
+  std::shared_future<void> beta_ready = beta_p.get_future().share();
   std::promise<void> done_p;
   std::shared_future<void> done = done_p.get_future().share();
   std::shared_ptr<VrfJob> after;  // run only once this job has finished (keeps the pool to one job)
@@ -519,6 +522,17 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         py::list r;
         for (auto& o : j.out) r.append(py::make_tuple(P(o.first), P(o.second)));
         return r;
+      })
+      // the outputs only: returns as soon as every Gamma = x*H is known, while the proofs finish
+      .def("betas", [](VrfJob& j) {
+        {
+          py::gil_scoped_release rel;
+          j.beta_ready.wait();
+        }
+        if (!j.beta_error.empty()) throw std::runtime_error(j.beta_error);
+        py::list r;
+        for (auto& o : j.out) r.append(P(o.first));
+        return r;
       });
   m.def("vrf_prove_batch_async", [](std::vector<py::bytes> seeds, py::bytes alpha, int threads,
                                     std::shared_ptr<VrfJob> after) {
@@ -527,17 +541,29 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     for (auto& s : seeds) job->seeds.push_back(B(s));
     job->alpha = B(alpha);
     job->out.resize(job->seeds.size());
+    job->stages.resize(job->seeds.size());
     VrfJob* jp = job.get();
     job->t_submit = std::chrono::steady_clock::now();
     job->th = std::thread([jp, threads] {
       if (jp->after) jp->after->done.wait();
       jp->t_start = std::chrono::steady_clock::now();
+      bool beta_set = false;
       try {
-        parallel_for(jp->seeds.size(), threads,
-                     [&](size_t i) { jp->out[i] = vrf_prove(VrfKey::cached(jp->seeds[i]), jp->alpha); });
+        // pass 1: every output (H, Gamma = x*H, beta); pass 2: the proofs (k*B, k*H, c, s)
+        parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+          jp->out[i].first = vrf_output(VrfKey::cached(jp->seeds[i]), jp->alpha, &jp->stages[i]);
+        });
+        jp->beta_p.set_value();
+        beta_set = true;
+        parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+          jp->out[i].second = vrf_finish(VrfKey::cached(jp->seeds[i]), jp->stages[i]);
+          jp->stages[i].st.reset();
+        });
       } catch (const std::exception& e) {
         jp->error = e.what();
+        if (!beta_set) jp->beta_error = jp->error;
       }
+      if (!beta_set) jp->beta_p.set_value();
       jp->t_end = std::chrono::steady_clock::now();
       jp->finished.store(true);
       jp->after.reset();

@@ -558,39 +558,59 @@ Bytes vrf_proof_to_hash(const Bytes& pi) {
   return out;
 }
 
-std::pair<Bytes, Bytes> vrf_prove(const VrfKey& key, const Bytes& alpha) {
+namespace {
+struct Staged {  // one proof between the output phase and the proof phase
+  Ge H, Gamma;
+  Bytes hstr;
+};
+}  // namespace
+
+Bytes vrf_output(const VrfKey& key, const Bytes& alpha, VrfStage* stage) {
+  auto st = std::make_shared<Staged>();
+  st->H = encode_to_curve(key.pk, alpha);
+  st->hstr = ge_tobytes(st->H);
+  st->Gamma = ge_mul(st->H, key.x);
+  Ge G8 = ge_dbl(ge_dbl(ge_dbl(st->Gamma)));
+  Sha512 bh;
+  u8 pre[2] = {SUITE, 0x03};
+  bh.update(pre, 2);
+  bh.update(ge_tobytes(G8));
+  u8 z = 0;
+  bh.update(&z, 1);
+  Bytes beta(64);
+  bh.final(beta.data());
+  stage->st = st;
+  return beta;
+}
+
+Bytes vrf_finish(const VrfKey& key, const VrfStage& stage) {
+  const Staged& st = *static_cast<const Staged*>(stage.st.get());
   const u8* x = key.x;
-  Ge H = encode_to_curve(key.pk, alpha);
-  Bytes hstr = ge_tobytes(H);
-  Ge Gamma = ge_mul(H, x);
   Sha512 kh;
   kh.update(key.prefix, 32);
-  kh.update(hstr);
+  kh.update(st.hstr);
   u8 kd[64];
   kh.final(kd);
   u8 k[32];
   sc_reduce(k, kd, 64);
-  // Gamma, k*B, k*H and 8*Gamma (for beta) share one inversion
-  Ge U = ge_mul_base(k), V = ge_mul(H, k);
-  Ge G8 = ge_dbl(ge_dbl(ge_dbl(Gamma)));
-  const Ge* pts[4] = {&Gamma, &U, &V, &G8};
-  Bytes enc[4];
-  ge_tobytes_batch(pts, 4, enc);
-  Bytes c = challenge_str(key.pk, hstr, enc[0], enc[1], enc[2]);
+  // Gamma, k*B and k*H share one inversion
+  Ge U = ge_mul_base(k), V = ge_mul(st.H, k);
+  const Ge* pts[3] = {&st.Gamma, &U, &V};
+  Bytes enc[3];
+  ge_tobytes_batch(pts, 3, enc);
+  Bytes c = challenge_str(key.pk, st.hstr, enc[0], enc[1], enc[2]);
   u8 s[32];
   sc_muladd(s, k, c.data(), 16, x);
   Bytes pi = enc[0];
   pi.insert(pi.end(), c.begin(), c.end());
   pi.insert(pi.end(), s, s + 32);
-  Sha512 bh;
-  u8 pre[2] = {SUITE, 0x03};
-  bh.update(pre, 2);
-  bh.update(enc[3]);
-  u8 z = 0;
-  bh.update(&z, 1);
-  Bytes beta(64);
-  bh.final(beta.data());
-  return {beta, pi};
+  return pi;
+}
+
+std::pair<Bytes, Bytes> vrf_prove(const VrfKey& key, const Bytes& alpha) {
+  VrfStage stage;
+  Bytes beta = vrf_output(key, alpha, &stage);
+  return {beta, vrf_finish(key, stage)};
 }
 
 bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* beta) {

@@ -8,6 +8,8 @@
 // 64-byte output.  Lottery code consumes only the output bytes, exactly like
 // getVRFNoisers (DistSys/vrf.go:54-100).
 #pragma once
+#include <memory>
+
 #include "common.hpp"
 
 namespace bsc {
@@ -24,6 +26,15 @@ struct VrfKey {
 
 // Returns (beta = 64-byte output, pi = 80-byte proof).
 std::pair<Bytes, Bytes> vrf_prove(const VrfKey& key, const Bytes& alpha);
+
+// The same proof in two phases.  The output beta needs only H = encode_to_curve(pk, alpha) and
+// Gamma = x*H -- half of the scalar multiplications -- so a caller that consumes beta (the noiser
+// lottery) can proceed while the proof itself (k*B, k*H, challenge, response) is finished.
+struct VrfStage {
+  std::shared_ptr<void> st;
+};
+Bytes vrf_output(const VrfKey& key, const Bytes& alpha, VrfStage* stage);
+Bytes vrf_finish(const VrfKey& key, const VrfStage& stage);
 // Returns true and fills beta on success.
 bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* beta);
 Bytes vrf_proof_to_hash(const Bytes& pi);

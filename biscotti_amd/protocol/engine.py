@@ -435,9 +435,10 @@ class BiscottiEngine:
             delta, qdelta, pending_commits = head["delta"], head["qdelta"], head["pending_commits"]
             inbox, row_of, spec = head["inbox"], head["row_of"], head["spec"]
         with tm.phase("vrf_join"):
-            outs = fut_noise.result() if fut_noise is not None else []
-            sel = R.select_noisers_batch(stake, [beta for beta, _ in outs], local_workers, cfg.num_noisers,
-                                         self.N) if outs else []
+            # the lottery needs the VRF outputs only; the proofs finish on the native threads and are
+            # joined at the end of the round
+            betas = fut_noise.betas() if fut_noise is not None else []
+            sel = R.select_noisers_batch(stake, betas, local_workers, cfg.num_noisers, self.N) if betas else []
             noisers = dict(zip(local_workers, sel))
         with tm.phase("noise"):
             X_fused = None
@@ -608,8 +609,9 @@ class BiscottiEngine:
             pending_signatures()
         with tm.phase("eval"):
             ev = eval_pending()
-            if fut_roles is not None:
-                fut_roles.result()
+            for fut in (fut_noise, fut_roles):   # every VRF proof of this round is complete
+                if fut is not None:
+                    fut.result()
             self._join_side_work()
         self.stats["total_updates"] += len(block.data.deltas)
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=len(block.data.deltas) == 0,

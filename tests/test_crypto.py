@@ -305,3 +305,17 @@ def test_pairing_bilinear_and_kzg_witnesses(rt):
     ok = rt.verify_secrets_batch([chunk_commits[1]] * 21, wits[21:42], g2, g2s, xs, [int(v) for v in ys[1]], 4,
                                  rt.g1_mul(g1, s ** 10))
     assert all(ok)
+
+
+def test_vrf_two_phase_outputs_match_full_proofs(rt):
+    """betas() returns once every output is known; the full results (beta, pi) agree with it and
+    with the one-shot prover, and every proof verifies."""
+    import os as _os
+    seeds = [bytes([i]) * 32 for i in range(1, 20)]
+    alpha = _os.urandom(32)
+    job = rt.vrf_prove_batch_async(seeds, alpha, 4)
+    betas = job.betas()
+    full = job.result()
+    assert betas == [b for b, _ in full]
+    for s, (b, pi) in zip(seeds, full):
+        assert (b, pi) == tuple(rt.vrf_prove(s, alpha))
