@@ -187,7 +187,7 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
 // commitment) or S = 1 (commit_only: chunk commitments only).  out_y: int64 [nrows][nchunks][T].
 extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
-    int poly, int T, int B0, int NW, int commit_only, uint32_t* out_pts, long long* out_y) {
+    int poly, int T, int B0, int NW, int commit_only, const int* alive, uint32_t* out_pts, long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
   const long long total = (long long)nrows * nchunks * S;
@@ -199,6 +199,10 @@ extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
   const long long grp = g / S;
   const int r = (int)(grp % nrows);
   const int k = (int)(grp / nrows);
+  // late cancellation of speculative work: rows the verifiers rejected (flag cleared by
+  // k_set_alive on the critical-path stream while this kernel runs) are skipped from then on;
+  // their outputs are never read.  A stale read only costs the work.
+  if (alive != nullptr && __hip_atomic_load(alive + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int row = rows[r];
   const int prev = k * poly;
   const int L = min(poly, d - prev);
@@ -502,14 +506,29 @@ extern "C" int bsc_fb_table(const uint32_t* bases, int bases_are_jac, int b0, in
 
 extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
                               const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
-                              uint32_t* out_pts, long long* out_y, void* stream) {
+                              const int* alive, uint32_t* out_pts, long long* out_y, void* stream) {
   if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;  // every int64 scalar must be covered
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
   const long long n = (long long)nrows * nchunks * S;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_shares_msm, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows,
-                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, out_pts, out_y);
+                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, out_pts, out_y);
+  return (int)hipGetLastError();
+}
+
+// alive[map[j]] = accept[j] for every verified update j with a speculative row (map[j] >= 0):
+// agent-scope stores, read by a k_shares_msm still running on another stream.
+extern "C" __global__ void k_set_alive(const int* accept, const int* map, int n, int* alive) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int r = map[j];
+  if (r >= 0) __hip_atomic_store(alive + r, accept[j] ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+extern "C" int bsc_set_alive(const int* accept, const int* map, int n, int* alive, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_set_alive, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, accept, map, n, alive);
   return (int)hipGetLastError();
 }
 

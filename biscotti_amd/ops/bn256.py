@@ -113,10 +113,13 @@ class DeviceCommitEngine:
         del scratch
 
     # ---------------------------------------------------------------- per-round kernels
-    def shares(self, coeffs: torch.Tensor, rows: torch.Tensor, commit_only: bool = False, check_rows: bool = True):
+    def shares(self, coeffs: torch.Tensor, rows: torch.Tensor, commit_only: bool = False, check_rows: bool = True,
+               alive: torch.Tensor | None = None):
         """Fused chunk commitments (+ witnesses and share values unless commit_only).
 
         coeffs: int64 [P, d] quantized deltas; rows: int32 [n] rows of `coeffs` to process.
+        alive: optional int32 [n] flags (1 = compute); a row whose flag is cleared while the kernel
+        runs (set_alive) is skipped from then on and its outputs are left undefined.
         Returns (pts [n, nchunks, S, 24] Jacobian with S = 1 or T+1, ys [n, nchunks, T] or None).
         """
         assert coeffs.dtype == torch.int64 and coeffs.dim() == 2 and coeffs.shape[1] == self.d
@@ -127,9 +130,11 @@ class DeviceCommitEngine:
         S = 1 if commit_only else self.T + 1
         pts = torch.empty((n, self.nchunks, S, 24), dtype=torch.int32, device=self.device)
         ys = None if commit_only else torch.empty((n, self.nchunks, self.T), dtype=torch.int64, device=self.device)
+        if alive is not None:
+            assert alive.dtype == torch.int32 and alive.numel() == n
         _check(hip().bsc_shares_msm(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), _ptr(self.tbl_wb),
-                                    self.poly, self.T, self.b0, self.nw, int(commit_only), _ptr(pts), _ptr(ys),
-                                    _stream()),
+                                    self.poly, self.T, self.b0, self.nw, int(commit_only), _ptr(alive), _ptr(pts),
+                                    _ptr(ys), _stream()),
                "shares_msm")
         return pts, ys
 
@@ -188,6 +193,15 @@ def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | 
     _check(hip().bsc_sum_rows2(_ptr(pts), Cn, _ptr(rows), nrows, _ptr(cols), ncols, _ptr(out), _stream()),
            "sum_rows2")
     return out
+
+
+def set_alive(accept: torch.Tensor, rows_map: torch.Tensor, alive: torch.Tensor) -> None:
+    """alive[rows_map[j]] = accept[j] for rows_map[j] >= 0 (device-scope stores: a share MSM running
+    on another stream sees them and skips the rejected rows).  accept, rows_map: int32 [n]."""
+    n = accept.numel()
+    assert accept.dtype == torch.int32 and rows_map.dtype == torch.int32 and rows_map.numel() == n
+    assert alive.dtype == torch.int32
+    _check(hip().bsc_set_alive(_ptr(accept), _ptr(rows_map), n, _ptr(alive), _stream()), "set_alive")
 
 
 def marshal_host(pts: torch.Tensor) -> "np.ndarray":

@@ -213,8 +213,11 @@ def noise_vector(noiser: int, iteration: int, D: int, seed: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------- K5 Multi-Krum
-def krum(X, groupsize: int, n_accept: int, ksplit: int = 256):
-    """Multi-Krum over the rows of X (fp32 [n, d]): returns (accept bool [n], scores fp64 [n])."""
+def krum(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
+    """Multi-Krum over the rows of X (fp32 [n, d]): returns (accept bool [n], scores fp64 [n]).
+
+    on_accept(acc_int32) (GPU): called right after the selection kernel is queued, before anything
+    waits for it -- e.g. to cancel speculative work for the rejected updates on the device."""
     n, D = X.shape
     if n == 0:
         return torch.zeros(0, dtype=torch.bool), torch.zeros(0, dtype=torch.float64)
@@ -228,6 +231,8 @@ def krum(X, groupsize: int, n_accept: int, ksplit: int = 256):
         acc = torch.empty((n,), dtype=torch.int32, device=X.device)
         _check(hip().bsc_krum(_p(X), n, D, ksplit, _p(part), _p(dist), _p(scores), _p(acc), groupsize, n_accept,
                               _stream()), "krum")
+        if on_accept is not None:
+            on_accept(acc)
         return acc.bool(), scores
     Xd = X.double()
     sq = (Xd * Xd).sum(1)

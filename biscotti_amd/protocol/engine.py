@@ -183,13 +183,15 @@ class DeviceCrypto:
         stream.wait_stream(main)                       # qdelta is produced on the main stream
         with torch.cuda.stream(stream):
             rows_t = h2d(rows, torch.int32, qdelta.device)
-            pts, ys = self.eng.shares(qdelta, rows_t, check_rows=False)
+            # per-row flags: verification clears the rejected rows' flags while the MSM runs
+            alive = torch.ones((len(rows),), dtype=torch.int32, device=qdelta.device)
+            pts, ys = self.eng.shares(qdelta, rows_t, check_rows=False, alive=alive)
             ev = torch.cuda.Event()
             ev.record(stream)
         qdelta.record_stream(stream)
-        for t in (pts, ys):                            # allocated on `stream`, consumed on main
+        for t in (pts, ys, alive):                     # allocated on `stream`, used on main
             t.record_stream(main)
-        return pts, ys, ev
+        return pts, ys, ev, alive
 
     def sum_rows(self, pts: torch.Tensor) -> torch.Tensor:
         """[R, C, 24] -> [C, 24]"""
@@ -515,6 +517,14 @@ class BiscottiEngine:
             # verifiers' accept masks; RONI depends on each verifier's own data and still gathers
             replicated = not single and cfg.defense == "KRUM"
             judges = [v for v in plan.verifiers if live[v]] if replicated else local_verifiers
+            on_accept = None
+            if need_X and spec is not None and cfg.defense == "KRUM":
+                # speculative shares of updates Krum rejects are cancelled on the device as soon as
+                # the selection kernel has run (Krum approvals are a superset of the approved set)
+                srow = {w: i for i, w in enumerate(spec[0])}
+                amap = h2d([srow.get(w, -1) for w in inbox], torch.int32, self.dev)
+                alive_flags = spec[1][3]
+                on_accept = lambda acc, amap=amap, alive_flags=alive_flags: B.set_alive(acc, amap, alive_flags)
             if need_X:
                 nv, ni = len(plan.verifiers), len(inbox)
                 if single:
@@ -532,7 +542,7 @@ class BiscottiEngine:
                 for v in judges:
                     with tm.phase("verify.defense"):
                         if cfg.defense == "KRUM":  # identical inputs -> identical Krum result
-                            krum_cache = krum_cache or self._verify(X, inbox, it, v)
+                            krum_cache = krum_cache or self._verify(X, inbox, it, v, on_accept)
                             accept = krum_cache
                         else:
                             accept = self._verify(X, inbox, it, v)
@@ -684,7 +694,7 @@ class BiscottiEngine:
             self._side_work.clear()
 
     # ------------------------------------------------------------------ verification defences
-    def _verify(self, X: torch.Tensor, inbox: list, it: int, verifier: int) -> list[bool]:
+    def _verify(self, X: torch.Tensor, inbox: list, it: int, verifier: int, on_accept=None) -> list[bool]:
         cfg = self.cfg
         n = len(inbox)
         if cfg.defense == "RONI":
@@ -695,7 +705,7 @@ class BiscottiEngine:
             base = self.task.train_error(self.W, verifier, it)
             return [self.task.train_error(self.W + X[i].double(), verifier, it) - base <= 0.02 for i in range(n)]
         clip = self.fsm.krum_clip(n)
-        acc, _ = K.krum(X, n - clip, n - clip)
+        acc, _ = K.krum(X, n - clip, n - clip, on_accept=on_accept)
         return [bool(a) for a in acc.cpu().tolist()]
 
     # ------------------------------------------------------------------ secure aggregation path
@@ -720,7 +730,7 @@ class BiscottiEngine:
             if local_approved and routes:  # workers share as soon as any miner is reachable
                 spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
                 if spec is not None and all(w in spec_row for w in local_approved):
-                    pts, ys, ev = spec[1]
+                    pts, ys, ev = spec[1][:3]
                     torch.cuda.current_stream().wait_event(ev)
                     ap_row = {w: spec_row[w] for w in local_approved}   # rows of the speculative tensors
                 else:

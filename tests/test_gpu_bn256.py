@@ -175,3 +175,23 @@ def test_chunk_check_audits_aggregate(rt, d, b0):
     hb = np.stack([np.frombuffer(key.commit(coeffs[k, :min(10, d - 10 * k)], 10 * k), np.uint8)
                    for k in range(eng.nchunks)])
     np.testing.assert_array_equal(B.marshal(csum.view(-1, 24)).cpu().numpy(), hb)
+
+
+def test_shares_msm_late_cancellation(rt):
+    """Rows whose alive flag is cleared are skipped; the others are bit-identical to a full run,
+    and set_alive maps verifier-order accept flags onto speculative rows."""
+    from biscotti_amd.ops import bn256 as B
+    d = 40
+    key = rt.CommitKey.generate(d, 3)
+    eng = B.DeviceCommitEngine(key, 10, 21, b0=10)
+    q = torch.from_numpy(np.random.default_rng(4).integers(-9000, 9000, size=(4, d), dtype=np.int64)).cuda()
+    rows = torch.arange(4, dtype=torch.int32, device="cuda")
+    full_p, full_y = eng.shares(q, rows)
+    alive = torch.ones(4, dtype=torch.int32, device="cuda")
+    # verifier order [2, 0, 3, 1 (not speculative)]: accept, reject, accept, reject
+    B.set_alive(torch.tensor([1, 0, 1, 0], dtype=torch.int32, device="cuda"),
+                torch.tensor([2, 0, 3, -1], dtype=torch.int32, device="cuda"), alive)
+    assert alive.tolist() == [0, 1, 1, 1]
+    p, y = eng.shares(q, rows, alive=alive)
+    for r in (1, 2, 3):
+        assert torch.equal(p[r], full_p[r]) and torch.equal(y[r], full_y[r])
