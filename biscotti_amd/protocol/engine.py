@@ -34,7 +34,7 @@ from ..native import rt
 from ..ops import bn256 as B
 from ..ops import ml as K
 from ..parallel.comm import Comm
-from ..utils import JsonlWriter, PhaseTimer, get_logger, h2d
+from ..utils import JsonlWriter, PhaseTimer, flush_logs, get_logger, h2d
 from .config import RunConfig
 
 
@@ -311,6 +311,7 @@ class BiscottiEngine:
     def close(self) -> None:
         """Join the pre-opened round's native VRF jobs and drain the device.  Idempotent; also
         registered with atexit so interpreter teardown never races native threads."""
+        flush_logs(self.log)
         head, self._head = self._head, None
         if head:
             for k in ("fut_noise", "fut_roles"):
@@ -638,6 +639,7 @@ class BiscottiEngine:
             import os
             import sys
 
+            flush_logs(self.log)
             sys.stderr.flush()
             os._exit(17)
         return res

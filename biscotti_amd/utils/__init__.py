@@ -29,10 +29,49 @@ class _GoFormatter(logging.Formatter):
                 f"{os.path.basename(record.pathname)}:{record.lineno}: {record.getMessage()}")
 
 
+class _BatchingHandler(logging.Handler):
+    """Writes formatted records in batches: one write + flush per `max_lines` records or
+    `max_delay` seconds instead of one per record.  A round logs two lines; flushing each one to
+    a pipe cost ~0.1 ms of the round's host critical path.  Flushed at exit and by flush()."""
+
+    def __init__(self, stream=None, path: str | None = None, max_lines: int = 64, max_delay: float = 0.25):
+        super().__init__()
+        import atexit
+
+        self.stream = open(path, "a") if path else (stream or sys.stderr)
+        self.lines: list[str] = []
+        self.max_lines, self.max_delay = max_lines, max_delay
+        self.t_last = time.monotonic()
+        atexit.register(self.flush)
+
+    def emit(self, record: logging.LogRecord) -> None:
+        try:
+            self.lines.append(self.format(record))
+            if len(self.lines) >= self.max_lines or time.monotonic() - self.t_last > self.max_delay:
+                self.flush()
+        except Exception:  # pragma: no cover
+            self.handleError(record)
+
+    def flush(self) -> None:
+        if self.lines:
+            out, self.lines = "\n".join(self.lines) + "\n", []
+            try:
+                self.stream.write(out)
+                self.stream.flush()
+            except ValueError:  # stream closed at interpreter teardown
+                pass
+        self.t_last = time.monotonic()
+
+
+def flush_logs(lg: logging.Logger) -> None:
+    for h in lg.handlers:
+        h.flush()
+
+
 def get_logger(name: str = "peer", path: str | None = None, level=logging.INFO) -> logging.Logger:
     lg = logging.getLogger(f"biscotti.{name}.{path or 'stderr'}")
     if not lg.handlers:
-        h = logging.FileHandler(path) if path else logging.StreamHandler(sys.stderr)
+        h = _BatchingHandler(path=path) if path else _BatchingHandler(sys.stderr)
         h.setFormatter(_GoFormatter(f"[{name}] "))
         lg.addHandler(h)
         lg.propagate = False
