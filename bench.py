@@ -130,6 +130,9 @@ def main() -> int:
     s_per_round = elapsed / max(a.steps, 1)
     acc = 1.0 - last.test_error if last is not None else float("nan")
     ok, why = eng.fsm.chain.verify() if not fedsys else (True, "")
+    from biscotti_amd.utils import flush_logs
+
+    flush_logs(eng.log)   # buffered log lines go out before the result line
     if comm.rank == 0:
         headline = a.config == "headline"
         out = {
