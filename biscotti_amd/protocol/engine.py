@@ -404,12 +404,10 @@ class BiscottiEngine:
         with tm.phase("local_step"):
             delta, qdelta = self.task.step(self.W, it, local_workers)
         with tm.phase("commit"):
-            # full-vector commitments on the background stream: their first consumer is the signing
-            # after Krum, so noise + Krum on the main stream do not queue behind them
-            pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
             # only the first krum_thresh arrivals reach the verifiers (verifier_inbox), so only they
             # can be approved: they secret-share while verification runs (kyber.go:533-646), the MSM
-            # on the CU-masked side stream; shares of workers the verifiers reject are never routed
+            # on the CU-masked side stream; shares of workers the verifiers reject are never routed.
+            # The MSM is the round's longest kernel, so it is launched first.
             inbox = fsm.verifier_inbox(workers) if cfg.verification else []
             row_of = {w: i for i, w in enumerate(local_workers)}
             spec = None
@@ -419,6 +417,9 @@ class BiscottiEngine:
                 if spec_workers:
                     spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
                                                                    self.side_stream))
+            # full-vector commitments on the background stream: their first consumer is the signing
+            # after Krum, so noise + Krum on the main stream do not queue behind them
+            pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inbox=inbox, row_of=row_of,
                     spec=spec)
         return head
@@ -664,6 +665,20 @@ class BiscottiEngine:
         self._side_work.append((ev, out))
         return out
 
+    def _d2h(self, *ts: torch.Tensor) -> list:
+        """Several device tensors to host numpy arrays with ONE wait (pinned, stream-ordered copies)."""
+        if not self.gpu:
+            return [t.numpy() for t in ts]
+        hs = []
+        for t in ts:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            hs.append(h)
+        ev = torch.cuda.Event()
+        ev.record()
+        ev.synchronize()
+        return [h.numpy() for h in hs]
+
     def _audit(self, coeffs: torch.Tensor, csum: torch.Tensor):
         """Queue the aggregate audit (recovered chunks vs the miners' summed chunk commitments);
         returns a callable giving ok int32 [n_miners, nchunks].  On the GPU the check runs on the
@@ -796,36 +811,35 @@ class BiscottiEngine:
             # every miner's summed chunk commitments (aggregateSecret, kyber.go:251-253): the audit
             # checks the recovered aggregate against them
             csum = torch.zeros((nc, nch, pw), dtype=pdt, device=self.dev)
+            agg_direct = xs_direct = None
             if single and self.gpu and contributing:
                 # aggregateSecret for every miner: the rows (contributing workers) are shared.  The
-                # chunk-commitment sums run first (the audit reads them); the 7 witness sums per
+                # chunk-commitment sums feed only the audit (side stream); the 7 witness sums per
                 # chunk and miner -- which nothing in a round reads: the reference's leader never
-                # checks aggregated witnesses -- run on the background stream, off the critical path
-                rows = recv[contributing[0]][2]
+                # checks aggregated witnesses -- run on the background stream, off the critical path.
+                # Every index list goes up in ONE upload; the share values go straight into the
+                # recovery's [nchunks, points] layout.
                 row_list = [ap_row[w] for w in node_list]
-                assert max(row_list) < pts.shape[0]        # index lists are validated on the host
-                rows_i = h2d(row_list, torch.int32, self.dev)
                 base = np.arange(nch) * (T + 1)
+                ycols = np.concatenate([spm * part_of[m] + np.arange(spm) for m in contributing])
+                wc = np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
+                                     for m in contributing])
+                assert max(row_list) < pts.shape[0] and wc.max() < nch * (T + 1) and ycols.max() < T
+                parts = [np.asarray(row_list), np.tile(base + T, nc), wc, ycols, ycols - 10]
+                idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
+                offs = np.cumsum([0] + [len(a) for a in parts])
+                rows_i, ccols, wcols, ycols_t, xs_t_ = (idx[offs[i]:offs[i + 1]] for i in range(5))
                 flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-                ccols = h2d(np.concatenate([base + T for _ in contributing]).astype(np.int32), torch.int32,
-                            self.dev)
-                # the sums feed only the audit: they run on the side stream from now on, next to the
-                # share-value sums and the recovery on the main stream
                 if audit:
                     st = self.side_stream
                     st.wait_stream(torch.cuda.current_stream())
                     with torch.cuda.stream(st):
                         csum = B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)
-                    for t in (pts, rows_i, ccols):   # main-stream tensors read on the side stream
+                    for t in (pts, idx):   # main-stream tensors read on the side stream
                         t.record_stream(st)
-                wc = np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
-                                     for m in contributing]).astype(np.int32)
-                assert wc.max() < nch * (T + 1)
-                wcols = h2d(wc, torch.int32, self.dev)
-                self._background(lambda: B.sum_rows(flat, rows_i, wcols, check=False), flat, rows_i, wcols)
-                ysum = ys.index_select(0, rows).sum(0)   # [nch, T]
-                for ci, m in enumerate(contributing):
-                    agg_y[ci] = ysum[:, spm * part_of[m]: spm * part_of[m] + spm]
+                self._background(lambda: B.sum_rows(flat, rows_i, wcols, check=False), flat, idx)
+                agg_direct = ys.index_select(0, rows_i).sum(0).index_select(1, ycols_t)   # [nch, npts]
+                xs_direct = ((ycols - 10).tolist(), xs_t_)
             else:
                 for ci, m in enumerate(contributing):
                     if m not in self.local:
@@ -869,17 +883,19 @@ class BiscottiEngine:
                 cs_all = got[2].view(comm.world, nc, nch, pw) if audit else None
             leader_rank = comm.owner(plan.leader, self.N)
             own = [0 if single else comm.owner(m, self.N) for m in contributing]
-            xs = [spm * part_of[m] + s_ - 10 for m in contributing for s_ in range(spm)]
-            agg = torch.cat([agg_all[own[ci], ci] for ci in range(nc)], dim=1).contiguous()   # [nchunks, npts]
-            xs_t = h2d(xs, torch.int32, self.dev)
+            if agg_direct is not None:
+                agg, (xs, xs_t) = agg_direct, xs_direct
+            else:
+                xs = [spm * part_of[m] + s_ - 10 for m in contributing for s_ in range(spm)]
+                agg = torch.cat([agg_all[own[ci], ci] for ci in range(nc)], dim=1).contiguous()   # [nchunks, npts]
+                xs_t = h2d(xs, torch.int32, self.dev)
             with tm.phase("recover.kernel"):
                 W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
                 audit_ok = None
                 if audit:
                     audit_ok = self._audit(coeffs, cs_all[0] if single else
                                            torch.stack([cs_all[own[ci], ci] for ci in range(nc)]))
-                st = status.cpu().numpy()
-                W_np = W_new.cpu().numpy()
+                st, W_np = self._d2h(status, W_new)
                 if ts_all is not None:
                     now = int(ts_all[leader_rank].reshape(-1)[0])   # the leader's clock stamps the block
             if not st.all():  # inconsistent shares: the reference's float64 least squares
