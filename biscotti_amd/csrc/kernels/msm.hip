@@ -389,8 +389,11 @@ extern "C" __global__ void __launch_bounds__(128) k_sum_rows(const uint32_t* pts
 // Two-level version: block = 32 columns x 8 row groups; each thread sums every 8th row of its
 // column, then an LDS tree over the 8 partials.  8x the parallelism of k_sum_rows, and the column
 // list may concatenate several miners' slots (one launch per rank).
+// row_mask (optional, indexed by input row): rows whose flag is 0 are left out -- the device-side
+// selection of the approved workers' shares, decided by the verification kernels on the GPU.
 extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
-                                                             int nrows, const int* cols, int ncols, uint32_t* out) {
+                                                             int nrows, const int* cols, int ncols,
+                                                             const int* row_mask, uint32_t* out) {
   __shared__ uint32_t sh[8][32][24];
   const int cx = threadIdx.x & 31, ry = threadIdx.x >> 5;
   const int i = blockIdx.x * 32 + cx;
@@ -398,12 +401,15 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
   if (i < ncols && ry < nrows) {
     const int col = cols ? cols[i] : i;
     // software pipeline: load row r + 8 while adding row r
-    jac cur = ld_jac(pts + 24 * ((size_t)(rows ? rows[ry] : ry) * ncols_in + col));
+    int row = rows ? rows[ry] : ry;
+    jac cur = ld_jac(pts + 24 * ((size_t)row * ncols_in + col));
     for (int r = ry; r < nrows; r += 8) {
       const int rn = r + 8 < nrows ? r + 8 : r;
-      const jac nxt = ld_jac(pts + 24 * ((size_t)(rows ? rows[rn] : rn) * ncols_in + col));
-      acc = jac_add(acc, cur);
+      const int rown = rows ? rows[rn] : rn;
+      const jac nxt = ld_jac(pts + 24 * ((size_t)rown * ncols_in + col));
+      if (row_mask == nullptr || row_mask[row] != 0) acc = jac_add(acc, cur);
       cur = nxt;
+      row = rown;
     }
   }
   st_jac(&sh[ry][cx][0], acc);
@@ -541,10 +547,10 @@ extern "C" int bsc_sum_rows(const uint32_t* pts, int ncols_in, const int* rows, 
 }
 
 extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
-                             int ncols, uint32_t* out, void* stream) {
+                             int ncols, const int* row_mask, uint32_t* out, void* stream) {
   if (ncols <= 0) return 0;
   hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 32)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
-                     rows, nrows, cols, ncols, out);
+                     rows, nrows, cols, ncols, row_mask, out);
   return (int)hipGetLastError();
 }
 

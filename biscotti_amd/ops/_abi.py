@@ -20,7 +20,7 @@ SIGNATURES = {
     "bsc_set_alive": [P, P, I, P, P],
     "bsc_sum_rows": [P, I, P, I, P, I, P, P],
     "bsc_segment_sum": [P, I, I, I, I, P, P],
-    "bsc_sum_rows2": [P, I, P, I, P, I, P, P],
+    "bsc_sum_rows2": [P, I, P, I, P, I, P, P, P],
     "bsc_commit_rows": [P, I, P, I, P, I, I, P, P, P],
     "bsc_stream_create_cumask": [I, P],
     "bsc_stream_destroy": [P],

@@ -176,11 +176,12 @@ class DeviceCommitEngine:
 
 
 def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | None,
-             check: bool = True) -> torch.Tensor:
+             check: bool = True, row_mask: torch.Tensor | None = None) -> torch.Tensor:
     """out[i] = sum_r pts[rows[r], cols[i]] for a [R, C, 24] Jacobian tensor.
 
     check=False: the caller validated the index lists on the host before uploading them (the
-    device-side max() would stall the host behind everything queued on the stream)."""
+    device-side max() would stall the host behind everything queued on the stream).
+    row_mask: optional int32 [R] -- rows flagged 0 are left out (device-side selection)."""
     assert pts.dim() == 3 and pts.shape[2] == 24
     R, Cn, _ = pts.shape
     nrows = R if rows is None else rows.numel()
@@ -189,9 +190,11 @@ def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | 
         assert rows.dtype == torch.int32 and (not check or nrows == 0 or int(rows.max()) < R)
     if cols is not None:
         assert cols.dtype == torch.int32 and (not check or ncols == 0 or int(cols.max()) < Cn)
+    if row_mask is not None:
+        assert row_mask.dtype == torch.int32 and row_mask.numel() == R
     out = torch.empty((ncols, 24), dtype=torch.int32, device=pts.device)
-    _check(hip().bsc_sum_rows2(_ptr(pts), Cn, _ptr(rows), nrows, _ptr(cols), ncols, _ptr(out), _stream()),
-           "sum_rows2")
+    _check(hip().bsc_sum_rows2(_ptr(pts), Cn, _ptr(rows), nrows, _ptr(cols), ncols, _ptr(row_mask), _ptr(out),
+                               _stream()), "sum_rows2")
     return out
 
 

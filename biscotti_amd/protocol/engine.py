@@ -9,13 +9,14 @@ VerifyUpdateKRUM -> RegisterSecret -> startShareDeadlineTimer -> createBlockSecA
   2. local step   fused gfx950 kernel for all local workers (softmax / logistic regression)
   3. commitments  fixed-base MSM (commit-only pass) for every online worker
   4. noising      counter-based DP noise averaged over each worker's noisers
-  5. verification all_gather of noised deltas + commitments; Multi-Krum (f64 MFMA Gram) on each
-                  rank that hosts a verifier; Schnorr signatures; all_gather of accept masks
-  6. secure agg.  fused share/witness MSM for approved workers; all_to_all of per-miner share
-                  slices; miner-side sums; all_gather of miner aggregates to the leader; exact
-                  recovery + W update
-  7. block        leader builds the block (gob + SHA-256), broadcast, every rank appends and
-                  re-verifies the hash; empty blocks on the reference's timeout paths
+  5. verification one packed all_gather of commitments + noised deltas; Multi-Krum (f64 MFMA
+                  Gram) replicated on every rank; Schnorr signatures of the local verifiers
+  6. secure agg.  speculative share/witness MSM (rows Krum rejects are cancelled on the device);
+                  one all_to_all of per-miner share bytes; miner-side sums; one packed all_gather
+                  of the miners' sums; exact recovery + W update replicated on every rank;
+                  device audit of the aggregate against the summed chunk commitments
+  7. block        every rank builds the leader's block (gob + SHA-256) from identical inputs and
+                  the leader's clock; empty blocks on the reference's timeout paths
   8. evaluation   test error / attack rate (logged in the reference's line format)
 
 Every decision (roles, inbox, approvals, share routing, leader quorum, block contents) comes from
@@ -299,6 +300,7 @@ class BiscottiEngine:
         if self.gpu and cfg.noising and cfg.noise_table and self.sigma > 0 and self.N * 100 * self.d * 4 <= (8 << 30):
             self.noise_tbl = K.noise_table(self.N, self.d, cfg.seed, self.dev)
         self._side_work: list = []   # (event, tensors) of off-critical-path device work of this round
+        self._spec_agg = None        # device-side aggregation queued behind Krum (see _spec_aggregate)
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         self.rounds_done = 0
         self._head = None
@@ -520,13 +522,20 @@ class BiscottiEngine:
             replicated = not single and cfg.defense == "KRUM"
             judges = [v for v in plan.verifiers if live[v]] if replicated else local_verifiers
             on_accept = None
+            self._spec_agg = None
             if need_X and spec is not None and cfg.defense == "KRUM":
                 # speculative shares of updates Krum rejects are cancelled on the device as soon as
-                # the selection kernel has run (Krum approvals are a superset of the approved set)
+                # the selection kernel has run (Krum approvals are a superset of the approved set);
+                # on one rank the whole aggregation of the kept rows is queued right behind it
                 srow = {w: i for i, w in enumerate(spec[0])}
                 amap = h2d([srow.get(w, -1) for w in inbox], torch.int32, self.dev)
                 alive_flags = spec[1][3]
-                on_accept = lambda acc, amap=amap, alive_flags=alive_flags: B.set_alive(acc, amap, alive_flags)
+                pred = self._predict_miners(plan, live) if single and cfg.secure_agg else None
+
+                def on_accept(acc, amap=amap, alive_flags=alive_flags, pred=pred, spec=spec):
+                    B.set_alive(acc, amap, alive_flags)
+                    if pred is not None:
+                        self._spec_agg = self._spec_aggregate(spec, pred)
             if need_X:
                 nv, ni = len(plan.verifiers), len(inbox)
                 if single:
@@ -563,6 +572,9 @@ class BiscottiEngine:
                             key_of.append(len(sks) - 1)
                             ids.append(w)
                             slots.append((vi, pos[w]))
+                if self._spec_agg is not None:   # the rows the device aggregation kept
+                    keep = set(spec[0])
+                    self._spec_agg["accepted"] = {w for w, a_ in zip(inbox, krum_cache or []) if a_ and w in keep}
                 # verifier signatures (main.go:1120-1140) sign on native threads while the GPU
                 # computes shares; they are joined where first needed (plain blocks carry them,
                 # --verify-signatures checks them) or at the end of the round
@@ -665,6 +677,56 @@ class BiscottiEngine:
         self._side_work.append((ev, out))
         return out
 
+    def _predict_miners(self, plan, live):
+        """(contributing miners, share part of each) exactly as leader_view / route_shares report them
+        whenever at least one update is approved: parts follow the live miners in address order
+        (route_shares), the leader comes first and then plan.miners order (leader_view)."""
+        if not live[plan.leader]:
+            return None
+        addr = self.fsm.addresses
+        part, k = {}, 0
+        for m in sorted(plan.miners, key=lambda m_: addr[m_]):
+            if live[m]:
+                part[m] = k
+                k += 1
+        contributing = [plan.leader] + [m for m in plan.miners if m != plan.leader and live[m]]
+        return contributing, part
+
+    def _spec_aggregate(self, spec, pred) -> dict:
+        """Queue the secure aggregation of every speculative row Krum keeps -- masked share-value
+        sums, exact recovery (main stream), the audit's commitment sums + check (side stream), the
+        witness sums (background stream) -- right behind the selection kernel, before the host has
+        read Krum's result.  The host later adopts it if the approvals, miners and parts match
+        (_secure_aggregation), so the GPU never idles while the host approves, routes and signs."""
+        contributing, part = pred
+        spm, T, nch, nc = self.pc.shares_per_miner, self.T, self.nchunks, len(pred[0])
+        pts, ys, ev, alive = spec[1]
+        main = torch.cuda.current_stream()
+        main.wait_event(ev)                      # the speculative MSM's shares
+        base = np.arange(nch) * (T + 1)
+        ycols = np.concatenate([spm * part[m] + np.arange(spm) for m in contributing])
+        wc = np.concatenate([(base[:, None] + spm * part[m] + np.arange(spm)[None, :]).reshape(-1)
+                             for m in contributing])
+        parts = [np.tile(base + T, nc), wc, ycols, ycols - 10]
+        idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
+        offs = np.cumsum([0] + [len(a) for a in parts])
+        ccols, wcols, ycols_t, xs_t = (idx[offs[i]:offs[i + 1]] for i in range(4))
+        agg = (ys * alive.view(-1, 1, 1)).sum(0).index_select(1, ycols_t)     # [nchunks, npts]
+        W_new, coeffs, status = K.recover(agg, xs_t, self.cfg.poly_size, self.d, self.W, 10.0 ** self.cfg.precision)
+        flat = pts.view(pts.shape[0], nch * (T + 1), 24)
+        audit_ok = None
+        if self.cfg.audit_aggregate:
+            st = self.side_stream
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                csum = B.sum_rows(flat, None, ccols, check=False, row_mask=alive).view(nc, nch, 24)
+            for t in (pts, idx, alive):
+                t.record_stream(st)
+            audit_ok = self._audit(coeffs, csum)
+        self._background(lambda: B.sum_rows(flat, None, wcols, check=False, row_mask=alive), flat, idx, alive)
+        return {"contributing": list(contributing), "part": dict(part), "accepted": None, "W_new": W_new,
+                "status": status, "agg": agg, "xs": (ycols - 10).tolist(), "audit_ok": audit_ok}
+
     def _d2h(self, *ts: torch.Tensor) -> list:
         """Several device tensors to host numpy arrays with ONE wait (pinned, stream-ordered copies)."""
         if not self.gpu:
@@ -757,6 +819,15 @@ class BiscottiEngine:
             return None
         node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
         part_of = {m: dict(routes[m])[node_list[0]] for m in contributing}
+        sa, self._spec_agg = self._spec_agg, None
+        if sa is not None and contributing == sa["contributing"] and part_of == sa["part"] \
+                and set(node_list) == sa["accepted"]:
+            # the device already aggregated exactly these workers' shares (queued behind Krum's
+            # selection kernel, before the host knew the approvals): recovery and audit are in flight
+            self.stats["device_aggregations"] = self.stats.get("device_aggregations", 0) + 1
+            with tm.phase("recover"):
+                return self._finish_secagg(plan, node_list, commit_of, sa["W_new"], sa["status"], sa["agg"],
+                                           sa["xs"], sa["audit_ok"], self._now(plan.iteration))
         pw, pdt = self.crypto.point_width, self.crypto.point_dtype
         esz = torch.empty((), dtype=pdt).element_size()
         ar = torch.arange(nch, dtype=torch.long, device=self.dev)
@@ -895,32 +966,39 @@ class BiscottiEngine:
                 if audit:
                     audit_ok = self._audit(coeffs, cs_all[0] if single else
                                            torch.stack([cs_all[own[ci], ci] for ci in range(nc)]))
-                st, W_np = self._d2h(status, W_new)
                 if ts_all is not None:
                     now = int(ts_all[leader_rank].reshape(-1)[0])   # the leader's clock stamps the block
-            if not st.all():  # inconsistent shares: the reference's float64 least squares
-                aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()
-                for k in np.nonzero(st == 0)[0]:
-                    c = R.recover_lstsq(xs, [int(v) for v in aggn[k]], cfg.poly_size - 1)
-                    for j, v in enumerate(c):
-                        i = k * cfg.poly_size + j
-                        if i < self.d:
-                            W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
-                self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
-            with tm.phase("recover.block"):
-                block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
-            if audit_ok is not None:
-                with tm.phase("recover.audit"):
-                    ok = audit_ok()
-                if not ok.all():
-                    # a miner's sums do not commit to the recovered update: refuse it (the round
-                    # ends like the reference's missing-quorum path, with an empty block)
-                    self.stats["audit_failures"] += 1
-                    self.log.info("aggregate audit failed for %d (miner, chunk) pairs in iteration %d: empty block",
-                                  int((ok == 0).sum()), plan.iteration)
-                    return None
-            self._last_nodes = node_list
-            return block
+            return self._finish_secagg(plan, node_list, commit_of, W_new, status, agg, xs, audit_ok, now)
+
+    def _finish_secagg(self, plan, node_list, commit_of, W_new, status, agg, xs, audit_ok, now):
+        """Read back the recovered model, fall back to least squares for inconsistent chunks, build
+        the block, then check the aggregate audit (running on the side stream meanwhile)."""
+        cfg, R, fsm, tm = self.cfg, self.R, self.fsm, self.timer
+        with tm.phase("recover.readback"):
+            st, W_np = self._d2h(status, W_new)
+        if not st.all():  # inconsistent shares: the reference's float64 least squares
+            aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()
+            for k in np.nonzero(st == 0)[0]:
+                c = R.recover_lstsq(xs, [int(v) for v in aggn[k]], cfg.poly_size - 1)
+                for j, v in enumerate(c):
+                    i = k * cfg.poly_size + j
+                    if i < self.d:
+                        W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
+            self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
+        with tm.phase("recover.block"):
+            block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
+        if audit_ok is not None:
+            with tm.phase("recover.audit"):
+                ok = audit_ok()
+            if not ok.all():
+                # a miner's sums do not commit to the recovered update: refuse it (the round
+                # ends like the reference's missing-quorum path, with an empty block)
+                self.stats["audit_failures"] += 1
+                self.log.info("aggregate audit failed for %d (miner, chunk) pairs in iteration %d: empty block",
+                              int((ok == 0).sum()), plan.iteration)
+                return None
+        self._last_nodes = node_list
+        return block
 
     # ------------------------------------------------------------------ plain aggregation path
     def _plain_aggregation(self, plan, live, approved, delta, noised, local_workers, commit_of, signatures,

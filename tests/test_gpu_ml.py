@@ -135,6 +135,9 @@ def test_engine_rounds_on_gpu():
     assert ok, why
     assert sum(not r.empty for r in res) >= 3
     assert min(r.test_error for r in res) < 0.8
+    # the device-side aggregation queued behind Krum was adopted (and matched the exact sums above)
+    assert eng.stats.get("device_aggregations", 0) >= 3
+    assert eng.stats["audit_failures"] == 0
     eng.close()
 
 
