@@ -232,7 +232,15 @@ def krum(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
         _check(hip().bsc_krum(_p(X), n, D, ksplit, _p(part), _p(dist), _p(scores), _p(acc), groupsize, n_accept,
                               _stream()), "krum")
         if on_accept is not None:
+            # the selection is downloaded right behind its kernel, so reading it waits for Krum
+            # only -- not for the work on_accept queues next on the same stream
+            host = torch.empty(acc.shape, dtype=acc.dtype, pin_memory=True)
+            host.copy_(acc, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
             on_accept(acc)
+            ev.synchronize()
+            return host.bool(), scores
         return acc.bool(), scores
     Xd = X.double()
     sq = (Xd * Xd).sum(1)
