@@ -213,35 +213,45 @@ def noise_vector(noiser: int, iteration: int, D: int, seed: int) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------- K5 Multi-Krum
+def krum_async(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
+    """Queue Multi-Krum over the rows of X (fp32 [n, d], GPU); returns a callable giving
+    (accept bool [n] on the host, scores fp64 [n] on the device).
+
+    The selection is downloaded right behind its kernel, so the callable waits for Krum only --
+    not for work queued later on the stream.  on_accept(acc_int32) is called right after the
+    selection kernel is queued (e.g. to cancel or aggregate speculative work on the device)."""
+    n, D = X.shape
+    assert X.device.type == "cuda" and 0 < n <= 128, "krum kernel handles 1..128 updates per verifier"
+    tiles = (n + 15) // 16
+    nsplit = (D + ksplit - 1) // ksplit
+    part = torch.empty((nsplit, tiles * 16, tiles * 16), dtype=torch.float64, device=X.device)
+    dist = torch.empty((n, n), dtype=torch.float64, device=X.device)
+    scores = torch.empty((n,), dtype=torch.float64, device=X.device)
+    acc = torch.empty((n,), dtype=torch.int32, device=X.device)
+    _check(hip().bsc_krum(_p(X), n, D, ksplit, _p(part), _p(dist), _p(scores), _p(acc), groupsize, n_accept,
+                          _stream()), "krum")
+    host = torch.empty(acc.shape, dtype=acc.dtype, pin_memory=True)
+    host.copy_(acc, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    if on_accept is not None:
+        on_accept(acc)
+
+    def result():
+        ev.synchronize()
+        return host.bool(), scores
+    return result
+
+
 def krum(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
     """Multi-Krum over the rows of X (fp32 [n, d]): returns (accept bool [n], scores fp64 [n]).
 
-    on_accept(acc_int32) (GPU): called right after the selection kernel is queued, before anything
-    waits for it -- e.g. to cancel speculative work for the rejected updates on the device."""
+    on_accept(acc_int32) (GPU): see krum_async."""
     n, D = X.shape
     if n == 0:
         return torch.zeros(0, dtype=torch.bool), torch.zeros(0, dtype=torch.float64)
     if X.device.type == "cuda":
-        assert n <= 128, "krum kernel handles up to 128 updates per verifier"
-        tiles = (n + 15) // 16
-        nsplit = (D + ksplit - 1) // ksplit
-        part = torch.empty((nsplit, tiles * 16, tiles * 16), dtype=torch.float64, device=X.device)
-        dist = torch.empty((n, n), dtype=torch.float64, device=X.device)
-        scores = torch.empty((n,), dtype=torch.float64, device=X.device)
-        acc = torch.empty((n,), dtype=torch.int32, device=X.device)
-        _check(hip().bsc_krum(_p(X), n, D, ksplit, _p(part), _p(dist), _p(scores), _p(acc), groupsize, n_accept,
-                              _stream()), "krum")
-        if on_accept is not None:
-            # the selection is downloaded right behind its kernel, so reading it waits for Krum
-            # only -- not for the work on_accept queues next on the same stream
-            host = torch.empty(acc.shape, dtype=acc.dtype, pin_memory=True)
-            host.copy_(acc, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            on_accept(acc)
-            ev.synchronize()
-            return host.bool(), scores
-        return acc.bool(), scores
+        return krum_async(X, groupsize, n_accept, ksplit, on_accept)()
     Xd = X.double()
     sq = (Xd * Xd).sum(1)
     dist = sq[:, None] + sq[None] - 2 * Xd @ Xd.T

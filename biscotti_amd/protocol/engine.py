@@ -300,7 +300,6 @@ class BiscottiEngine:
         if self.gpu and cfg.noising and cfg.noise_table and self.sigma > 0 and self.N * 100 * self.d * 4 <= (8 << 30):
             self.noise_tbl = K.noise_table(self.N, self.d, cfg.seed, self.dev)
         self._side_work: list = []   # (event, tensors) of off-critical-path device work of this round
-        self._spec_agg = None        # device-side aggregation queued behind Krum (see _spec_aggregate)
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         self.rounds_done = 0
         self._head = None
@@ -424,7 +423,63 @@ class BiscottiEngine:
             pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inbox=inbox, row_of=row_of,
                     spec=spec)
+        # one rank, Multi-Krum: the noise and Krum kernels (and, behind Krum's selection, the whole
+        # device-side aggregation) depend only on this head, so they are queued now as well -- the
+        # GPU then runs the round's dependency chain without waiting for the host in between
+        if (self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.verification and cfg.defense == "KRUM"
+                and inbox and spec is not None and self.noise_tbl is not None and cfg.noising and self.sigma > 0
+                and fut_noise is not None and any(live[v] for v in plan.verifiers)):
+            with tm.phase("vrf_join"):
+                noisers = self._select_noisers(fut_noise, head["stake"], local_workers)
+            with tm.phase("noise"):
+                _, X = self._noise(delta, noisers, local_workers, inbox, row_of, it)
+            with tm.phase("verify.launch"):
+                box: dict = {}
+                n = len(inbox)
+                clip = fsm.krum_clip(n)
+                wait = K.krum_async(X, n - clip, n - clip, on_accept=self._on_accept(spec, inbox, plan, live, box))
+            head["early"] = {"noisers": noisers, "krum": wait, "box": box}
         return head
+
+    def _select_noisers(self, fut_noise, stake, local_workers) -> dict:
+        """Each worker's noisers from its own VRF output (getVRFNoisers, vrf.go:54-100).  Waits for
+        the outputs only; the proofs finish on the native threads and are joined at round end."""
+        betas = fut_noise.betas() if fut_noise is not None else []
+        sel = self.R.select_noisers_batch(stake, betas, local_workers, self.cfg.num_noisers, self.N) if betas else []
+        return dict(zip(local_workers, sel))
+
+    def _noise(self, delta, noisers, local_workers, inbox, row_of, it):
+        """Noised deltas (requestNoise + NoisedDelta, main.go:1513-1660) -> (noised [n, d] or None,
+        X_inbox or None).  On one rank with the secure path the noised deltas only feed Krum, so the
+        noise kernel writes the verifiers' inbox directly, in arrival order."""
+        cfg = self.cfg
+        if not (cfg.noising and self.sigma > 0 and local_workers):
+            return delta, None
+        ids = [noisers[w] for w in local_workers]
+        assert all(0 <= j < self.N for row in ids for j in row), "noiser id out of range"
+        nz = h2d(ids, torch.int32, self.dev)
+        sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma) for j in noisers[w]]
+                  for w in local_workers], torch.float32, self.dev)
+        if self.comm.world == 1 and cfg.secure_agg and cfg.verification and inbox and self.noise_tbl is not None:
+            rr = [row_of[w] for w in inbox]
+            assert max(rr) < delta.shape[0]
+            X = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl, rows=h2d(rr, torch.int32, self.dev))
+            return None, X
+        return K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl), None
+
+    def _on_accept(self, spec, inbox, plan, live, box):
+        """Device-side follow-up of Krum's selection kernel: cancel the rejected speculative rows and
+        (one rank) queue the aggregation of the kept rows; its handle lands in box['sa']."""
+        srow = {w: i for i, w in enumerate(spec[0])}
+        amap = h2d([srow.get(w, -1) for w in inbox], torch.int32, self.dev)
+        alive_flags = spec[1][3]
+        pred = self._predict_miners(plan, live) if self.comm.world == 1 and self.cfg.secure_agg else None
+
+        def on_accept(acc):
+            B.set_alive(acc, amap, alive_flags)
+            if pred is not None:
+                box["sa"] = self._spec_aggregate(spec, pred)
+        return on_accept
 
     def run_round(self) -> RoundResult | None:
         cfg, R, fsm, comm = self.cfg, self.R, self.fsm, self.comm
@@ -440,32 +495,12 @@ class BiscottiEngine:
             fut_noise, fut_roles = head["fut_noise"], head["fut_roles"]
             delta, qdelta, pending_commits = head["delta"], head["qdelta"], head["pending_commits"]
             inbox, row_of, spec = head["inbox"], head["row_of"], head["spec"]
+        early = head.get("early")
         with tm.phase("vrf_join"):
-            # the lottery needs the VRF outputs only; the proofs finish on the native threads and are
-            # joined at the end of the round
-            betas = fut_noise.betas() if fut_noise is not None else []
-            sel = R.select_noisers_batch(stake, betas, local_workers, cfg.num_noisers, self.N) if betas else []
-            noisers = dict(zip(local_workers, sel))
+            noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake, local_workers)
         with tm.phase("noise"):
-            X_fused = None
-            if cfg.noising and self.sigma > 0 and local_workers:
-                ids = [noisers[w] for w in local_workers]
-                assert all(0 <= j < self.N for row in ids for j in row), "noiser id out of range"
-                nz = h2d(ids, torch.int32, self.dev)
-                sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma)
-                           for j in noisers[w]] for w in local_workers], torch.float32, self.dev)
-                if comm.world == 1 and cfg.secure_agg and cfg.verification and inbox and self.noise_tbl is not None:
-                    # secure path on one rank: the noised deltas only feed Krum, so the noise kernel
-                    # writes the verifiers' inbox directly, in arrival order
-                    rr = [row_of[w] for w in inbox]
-                    assert max(rr) < delta.shape[0]
-                    X_fused = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl,
-                                         rows=h2d(rr, torch.int32, self.dev))
-                    noised = None
-                else:
-                    noised = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl)
-            else:
-                noised = delta
+            noised, X_fused = (None, None) if early else \
+                self._noise(delta, noisers, local_workers, inbox, row_of, it)
         # ---------------------------------------------------------------- verification
         with tm.phase("verify"):
             single = comm.world == 1
@@ -521,25 +556,17 @@ class BiscottiEngine:
             # verifiers' accept masks; RONI depends on each verifier's own data and still gathers
             replicated = not single and cfg.defense == "KRUM"
             judges = [v for v in plan.verifiers if live[v]] if replicated else local_verifiers
+            # speculative shares of updates Krum rejects are cancelled on the device as soon as the
+            # selection kernel has run (Krum approvals are a superset of the approved set); on one
+            # rank the whole aggregation of the kept rows is queued right behind it
             on_accept = None
-            self._spec_agg = None
-            if need_X and spec is not None and cfg.defense == "KRUM":
-                # speculative shares of updates Krum rejects are cancelled on the device as soon as
-                # the selection kernel has run (Krum approvals are a superset of the approved set);
-                # on one rank the whole aggregation of the kept rows is queued right behind it
-                srow = {w: i for i, w in enumerate(spec[0])}
-                amap = h2d([srow.get(w, -1) for w in inbox], torch.int32, self.dev)
-                alive_flags = spec[1][3]
-                pred = self._predict_miners(plan, live) if single and cfg.secure_agg else None
-
-                def on_accept(acc, amap=amap, alive_flags=alive_flags, pred=pred, spec=spec):
-                    B.set_alive(acc, amap, alive_flags)
-                    if pred is not None:
-                        self._spec_agg = self._spec_aggregate(spec, pred)
+            box = early["box"] if early else {}
+            if not early and need_X and spec is not None and cfg.defense == "KRUM":
+                on_accept = self._on_accept(spec, inbox, plan, live, box)
             if need_X:
                 nv, ni = len(plan.verifiers), len(inbox)
                 if single:
-                    X = None if not judges else X_fused if X_fused is not None else \
+                    X = None if (not judges or early) else X_fused if X_fused is not None else \
                         noised.index_select(0, h2d([row_of[w] for w in inbox], torch.long, self.dev))
                 else:
                     X = g_noised.index_select(0, h2d([self.flat[w] for w in inbox], torch.long, self.dev)) \
@@ -552,7 +579,9 @@ class BiscottiEngine:
                 msgs, key_of, ids, slots, sks, bases = [], [], [], [], [], []
                 for v in judges:
                     with tm.phase("verify.defense"):
-                        if cfg.defense == "KRUM":  # identical inputs -> identical Krum result
+                        if cfg.defense == "KRUM" and early:   # queued with the round head
+                            krum_cache = krum_cache or [bool(a) for a in early["krum"]()[0].tolist()]
+                        elif cfg.defense == "KRUM":  # identical inputs -> identical Krum result
                             krum_cache = krum_cache or self._verify(X, inbox, it, v, on_accept)
                             accept = krum_cache
                         else:
@@ -572,9 +601,9 @@ class BiscottiEngine:
                             key_of.append(len(sks) - 1)
                             ids.append(w)
                             slots.append((vi, pos[w]))
-                if self._spec_agg is not None:   # the rows the device aggregation kept
+                if box.get("sa") is not None:   # the rows the device aggregation kept
                     keep = set(spec[0])
-                    self._spec_agg["accepted"] = {w for w, a_ in zip(inbox, krum_cache or []) if a_ and w in keep}
+                    box["sa"]["accepted"] = {w for w, a_ in zip(inbox, krum_cache or []) if a_ and w in keep}
                 # verifier signatures (main.go:1120-1140) sign on native threads while the GPU
                 # computes shares; they are joined where first needed (plain blocks carry them,
                 # --verify-signatures checks them) or at the end of the round
@@ -613,7 +642,7 @@ class BiscottiEngine:
         # ---------------------------------------------------------------- aggregation + block
         if cfg.secure_agg:
             block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, row_of,
-                                             commit_of, signatures, spec)
+                                             commit_of, signatures, spec, box.get("sa") if cfg.verification else None)
         else:
             block = self._plain_aggregation(plan, live, approved, delta, noised, local_workers, commit_of,
                                             signatures, (g_delta, g_noised, g_ts))
@@ -789,7 +818,7 @@ class BiscottiEngine:
 
     # ------------------------------------------------------------------ secure aggregation path
     def _secure_aggregation(self, plan, live, approved, delta, qdelta, local_workers, row_of, commit_of,
-                            signatures, spec=None):
+                            signatures, spec=None, sa=None):
         cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
         self._last_nodes = []
         spm, T, nch = self.pc.shares_per_miner, self.T, self.nchunks
@@ -819,8 +848,7 @@ class BiscottiEngine:
             return None
         node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
         part_of = {m: dict(routes[m])[node_list[0]] for m in contributing}
-        sa, self._spec_agg = self._spec_agg, None
-        if sa is not None and contributing == sa["contributing"] and part_of == sa["part"] \
+        if sa is not None and sa.get("accepted") is not None and contributing == sa["contributing"] and part_of == sa["part"] \
                 and set(node_list) == sa["accepted"]:
             # the device already aggregated exactly these workers' shares (queued behind Krum's
             # selection kernel, before the host knew the approvals): recovery and audit are in flight
