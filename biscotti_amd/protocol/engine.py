@@ -581,6 +581,7 @@ class BiscottiEngine:
                     with tm.phase("verify.defense"):
                         if cfg.defense == "KRUM" and early:   # queued with the round head
                             krum_cache = krum_cache or [bool(a) for a in early["krum"]()[0].tolist()]
+                            accept = krum_cache
                         elif cfg.defense == "KRUM":  # identical inputs -> identical Krum result
                             krum_cache = krum_cache or self._verify(X, inbox, it, v, on_accept)
                             accept = krum_cache
