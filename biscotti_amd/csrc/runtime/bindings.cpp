@@ -667,6 +667,8 @@ PYBIND11_MODULE(_biscotti_rt, m) {
                       d.global_w.assign(a.data(), a.data() + a.size());
                     })
       .def_readwrite("deltas", &BlockData::deltas)
+      // `deltas` converts every Update (and its d-long vectors) into Python objects on each access
+      .def_property_readonly("n_deltas", [](const BlockData& d) { return d.deltas.size(); })
       .def("gob", [](const BlockData& d) { return P(gob_encode_blockdata(d)); })
       .def("__str__", &blockdata_string);
   py::class_<Block>(m, "Block")

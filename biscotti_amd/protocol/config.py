@@ -60,6 +60,8 @@ class RunConfig:
     comm_timeout_s: float = 300.0   # collective timeout: a dead rank fails the job instead of hanging it
     fail_at: int = -1               # fault injection: rank `fail_rank` dies right after committing this
     fail_rank: int = 0              #   iteration (the reference's FAIL_PROB crash, made deterministic)
+    early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
+    #                                 (shortens the GPU chain; costs host time before the previous round ends)
 
     def protocol(self, rt):
         pc = rt.ProtocolConfig()

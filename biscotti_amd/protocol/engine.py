@@ -300,6 +300,7 @@ class BiscottiEngine:
         if self.gpu and cfg.noising and cfg.noise_table and self.sigma > 0 and self.N * 100 * self.d * 4 <= (8 << 30):
             self.noise_tbl = K.noise_table(self.N, self.d, cfg.seed, self.dev)
         self._side_work: list = []   # (event, tensors) of off-critical-path device work of this round
+        self._W_next = None          # device copy of the model a block under construction carries
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         self.rounds_done = 0
         self._head = None
@@ -426,7 +427,8 @@ class BiscottiEngine:
         # one rank, Multi-Krum: the noise and Krum kernels (and, behind Krum's selection, the whole
         # device-side aggregation) depend only on this head, so they are queued now as well -- the
         # GPU then runs the round's dependency chain without waiting for the host in between
-        if (self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.verification and cfg.defense == "KRUM"
+        if (cfg.early_krum and self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.verification
+                and cfg.defense == "KRUM"
                 and inbox and spec is not None and self.noise_tbl is not None and cfg.noising and self.sigma > 0
                 and fut_noise is not None and any(live[v] for v in plan.verifiers)):
             with tm.phase("vrf_join"):
@@ -655,7 +657,12 @@ class BiscottiEngine:
                 raise RuntimeError("block refused by the ledger")
             if cfg.chain_file and comm.rank == 0:
                 R.Blockchain.append_to_file(cfg.chain_file, block)
-            self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
+            W_dev, self._W_next = self._W_next, None
+            n_up = block.data.n_deltas
+            if W_dev is not None and n_up:   # the recovered model is already on the device (same bits)
+                self.W = W_dev
+            elif n_up:
+                self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
             eval_pending = self.task.evaluate_async(self.W)   # queued ahead of the next round's MSMs
         with tm.phase("next_head"):
             self._head = self._open_round()   # next round's committee + VRF proofs start now
@@ -667,8 +674,8 @@ class BiscottiEngine:
                 if fut is not None:
                     fut.result()
             self._join_side_work()
-        self.stats["total_updates"] += len(block.data.deltas)
-        res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=len(block.data.deltas) == 0,
+        self.stats["total_updates"] += n_up
+        res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=n_up == 0,
                           node_list=self._last_nodes, approved=list(approved), verifiers=list(plan.verifiers),
                           miners=list(plan.miners), test_error=ev["test_error"], attack_rate=ev["attack_rate"],
                           phases=tm.reset(), wall=time.perf_counter() - t_round)
@@ -1016,6 +1023,7 @@ class BiscottiEngine:
             self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
         with tm.phase("recover.block"):
             block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
+        self._W_next = W_new if st.all() and self.gpu else None
         if audit_ok is not None:
             with tm.phase("recover.audit"):
                 ok = audit_ok()

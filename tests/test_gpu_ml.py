@@ -110,7 +110,8 @@ def test_recover_exact(rt):
     np.testing.assert_array_equal(got3.cpu().numpy(), coeffs)
 
 
-def test_engine_rounds_on_gpu():
+@pytest.mark.parametrize("early", [False, True])
+def test_engine_rounds_on_gpu(early):
     """Whole GPU round pipeline (speculative shares on the CU-masked stream, async commitments,
     pipelined round heads): each block's model is EXACTLY the old model plus the sum of the
     included workers' quantised updates, recomputed independently through the Philox step."""
@@ -118,7 +119,7 @@ def test_engine_rounds_on_gpu():
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
-    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100)
+    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, early_krum=early)
     eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
     res = []
     for _ in range(5):
