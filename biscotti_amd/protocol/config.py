@@ -60,6 +60,8 @@ class RunConfig:
     comm_timeout_s: float = 300.0   # collective timeout: a dead rank fails the job instead of hanging it
     fail_at: int = -1               # fault injection: rank `fail_rank` dies right after committing this
     fail_rank: int = 0              #   iteration (the reference's FAIL_PROB crash, made deterministic)
+    spec_msm: bool = True           # share MSM of the whole inbox alongside verification (False: after Krum,
+    #                                 kept rows only -- half the MSM work, started later)
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
     #                                 (shortens the GPU chain; costs host time before the previous round ends)
 

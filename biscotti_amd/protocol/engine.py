@@ -141,6 +141,32 @@ class HostCrypto:
         return ok
 
 
+class _SpecShares:
+    """Speculative share/witness MSM of some workers' rows on a side stream.  `alive` (int32, one
+    flag per row) is cleared for rows the verifiers reject; the MSM skips flagged rows, whether the
+    flags were cleared before it started or while it runs.  Consumers wait on `ev`."""
+
+    def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream):
+        self.eng, self.qdelta, self.rows, self.stream = eng, qdelta, rows, stream
+        self.alive = torch.ones((len(rows),), dtype=torch.int32, device=qdelta.device)
+        self.pts = self.ys = self.ev = None
+
+    def launch(self) -> None:
+        if self.ev is not None:
+            return
+        main = torch.cuda.current_stream()
+        self.stream.wait_stream(main)              # qdelta (and any flag updates) come from main
+        with torch.cuda.stream(self.stream):
+            rows_t = h2d(self.rows, torch.int32, self.qdelta.device)
+            self.pts, self.ys = self.eng.shares(self.qdelta, rows_t, check_rows=False, alive=self.alive)
+            self.ev = torch.cuda.Event()
+            self.ev.record(self.stream)
+        for t in (self.qdelta, self.alive):
+            t.record_stream(self.stream)
+        for t in (self.pts, self.ys):              # allocated on the side stream, used on main
+            t.record_stream(main)
+
+
 class DeviceCrypto:
     """GPU crypto backend: HBM-resident tables, Jacobian points [.., 24] int32."""
 
@@ -177,22 +203,15 @@ class DeviceCrypto:
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
         return self.eng.shares(qdelta, rows)
 
-    def shares_async(self, qdelta: torch.Tensor, rows: list, stream):
+    def shares_async(self, qdelta: torch.Tensor, rows: list, stream, launch: bool = True) -> "_SpecShares":
         """Shares + witnesses of qdelta[rows] on `stream` (the caller's work keeps flowing on its own
-        stream); returns (pts, ys, event).  Consumers wait on the event before touching them."""
-        main = torch.cuda.current_stream()
-        stream.wait_stream(main)                       # qdelta is produced on the main stream
-        with torch.cuda.stream(stream):
-            rows_t = h2d(rows, torch.int32, qdelta.device)
-            # per-row flags: verification clears the rejected rows' flags while the MSM runs
-            alive = torch.ones((len(rows),), dtype=torch.int32, device=qdelta.device)
-            pts, ys = self.eng.shares(qdelta, rows_t, check_rows=False, alive=alive)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-        qdelta.record_stream(stream)
-        for t in (pts, ys, alive):                     # allocated on `stream`, used on main
-            t.record_stream(main)
-        return pts, ys, ev, alive
+        stream).  launch=False prepares the per-row flags only; launch() then starts the MSM after
+        everything queued so far on the caller's stream (e.g. Krum's selection), so rows already
+        rejected cost nothing."""
+        sp = _SpecShares(self.eng, qdelta, rows, stream)
+        if launch:
+            sp.launch()
+        return sp
 
     def sum_rows(self, pts: torch.Tensor) -> torch.Tensor:
         """[R, C, 24] -> [C, 24]"""
@@ -417,8 +436,11 @@ class BiscottiEngine:
                 cand = set(inbox) if cfg.verification else set(workers)
                 spec_workers = [w for w in local_workers if w in cand]
                 if spec_workers:
+                    # with Krum the MSM can also wait for the selection (spec_msm=False): only the kept
+                    # rows are then computed, after the verification instead of alongside it
+                    defer = not cfg.spec_msm and cfg.verification and cfg.defense == "KRUM"
                     spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
-                                                                   self.side_stream))
+                                                                   self.side_stream, launch=not defer))
             # full-vector commitments on the background stream: their first consumer is the signing
             # after Krum, so noise + Krum on the main stream do not queue behind them
             pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
@@ -474,11 +496,12 @@ class BiscottiEngine:
         (one rank) queue the aggregation of the kept rows; its handle lands in box['sa']."""
         srow = {w: i for i, w in enumerate(spec[0])}
         amap = h2d([srow.get(w, -1) for w in inbox], torch.int32, self.dev)
-        alive_flags = spec[1][3]
+        sp = spec[1]
         pred = self._predict_miners(plan, live) if self.comm.world == 1 and self.cfg.secure_agg else None
 
         def on_accept(acc):
-            B.set_alive(acc, amap, alive_flags)
+            B.set_alive(acc, amap, sp.alive)
+            sp.launch()   # no-op when the MSM already runs speculatively
             if pred is not None:
                 box["sa"] = self._spec_aggregate(spec, pred)
         return on_accept
@@ -737,7 +760,9 @@ class BiscottiEngine:
         (_secure_aggregation), so the GPU never idles while the host approves, routes and signs."""
         contributing, part = pred
         spm, T, nch, nc = self.pc.shares_per_miner, self.T, self.nchunks, len(pred[0])
-        pts, ys, ev, alive = spec[1]
+        sp = spec[1]
+        sp.launch()
+        pts, ys, ev, alive = sp.pts, sp.ys, sp.ev, sp.alive
         main = torch.cuda.current_stream()
         main.wait_event(ev)                      # the speculative MSM's shares
         base = np.arange(nch) * (T + 1)
@@ -846,7 +871,8 @@ class BiscottiEngine:
             if local_approved and routes:  # workers share as soon as any miner is reachable
                 spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
                 if spec is not None and all(w in spec_row for w in local_approved):
-                    pts, ys, ev = spec[1][:3]
+                    spec[1].launch()
+                    pts, ys, ev = spec[1].pts, spec[1].ys, spec[1].ev
                     torch.cuda.current_stream().wait_event(ev)
                     ap_row = {w: spec_row[w] for w in local_approved}   # rows of the speculative tensors
                 else:

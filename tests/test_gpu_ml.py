@@ -110,8 +110,8 @@ def test_recover_exact(rt):
     np.testing.assert_array_equal(got3.cpu().numpy(), coeffs)
 
 
-@pytest.mark.parametrize("early", [False, True])
-def test_engine_rounds_on_gpu(early):
+@pytest.mark.parametrize("early,spec_msm", [(False, True), (True, True), (False, False)])
+def test_engine_rounds_on_gpu(early, spec_msm):
     """Whole GPU round pipeline (speculative shares on the CU-masked stream, async commitments,
     pipelined round heads): each block's model is EXACTLY the old model plus the sum of the
     included workers' quantised updates, recomputed independently through the Philox step."""
@@ -119,7 +119,7 @@ def test_engine_rounds_on_gpu(early):
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
-    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, early_krum=early)
+    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, early_krum=early, spec_msm=spec_msm)
     eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
     res = []
     for _ in range(5):
