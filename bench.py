@@ -118,6 +118,8 @@ def main() -> int:
         attacks.append(last.attack_rate)
         for k, v in last.phases.items():
             phases[k] = phases.get(k, 0.0) + v
+    if hasattr(eng, "drain"):
+        eng.drain()   # host work of the timed rounds still in flight is inside the clock
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0

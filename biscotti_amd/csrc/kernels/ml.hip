@@ -425,17 +425,20 @@ extern "C" __global__ void __launch_bounds__(128) k_krum_accept(const double* sc
 extern "C" __global__ void __launch_bounds__(256) k_eval_error(const float* X, const int* y, int N, int D_IN,
                                                               int D_OUT, const double* W, int transform, int split,
                                                               unsigned int* err) {
+  // one block per 16-row tile; its 4 waves split K and reduce the logits through LDS
+  __shared__ float red[4][4][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int row0 = (blockIdx.x * 4 + wid) * 16;
-  if (row0 >= N) return;  // uniform per wave
+  const int row0 = blockIdx.x * 16;
   const int i = lane & 15, kk = lane >> 4;
   const float* xr = X + (size_t)min(row0 + i, N - 1) * D_IN;
   const bool cval = i < D_OUT;
   const double* wr = W + (size_t)(cval ? i : 0) * D_IN;
   const float tsub = transform ? 0.5f : 0.f, tmul = transform ? 2.f : 1.f;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  int k0 = 0;
-  for (; k0 + 32 <= D_IN; k0 += 32) {
+  const int kq = ((D_IN + 15) / 16) * 4;  // this wave's K range: multiple of 4
+  int k0 = wid * kq;
+  const int kend = min(D_IN, k0 + kq);
+  for (; k0 + 32 <= kend; k0 += 32) {
     float a[8], b[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -449,18 +452,23 @@ extern "C" __global__ void __launch_bounds__(256) k_eval_error(const float* X, c
       acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32((a[u + 1] - tsub) * tmul, b[u + 1], acc1, 0, 0, 0);
     }
   }
-  for (; k0 < D_IN; k0 += 4) {
+  for (; k0 < kend; k0 += 4) {
     const int k = k0 + kk;
-    const float a = k < D_IN ? (xr[k] - tsub) * tmul : 0.f;
-    const float b = (k < D_IN && cval) ? (float)wr[k] : 0.f;
+    const float a = k < kend ? (xr[k] - tsub) * tmul : 0.f;
+    const float b = (k < kend && cval) ? (float)wr[k] : 0.f;
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
   }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][r][lane] = acc0[r] + acc1[r];
+  __syncthreads();
+  if (wid != 0) return;
   const float bias = cval ? (float)W[(size_t)D_OUT * D_IN + i] : 0.f;
   unsigned int cnt0 = 0, cnt1 = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     // D layout of 16x16x4 f32: lane l holds D[row (l>>4)*4 + r][class l&15]
-    float bv = cval ? (acc0[r] + acc1[r]) + bias : -__builtin_huge_valf();
+    const float logit = (red[0][r][lane] + red[1][r][lane]) + (red[2][r][lane] + red[3][r][lane]);
+    float bv = cval ? logit + bias : -__builtin_huge_valf();
     int bc = i;
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) {
@@ -639,8 +647,8 @@ extern "C" int bsc_eval_error(const float* X, const int* y, int N, int D_IN, int
   if (D_OUT > 16 || D_IN <= 0) return -1;
   if (N <= 0) return 0;
   const int tiles = (N + 15) / 16;
-  hipLaunchKernelGGL(k_eval_error, dim3((tiles + 3) / 4), dim3(256), 0, (hipStream_t)stream, X, y, N, D_IN, D_OUT,
-                     W, transform, split, err);
+  hipLaunchKernelGGL(k_eval_error, dim3(tiles), dim3(256), 0, (hipStream_t)stream, X, y, N, D_IN, D_OUT, W,
+                     transform, split, err);
   return (int)hipGetLastError();
 }
 

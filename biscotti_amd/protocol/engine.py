@@ -329,10 +329,17 @@ class BiscottiEngine:
         atexit.register(lambda: ref() is not None and ref().close())
 
     # ------------------------------------------------------------------ lifecycle
+    def drain(self) -> None:
+        """Join host work that belongs to rounds already returned (the last roles-VRF batch)."""
+        fut, self._pending_roles = getattr(self, "_pending_roles", None), None
+        if fut is not None:
+            fut.result()
+
     def close(self) -> None:
         """Join the pre-opened round's native VRF jobs and drain the device.  Idempotent; also
         registered with atexit so interpreter teardown never races native threads."""
         flush_logs(self.log)
+        self.drain()
         head, self._head = self._head, None
         if head:
             for k in ("fut_noise", "fut_roles"):
@@ -693,9 +700,12 @@ class BiscottiEngine:
             pending_signatures()
         with tm.phase("eval"):
             ev = eval_pending()
-            for fut in (fut_noise, fut_roles):   # every VRF proof of this round is complete
-                if fut is not None:
-                    fut.result()
+            if fut_noise is not None:   # every noiser proof of this round is complete
+                fut_noise.result()
+            # the discarded roles proofs (Q7) run in the background behind the noiser proofs; they
+            # are joined one round later (drain() joins the last one), so the round does not wait
+            self.drain()
+            self._pending_roles = fut_roles
             self._join_side_work()
         self.stats["total_updates"] += n_up
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=n_up == 0,
