@@ -609,8 +609,11 @@ extern "C" void* bsc_stream_create_cumask(int skip_every, int* ncu_used) {
   const int ncu = prop.multiProcessorCount;
   std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
   int used = 0;
+  // skip_every < 0: the complement -- ONLY the CUs a stream created with -skip_every leaves free
+  const int k = skip_every < 0 ? -skip_every : skip_every;
   for (int c = 0; c < ncu; ++c) {
-    if (skip_every > 0 && c % skip_every == skip_every - 1) continue;
+    const bool skipped = k > 0 && c % k == k - 1;
+    if (skip_every < 0 ? !skipped : skipped) continue;
     mask[c / 32] |= 1u << (c % 32);
     ++used;
   }

@@ -291,7 +291,12 @@ class BiscottiEngine:
             # protocol critical path on a high-priority stream; speculative share MSMs on a
             # low-priority one so they fill the GPU while the host waits for VRF proofs / Krum
             lo, hi = torch.cuda.Stream.priority_range()
-            self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
+            self.main_cus = 0
+            if cfg.main_stream_exclusive and cfg.side_stream_skip_every > 0:
+                # the critical path on exactly the CUs the MSM stream leaves free (no SIMD sharing)
+                self.main_stream, self.main_cus = B.cu_masked_stream(self.dev, -cfg.side_stream_skip_every)
+            else:
+                self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
             # speculative MSMs: a stream masked to 3/4 of the CUs (critical path keeps the rest)
             self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, cfg.side_stream_skip_every) \
                 if cfg.side_stream_skip_every > 0 else (torch.cuda.Stream(device=self.dev, priority=lo), 0)
@@ -359,6 +364,9 @@ class BiscottiEngine:
                 torch.cuda.synchronize(self.dev)
                 torch.cuda.empty_cache()
                 B.hip().bsc_stream_destroy(self.side_stream.cuda_stream)
+            if getattr(self, "main_cus", 0):
+                B.hip().bsc_stream_destroy(self.main_stream.cuda_stream)
+                self.main_cus = 0
             self.side_stream = None
 
     # ------------------------------------------------------------------ helpers
