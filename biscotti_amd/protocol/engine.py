@@ -332,6 +332,12 @@ class BiscottiEngine:
         import weakref
         ref = weakref.ref(self)
         atexit.register(lambda: ref() is not None and ref().close())
+        # everything allocated so far (torch, datasets, keys, tables) lives for the whole run: move it
+        # out of the cyclic collector's generations, so an occasional full collection scans only
+        # the rounds' garbage instead of pausing a round for ~0.1 s
+        import gc
+        gc.collect()
+        gc.freeze()
 
     # ------------------------------------------------------------------ lifecycle
     def drain(self) -> None:
