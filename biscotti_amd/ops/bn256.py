@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from ..native import hip, rt
+from ..utils import streams as S
 
 TBL_ENTRIES = 128    # entries of an 8-bit signed window
 B0_CHOICES = (14, 13, 12, 11, 10, 9, 8)   # first-window widths, widest that fits in HBM wins
@@ -49,7 +50,7 @@ def choose_b0(d: int, poly: int, total_shares: int, device, fraction: float = 0.
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return S.raw()
 
 
 def _ptr(t: torch.Tensor | None) -> int | None:
@@ -99,6 +100,10 @@ class DeviceCommitEngine:
 
     def table_bytes(self) -> int:
         return (self.tbl_pk.numel() + self.tbl_wb.numel()) * 4
+
+    def release(self) -> None:
+        """Drop the device tables (engine shutdown); the engine is unusable afterwards."""
+        self.tbl_pk = self.tbl_wb = self.wbases = None
 
     def _build_table(self, bases, jac: bool, nbases: int, inner: int, strides, table) -> None:
         lib = hip()

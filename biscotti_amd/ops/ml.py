@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from ..native import hip
+from ..utils import streams as S
 
 PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
 PHILOX_W0, PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
@@ -18,7 +19,7 @@ MASK32 = 0xFFFFFFFF
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return S.raw()
 
 
 def _p(t):
@@ -232,8 +233,7 @@ def krum_async(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=No
                           _stream()), "krum")
     host = torch.empty(acc.shape, dtype=acc.dtype, pin_memory=True)
     host.copy_(acc, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
+    ev = S.record()
     if on_accept is not None:
         on_accept(acc)
 
@@ -281,8 +281,7 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
     # whatever the caller queues on the stream afterwards (the next round's head)
     host = torch.empty((2,), dtype=torch.int32, pin_memory=True)
     host.copy_(err, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
+    ev = S.record()
 
     def result():
         ev.synchronize()

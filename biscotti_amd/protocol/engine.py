@@ -36,6 +36,7 @@ from ..ops import bn256 as B
 from ..ops import ml as K
 from ..parallel.comm import Comm
 from ..utils import JsonlWriter, PhaseTimer, flush_logs, get_logger, h2d
+from ..utils import streams as S
 from .config import RunConfig
 
 
@@ -154,9 +155,9 @@ class _SpecShares:
     def launch(self) -> None:
         if self.ev is not None:
             return
-        main = torch.cuda.current_stream()
-        self.stream.wait_stream(main)              # qdelta (and any flag updates) come from main
-        with torch.cuda.stream(self.stream):
+        main = S.current()
+        S.wait(self.stream, main)              # qdelta (and any flag updates) come from main
+        with S.use(self.stream):
             rows_t = h2d(self.rows, torch.int32, self.qdelta.device)
             self.pts, self.ys = self.eng.shares(self.qdelta, rows_t, check_rows=False, alive=self.alive)
             self.ev = torch.cuda.Event()
@@ -181,10 +182,10 @@ class DeviceCrypto:
         n = qdelta.shape[0]
         if n == 0:
             return _Ready(np.zeros((0, 64), np.uint8))
-        main = torch.cuda.current_stream()
+        main = S.current()
         stream = stream or main
-        stream.wait_stream(main)
-        with torch.cuda.stream(stream):
+        S.wait(stream, main)
+        with S.use(stream):
             rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
             jac = self.eng.commit_rows(qdelta.contiguous(), rows, check_rows=False)
             host = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
@@ -221,7 +222,7 @@ class DeviceCrypto:
     point_width, point_dtype = 24, torch.int32
 
     def commit_rows_tensor(self, pending) -> torch.Tensor:
-        torch.cuda.current_stream().wait_event(pending.event)   # produced on the background stream
+        S.current().wait_event(pending.event)   # produced on the background stream
         return pending.jac
 
     def marshal_rows(self, t: torch.Tensor) -> np.ndarray:
@@ -358,14 +359,19 @@ class BiscottiEngine:
                     head[k].result()
         head = None  # drop the round's tensors while their streams are all still alive
         self._side_work = []
+        import gc
+        gc.unfreeze()   # the engine's own reference cycles become collectable again (see __init__)
         if self.gpu and getattr(self, "side_stream", None) is not None:
             torch.cuda.synchronize(self.dev)
             torch.cuda.set_stream(torch.cuda.default_stream(self.dev))
+            # the HBM-resident tables (up to ~90 GB) go now, not whenever the engine is collected
+            if isinstance(self.crypto, DeviceCrypto):
+                self.crypto.eng.release()
+            self.noise_tbl = None
             if getattr(self, "side_cus", 0):
                 # every tensor used on the CU-masked stream is gone (round locals, the head above):
                 # flush the allocator's stream-use events, then release the stream before
                 # interpreter teardown (the HIP runtime must not be left to destroy it at exit)
-                import gc
                 gc.collect()
                 torch.cuda.synchronize(self.dev)
                 torch.cuda.empty_cache()
@@ -748,10 +754,10 @@ class BiscottiEngine:
         (stream-ordered, no host wait) at the end of the round.  Without a GPU it runs inline."""
         if not self.gpu:
             return fn()
-        main = torch.cuda.current_stream()
+        main = S.current()
         bg = self.bg_stream
-        bg.wait_stream(main)
-        with torch.cuda.stream(bg):
+        S.wait(bg, main)
+        with S.use(bg):
             out = fn()
             ev = torch.cuda.Event()
             ev.record(bg)
@@ -787,7 +793,7 @@ class BiscottiEngine:
         sp = spec[1]
         sp.launch()
         pts, ys, ev, alive = sp.pts, sp.ys, sp.ev, sp.alive
-        main = torch.cuda.current_stream()
+        main = S.current()
         main.wait_event(ev)                      # the speculative MSM's shares
         base = np.arange(nch) * (T + 1)
         ycols = np.concatenate([spm * part[m] + np.arange(spm) for m in contributing])
@@ -803,8 +809,8 @@ class BiscottiEngine:
         audit_ok = None
         if self.cfg.audit_aggregate:
             st = self.side_stream
-            st.wait_stream(main)
-            with torch.cuda.stream(st):
+            S.wait(st, main)
+            with S.use(st):
                 csum = B.sum_rows(flat, None, ccols, check=False, row_mask=alive).view(nc, nch, 24)
             for t in (pts, idx, alive):
                 t.record_stream(st)
@@ -822,8 +828,7 @@ class BiscottiEngine:
             h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             h.copy_(t, non_blocking=True)
             hs.append(h)
-        ev = torch.cuda.Event()
-        ev.record()
+        ev = S.record()
         ev.synchronize()
         return [h.numpy() for h in hs]
 
@@ -834,10 +839,10 @@ class BiscottiEngine:
         if not self.gpu:
             ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
             return lambda: ok
-        main = torch.cuda.current_stream()
+        main = S.current()
         st = self.side_stream
-        st.wait_stream(main)
-        with torch.cuda.stream(st):
+        S.wait(st, main)
+        with S.use(st):
             ok = self.crypto.check_aggregate(coeffs, csum)
             host = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
             host.copy_(ok, non_blocking=True)
@@ -853,7 +858,7 @@ class BiscottiEngine:
 
     def _join_side_work(self) -> None:
         if self._side_work:
-            main = torch.cuda.current_stream()
+            main = S.current()
             for ev, _ in self._side_work:
                 main.wait_event(ev)
             self._side_work.clear()
@@ -897,7 +902,7 @@ class BiscottiEngine:
                 if spec is not None and all(w in spec_row for w in local_approved):
                     spec[1].launch()
                     pts, ys, ev = spec[1].pts, spec[1].ys, spec[1].ev
-                    torch.cuda.current_stream().wait_event(ev)
+                    S.current().wait_event(ev)
                     ap_row = {w: spec_row[w] for w in local_approved}   # rows of the speculative tensors
                 else:
                     sel = h2d([row_of[w] for w in local_approved], torch.long, self.dev)
@@ -989,8 +994,8 @@ class BiscottiEngine:
                 flat = pts.view(pts.shape[0], nch * (T + 1), pw)
                 if audit:
                     st = self.side_stream
-                    st.wait_stream(torch.cuda.current_stream())
-                    with torch.cuda.stream(st):
+                    S.wait(st, S.current())
+                    with S.use(st):
                         csum = B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)
                     for t in (pts, idx):   # main-stream tensors read on the side stream
                         t.record_stream(st)

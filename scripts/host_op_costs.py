@@ -9,6 +9,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from biscotti_amd.utils import h2d  # noqa: E402
+from biscotti_amd.utils import streams as S  # noqa: E402
 
 
 def per_call(fn, n=2000):
@@ -32,6 +33,13 @@ def main():
     res = {
         "h2d_list70": per_call(lambda: h2d(idx, torch.int32, dev)),
         "h2d_np3000": per_call(lambda: h2d(arr, torch.int32, dev)),
+        "h2d_list70_pin_memory": per_call(lambda: torch.as_tensor(idx, dtype=torch.int32).pin_memory().to(
+            dev, non_blocking=True)),
+        "streams.current": per_call(S.current),
+        "streams.raw": per_call(S.raw),
+        "streams.wait": per_call(lambda: S.wait(s, S.current())),
+        "streams.use": per_call(lambda: S.use(s).__enter__() and None or S.use(torch.cuda.default_stream()).__enter__()),
+        "stream_ctx": per_call(lambda: torch.cuda.stream(s).__enter__()),
         "torch_empty": per_call(lambda: torch.empty((70, 24), dtype=torch.int32, device=dev)),
         "torch_zeros": per_call(lambda: torch.zeros((70, 24), dtype=torch.int32, device=dev)),
         "event_record": per_call(lambda: torch.cuda.Event().record()),
