@@ -527,10 +527,11 @@ class BiscottiEngine:
         pred = self._predict_miners(plan, live) if self.comm.world == 1 and self.cfg.secure_agg else None
 
         def on_accept(acc):
-            B.set_alive(acc, amap, sp.alive)
-            sp.launch()   # no-op when the MSM already runs speculatively
-            if pred is not None:
-                box["sa"] = self._spec_aggregate(spec, pred)
+            with self.timer.phase("verify.queue_agg"):
+                B.set_alive(acc, amap, sp.alive)
+                sp.launch()   # no-op when the MSM already runs speculatively
+                if pred is not None:
+                    box["sa"] = self._spec_aggregate(spec, pred)
         return on_accept
 
     def run_round(self) -> RoundResult | None:
@@ -693,6 +694,10 @@ class BiscottiEngine:
                 approved, _ = fsm.approve({})
             _materialize_commits()
         # ---------------------------------------------------------------- aggregation + block
+        # host work nothing before the block needs: one rank runs it while it waits for the aggregate
+        # audit (_finish_secagg); several ranks run it after the block (its signature all_gather
+        # must come at the same point on every rank)
+        self._idle_work = pending_signatures
         if cfg.secure_agg:
             block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, row_of,
                                              commit_of, signatures, spec, box.get("sa") if cfg.verification else None)
@@ -716,10 +721,11 @@ class BiscottiEngine:
             eval_pending = self.task.evaluate_async(self.W)   # queued ahead of the next round's MSMs
         with tm.phase("next_head"):
             self._head = self._open_round()   # next round's committee + VRF proofs start now
-        if pending_signatures is not None:  # every rank, same point: the collective stays aligned
-            pending_signatures()
+        if self._idle_work is not None:  # every rank, same point: the collective stays aligned
+            self._idle_work()
         with tm.phase("eval"):
             ev = eval_pending()
+        with tm.phase("vrf_drain"):
             if fut_noise is not None:   # every noiser proof of this round is complete
                 fut_noise.result()
             # the discarded roles proofs (Q7) run in the background behind the noiser proofs; they
@@ -803,18 +809,20 @@ class BiscottiEngine:
         idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
         offs = np.cumsum([0] + [len(a) for a in parts])
         ccols, wcols, ycols_t, xs_t = (idx[offs[i]:offs[i + 1]] for i in range(4))
-        agg = (ys * alive.view(-1, 1, 1)).sum(0).index_select(1, ycols_t)     # [nchunks, npts]
-        W_new, coeffs, status = K.recover(agg, xs_t, self.cfg.poly_size, self.d, self.W, 10.0 ** self.cfg.precision)
         flat = pts.view(pts.shape[0], nch * (T + 1), 24)
-        audit_ok = None
+        csum = None
         if self.cfg.audit_aggregate:
+            # the miners' chunk-commitment sums need only the MSM + the flags: they run on the side
+            # stream alongside the share sums and the recovery below, not after them
             st = self.side_stream
             S.wait(st, main)
             with S.use(st):
                 csum = B.sum_rows(flat, None, ccols, check=False, row_mask=alive).view(nc, nch, 24)
             for t in (pts, idx, alive):
                 t.record_stream(st)
-            audit_ok = self._audit(coeffs, csum)
+        agg = (ys * alive.view(-1, 1, 1)).sum(0).index_select(1, ycols_t)     # [nchunks, npts]
+        W_new, coeffs, status = K.recover(agg, xs_t, self.cfg.poly_size, self.d, self.W, 10.0 ** self.cfg.precision)
+        audit_ok = self._audit(coeffs, csum) if csum is not None else None
         self._background(lambda: B.sum_rows(flat, None, wcols, check=False, row_mask=alive), flat, idx, alive)
         return {"contributing": list(contributing), "part": dict(part), "accepted": None, "W_new": W_new,
                 "status": status, "agg": agg, "xs": (ycols - 10).tolist(), "audit_ok": audit_ok}
@@ -875,7 +883,12 @@ class BiscottiEngine:
             base = self.task.train_error(self.W, verifier, it)
             return [self.task.train_error(self.W + X[i].double(), verifier, it) - base <= 0.02 for i in range(n)]
         clip = self.fsm.krum_clip(n)
-        acc, _ = K.krum(X, n - clip, n - clip, on_accept=on_accept)
+        if X.device.type == "cuda" and n:
+            wait = K.krum_async(X, n - clip, n - clip, on_accept=on_accept)
+            with self.timer.phase("verify.krum_wait"):
+                acc, _ = wait()
+        else:
+            acc, _ = K.krum(X, n - clip, n - clip, on_accept=on_accept)
         return [bool(a) for a in acc.cpu().tolist()]
 
     # ------------------------------------------------------------------ secure aggregation path
@@ -1080,6 +1093,9 @@ class BiscottiEngine:
             block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
         self._W_next = W_new if st.all() and self.gpu else None
         if audit_ok is not None:
+            if self.comm.world == 1 and self._idle_work is not None:
+                self._idle_work()
+                self._idle_work = None
             with tm.phase("recover.audit"):
                 ok = audit_ok()
             if not ok.all():
