@@ -325,6 +325,7 @@ class BiscottiEngine:
         if self.gpu and cfg.noising and cfg.noise_table and self.sigma > 0 and self.N * 100 * self.d * 4 <= (8 << 30):
             self.noise_tbl = K.noise_table(self.N, self.d, cfg.seed, self.dev)
         self._side_work: list = []   # (event, tensors) of off-critical-path device work of this round
+        self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         self.rounds_done = 0
@@ -359,6 +360,7 @@ class BiscottiEngine:
                     head[k].result()
         head = None  # drop the round's tensors while their streams are all still alive
         self._side_work = []
+        self._agg_idx.clear()   # resident index tensors were used on the side stream destroyed below
         import gc
         gc.unfreeze()   # the engine's own reference cycles become collectable again (see __init__)
         if self.gpu and getattr(self, "side_stream", None) is not None:
@@ -801,14 +803,22 @@ class BiscottiEngine:
         pts, ys, ev, alive = sp.pts, sp.ys, sp.ev, sp.alive
         main = S.current()
         main.wait_event(ev)                      # the speculative MSM's shares
-        base = np.arange(nch) * (T + 1)
-        ycols = np.concatenate([spm * part[m] + np.arange(spm) for m in contributing])
-        wc = np.concatenate([(base[:, None] + spm * part[m] + np.arange(spm)[None, :]).reshape(-1)
-                             for m in contributing])
-        parts = [np.tile(base + T, nc), wc, ycols, ycols - 10]
-        idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
-        offs = np.cumsum([0] + [len(a) for a in parts])
-        ccols, wcols, ycols_t, xs_t = (idx[offs[i]:offs[i + 1]] for i in range(4))
+        key = (tuple(contributing), tuple(part[m] for m in contributing))
+        hit = self._agg_idx.get(key)
+        if hit is None:
+            # a handful of miner layouts recur (the miners' parts are a permutation of 0..M-1): the
+            # index tensors are built and uploaded once per layout and stay resident
+            base = np.arange(nch) * (T + 1)
+            ycols = np.concatenate([spm * part[m] + np.arange(spm) for m in contributing])
+            wc = np.concatenate([(base[:, None] + spm * part[m] + np.arange(spm)[None, :]).reshape(-1)
+                                 for m in contributing])
+            parts = [np.tile(base + T, nc), wc, ycols, ycols - 10]
+            idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
+            offs = np.cumsum([0] + [len(a) for a in parts])
+            hit = (idx, [idx[offs[i]:offs[i + 1]] for i in range(4)], (ycols - 10).tolist())
+            if len(self._agg_idx) < 256:
+                self._agg_idx[key] = hit
+        idx, (ccols, wcols, ycols_t, xs_t), xs_list = hit
         flat = pts.view(pts.shape[0], nch * (T + 1), 24)
         csum = None
         if self.cfg.audit_aggregate:
@@ -825,7 +835,7 @@ class BiscottiEngine:
         audit_ok = self._audit(coeffs, csum) if csum is not None else None
         self._background(lambda: B.sum_rows(flat, None, wcols, check=False, row_mask=alive), flat, idx, alive)
         return {"contributing": list(contributing), "part": dict(part), "accepted": None, "W_new": W_new,
-                "status": status, "agg": agg, "xs": (ycols - 10).tolist(), "audit_ok": audit_ok}
+                "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok}
 
     def _d2h(self, *ts: torch.Tensor) -> list:
         """Several device tensors to host numpy arrays with ONE wait (pinned, stream-ordered copies)."""
