@@ -523,6 +523,14 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         for (auto& o : j.out) r.append(py::make_tuple(P(o.first), P(o.second)));
         return r;
       })
+      // join without materialising the proofs as Python objects (callers that discard them)
+      .def("wait", [](VrfJob& j) {
+        {
+          py::gil_scoped_release rel;
+          j.done.wait();
+        }
+        if (!j.error.empty()) throw std::runtime_error(j.error);
+      })
       // the outputs only: returns as soon as every Gamma = x*H is known, while the proofs finish
       .def("betas", [](VrfJob& j) {
         {

@@ -344,9 +344,10 @@ class BiscottiEngine:
     # ------------------------------------------------------------------ lifecycle
     def drain(self) -> None:
         """Join host work that belongs to rounds already returned (the last roles-VRF batch)."""
-        fut, self._pending_roles = getattr(self, "_pending_roles", None), None
-        if fut is not None:
-            fut.result()
+        futs, self._pending_roles = getattr(self, "_pending_roles", None), None
+        for fut in futs or ():
+            if fut is not None:
+                fut.wait()   # the proofs themselves are discarded: no Python objects built
 
     def close(self) -> None:
         """Join the pre-opened round's native VRF jobs and drain the device.  Idempotent; also
@@ -728,12 +729,13 @@ class BiscottiEngine:
         with tm.phase("eval"):
             ev = eval_pending()
         with tm.phase("vrf_drain"):
-            if fut_noise is not None:   # every noiser proof of this round is complete
-                fut_noise.result()
-            # the discarded roles proofs (Q7) run in the background behind the noiser proofs; they
-            # are joined one round later (drain() joins the last one), so the round does not wait
+            # the noiser proofs (nothing in the round consumes them once the lottery has joined on
+            # the VRF outputs) and the discarded roles proofs (Q7) finish on the native threads;
+            # they are joined one round later (drain() joins the last ones), so the round does not
+            # wait for them
             self.drain()
-            self._pending_roles = fut_roles
+            self._pending_roles = (fut_noise, fut_roles)
+        with tm.phase("side_join"):
             self._join_side_work()
         self.stats["total_updates"] += n_up
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=n_up == 0,
