@@ -69,8 +69,12 @@ Fe fe_mul(const Fe& a, const Fe& b) {
     r.v[i] = u64(t[i]) & MASK51;
     c = t[i] >> 51;
   }
+  // every limb is < 2^51 here; the wrap-around term only needs one more carry (limb 0 -> limb 1)
+  // to give limbs < 2^51 + 2^13, which is all fe_add / fe_sub / fe_mul assume of their inputs
   r.v[0] += u64(c) * 19;
-  return fe_carry1(r);
+  r.v[1] += r.v[0] >> 51;
+  r.v[0] &= MASK51;
+  return r;
 }
 Fe fe_sq(const Fe& a) {
   const u64* x = a.v;
@@ -88,8 +92,12 @@ Fe fe_sq(const Fe& a) {
     r.v[i] = u64(t[i]) & MASK51;
     c = t[i] >> 51;
   }
+  // every limb is < 2^51 here; the wrap-around term only needs one more carry (limb 0 -> limb 1)
+  // to give limbs < 2^51 + 2^13, which is all fe_add / fe_sub / fe_mul assume of their inputs
   r.v[0] += u64(c) * 19;
-  return fe_carry1(r);
+  r.v[1] += r.v[0] >> 51;
+  r.v[0] &= MASK51;
+  return r;
 }
 Fe fe_sqn(Fe a, int n) {
   for (int i = 0; i < n; ++i) a = fe_sq(a);
@@ -237,7 +245,8 @@ Ge ge_neg(const Ge& p) { return Ge{fe_neg(p.X), p.Y, p.Z, fe_neg(p.T)}; }
 // dbl-2008-hwcd for a = -1: 4M + 4S (vs 9M for the unified addition)
 Ge ge_dbl(const Ge& p) {
   Fe A = fe_sq(p.X), Bv = fe_sq(p.Y);
-  Fe C = fe_add(fe_sq(p.Z), fe_sq(p.Z));
+  Fe zz = fe_sq(p.Z);
+  Fe C = fe_add(zz, zz);
   Fe Dd = fe_neg(A);
   Fe E = fe_sub(fe_sub(fe_sq(fe_add(p.X, p.Y)), A), Bv);
   Fe G = fe_add(Dd, Bv), F = fe_sub(G, C), H = fe_sub(Dd, Bv);
