@@ -55,7 +55,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="headline", choices=sorted(PRESETS))
     ap.add_argument("--peers", type=int, default=None, help="override the preset's peer count")
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",

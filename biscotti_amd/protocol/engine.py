@@ -302,7 +302,11 @@ class BiscottiEngine:
             self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, cfg.side_stream_skip_every) \
                 if cfg.side_stream_skip_every > 0 else (torch.cuda.Stream(device=self.dev, priority=lo), 0)
             # work no consumer in the round waits for (the miners' witness sums) runs here
-            self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
+            self.bg_cus = 0
+            if cfg.bg_stream_complement and cfg.side_stream_skip_every > 0:
+                self.bg_stream, self.bg_cus = B.cu_masked_stream(self.dev, -cfg.side_stream_skip_every)
+            else:
+                self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
             torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
             torch.cuda.set_stream(self.main_stream)
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
@@ -382,6 +386,9 @@ class BiscottiEngine:
             if getattr(self, "main_cus", 0):
                 B.hip().bsc_stream_destroy(self.main_stream.cuda_stream)
                 self.main_cus = 0
+            if getattr(self, "bg_cus", 0):
+                B.hip().bsc_stream_destroy(self.bg_stream.cuda_stream)
+                self.bg_cus = 0
             self.side_stream = None
 
     # ------------------------------------------------------------------ helpers
