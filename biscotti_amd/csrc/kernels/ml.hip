@@ -414,6 +414,163 @@ extern "C" __global__ void __launch_bounds__(128) k_krum_accept(const double* sc
 }
 
 // =====================================================================================
+// K5 committee form: every verifier runs Multi-Krum on ITS OWN inbox (krum.go:284-322 runs in each
+// verifier process over the first KRUM_UPDATETHRESH updates that process received), and an update
+// is approved with >= floor(nv/2) signatures (main.go:1686); the leader then builds its block from
+// the first NUM_SAMPLES/2 approved arrivals (main.go:360).  All inboxes are subsets of one row set
+// X [U, D] (the submitted workers' noised deltas), so the Gram matrix is computed ONCE over X and
+// each verifier's distances are gathered out of it:
+//   KC1 k_gram_pairs     upper-triangular 16x16 tile pairs x K splits, f64 MFMA, 4 waves per block
+//                        split K further and reduce through LDS -> part[split][pair][16][16]
+//   KC2 k_krum_rows      one block per (inbox row, verifier): D_ij from the (deterministically
+//                        reduced) Gram, rank-select of the groupsize-2 nearest neighbours, score
+//   KC3 k_krum_vote      one block: per-verifier selection of the n_accept lowest scores, signature
+//                        count per worker row, approval (>= need), leader cap by arrival rank
+// Limits: U <= 1024 rows, inbox n <= 256, verifiers V <= 64 (checked by the launcher).
+// =====================================================================================
+namespace {
+__device__ __forceinline__ int pair_index(int ti, int tj, int T) {
+  // row-major enumeration of the upper triangle ti <= tj of a T x T tile grid
+  return ti * T - (ti * (ti - 1)) / 2 + (tj - ti);
+}
+// Gram entry G[a][b] summed over the K splits in split order (bit-reproducible on every rank)
+__device__ __forceinline__ double gram_at(const double* part, int nsplit, int npairs, int T, int a, int b) {
+  int ta = a >> 4, tb = b >> 4, ra = a & 15, rb = b & 15;
+  if (ta > tb) {
+    const int t = ta; ta = tb; tb = t;
+    const int r = ra; ra = rb; rb = r;
+  }
+  const double* p = part + (size_t)pair_index(ta, tb, T) * 256 + ra * 16 + rb;
+  double s = 0.0;
+  for (int sp = 0; sp < nsplit; ++sp) s += p[(size_t)sp * npairs * 256];
+  return s;
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, int U, int D, int kchunk, int T,
+                                                              double* part) {
+  __shared__ double red[4][256];
+  const int pair = blockIdx.x, sp = blockIdx.y;
+  const int npairs = gridDim.x;
+  // decode the pair index (T <= 64: a short scan)
+  int ti = 0, rem = pair;
+  while (rem >= T - ti) {
+    rem -= T - ti;
+    ++ti;
+  }
+  const int tj = ti + rem;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = ti * 16 + (lane & 15), j = tj * 16 + (lane & 15), kk = lane >> 4;
+  const bool va = i < U, vb = j < U;
+  const float* xa = X + (size_t)(va ? i : 0) * D;
+  const float* xb = X + (size_t)(vb ? j : 0) * D;
+  // this block's K range, split into 4 wave ranges that are multiples of 4
+  const int k0b = sp * kchunk, k1b = min(D, k0b + kchunk);
+  const int per = (((k1b - k0b) + 15) / 16) * 4;
+  int k = k0b + wid * per;
+  const int kend = min(k1b, k + per);
+  f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  for (; k + 32 <= kend; k += 32) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = xa[k + 4 * u + kk];
+      b[u] = xb[k + 4 * u + kk];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a[u] : 0.0, vb ? (double)b[u] : 0.0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a[u + 1] : 0.0, vb ? (double)b[u + 1] : 0.0, acc1,
+                                                  0, 0, 0);
+    }
+  }
+  for (; k < kend; k += 4) {
+    const int kx = k + kk;
+    const double a = (va && kx < kend) ? (double)xa[kx] : 0.0;
+    const double b = (vb && kx < kend) ? (double)xb[kx] : 0.0;
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc0, 0, 0, 0);
+  }
+  const f64x4 acc = acc0 + acc1;
+  // D layout: lane l holds D[row (l>>4) + 4r][col l&15]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+  __syncthreads();
+  const int e = threadIdx.x;  // 256 threads = the 16x16 tile
+  part[((size_t)sp * npairs + pair) * 256 + e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_krum_rows(const double* part, int nsplit, int npairs, int T,
+                                                             const int* inbox, int n, int groupsize,
+                                                             double* scores) {
+  __shared__ double row[256];
+  __shared__ double kept[256];
+  __shared__ double gdiag_a;
+  const int i = blockIdx.x, v = blockIdx.y, t = threadIdx.x;
+  const int* box = inbox + (size_t)v * n;
+  const int a = box[i];
+  if (t == 0) gdiag_a = gram_at(part, nsplit, npairs, T, a, a);
+  __syncthreads();
+  if (t < n) {
+    const int b = box[t];
+    const double gab = gram_at(part, nsplit, npairs, T, a, b);
+    const double gbb = gram_at(part, nsplit, npairs, T, b, b);
+    row[t] = gdiag_a + gbb - 2.0 * gab;
+  }
+  __syncthreads();
+  if (t < n) {
+    const double val = row[t];
+    int rank = 0;
+    for (int k2 = 0; k2 < n; ++k2) {
+      const double u = row[k2];
+      rank += (u < val) || (u == val && k2 < t);
+    }
+    kept[t] = (rank >= 1 && rank < groupsize - 1) ? val : 0.0;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s += kept[j];
+    scores[(size_t)v * n + i] = s;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(1024) k_krum_vote(const double* scores, const int* inbox, int V, int n,
+                                                              int n_accept, int U, int need, const int* lead_rank,
+                                                              int cap, int* acc, int* node) {
+  __shared__ int sigs[1024];
+  __shared__ int appr[1024];
+  const int t = threadIdx.x;
+  for (int w = t; w < U; w += 1024) sigs[w] = 0;
+  __syncthreads();
+  // per-verifier Multi-Krum selection: the n_accept lowest scores (index tie-break)
+  for (int e = t; e < V * n; e += 1024) {
+    const int v = e / n, i = e % n;
+    const double* sv = scores + (size_t)v * n;
+    const double s = sv[i];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += (sv[j] < s) || (sv[j] == s && j < i);
+    const int ok = rank < n_accept ? 1 : 0;
+    acc[e] = ok;
+    if (ok) atomicAdd(&sigs[inbox[e]], 1);
+  }
+  __syncthreads();
+  // approval: >= need signatures among the submitted workers (lead_rank >= 0)
+  for (int w = t; w < U; w += 1024) appr[w] = (lead_rank[w] >= 0 && sigs[w] >= need) ? 1 : 0;
+  __syncthreads();
+  // the leader's block: the first `cap` approved rows in leader arrival order (cap <= 0: all)
+  for (int w = t; w < U; w += 1024) {
+    int keep = appr[w];
+    if (keep && cap > 0) {
+      int before = 0;
+      const int r = lead_rank[w];
+      for (int x = 0; x < U; ++x) before += appr[x] && lead_rank[x] < r;
+      keep = before < cap;
+    }
+    node[w] = keep;
+  }
+}
+
+// =====================================================================================
 // K2: classification error of a softmax model over up to two row sets in ONE launch (test rows
 // [0, split), attack rows [split, N)): err[row >= split] += #(argmax != label).
 // One wave per 16-row tile: logits = X_tile[16 x D_IN] . W^T on v_mfma_f32_16x16x4f32 (lane l
@@ -639,6 +796,25 @@ extern "C" int bsc_krum(const float* X, int n, int D, int ksplit, double* part, 
   hipLaunchKernelGGL(k_krum_scores, dim3(n), dim3(64), 0, (hipStream_t)stream, part, nsplit, n, tiles * 16,
                      groupsize, dist, scores);
   hipLaunchKernelGGL(k_krum_accept, dim3(1), dim3(128), 0, (hipStream_t)stream, scores, n, n_accept, accept);
+  return (int)hipGetLastError();
+}
+
+// Committee Multi-Krum: X [U, D] fp32; inbox [V, n] rows of X; lead_rank [U] (-1: not submitted).
+// part: [nsplit, npairs, 256] f64 scratch (npairs = T(T+1)/2, T = ceil(U/16), nsplit = ceil(D/kchunk));
+// scores [V, n] f64; acc [V, n] int32; node [U] int32.
+extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, const int* inbox, int V, int n,
+                                  int groupsize, int n_accept, int need, const int* lead_rank, int cap, double* part,
+                                  double* scores, int* acc, int* node, void* stream) {
+  if (U <= 0 || V <= 0 || n <= 0) return 0;
+  if (U > 1024 || n > 256 || V > 64 || n > U || kchunk <= 0) return -1;
+  const int T = (U + 15) / 16;
+  const int npairs = T * (T + 1) / 2;
+  const int nsplit = (D + kchunk - 1) / kchunk;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part);
+  hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, part, nsplit, npairs, T, inbox, n, groupsize, scores);
+  hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U, need, lead_rank, cap,
+                     acc, node);
   return (int)hipGetLastError();
 }
 

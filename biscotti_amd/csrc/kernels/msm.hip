@@ -187,18 +187,23 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
 // commitment) or S = 1 (commit_only: chunk commitments only).  out_y: int64 [nrows][nchunks][T].
 extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
-    int poly, int T, int B0, int NW, int commit_only, const int* alive, uint32_t* out_pts, long long* out_y) {
+    int poly, int T, int B0, int NW, int commit_only, const int* alive, const int* compact, uint32_t* out_pts,
+    long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
-  const long long total = (long long)nrows * nchunks * S;
+  // compact (optional): [count, row...] -- only the listed rows are computed, packed densely over the
+  // grid (a rejected row costs no SIMD lanes); the grid is sized for nrows, the surplus exits at once
+  const int neff = compact != nullptr ? compact[0] : nrows;
+  const long long total = (long long)neff * nchunks * S;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const long long g = (long long)lb * blockDim.x + threadIdx.x;
   if (g >= total) return;
   // chunk-major: consecutive groups share a chunk (and its table lines)
   const int slot = (int)(g % S);
   const long long grp = g / S;
-  const int r = (int)(grp % nrows);
-  const int k = (int)(grp / nrows);
+  const int pos = (int)(grp % neff);
+  const int r = compact != nullptr ? compact[1 + pos] : pos;
+  const int k = (int)(grp / neff);
   // late cancellation of speculative work: rows the verifiers rejected (flag cleared by
   // k_set_alive on the critical-path stream while this kernel runs) are skipped from then on;
   // their outputs are never read.  A stale read only costs the work.
@@ -512,14 +517,44 @@ extern "C" int bsc_fb_table(const uint32_t* bases, int bases_are_jac, int b0, in
 
 extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
                               const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
-                              const int* alive, uint32_t* out_pts, long long* out_y, void* stream) {
+                              const int* alive, const int* compact, uint32_t* out_pts, long long* out_y,
+                              void* stream) {
   if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;  // every int64 scalar must be covered
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
   const long long n = (long long)nrows * nchunks * S;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_shares_msm, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows,
-                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, out_pts, out_y);
+                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, compact, out_pts, out_y);
+  return (int)hipGetLastError();
+}
+
+// compact = [count, r0, r1, ...]: the rows r with alive[r] != 0, ascending (one block, n <= 4096)
+extern "C" __global__ void __launch_bounds__(1024) k_alive_compact(const int* alive, int n, int* compact) {
+  __shared__ int cnt[1024];
+  const int t = threadIdx.x;
+  const int per = (n + 1023) / 1024;
+  const int lo = t * per, hi = min(n, lo + per);
+  int c = 0;
+  for (int r = lo; r < hi; ++r) c += alive[r] != 0;
+  cnt[t] = c;
+  __syncthreads();
+  // inclusive scan over the 1024 per-thread counts (Hillis-Steele)
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = t >= o ? cnt[t - o] : 0;
+    __syncthreads();
+    cnt[t] += v;
+    __syncthreads();
+  }
+  int w = cnt[t] - c;
+  for (int r = lo; r < hi; ++r)
+    if (alive[r] != 0) compact[1 + w++] = r;
+  if (t == 1023) compact[0] = cnt[1023];
+}
+
+extern "C" int bsc_alive_compact(const int* alive, int n, int* compact, void* stream) {
+  if (n < 0 || n > 4096) return -1;
+  hipLaunchKernelGGL(k_alive_compact, dim3(1), dim3(1024), 0, (hipStream_t)stream, alive, n, compact);
   return (int)hipGetLastError();
 }
 

@@ -744,6 +744,8 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       .def_readwrite("default_stake", &ProtocolConfig::default_stake)
       .def_readwrite("stake_unit", &ProtocolConfig::stake_unit)
       .def_readwrite("seed", &ProtocolConfig::seed)
+      .def_readwrite("shared_inbox", &ProtocolConfig::shared_inbox)
+      .def_readwrite("miner_cap", &ProtocolConfig::miner_cap)
       .def_readonly("num_samples", &ProtocolConfig::num_samples)
       .def_readonly("krum_thresh", &ProtocolConfig::krum_thresh)
       .def_readonly("total_shares", &ProtocolConfig::total_shares)
@@ -775,6 +777,10 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       .def_readonly("plan", &RoundFSM::plan)
       .def("begin_round", &RoundFSM::begin_round, py::return_value_policy::copy)
       .def("verifier_inbox", &RoundFSM::verifier_inbox)
+      .def("verifier_inboxes", &RoundFSM::verifier_inboxes)
+      .def("leader_arrivals", &RoundFSM::leader_arrivals)
+      .def("leader_cap", &RoundFSM::leader_cap)
+      .def("leader_cap_size", &RoundFSM::leader_cap_size)
       .def("krum_clip", &RoundFSM::krum_clip)
       .def("approve", [](const RoundFSM& f, const std::map<i64, std::vector<i64>>& acc) {
         bool online = false;

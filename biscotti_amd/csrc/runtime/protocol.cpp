@@ -184,6 +184,69 @@ std::vector<i64> RoundFSM::verifier_inbox(const std::vector<i64>& submitted) con
   return inbox;
 }
 
+std::vector<std::vector<i64>> RoundFSM::verifier_inboxes(const std::vector<i64>& submitted) const {
+  std::vector<std::vector<i64>> out;
+  if (cfg.shared_inbox) {
+    std::vector<i64> one = verifier_inbox(submitted);
+    out.assign(plan.verifiers.size(), one);
+    return out;
+  }
+  for (size_t k = 0; k < plan.verifiers.size(); ++k) {
+    // verifier k's own arrival order (the network race each verifier process sees)
+    std::vector<i64> order = seeded_permutation(i64(submitted.size()), round_seed(1000 + u64(plan.verifiers[k])));
+    std::vector<i64> inbox;
+    for (i64 j : order) {
+      if (i64(inbox.size()) >= cfg.krum_thresh) break;
+      inbox.push_back(submitted[size_t(j)]);
+    }
+    std::sort(inbox.begin(), inbox.end());  // sort.Slice by SourceID (krum.go:304-306)
+    if (cfg.rand_sample) {
+      // sampleUpdates seeds with the iteration, so every verifier draws the same positions
+      std::vector<i64> perm = seeded_permutation(i64(inbox.size()), round_seed(2));
+      std::vector<i64> s;
+      for (i64 j : perm) {
+        if (i64(s.size()) >= cfg.num_samples) break;
+        s.push_back(inbox[size_t(j)]);
+      }
+      inbox = s;
+    }
+    out.push_back(inbox);
+  }
+  return out;
+}
+
+std::vector<i64> RoundFSM::leader_arrivals() const {
+  std::vector<i64> perm = seeded_permutation(i64(plan.workers.size()), round_seed(3));
+  std::vector<i64> out;
+  out.reserve(perm.size());
+  for (i64 j : perm) out.push_back(plan.workers[size_t(j)]);
+  return out;
+}
+
+i64 RoundFSM::leader_cap_size() const {
+  if (!cfg.miner_cap) return 0;
+  // NUM_SAMPLES/2 (main.go:360), at least 2: the leader only builds a block from > 1 node
+  // (main.go:2079) -- in the reference a second share lands while the leader queries the other
+  // miners; the same floor as its minBlockSize rule (main.go:347-351)
+  return std::max<i64>(cfg.miner_share_thresh, 2);
+}
+
+std::vector<i64> RoundFSM::leader_cap(const std::vector<i64>& candidates) const {
+  std::vector<i64> out;
+  const i64 cap = leader_cap_size();
+  if (cap <= 0 || i64(candidates.size()) <= cap) {
+    out = candidates;
+  } else {
+    std::set<i64> cand(candidates.begin(), candidates.end());
+    for (i64 w : leader_arrivals()) {
+      if (i64(out.size()) >= cap) break;
+      if (cand.count(w)) out.push_back(w);
+    }
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
 std::vector<i64> RoundFSM::approve(const std::map<i64, std::vector<i64>>& accepted, bool* verifiers_online) const {
   std::map<i64, i64> sigs;
   bool any = false;
@@ -244,7 +307,8 @@ RoundFSM::LeaderView RoundFSM::leader_view(const std::map<i64, std::vector<std::
     inter = nx;
     lv.contributing_miners.push_back(m);
   }
-  lv.node_list.assign(inter.begin(), inter.end());
+  // the leader fires at NUM_SAMPLES/2 received shares (main.go:360): its list is the first arrivals
+  lv.node_list = leader_cap(std::vector<i64>(inter.begin(), inter.end()));
   lv.quorum = cfg.shares_per_miner * i64(lv.contributing_miners.size()) >= cfg.poly_size &&
               lv.node_list.size() > 1;
   return lv;
@@ -259,6 +323,9 @@ std::map<i64, std::vector<i64>> RoundFSM::route_updates(const std::vector<i64>& 
       if (plan.live[size_t(m)]) { r[m].push_back(w); break; }
     }
   }
+  // the leader creates its block at NUM_SAMPLES/2 received updates (processUpdate, main.go:1222-1230)
+  auto it = r.find(plan.leader);
+  if (it != r.end()) it->second = leader_cap(it->second);
   return r;
 }
 

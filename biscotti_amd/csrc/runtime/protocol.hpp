@@ -45,6 +45,9 @@ struct ProtocolConfig {
   i64 default_stake = 10;
   i64 stake_unit = 5;
   u64 seed = 0;            // arrival-order / sampling seed
+  bool shared_inbox = false;  // every verifier sees the same inbox (round-1 model; the reference's
+  //                             verifiers each keep their own first-arrivals list)
+  bool miner_cap = true;   // leader fires at NUM_SAMPLES/2 shares (main.go:360): block = first arrivals
   // derived (call derive())
   i64 num_samples = 0, krum_thresh = 0, total_shares = 0, shares_per_miner = 0;
   i64 miner_share_thresh = 0, poisoning_index = 0, collusion_thresh = 0;
@@ -98,6 +101,16 @@ class RoundFSM {
   // The updates each online verifier collects: first krum_thresh arrivals (seeded order),
   // sorted by SourceID, optional random sampling (krum.go:296-312,368-388).
   std::vector<i64> verifier_inbox(const std::vector<i64>& submitted) const;
+  // Every verifier's own inbox (plan.verifiers order): each verifier receives the updates in its own
+  // seeded arrival order and keeps the first krum_thresh (krum.go:284-322 runs per verifier process).
+  std::vector<std::vector<i64>> verifier_inboxes(const std::vector<i64>& submitted) const;
+  // Arrival order of the workers' shares / updates at the leader miner (a permutation of
+  // plan.workers); the leader builds its block from the first miner_share_thresh approved ones.
+  std::vector<i64> leader_arrivals() const;
+  // approved workers the leader's block can carry: the first miner_share_thresh in leader arrival
+  // order (all of them when miner_cap is off), returned sorted
+  std::vector<i64> leader_cap(const std::vector<i64>& candidates) const;
+  i64 leader_cap_size() const;  // 0: no cap
   i64 krum_clip(i64 n) const { return i64(0.5 * double(n)); }
   // accepted[v] = SourceIDs verifier v accepted; returns approved workers (>= nv/2 signatures)
   std::vector<i64> approve(const std::map<i64, std::vector<i64>>& accepted, bool* verifiers_online) const;

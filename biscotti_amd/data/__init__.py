@@ -26,10 +26,16 @@ import numpy as np
 
 FILES = Path(__file__).resolve().parent / "files"
 TRAIN_CUT = 0.8
-# Augmentation strength, calibrated so a multinomial logistic regression (sklearn, full batch)
-# reaches ~92% test accuracy, like real MNIST (measured 92.7% on 30% of the synthetic train set).
-ROT_DEG = 6.0
-SHIFT_PX = 1.25
+# Augmentation strength, calibrated against the reference's own *federated* learning curve rather
+# than a full-batch fit: Biscotti's update is the SUM of ~35 clipped minibatch gradients with lr = 1
+# (honest.go:405-411), so how far the model oscillates round to round depends on how coherent the
+# peers' gradients are -- which the augmentation controls.  The calibration target is the undefended,
+# un-noised FedSys run over real MNIST (eval/eval_poison/mnist_poison_30_100.pdf "Federated Learning -
+# No Poison", last-10 test error 0.0775; nsdi-eval/scaleup/fed_baseline_100: 0.064).  Measured with
+# scripts/robustness_sim.py (3 seeds, 100 peers): rot 6 / shift 1.25 (round 1) gave 0.132 and a clean
+# digit-1 error of 0.20; rot 3 / shift 0.6 gives 0.072 and 0.070 (docs/ROBUSTNESS.md).
+ROT_DEG = 3.0
+SHIFT_PX = 0.6
 
 
 def standardize_cols(X, mu=None, sigma=None):

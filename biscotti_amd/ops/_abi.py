@@ -16,7 +16,8 @@ SIGNATURES = {
     "bsc_point_op": [P, P, P, P, I, I, P],
     "bsc_witness_bases": [P, I, I, I, P, P],
     "bsc_fb_table": [P, I, I, I, I, I, I, L, L, L, P, P, P],
-    "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, I, P, P, P, P],
+    "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, I, P, P, P, P, P],
+    "bsc_alive_compact": [P, I, P, P],
     "bsc_set_alive": [P, P, I, P, P],
     "bsc_sum_rows": [P, I, P, I, P, I, P, P],
     "bsc_segment_sum": [P, I, I, I, I, P, P],
@@ -32,6 +33,7 @@ SIGNATURES = {
     "bsc_logreg_step": [P, P, P, P, P, P, I, I, I, U64, P, D, D, P, D, P, P, P],
     "bsc_dp_noise": [P, I, I, P, I, P, U64, I, P, P],
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],
+    "bsc_krum_committee": [P, I, I, I, P, I, I, I, I, I, P, I, P, P, P, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_noise_table": [I, I, U64, P, P],
     "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P, P],

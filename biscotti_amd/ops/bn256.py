@@ -119,12 +119,14 @@ class DeviceCommitEngine:
 
     # ---------------------------------------------------------------- per-round kernels
     def shares(self, coeffs: torch.Tensor, rows: torch.Tensor, commit_only: bool = False, check_rows: bool = True,
-               alive: torch.Tensor | None = None):
+               alive: torch.Tensor | None = None, compact: bool = False):
         """Fused chunk commitments (+ witnesses and share values unless commit_only).
 
         coeffs: int64 [P, d] quantized deltas; rows: int32 [n] rows of `coeffs` to process.
         alive: optional int32 [n] flags (1 = compute); a row whose flag is cleared while the kernel
         runs (set_alive) is skipped from then on and its outputs are left undefined.
+        compact: the flags are final when the kernel starts -- the flagged rows are packed densely
+        over the grid (a skipped row then costs no SIMD lanes, unlike the per-thread skip).
         Returns (pts [n, nchunks, S, 24] Jacobian with S = 1 or T+1, ys [n, nchunks, T] or None).
         """
         assert coeffs.dtype == torch.int64 and coeffs.dim() == 2 and coeffs.shape[1] == self.d
@@ -135,11 +137,15 @@ class DeviceCommitEngine:
         S = 1 if commit_only else self.T + 1
         pts = torch.empty((n, self.nchunks, S, 24), dtype=torch.int32, device=self.device)
         ys = None if commit_only else torch.empty((n, self.nchunks, self.T), dtype=torch.int64, device=self.device)
+        cidx = None
         if alive is not None:
             assert alive.dtype == torch.int32 and alive.numel() == n
+            if compact and n:
+                cidx = torch.empty((n + 1,), dtype=torch.int32, device=self.device)
+                _check(hip().bsc_alive_compact(_ptr(alive), n, _ptr(cidx), _stream()), "alive_compact")
         _check(hip().bsc_shares_msm(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), _ptr(self.tbl_wb),
-                                    self.poly, self.T, self.b0, self.nw, int(commit_only), _ptr(alive), _ptr(pts),
-                                    _ptr(ys), _stream()),
+                                    self.poly, self.T, self.b0, self.nw, int(commit_only), _ptr(alive), _ptr(cidx),
+                                    _ptr(pts), _ptr(ys), _stream()),
                "shares_msm")
         return pts, ys
 

@@ -264,6 +264,83 @@ def krum(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
     return acc, scores
 
 
+def _committee_host(X, inbox, groupsize, n_accept, need, lead_rank, cap):
+    """fp64 torch reference of the committee Krum (same tie-breaks as the kernels)."""
+    Xd = X.double().cpu()
+    ib = inbox.cpu().long()
+    V, n = ib.shape
+    U = Xd.shape[0]
+    G = Xd @ Xd.T
+    sq = torch.diagonal(G)
+    acc = torch.zeros((V, n), dtype=torch.bool)
+    sigs = torch.zeros((U,), dtype=torch.long)
+    hi = max(1, min(groupsize - 1, n))
+    for v in range(V):
+        rows = ib[v]
+        D = sq[rows][:, None] + sq[rows][None] - 2 * G[rows][:, rows]
+        srt, _ = torch.sort(D, dim=1)
+        sc = srt[:, 1:hi].sum(1) if hi > 1 else torch.zeros(n, dtype=torch.float64)
+        order = sorted(range(n), key=lambda i: (float(sc[i]), i))
+        acc[v, order[:n_accept]] = True
+        sigs.index_add_(0, rows[acc[v]], torch.ones(int(acc[v].sum()), dtype=torch.long))
+    lr = lead_rank.cpu().long()
+    appr = (lr >= 0) & (sigs >= need)
+    node = appr.clone()
+    if cap > 0 and int(appr.sum()) > cap:
+        idx = [int(w) for w in torch.nonzero(appr).flatten()]
+        idx.sort(key=lambda w: int(lr[w]))
+        node[:] = False
+        node[idx[:cap]] = True
+    return acc, node
+
+
+def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lead_rank, cap: int,
+                         kchunk: int = 512, on_accept=None):
+    """Multi-Krum of a whole verifier committee in one pass (the reference runs Krum once per
+    verifier process on that verifier's own inbox, krum.go:284-322).
+
+    X fp32 [U, d]: the candidate rows (submitted workers' noised deltas); inbox int32 [V, n]: each
+    live verifier's inbox as rows of X (sorted by SourceID); lead_rank int32 [U]: arrival rank of
+    each row at the leader miner (-1: row is not a submitted worker); need = floor(nv / 2)
+    signatures; cap = NUM_SAMPLES/2 leader threshold (0: no cap).
+
+    Returns a callable giving (acc bool [V, n], node bool [U]) on the host: acc[v, i] = verifier v
+    signs inbox[v, i]; node = rows the leader's block carries.  On a GPU on_accept(node_int32) is
+    called with the device mask right after the vote kernel is queued."""
+    U, D = X.shape
+    V, n = inbox.shape
+    if X.device.type != "cuda":
+        acc, node = _committee_host(X, inbox, groupsize, n_accept, need, lead_rank, cap)
+        if on_accept is not None:
+            on_accept(node.to(torch.int32))
+        return lambda: (acc, node)
+    assert X.dtype == torch.float32 and inbox.dtype == torch.int32 and lead_rank.dtype == torch.int32
+    assert 0 < U <= 1024 and 0 < n <= 256 and 0 < V <= 64 and n <= U, "committee Krum size limits"
+    assert lead_rank.numel() == U
+    T = (U + 15) // 16
+    npairs = T * (T + 1) // 2
+    nsplit = (D + kchunk - 1) // kchunk
+    dev = X.device
+    part = torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev)
+    scores = torch.empty((V, n), dtype=torch.float64, device=dev)
+    out = torch.empty((V * n + U,), dtype=torch.int32, device=dev)
+    acc, node = out[: V * n], out[V * n:]
+    _check(hip().bsc_krum_committee(_p(X.contiguous()), U, D, kchunk, _p(inbox.contiguous()), V, n, groupsize, n_accept,
+                                    need, _p(lead_rank.contiguous()), cap, _p(part), _p(scores), _p(acc), _p(node),
+                                    _stream()), "krum_committee")
+    host = torch.empty(out.shape, dtype=torch.int32, pin_memory=True)
+    host.copy_(out, non_blocking=True)
+    ev = S.record()
+    if on_accept is not None:
+        on_accept(node)
+
+    def result():
+        ev.synchronize()
+        h = host.bool()
+        return h[: V * n].view(V, n), h[V * n:]
+    return result
+
+
 # ---------------------------------------------------------------------------- K2 evaluation
 def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
     """Error rates of W on rows [0, split) and [split, N) of X from ONE kernel launch and one

@@ -2,16 +2,22 @@
 
 The reference moves every protocol message as a point-to-point Go net/rpc call (DistSys/main.go,
 SURVEY.md section 2.7).  Here peers are *virtual* and packed into contiguous blocks per rank (one
-process per GPU); per-round traffic is a handful of collectives:
+process per GPU); a secure-aggregation round issues two collectives, both one-shot all_gathers that
+use every xGMI link at once:
 
-  noised deltas + commitments -> verifiers      all_gather (one-shot, every link at once)
-  accept masks + Schnorr signatures -> workers  all_gather
-  Shamir shares worker -> miner                 all_to_all (personalised, variable sizes)
-  miner aggregates -> leader                    all_gather
-  block (header + GlobalW) leader -> everyone   broadcast
+  commitments + noised deltas -> verifiers       all_gather (every rank replicates the committee's
+                                                 Multi-Krum on identical inputs: no accept-mask or
+                                                 signature traffic on the secure path)
+  share sums -> miners -> leader                 all_gather of each rank's per-miner partial share
+                                                 sums + chunk-commitment sums + clock (the reduce-
+                                                 scatter to the miners fused with the leader's
+                                                 gather; every rank recovers the aggregate itself,
+                                                 so no block broadcast follows)
 
-With world size 1 all of these are local no-ops.  Backend "nccl" is RCCL on ROCm (xGMI); "gloo"
-runs the same code on CPU for tests and the plumbing configuration.
+The plain (-sa=false) path adds the deltas and clocks to the first gather; RONI verification and
+--verify-signatures add one all_gather of accept masks / signatures.  With world size 1 all of these
+are local no-ops.  Backend "nccl" is RCCL on ROCm (xGMI); "gloo" runs the same code on CPU for tests
+and the plumbing configuration.
 """
 from __future__ import annotations
 
@@ -49,9 +55,15 @@ class Comm:
         if world > 1 and not dist.is_initialized():
             be = backend or ("nccl" if dev.type == "cuda" else "gloo")
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+            be = os.environ.get("BISCOTTI_BACKEND", be)
             if be == "nccl" and torch.cuda.device_count() < local_world:
                 # several ranks share one device (rehearsals on a 1-GPU box): RCCL refuses
-                # duplicate devices, gloo moves the same device tensors through host memory
+                # duplicate devices, gloo moves the same device tensors through host memory.  Said
+                # out loud: a multi-GPU run must never end up on gloo by accident.
+                import warnings
+
+                warnings.warn(f"{local_world} local ranks on {torch.cuda.device_count()} visible GPU(s): "
+                              "using gloo instead of RCCL", RuntimeWarning)
                 be = "gloo"
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = {"device_id": dev} if be == "nccl" else {}
@@ -131,54 +143,3 @@ class Comm:
         if self.world > 1:
             dist.broadcast(t, src)
         return t
-
-    def broadcast_bytes(self, data: bytes | None, src: int) -> bytes:
-        if self.world == 1:
-            assert data is not None
-            return data
-        n = torch.zeros((1,), dtype=torch.int64, device=self.device)
-        if self.rank == src:
-            n[0] = len(data)
-        dist.broadcast(n, src)
-        buf = torch.empty((int(n.item()),), dtype=torch.uint8, device=self.device)
-        if self.rank == src:
-            buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
-        dist.broadcast(buf, src)
-        return data if self.rank == src else bytes(buf.cpu().numpy())
-
-    def all_to_all(self, send: list[torch.Tensor], recv_sizes: list[int] | None = None) -> list[torch.Tensor]:
-        """Personalised exchange of 1-D tensors of one dtype; send[r] goes to rank r.
-
-        When the caller already knows what it will receive (the round's routing is replicated on
-        every rank) it passes `recv_sizes` and the exchange is ONE all_to_all_single; otherwise the
-        sizes travel first in a tiny all_gather."""
-        assert len(send) == self.world
-        if self.world == 1:
-            return [send[0]]
-        dtype = send[0].dtype
-        allsizes = None
-        if recv_sizes is None:
-            sizes = torch.tensor([s.numel() for s in send], dtype=torch.int64, device=self.device)
-            allsizes = self.all_gather(sizes)  # [src, dst]
-            recv_sizes = [int(v) for v in allsizes[:, self.rank].tolist()]
-        inp = torch.cat([s.reshape(-1) for s in send]) if any(s.numel() for s in send) else \
-            torch.empty((0,), dtype=dtype, device=self.device)
-        out = torch.empty((sum(recv_sizes),), dtype=dtype, device=self.device)
-        try:
-            dist.all_to_all_single(out, inp, recv_sizes, [s.numel() for s in send])
-        except (RuntimeError, NotImplementedError):
-            # backends without alltoall: padded all_gather
-            if allsizes is None:
-                sizes = torch.tensor([s.numel() for s in send], dtype=torch.int64, device=self.device)
-                allsizes = self.all_gather(sizes)
-            m = max(int(allsizes.max()), 1)
-            pad = torch.zeros((self.world, m), dtype=dtype, device=self.device)
-            for r, s in enumerate(send):
-                pad[r, : s.numel()] = s.reshape(-1)
-            g = self.all_gather(pad)  # [src, dst, m]
-            out = torch.cat([g[src, self.rank, : recv_sizes[src]] for src in range(self.world)])
-        res, o = [], 0
-        for n in recv_sizes:
-            res.append(out[o:o + n])
-            o += n
-        return res

@@ -65,6 +65,11 @@ class RunConfig:
     fail_rank: int = 0              #   iteration (the reference's FAIL_PROB crash, made deterministic)
     spec_msm: bool = True           # share MSM of the whole inbox alongside verification (False: after Krum,
     #                                 kept rows only -- half the MSM work, started later)
+    shared_inbox: bool = False      # all verifiers judge one inbox (round-1 model); default: each verifier
+    #                                 collects its own first krum_thresh arrivals (krum.go:284-322)
+    miner_cap: bool = True          # leader's block = first NUM_SAMPLES/2 approved arrivals (main.go:360)
+    noise_independent: bool = False  # ablation: each worker draws private noise instead of its noisers'
+    #                                  shared pre-sampled vectors (client_obj.py:97-98); not the reference
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
     #                                 (shortens the GPU chain; costs host time before the previous round ends)
 
@@ -89,6 +94,8 @@ class RunConfig:
         pc.default_stake = self.default_stake
         pc.stake_unit = self.stake_unit
         pc.seed = self.seed & (2**64 - 1)
+        pc.shared_inbox = self.shared_inbox
+        pc.miner_cap = self.miner_cap
         pc.derive()
         return pc
 

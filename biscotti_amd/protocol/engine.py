@@ -9,12 +9,15 @@ VerifyUpdateKRUM -> RegisterSecret -> startShareDeadlineTimer -> createBlockSecA
   2. local step   fused gfx950 kernel for all local workers (softmax / logistic regression)
   3. commitments  fixed-base MSM (commit-only pass) for every online worker
   4. noising      counter-based DP noise averaged over each worker's noisers
-  5. verification one packed all_gather of commitments + noised deltas; Multi-Krum (f64 MFMA
-                  Gram) replicated on every rank; Schnorr signatures of the local verifiers
-  6. secure agg.  speculative share/witness MSM (rows Krum rejects are cancelled on the device);
-                  one all_to_all of per-miner share bytes; miner-side sums; one packed all_gather
-                  of the miners' sums; exact recovery + W update replicated on every rank;
-                  device audit of the aggregate against the summed chunk commitments
+  5. verification one packed all_gather of commitments + noised deltas; the committee's Multi-Krum
+                  (one f64-MFMA Gram, every verifier's selection on its own inbox, the
+                  >= floor(nv/2) vote and the leader's NUM_SAMPLES/2 arrival cap) replicated on
+                  every rank; Schnorr signatures of the local verifiers on native threads
+  6. secure agg.  share/witness MSM of exactly the kept rows (launched by the selection kernel,
+                  packed densely over the grid); per-rank partial share sums for every miner; ONE
+                  packed all_gather of the partial sums + chunk-commitment sums + clocks; exact
+                  recovery + W update replicated on every rank; device audit of the aggregate
+                  against the summed chunk commitments
   7. block        every rank builds the leader's block (gob + SHA-256) from identical inputs and
                   the leader's clock; empty blocks on the reference's timeout paths
   8. evaluation   test error / attack rate (logged in the reference's line format)
@@ -66,6 +69,8 @@ class RoundResult:
     attack_rate: float = float("nan")
     phases: dict = field(default_factory=dict)
     wall: float = 0.0
+    inboxes: dict = field(default_factory=dict)        # live verifier -> the updates it judged
+    approved_by_krum: list = field(default_factory=list)  # updates at least one verifier accepted
 
 
 class _Ready:
@@ -147,10 +152,13 @@ class _SpecShares:
     flag per row) is cleared for rows the verifiers reject; the MSM skips flagged rows, whether the
     flags were cleared before it started or while it runs.  Consumers wait on `ev`."""
 
-    def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream):
+    def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream, deferred: bool = False):
         self.eng, self.qdelta, self.rows, self.stream = eng, qdelta, rows, stream
         self.alive = torch.ones((len(rows),), dtype=torch.int32, device=qdelta.device)
         self.pts = self.ys = self.ev = None
+        # deferred: launched once the selection has set the flags -> only the kept rows are computed,
+        # packed densely over the grid
+        self.deferred = deferred
 
     def launch(self) -> None:
         if self.ev is not None:
@@ -159,7 +167,8 @@ class _SpecShares:
         S.wait(self.stream, main)              # qdelta (and any flag updates) come from main
         with S.use(self.stream):
             rows_t = h2d(self.rows, torch.int32, self.qdelta.device)
-            self.pts, self.ys = self.eng.shares(self.qdelta, rows_t, check_rows=False, alive=self.alive)
+            self.pts, self.ys = self.eng.shares(self.qdelta, rows_t, check_rows=False, alive=self.alive,
+                                                compact=self.deferred)
             self.ev = torch.cuda.Event()
             self.ev.record(self.stream)
         for t in (self.qdelta, self.alive):
@@ -209,7 +218,7 @@ class DeviceCrypto:
         stream).  launch=False prepares the per-row flags only; launch() then starts the MSM after
         everything queued so far on the caller's stream (e.g. Krum's selection), so rows already
         rejected cost nothing."""
-        sp = _SpecShares(self.eng, qdelta, rows, stream)
+        sp = _SpecShares(self.eng, qdelta, rows, stream, deferred=not launch)
         if launch:
             sp.launch()
         return sp
@@ -462,45 +471,56 @@ class BiscottiEngine:
         with tm.phase("local_step"):
             delta, qdelta = self.task.step(self.W, it, local_workers)
         with tm.phase("commit"):
-            # only the first krum_thresh arrivals reach the verifiers (verifier_inbox), so only they
-            # can be approved: they secret-share while verification runs (kyber.go:533-646), the MSM
-            # on the CU-masked side stream; shares of workers the verifiers reject are never routed.
-            # The MSM is the round's longest kernel, so it is launched first.
-            inbox = fsm.verifier_inbox(workers) if cfg.verification else []
+            # every live verifier collects its own first krum_thresh arrivals (krum.go:284-322); only
+            # updates that can end in the leader's block secret-share: the MSM runs on the CU-masked
+            # side stream, launched by the committee's selection (only the kept rows are computed) or,
+            # with spec_msm, speculatively over every candidate (rows rejected later are cancelled)
+            inboxes = {}
+            if cfg.verification:
+                for v, ib in zip(plan.verifiers, fsm.verifier_inboxes(workers)):
+                    if live[v]:
+                        inboxes[v] = list(ib)
             row_of = {w: i for i, w in enumerate(local_workers)}
             spec = None
             if self.gpu and cfg.secure_agg and local_workers:
-                cand = set(inbox) if cfg.verification else set(workers)
+                cand = self._block_candidates(plan, workers, inboxes)
                 spec_workers = [w for w in local_workers if w in cand]
                 if spec_workers:
-                    # with Krum the MSM can also wait for the selection (spec_msm=False): only the kept
-                    # rows are then computed, after the verification instead of alongside it
-                    defer = not cfg.spec_msm and cfg.verification and cfg.defense == "KRUM"
+                    defer = cfg.verification and not cfg.spec_msm
                     spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
                                                                    self.side_stream, launch=not defer))
             # full-vector commitments on the background stream: their first consumer is the signing
             # after Krum, so noise + Krum on the main stream do not queue behind them
             pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
-        head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inbox=inbox, row_of=row_of,
+        head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
                     spec=spec)
-        # one rank, Multi-Krum: the noise and Krum kernels (and, behind Krum's selection, the whole
-        # device-side aggregation) depend only on this head, so they are queued now as well -- the
-        # GPU then runs the round's dependency chain without waiting for the host in between
-        if (cfg.early_krum and self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.verification
-                and cfg.defense == "KRUM"
-                and inbox and spec is not None and self.noise_tbl is not None and cfg.noising and self.sigma > 0
-                and fut_noise is not None and any(live[v] for v in plan.verifiers)):
+        # one rank, Multi-Krum: the noise and committee-Krum kernels (and, behind the selection, the
+        # whole device-side aggregation) depend only on this head, so they can be queued now as well
+        if (cfg.early_krum and self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.defense == "KRUM"
+                and inboxes and spec is not None and cfg.noising and self.sigma > 0 and fut_noise is not None):
             with tm.phase("vrf_join"):
                 noisers = self._select_noisers(fut_noise, head["stake"], local_workers)
             with tm.phase("noise"):
-                _, X = self._noise(delta, noisers, local_workers, inbox, row_of, it)
+                noised = self._noise(delta, noisers, local_workers, it)
             with tm.phase("verify.launch"):
                 box: dict = {}
-                n = len(inbox)
-                clip = fsm.krum_clip(n)
-                wait = K.krum_async(X, n - clip, n - clip, on_accept=self._on_accept(spec, inbox, plan, live, box))
-            head["early"] = {"noisers": noisers, "krum": wait, "box": box}
+                wait = self._launch_krum(noised, row_of, plan, live, inboxes, spec, box)
+            head["early"] = {"noisers": noisers, "krum": wait, "box": box, "noised": noised}
         return head
+
+    def _block_candidates(self, plan, workers, inboxes) -> set:
+        """Workers whose update can end in this round's block: without verification every live worker
+        (capped to the leader's first arrivals); with it, every update some live verifier judges --
+        or every live worker when floor(nv/2) == 0 signatures suffice (the nv = 1 quirk,
+        main.go:1686: updates no verifier saw are approved too)."""
+        if not self.cfg.verification:
+            return set(self.fsm.leader_cap(workers))
+        if len(plan.verifiers) // 2 == 0:
+            return set(workers)
+        out: set = set()
+        for ib in inboxes.values():
+            out.update(ib)
+        return out
 
     def _select_noisers(self, fut_noise, stake, local_workers) -> dict:
         """Each worker's noisers from its own VRF output (getVRFNoisers, vrf.go:54-100).  Waits for
@@ -509,39 +529,67 @@ class BiscottiEngine:
         sel = self.R.select_noisers_batch(stake, betas, local_workers, self.cfg.num_noisers, self.N) if betas else []
         return dict(zip(local_workers, sel))
 
-    def _noise(self, delta, noisers, local_workers, inbox, row_of, it):
-        """Noised deltas (requestNoise + NoisedDelta, main.go:1513-1660) -> (noised [n, d] or None,
-        X_inbox or None).  On one rank with the secure path the noised deltas only feed Krum, so the
-        noise kernel writes the verifiers' inbox directly, in arrival order."""
+    def _noise(self, delta, noisers, local_workers, it):
+        """Noised deltas of the local workers (requestNoise + NoisedDelta, main.go:1513-1660): each
+        worker's noisers' pre-sampled vectors averaged and added (HBM-resident table on the GPU)."""
         cfg = self.cfg
         if not (cfg.noising and self.sigma > 0 and local_workers):
-            return delta, None
+            return delta
         ids = [noisers[w] for w in local_workers]
         assert all(0 <= j < self.N for row in ids for j in row), "noiser id out of range"
-        nz = h2d(ids, torch.int32, self.dev)
         sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma) for j in noisers[w]]
                   for w in local_workers], torch.float32, self.dev)
-        if self.comm.world == 1 and cfg.secure_agg and cfg.verification and inbox and self.noise_tbl is not None:
-            rr = [row_of[w] for w in inbox]
-            assert max(rr) < delta.shape[0]
-            X = K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl, rows=h2d(rr, torch.int32, self.dev))
-            return None, X
-        return K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl), None
+        if cfg.noise_independent:
+            # ablation (not the reference): every (worker, noiser slot) draws its own vector, so no two
+            # workers share noise -- isolates the effect of the noisers' shared pre-sampled vectors
+            nn_ = len(ids[0]) if ids else 0
+            nz = h2d([[self.N + w * nn_ + j for j in range(nn_)] for w in local_workers], torch.int32, self.dev)
+            return K.dp_noise(delta, nz, sc, cfg.seed, it, table=None)
+        nz = h2d(ids, torch.int32, self.dev)
+        return K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl)
 
-    def _on_accept(self, spec, inbox, plan, live, box):
-        """Device-side follow-up of Krum's selection kernel: cancel the rejected speculative rows and
-        (one rank) queue the aggregation of the kept rows; its handle lands in box['sa']."""
-        srow = {w: i for i, w in enumerate(spec[0])}
-        amap = h2d([srow.get(w, -1) for w in inbox], torch.int32, self.dev)
-        sp = spec[1]
-        pred = self._predict_miners(plan, live) if self.comm.world == 1 and self.cfg.secure_agg else None
+    def _launch_krum(self, X, xrow, plan, live, inboxes, spec, box):
+        """Queue the committee's Multi-Krum (one Gram over the candidate rows X, every live verifier's
+        selection on its own inbox, the >= floor(nv/2) vote and the leader's arrival cap) and, behind
+        it, the device-side follow-up of the selection (_on_accept).  xrow: worker -> row of X.
+        Returns the callable of krum_committee_async."""
+        cfg, fsm = self.cfg, self.fsm
+        vs = [v for v in plan.verifiers if v in inboxes]
+        n = len(inboxes[vs[0]])
+        U = X.shape[0]
+        inbox_t = h2d([[xrow[w] for w in inboxes[v]] for v in vs], torch.int32, self.dev)
+        rank = np.full(U, -1, np.int32)
+        for r, w in enumerate(fsm.leader_arrivals()):
+            if live[w] and w in xrow:
+                rank[xrow[w]] = r
+        cap = fsm.leader_cap_size()
+        need = len(plan.verifiers) // 2
+        clip = fsm.krum_clip(n)
+        on_accept = self._on_accept(spec, xrow, U, plan, live, box)
+        return K.krum_committee_async(X, inbox_t, n - clip, n - clip, need, h2d(rank, torch.int32, self.dev), cap,
+                                      on_accept=on_accept)
 
-        def on_accept(acc):
+    def _on_accept(self, spec, xrow, U, plan, live, box):
+        """Device-side follow-up of the committee's selection: this rank's share rows' flags become the
+        leader's block mask (rows outside it are cancelled, or never computed when the MSM was
+        deferred) and the aggregation of the kept rows is queued -- on EVERY rank, with or without
+        local rows, so the aggregation's collective lines up; its handle lands in box['sa']."""
+        amap_t = sp = None
+        if spec is not None:
+            amap = np.full(U, -1, np.int32)
+            for i, w in enumerate(spec[0]):
+                amap[xrow[w]] = i
+            amap_t = h2d(amap, torch.int32, self.dev)
+            sp = spec[1]
+        pred = self._predict_miners(plan, live) if self.gpu and self.cfg.secure_agg else None
+
+        def on_accept(node):
             with self.timer.phase("verify.queue_agg"):
-                B.set_alive(acc, amap, sp.alive)
-                sp.launch()   # no-op when the MSM already runs speculatively
+                if sp is not None:
+                    B.set_alive(node, amap_t, sp.alive)
+                    sp.launch()   # no-op when the MSM already runs speculatively
                 if pred is not None:
-                    box["sa"] = self._spec_aggregate(spec, pred)
+                    box["sa"] = self._spec_aggregate(spec, pred, node)
         return on_accept
 
     def run_round(self) -> RoundResult | None:
@@ -557,19 +605,18 @@ class BiscottiEngine:
             workers, local_workers, stake = head["workers"], head["local_workers"], head["stake"]
             fut_noise, fut_roles = head["fut_noise"], head["fut_roles"]
             delta, qdelta, pending_commits = head["delta"], head["qdelta"], head["pending_commits"]
-            inbox, row_of, spec = head["inbox"], head["row_of"], head["spec"]
+            inboxes, row_of, spec = head["inboxes"], head["row_of"], head["spec"]
         early = head.get("early")
         with tm.phase("vrf_join"):
             noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake, local_workers)
         with tm.phase("noise"):
-            noised, X_fused = (None, None) if early else \
-                self._noise(delta, noisers, local_workers, inbox, row_of, it)
+            noised = early["noised"] if early else self._noise(delta, noisers, local_workers, it)
         # ---------------------------------------------------------------- verification
         with tm.phase("verify"):
             single = comm.world == 1
             commit_of: dict = {}
             g_commit = g_noised = g_delta = g_ts = None
-            need_X = cfg.verification and bool(inbox)
+            need_X = cfg.verification and bool(inboxes)
 
             def _materialize_commits():  # first use comes after the Krum kernels are queued
                 if commit_of:
@@ -613,88 +660,82 @@ class BiscottiEngine:
             accepted_map: dict = {}
             signatures: dict = {}
             pending_signatures = None
-            local_verifiers = [v for v in plan.verifiers if live[v] and v in self.local]
-            # Multi-Krum is a pure function of the gathered inbox, so on several ranks EVERY rank
-            # evaluates it (identical inputs, deterministic kernel) instead of all_gathering the
-            # verifiers' accept masks; RONI depends on each verifier's own data and still gathers
-            replicated = not single and cfg.defense == "KRUM"
-            judges = [v for v in plan.verifiers if live[v]] if replicated else local_verifiers
-            # speculative shares of updates Krum rejects are cancelled on the device as soon as the
-            # selection kernel has run (Krum approvals are a superset of the approved set); on one
-            # rank the whole aggregation of the kept rows is queued right behind it
-            on_accept = None
             box = early["box"] if early else {}
-            if not early and need_X and spec is not None and cfg.defense == "KRUM":
-                on_accept = self._on_accept(spec, inbox, plan, live, box)
             if need_X:
-                nv, ni = len(plan.verifiers), len(inbox)
-                if single:
-                    X = None if (not judges or early) else X_fused if X_fused is not None else \
-                        noised.index_select(0, h2d([row_of[w] for w in inbox], torch.long, self.dev))
-                else:
-                    X = g_noised.index_select(0, h2d([self.flat[w] for w in inbox], torch.long, self.dev)) \
-                        if judges else None
-                acc_np = np.zeros((nv, ni), np.uint8)
-                sig_np = np.zeros((nv, ni, 64), np.uint8)
-                krum_cache = None
-                pos = {w: j for j, w in enumerate(inbox)}
-                # every verifier's accept list first, then ONE native call signs the local ones' lists
-                msgs, key_of, ids, slots, sks, bases = [], [], [], [], [], []
-                for v in judges:
+                vs = [v for v in plan.verifiers if v in inboxes]   # live verifiers, plan order
+                nv = len(plan.verifiers)
+                ni = len(inboxes[vs[0]])
+                X, xrow = (noised, row_of) if single else (g_noised, self.flat)
+                if cfg.defense == "KRUM":
+                    # Multi-Krum is a pure function of the (gathered) noised deltas, so every rank
+                    # evaluates the whole committee itself (identical inputs, deterministic kernels)
                     with tm.phase("verify.defense"):
-                        if cfg.defense == "KRUM" and early:   # queued with the round head
-                            krum_cache = krum_cache or [bool(a) for a in early["krum"]()[0].tolist()]
-                            accept = krum_cache
-                        elif cfg.defense == "KRUM":  # identical inputs -> identical Krum result
-                            krum_cache = krum_cache or self._verify(X, inbox, it, v, on_accept)
-                            accept = krum_cache
-                        else:
-                            accept = self._verify(X, inbox, it, v)
-                    vi = plan.verifiers.index(v)
-                    for j, a_ in enumerate(accept):
-                        if a_:
-                            acc_np[vi, j] = 1
-                    if v not in self.local:
-                        continue   # the verifier's own rank signs its approvals
+                        wait = early["krum"] if early else self._launch_krum(X, xrow, plan, live, inboxes, spec,
+                                                                             box)
+                        with tm.phase("verify.krum_wait"):
+                            acc_t, node_t = wait()
+                    acc_np = acc_t.numpy().astype(np.uint8)   # [len(vs), ni]
+                    acc_row = {v: k for k, v in enumerate(vs)}
+                    if box.get("sa") is not None:   # the rows the device aggregation kept
+                        box["sa"]["accepted"] = {w for w in workers if bool(node_t[xrow[w]])}
+                else:
+                    # RONI: each verifier judges with its own data, so only its rank can decide; the
+                    # accept matrix [nv, ni] travels in one all_gather on several ranks
+                    mine = np.zeros((nv, ni), np.uint8)
+                    for v in vs:
+                        if v in self.local:
+                            rows_v = h2d([xrow[w] for w in inboxes[v]], torch.long, self.dev)
+                            with tm.phase("verify.defense"):
+                                ok = self._verify(X.index_select(0, rows_v), inboxes[v], it, v)
+                            mine[plan.verifiers.index(v)] = np.asarray(ok, np.uint8)
+                    if single:
+                        allm = mine
+                    else:
+                        allm = comm.all_gather(torch.from_numpy(mine).to(self.dev)).cpu().numpy()
+                        allm = np.stack([allm[comm.owner(v, self.N), plan.verifiers.index(v)] for v in plan.verifiers])
+                    acc_np = np.stack([allm[plan.verifiers.index(v)] for v in vs])
+                    acc_row = {v: k for k, v in enumerate(vs)}
+                for v in vs:
+                    accepted_map[v] = [w for w, a_ in zip(inboxes[v], acc_np[acc_row[v]]) if a_]
+                # the local verifiers sign their accepted commitments on native threads while the GPU
+                # computes shares (main.go:1120-1140); joined where first needed (plain blocks carry
+                # them, --verify-signatures checks them) or at the end of the round
+                msgs, key_of, ids, slots, sks, bases = [], [], [], [], [], []
+                local_vs = [v for v in vs if v in self.local]
+                if local_vs:
                     _materialize_commits()
+                for v in local_vs:
                     sks.append(self.sk[v])
                     bases.append(_seed_bytes(cfg.seed, f"nonce-{it}", v))
-                    for w, a_ in zip(inbox, accept):
+                    for j, (w, a_) in enumerate(zip(inboxes[v], acc_np[acc_row[v]])):
                         if a_:
                             msgs.append(commit_of[w])
                             key_of.append(len(sks) - 1)
                             ids.append(w)
-                            slots.append((vi, pos[w]))
-                if box.get("sa") is not None:   # the rows the device aggregation kept
-                    keep = set(spec[0])
-                    box["sa"]["accepted"] = {w for w, a_ in zip(inbox, krum_cache or []) if a_ and w in keep}
-                # verifier signatures (main.go:1120-1140) sign on native threads while the GPU
-                # computes shares; they are joined where first needed (plain blocks carry them,
-                # --verify-signatures checks them) or at the end of the round
+                            slots.append((plan.verifiers.index(v), j))
                 sign_job = R.schnorr_sign_multi_async(msgs, sks, key_of, bases, ids, cfg.host_threads) \
                     if msgs else None
-                acc_all = acc_np[None] if (single or replicated) else \
-                    comm.all_gather(torch.from_numpy(acc_np).to(self.dev)).cpu().numpy()
-                acc_row = {v: 0 if (single or replicated) else comm.owner(v, self.N) for v in plan.verifiers}
-                for vi, v in enumerate(plan.verifiers):
-                    if not live[v]:
-                        continue
-                    accepted_map[v] = [inbox[j] for j in np.nonzero(acc_all[acc_row[v], vi])[0]]
+                sig_np = np.zeros((nv, ni, 64), np.uint8)
 
-                def _join_signatures(sign_job=sign_job, slots=slots, sig_np=sig_np, acc_all=acc_all,
-                                     acc_row=acc_row, inbox=inbox, live=live, plan=plan):
+                def _join_signatures(sign_job=sign_job, slots=slots, sig_np=sig_np, vs=vs):
                     with tm.phase("verify.sign_join"):
                         sigs = sign_job.result() if sign_job is not None else []
                         for (vi, j), sg in zip(slots, sigs):
                             sig_np[vi, j] = np.frombuffer(sg, np.uint8)
-                        sig_all = sig_np[None] if single else \
-                            comm.all_gather(torch.from_numpy(sig_np).to(self.dev)).cpu().numpy()
-                        for vi, v in enumerate(plan.verifiers):
-                            if not live[v]:
+                        # the signatures travel to the workers (and on to the miners) only where a
+                        # consumer reads them: plain blocks carry them, --verify-signatures checks them;
+                        # on the secure path each rank keeps the ones its verifiers produced (Q5)
+                        gather = not single and (not cfg.secure_agg or cfg.verify_signatures)
+                        sig_all = comm.all_gather(torch.from_numpy(sig_np).to(self.dev)).cpu().numpy() if gather \
+                            else sig_np[None]
+                        for v in vs:
+                            if not gather and v not in self.local:
                                 continue
-                            o = 0 if single else comm.owner(v, self.N)
-                            for j in np.nonzero(acc_all[acc_row[v], vi])[0]:
-                                signatures.setdefault(inbox[j], []).append(sig_all[o, vi, j].tobytes())
+                            vi = plan.verifiers.index(v)
+                            o = comm.owner(v, self.N) if gather else 0
+                            for w in accepted_map[v]:
+                                j = inboxes[v].index(w)
+                                signatures.setdefault(w, []).append(sig_all[o, vi, j].tobytes())
                 pending_signatures = _join_signatures
                 if not cfg.secure_agg or cfg.verify_signatures:
                     pending_signatures()
@@ -748,7 +789,8 @@ class BiscottiEngine:
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=n_up == 0,
                           node_list=self._last_nodes, approved=list(approved), verifiers=list(plan.verifiers),
                           miners=list(plan.miners), test_error=ev["test_error"], attack_rate=ev["attack_rate"],
-                          phases=tm.reset(), wall=time.perf_counter() - t_round)
+                          phases=tm.reset(), wall=time.perf_counter() - t_round, inboxes=dict(inboxes),
+                          approved_by_krum=sorted(set().union(*accepted_map.values())) if accepted_map else [])
         self._log_round(res)
         self.rounds_done += 1
         if it == cfg.fail_at and comm.rank == cfg.fail_rank:
@@ -799,52 +841,118 @@ class BiscottiEngine:
         contributing = [plan.leader] + [m for m in plan.miners if m != plan.leader and live[m]]
         return contributing, part
 
-    def _spec_aggregate(self, spec, pred) -> dict:
-        """Queue the secure aggregation of every speculative row Krum keeps -- masked share-value
-        sums, exact recovery (main stream), the audit's commitment sums + check (side stream), the
-        witness sums (background stream) -- right behind the selection kernel, before the host has
-        read Krum's result.  The host later adopts it if the approvals, miners and parts match
-        (_secure_aggregation), so the GPU never idles while the host approves, routes and signs."""
+    def _spec_aggregate(self, spec, pred, node) -> dict:
+        """Queue the secure aggregation of the rows the committee's selection kept -- masked share-value
+        sums, the cross-rank combination, exact recovery (main stream), the audit's commitment sums +
+        check (side stream), the witness sums (background stream) -- right behind the selection
+        kernels, before the host has read the selection.  Every rank queues it at the same point
+        (the selection is replicated), so its collective lines up.  The host later adopts it if the
+        approvals, miners and parts match (_secure_aggregation).  node: device int32 mask over the
+        Krum rows (the leader's block)."""
         contributing, part = pred
-        spm, T, nch, nc = self.pc.shares_per_miner, self.T, self.nchunks, len(pred[0])
-        sp = spec[1]
-        sp.launch()
-        pts, ys, ev, alive = sp.pts, sp.ys, sp.ev, sp.alive
-        main = S.current()
-        main.wait_event(ev)                      # the speculative MSM's shares
+        sp = spec[1] if spec is not None else None
+        pts = ys = alive = None
+        if sp is not None:
+            sp.launch()
+            pts, ys, alive = sp.pts, sp.ys, sp.alive
+            S.current().wait_event(sp.ev)          # the MSM's shares
+        agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration))
+        agg["contributing"], agg["part"], agg["accepted"], agg["node"] = list(contributing), dict(part), None, node
+        return agg
+
+    def _agg_index(self, contributing, part):
+        """Resident index tensors of one miner layout (a handful recur: the parts are a permutation of
+        0..M-1): chunk-commitment columns, witness columns, the contributing miners' share columns and
+        their x-points, uploaded once."""
         key = (tuple(contributing), tuple(part[m] for m in contributing))
         hit = self._agg_idx.get(key)
         if hit is None:
-            # a handful of miner layouts recur (the miners' parts are a permutation of 0..M-1): the
-            # index tensors are built and uploaded once per layout and stay resident
+            spm, T, nch = self.pc.shares_per_miner, self.T, self.nchunks
             base = np.arange(nch) * (T + 1)
             ycols = np.concatenate([spm * part[m] + np.arange(spm) for m in contributing])
             wc = np.concatenate([(base[:, None] + spm * part[m] + np.arange(spm)[None, :]).reshape(-1)
                                  for m in contributing])
-            parts = [np.tile(base + T, nc), wc, ycols, ycols - 10]
+            assert wc.max() < nch * (T + 1) and ycols.max() < T
+            parts = [base + T, wc, ycols, ycols - 10]
             idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
-            offs = np.cumsum([0] + [len(a) for a in parts])
-            hit = (idx, [idx[offs[i]:offs[i + 1]] for i in range(4)], (ycols - 10).tolist())
+            offs = np.cumsum([0] + [len(x) for x in parts])
+            hit = ([idx[offs[i]:offs[i + 1]] for i in range(4)], (ycols - 10).tolist())
             if len(self._agg_idx) < 256:
                 self._agg_idx[key] = hit
-        idx, (ccols, wcols, ycols_t, xs_t), xs_list = hit
-        flat = pts.view(pts.shape[0], nch * (T + 1), 24)
-        csum = None
-        if self.cfg.audit_aggregate:
-            # the miners' chunk-commitment sums need only the MSM + the flags: they run on the side
-            # stream alongside the share sums and the recovery below, not after them
-            st = self.side_stream
-            S.wait(st, main)
-            with S.use(st):
-                csum = B.sum_rows(flat, None, ccols, check=False, row_mask=alive).view(nc, nch, 24)
-            for t in (pts, idx, alive):
-                t.record_stream(st)
-        agg = (ys * alive.view(-1, 1, 1)).sum(0).index_select(1, ycols_t)     # [nchunks, npts]
-        W_new, coeffs, status = K.recover(agg, xs_t, self.cfg.poly_size, self.d, self.W, 10.0 ** self.cfg.precision)
-        audit_ok = self._audit(coeffs, csum) if csum is not None else None
-        self._background(lambda: B.sum_rows(flat, None, wcols, check=False, row_mask=alive), flat, idx, alive)
-        return {"contributing": list(contributing), "part": dict(part), "accepted": None, "W_new": W_new,
-                "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok}
+        return hit
+
+    def _aggregate(self, pts, ys, rowsel, contributing, part, now) -> dict:
+        """Secure aggregation of this rank's kept rows, combined over ranks, then exact recovery.
+
+        Every miner sums the shares it received (aggregateSecret, kyber.go:244-287) and the leader
+        recovers from the miners' sums (kyber.go:809-857).  Share sums are additive, so each rank sums
+        its own workers' share columns for all miners at once and ONE all_gather (the reduce-scatter
+        to the miners fused with the leader's gather) hands every rank the totals; every
+        rank then recovers the aggregate itself -- exact integer recovery on identical inputs, so all
+        ranks build the leader's block bit for bit.  The chunk-commitment sums (identical for every
+        miner: same node list) travel in the same buffer for the audit; the witness sums, which no
+        consumer reads (the reference's leader never checks them), stay per-rank partials on the
+        background stream.
+
+        pts [R, nch, T+1, pw] / ys [R, nch, T] (None: no local rows); rowsel: device int32 mask [R]
+        or a host list of row indices.  Returns the handles _finish_secagg consumes."""
+        cfg, comm = self.cfg, self.comm
+        T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
+        audit = cfg.audit_aggregate
+        (ccols, wcols, ycols_t, xs_t), xs_list = self._agg_index(contributing, part)
+        main = S.current() if self.gpu else None
+        # ---- this rank's partial sums
+        ys_part = torch.zeros((nch, T), dtype=torch.int64, device=self.dev)
+        cs_part = None
+        if pts is not None and (not isinstance(rowsel, list) or rowsel):
+            flat = pts.view(pts.shape[0], nch * (T + 1), pw)
+            if self.gpu:
+                rows_t = None if not isinstance(rowsel, list) else h2d(rowsel, torch.int32, self.dev)
+                mask = rowsel if rows_t is None else None
+                if rows_t is None:
+                    ys_part = (ys * mask.view(-1, 1, 1)).sum(0)
+                else:
+                    ys_part = ys.index_select(0, rows_t.long()).sum(0)
+                if audit:
+                    st = self.side_stream if comm.world == 1 else main
+                    if st is not main:
+                        S.wait(st, main)
+                    with S.use(st):
+                        cs_part = B.sum_rows(flat, rows_t, ccols, check=False, row_mask=mask)
+                    if st is not main:
+                        for t in (pts, ccols) + ((mask,) if mask is not None else (rows_t,)):
+                            t.record_stream(st)
+                self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
+                                 flat, wcols, mask if mask is not None else rows_t)
+            else:
+                rows_l = list(rowsel)
+                ys_part = ys[rows_l].sum(0)
+                if audit:
+                    cs_part = self.crypto.sum_rows(flat[rows_l][:, ccols.long()])
+        if audit and cs_part is None:   # no local rows: the neutral element (point at infinity)
+            cs_part = torch.zeros((nch, pw), dtype=pdt, device=self.dev)
+        # ---- combine over ranks: ONE all_gather (share sums, commitment sums, clock)
+        clock = None
+        if comm.world > 1:
+            parts = [ys_part.reshape(1, -1), torch.full((1, 1), now, dtype=torch.int64, device=self.dev)]
+            if audit:
+                parts.append(cs_part.reshape(1, -1))
+            got = comm.all_gather_packed(parts)
+            ys_tot = got[0].view(comm.world, nch, T).sum(0)
+            clock = got[1].reshape(comm.world)
+            if audit:
+                cs_all = got[2].view(comm.world, nch, pw)
+                cs_tot = B.sum_rows(cs_all.contiguous(), None, None, check=False) if self.gpu else \
+                    self.crypto.sum_rows(cs_all)
+        else:
+            ys_tot = ys_part
+            cs_tot = cs_part
+        agg = ys_tot.index_select(1, ycols_t.long() if not self.gpu else ycols_t).contiguous()   # [nch, npts]
+        W_new, coeffs, status = K.recover(agg, xs_t if self.gpu else xs_t.cpu(), cfg.poly_size, self.d, self.W,
+                                          10.0 ** cfg.precision)
+        audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
+        return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
+                "clock": clock, "now": now}
 
     def _d2h(self, *ts: torch.Tensor) -> list:
         """Several device tensors to host numpy arrays with ONE wait (pinned, stream-ordered copies)."""
@@ -913,10 +1021,8 @@ class BiscottiEngine:
     # ------------------------------------------------------------------ secure aggregation path
     def _secure_aggregation(self, plan, live, approved, delta, qdelta, local_workers, row_of, commit_of,
                             signatures, spec=None, sa=None):
-        cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
+        cfg, R, fsm, tm = self.cfg, self.R, self.fsm, self.timer
         self._last_nodes = []
-        spm, T, nch = self.pc.shares_per_miner, self.T, self.nchunks
-        single = comm.world == 1
         if cfg.verify_signatures and cfg.verification:
             # miners reject shares without >= nv/2 valid verifier signatures (main.go:269-277, Q5)
             need = len(plan.verifiers) // 2
@@ -926,179 +1032,56 @@ class BiscottiEngine:
         with tm.phase("shares"):
             routes = fsm.route_shares(approved)
             lv = fsm.leader_view(routes)
-            local_approved = [w for w in approved if w in self.local]
-            pts = ys = None
-            ap_row = {w: i for i, w in enumerate(local_approved)}
-            if local_approved and routes:  # workers share as soon as any miner is reachable
-                spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
-                if spec is not None and all(w in spec_row for w in local_approved):
-                    spec[1].launch()
-                    pts, ys, ev = spec[1].pts, spec[1].ys, spec[1].ev
-                    S.current().wait_event(ev)
-                    ap_row = {w: spec_row[w] for w in local_approved}   # rows of the speculative tensors
-                else:
-                    sel = h2d([row_of[w] for w in local_approved], torch.long, self.dev)
-                    pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
         if not (lv.leader_online and lv.quorum):
             return None
         node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
         part_of = {m: dict(routes[m])[node_list[0]] for m in contributing}
-        if sa is not None and sa.get("accepted") is not None and contributing == sa["contributing"] and part_of == sa["part"] \
-                and set(node_list) == sa["accepted"]:
-            # the device already aggregated exactly these workers' shares (queued behind Krum's
-            # selection kernel, before the host knew the approvals): recovery and audit are in flight
+        if sa is not None and sa.get("accepted") is not None and contributing == sa["contributing"] \
+                and part_of == sa["part"] and set(node_list) == sa["accepted"]:
+            # the device already aggregated exactly these workers' shares (queued behind the
+            # committee's selection, before the host knew the approvals): recovery and audit are in flight
             self.stats["device_aggregations"] = self.stats.get("device_aggregations", 0) + 1
             with tm.phase("recover"):
-                return self._finish_secagg(plan, node_list, commit_of, sa["W_new"], sa["status"], sa["agg"],
-                                           sa["xs"], sa["audit_ok"], self._now(plan.iteration))
-        pw, pdt = self.crypto.point_width, self.crypto.point_dtype
-        esz = torch.empty((), dtype=pdt).element_size()
-        ar = torch.arange(nch, dtype=torch.long, device=self.dev)
-        nc = len(contributing)
-        audit = cfg.audit_aggregate
-
-        def cols_of(part):  # the miner's witness slots + the chunk-commitment slot
-            return list(range(spm * part, spm * part + spm)) + [T]
-
-        with tm.phase("share_exchange"):
-            recv: dict = {}  # miner -> (pts [E, nch, spm+1, pw] or None, ys [E, nch, spm], rows or None)
-            if single:
-                rows = h2d([ap_row[w] for w in node_list], torch.long, self.dev)
-                for m in contributing:
-                    recv[m] = (None, None, rows)
-            else:
-                # ONE all_to_all: per (miner, worker) entry the miner's witness + chunk-commitment
-                # points, then its share values, as raw bytes.  Every rank derives what it receives
-                # from the replicated routing, so no size exchange precedes it.
-                per_p, per_y = nch * (spm + 1) * pw, nch * spm
-                pbytes = per_p * esz
-                ent_bytes = pbytes + per_y * 8
-                send = []
-                for dst in range(comm.world):
-                    ents = [(m, w) for m in contributing if comm.owner(m, self.N) == dst
-                            for w in node_list if w in ap_row]
-                    if ents:
-                        ir = h2d([ap_row[w] for _, w in ents], torch.long, self.dev)
-                        ic = h2d([cols_of(part_of[m]) for m, _ in ents], torch.long, self.dev)
-                        g = pts[ir[:, None, None], ar[None, :, None], ic[:, None, :]]       # [E, nch, spm+1, pw]
-                        gy = ys[ir[:, None, None], ar[None, :, None], ic[:, None, :spm]]  # [E, nch, spm]
-                        send.append(torch.cat([g.reshape(len(ents), -1).view(torch.uint8),
-                                               gy.reshape(len(ents), -1).view(torch.uint8)], dim=1).reshape(-1))
-                    else:
-                        send.append(torch.empty((0,), dtype=torch.uint8, device=self.dev))
-                src_ents = {src: [(mm, w) for mm in contributing if comm.owner(mm, self.N) == comm.rank
-                                  for w in node_list if comm.owner(w, self.N) == src] for src in range(comm.world)}
-                rb = comm.all_to_all(send, [len(src_ents[s]) * ent_bytes for s in range(comm.world)])
-                for m in contributing:
-                    if m not in self.local:
-                        continue
-                    ps_, ys_ = [], []
-                    for src in range(comm.world):
-                        for k, (mm, w) in enumerate(src_ents[src]):
-                            if mm == m:
-                                e = rb[src][k * ent_bytes:(k + 1) * ent_bytes]
-                                ps_.append(_bytes_as(e[:pbytes], pdt).view(nch, spm + 1, pw))
-                                ys_.append(_bytes_as(e[pbytes:], torch.int64).view(nch, spm))
-                    recv[m] = (torch.stack(ps_), torch.stack(ys_), None)
-        with tm.phase("miner_aggregate"):
-            agg_y = torch.zeros((nc, nch, spm), dtype=torch.int64, device=self.dev)
-            # every miner's summed chunk commitments (aggregateSecret, kyber.go:251-253): the audit
-            # checks the recovered aggregate against them
-            csum = torch.zeros((nc, nch, pw), dtype=pdt, device=self.dev)
-            agg_direct = xs_direct = None
-            if single and self.gpu and contributing:
-                # aggregateSecret for every miner: the rows (contributing workers) are shared.  The
-                # chunk-commitment sums feed only the audit (side stream); the 7 witness sums per
-                # chunk and miner -- which nothing in a round reads: the reference's leader never
-                # checks aggregated witnesses -- run on the background stream, off the critical path.
-                # Every index list goes up in ONE upload; the share values go straight into the
-                # recovery's [nchunks, points] layout.
-                row_list = [ap_row[w] for w in node_list]
-                base = np.arange(nch) * (T + 1)
-                ycols = np.concatenate([spm * part_of[m] + np.arange(spm) for m in contributing])
-                wc = np.concatenate([(base[:, None] + spm * part_of[m] + np.arange(spm)[None, :]).reshape(-1)
-                                     for m in contributing])
-                assert max(row_list) < pts.shape[0] and wc.max() < nch * (T + 1) and ycols.max() < T
-                parts = [np.asarray(row_list), np.tile(base + T, nc), wc, ycols, ycols - 10]
-                idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
-                offs = np.cumsum([0] + [len(a) for a in parts])
-                rows_i, ccols, wcols, ycols_t, xs_t_ = (idx[offs[i]:offs[i + 1]] for i in range(5))
-                flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-                if audit:
-                    st = self.side_stream
-                    S.wait(st, S.current())
-                    with S.use(st):
-                        csum = B.sum_rows(flat, rows_i, ccols, check=False).view(nc, nch, pw)
-                    for t in (pts, idx):   # main-stream tensors read on the side stream
-                        t.record_stream(st)
-                self._background(lambda: B.sum_rows(flat, rows_i, wcols, check=False), flat, idx)
-                agg_direct = ys.index_select(0, rows_i).sum(0).index_select(1, ycols_t)   # [nch, npts]
-                xs_direct = ((ycols - 10).tolist(), xs_t_)
-            else:
-                for ci, m in enumerate(contributing):
-                    if m not in self.local:
-                        continue
-                    p_, y_, rows = recv[m]
-                    part = part_of[m]
-                    if rows is not None:  # single rank (CPU): aggregate straight out of the share tensors
-                        cols = h2d([k * (T + 1) + c for k in range(nch) for c in cols_of(part)], torch.long,
-                                   self.dev)
-                        flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-                        s = self.crypto.sum_rows(flat.index_select(0, rows).index_select(1, cols))
-                        csum[ci] = s.view(nch, spm + 1, pw)[:, spm]
-                        agg_y[ci] = ys.index_select(0, rows)[:, :, spm * part: spm * part + spm].sum(0)
-                    elif self.gpu:
-                        flatm = p_.reshape(p_.shape[0], nch * (spm + 1), pw)
-                        cc = h2d(np.arange(nch, dtype=np.int32) * (spm + 1) + spm, torch.int32, self.dev)
-                        csum[ci] = B.sum_rows(flatm, None, cc, check=False)
-                        wc = h2d((np.arange(nch)[:, None] * (spm + 1) + np.arange(spm)[None, :]).reshape(-1)
-                                 .astype(np.int32), torch.int32, self.dev)
-                        self._background(lambda f=flatm, c=wc: B.sum_rows(f, None, c, check=False), flatm, wc)
-                        agg_y[ci] = y_.sum(0)
-                    else:
-                        s = self.crypto.sum_rows(p_.reshape(p_.shape[0], -1, pw))
-                        csum[ci] = s.view(nch, spm + 1, pw)[:, spm]
-                        agg_y[ci] = y_.sum(0)
+                return self._finish_secagg(plan, node_list, commit_of, sa)
+        # host-decided path (no device selection, RONI, or a prediction mismatch): the leader's block
+        # carries lv.node_list only (its first NUM_SAMPLES/2 arrivals), so only those workers' shares
+        # are computed; every rank takes this branch together (replicated decisions)
+        with tm.phase("shares"):
+            local_used = [w for w in node_list if w in self.local]
+            pts = ys = None
+            rowsel: list = []
+            if local_used:
+                spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
+                if spec is not None and all(w in spec_row for w in local_used):
+                    sp = spec[1]
+                    if sp.ev is None:   # deferred and not launched by a device-side selection
+                        used = set(local_used)
+                        sp.alive.copy_(h2d([1 if w in used else 0 for w in spec[0]], torch.int32, self.dev))
+                    sp.launch()
+                    pts, ys = sp.pts, sp.ys
+                    S.current().wait_event(sp.ev)
+                    rowsel = [spec_row[w] for w in local_used]   # rows of the speculative tensors
+                else:
+                    sel = h2d([row_of[w] for w in local_used], torch.long, self.dev)
+                    pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
+                    rowsel = list(range(len(local_used)))
         with tm.phase("recover"):
-            now = self._now(plan.iteration)
-            if single:
-                agg_all, cs_all, ts_all = agg_y[None], csum[None], None
-            else:
-                # ONE all_gather: every miner's share sums (+ its chunk-commitment sums for the audit)
-                # and every rank's clock.  Each rank then recovers the aggregate itself -- exact
-                # integer recovery on identical inputs, so every rank builds the leader's block bit
-                # for bit -- instead of waiting for a block broadcast.
-                parts = [agg_y.reshape(1, -1), torch.full((1, 1), now, dtype=torch.int64, device=self.dev)]
-                if audit:
-                    parts.append(csum.reshape(1, -1))
-                got = comm.all_gather_packed(parts)
-                agg_all = got[0].view(comm.world, nc, nch, spm)
-                ts_all = got[1]
-                cs_all = got[2].view(comm.world, nc, nch, pw) if audit else None
-            leader_rank = comm.owner(plan.leader, self.N)
-            own = [0 if single else comm.owner(m, self.N) for m in contributing]
-            if agg_direct is not None:
-                agg, (xs, xs_t) = agg_direct, xs_direct
-            else:
-                xs = [spm * part_of[m] + s_ - 10 for m in contributing for s_ in range(spm)]
-                agg = torch.cat([agg_all[own[ci], ci] for ci in range(nc)], dim=1).contiguous()   # [nchunks, npts]
-                xs_t = h2d(xs, torch.int32, self.dev)
-            with tm.phase("recover.kernel"):
-                W_new, coeffs, status = K.recover(agg, xs_t, cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
-                audit_ok = None
-                if audit:
-                    audit_ok = self._audit(coeffs, cs_all[0] if single else
-                                           torch.stack([cs_all[own[ci], ci] for ci in range(nc)]))
-                if ts_all is not None:
-                    now = int(ts_all[leader_rank].reshape(-1)[0])   # the leader's clock stamps the block
-            return self._finish_secagg(plan, node_list, commit_of, W_new, status, agg, xs, audit_ok, now)
+            agg = self._aggregate(pts, ys, rowsel, contributing, part_of, self._now(plan.iteration))
+            return self._finish_secagg(plan, node_list, commit_of, agg)
 
-    def _finish_secagg(self, plan, node_list, commit_of, W_new, status, agg, xs, audit_ok, now):
-        """Read back the recovered model, fall back to least squares for inconsistent chunks, build
-        the block, then check the aggregate audit (running on the side stream meanwhile)."""
+    def _finish_secagg(self, plan, node_list, commit_of, h):
+        """Read back the recovered model (and the ranks' clocks), fall back to least squares for
+        inconsistent chunks, build the block, then check the aggregate audit (running on the side
+        stream meanwhile)."""
         cfg, R, fsm, tm = self.cfg, self.R, self.fsm, self.timer
+        W_new, status, agg, xs, audit_ok = h["W_new"], h["status"], h["agg"], h["xs"], h["audit_ok"]
         with tm.phase("recover.readback"):
-            st, W_np = self._d2h(status, W_new)
+            if h["clock"] is not None:
+                st, W_np, clk = self._d2h(status, W_new, h["clock"])
+                now = int(clk[self.comm.owner(plan.leader, self.N)])   # the leader's clock stamps the block
+            else:
+                st, W_np = self._d2h(status, W_new)
+                now = h["now"]
         if not st.all():  # inconsistent shares: the reference's float64 least squares
             aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()
             for k in np.nonzero(st == 0)[0]:
@@ -1112,7 +1095,7 @@ class BiscottiEngine:
             block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
         self._W_next = W_new if st.all() and self.gpu else None
         if audit_ok is not None:
-            if self.comm.world == 1 and self._idle_work is not None:
+            if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()
                 self._idle_work = None
             with tm.phase("recover.audit"):

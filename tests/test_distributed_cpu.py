@@ -27,10 +27,28 @@ def _worker(rank, world, port, kw, rounds, q):
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
+    count = kw.pop("_count_collectives", False)
     comm = Comm.init(device="cpu")
     eng = BiscottiEngine(RunConfig(**kw), comm)
+    calls = []
+    if count:
+        import torch.distributed as dist
+
+        real = dist.all_gather_into_tensor
+
+        def counting(*a, **k):
+            calls.append(1)
+            return real(*a, **k)
+        dist.all_gather_into_tensor = counting
+    per_round = []
     for _ in range(rounds):
-        eng.run_round()
+        n0 = len(calls)
+        r = eng.run_round()
+        per_round.append((len(calls) - n0, r.empty))
+    if count:
+        # every non-empty secure round: verification gather + aggregation gather
+        assert all(c == 2 for c, empty in per_round if not empty), per_round
+        assert any(not empty for _, empty in per_round)
     q.put((rank, [bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))]))
     comm.barrier()
     comm.shutdown()
@@ -79,9 +97,20 @@ def test_two_ranks_match_single_process(secure_agg):
 
 
 def test_three_ranks_uneven_packing():
-    single = _run(1, KW, 3)[0]
-    multi = _run(3, dict(KW, num_nodes=7), 3)
+    kw = dict(KW, num_nodes=7)
+    single = _run(1, kw, 3)[0]
+    multi = _run(3, kw, 3)
     assert multi[0] == multi[1] == multi[2]
+    assert multi[0] == single
+
+
+def test_collectives_per_round():
+    """A secure-aggregation round with Multi-Krum issues exactly two collectives on several ranks
+    (the verification all_gather and the aggregation all_gather): no accept-mask, signature or
+    block traffic (every rank replicates the committee and the recovery)."""
+    kw = dict(KW, num_nodes=8, seed=3)
+    out = _run(2, dict(kw, _count_collectives=True), 3)
+    assert out[0] == out[1]
 
 
 def test_peer_processes_localtest_oracle():

@@ -142,6 +142,42 @@ def test_engine_rounds_on_gpu(early, spec_msm):
     eng.close()
 
 
+@pytest.mark.parametrize("U,n,V", [(94, 70, 3), (150, 140, 5), (256, 256, 3), (300, 200, 26)])
+def test_krum_committee_matches_reference(U, n, V):
+    """Committee Multi-Krum (one Gram over the candidate rows, per-verifier inboxes, vote and leader
+    cap) against the fp64 torch reference, incl. inboxes of 140 and 256 updates (200-peer runs)."""
+    g = torch.Generator().manual_seed(U + n + V)
+    X = torch.randn((U, 7850), generator=g) * 0.1
+    bad = torch.randperm(U, generator=g)[: U // 5]
+    X[bad] += 0.5 * torch.randn((1, 7850), generator=g)        # a tight cluster of outliers
+    inbox = torch.stack([torch.sort(torch.randperm(U, generator=g)[:n]).values for _ in range(V)]).int()
+    rank = torch.randperm(U, generator=g).int()
+    rank[torch.randperm(U, generator=g)[:3]] = -1                # rows that did not submit
+    clip = n // 2
+    need, cap = V // 2, max(2, n // 4)
+    acc_ref, node_ref = K.krum_committee_async(X, inbox, n - clip, n - clip, need, rank, cap)()
+    acc, node = K.krum_committee_async(X.cuda(), inbox.cuda(), n - clip, n - clip, need, rank.cuda(), cap)()
+    assert torch.equal(acc, acc_ref)
+    assert torch.equal(node, node_ref)
+    assert int(node.sum()) <= cap
+    # the outliers are rejected by every verifier that saw them
+    for v in range(V):
+        rows = inbox[v].long()
+        assert not acc[v][torch.isin(rows, bad)].any()
+
+
+def test_krum_committee_single_verifier_equals_krum():
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn((70, 7850), generator=g) * 0.1
+    X[60:] += 3.0
+    acc_ref, _ = K.krum(X, 35, 35)
+    inbox = torch.arange(70, dtype=torch.int32)[None]
+    acc, node = K.krum_committee_async(X.cuda(), inbox.cuda(), 35, 35, 1, torch.arange(70, dtype=torch.int32).cuda(),
+                                       0)()
+    assert torch.equal(acc[0], acc_ref)
+    assert torch.equal(node, acc_ref)
+
+
 def test_eval_errors_two_sets_one_launch():
     """Test error and attack rate from one MFMA kernel launch, against the fp32 torch reference."""
     X, y, off, nt, pid, W = _fed(P=1, n=2347)

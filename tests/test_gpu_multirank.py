@@ -1,7 +1,8 @@
-"""Multi-rank engine on the GPU: 2 ranks share cuda:0 over the gloo backend (RCCL cannot put two
-ranks on one device), which runs every device-side multi-rank path -- all_gather of noised
-deltas, all_to_all of share tensors, leader gather, block broadcast -- and must reproduce the
-single-process GPU chain byte for byte (deterministic timestamps)."""
+"""Multi-rank engine on the GPU: 2 and 4 ranks share cuda:0 over the gloo backend (RCCL cannot put
+two ranks on one device), which runs every device-side multi-rank path -- the all_gather of
+commitments + noised deltas, the replicated committee Krum, per-rank partial share sums and their
+all_gather, replicated exact recovery -- and must reproduce the single-process GPU chain byte for
+byte (deterministic timestamps), also with poisoners and churn."""
 import os
 import queue
 import sys
@@ -69,4 +70,13 @@ def test_gpu_two_ranks_match_single_process(secure_agg):
     single = _run(1, kw, 3)[0]
     multi = _run(2, kw, 3)
     assert multi[0] == multi[1]
+    assert multi[0] == single
+
+
+def test_gpu_four_ranks_poisoning_and_churn_match_single_process():
+    kw = dict(num_nodes=16, dataset="mnist", seed=9, deterministic_time=True, max_iterations=100, poisoning=0.3,
+              churn=0.1, num_verifiers=3)
+    single = _run(1, kw, 4)[0]
+    multi = _run(4, kw, 4)
+    assert multi[0] == multi[1] == multi[2] == multi[3]
     assert multi[0] == single
