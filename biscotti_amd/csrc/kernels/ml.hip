@@ -433,23 +433,21 @@ __device__ __forceinline__ int pair_index(int ti, int tj, int T) {
   // row-major enumeration of the upper triangle ti <= tj of a T x T tile grid
   return ti * T - (ti * (ti - 1)) / 2 + (tj - ti);
 }
-// Gram entry G[a][b] summed over the K splits in split order (bit-reproducible on every rank)
-__device__ __forceinline__ double gram_at(const double* part, int nsplit, int npairs, int T, int a, int b) {
+// Gram entry G[a][b] out of the reduced upper-triangular tiles
+__device__ __forceinline__ double gram_at(const double* gram, int T, int a, int b) {
   int ta = a >> 4, tb = b >> 4, ra = a & 15, rb = b & 15;
   if (ta > tb) {
     const int t = ta; ta = tb; tb = t;
     const int r = ra; ra = rb; rb = r;
   }
-  const double* p = part + (size_t)pair_index(ta, tb, T) * 256 + ra * 16 + rb;
-  double s = 0.0;
-  for (int sp = 0; sp < nsplit; ++sp) s += p[(size_t)sp * npairs * 256];
-  return s;
+  return gram[(size_t)pair_index(ta, tb, T) * 256 + ra * 16 + rb];
 }
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, int U, int D, int kchunk, int T,
-                                                              double* part) {
+                                                              double* part, double* gram, unsigned int* count) {
   __shared__ double red[4][256];
+  __shared__ unsigned int last;
   const int pair = blockIdx.x, sp = blockIdx.y;
   const int npairs = gridDim.x;
   // decode the pair index (T <= 64: a short scan)
@@ -497,23 +495,35 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
   __syncthreads();
   const int e = threadIdx.x;  // 256 threads = the 16x16 tile
   part[((size_t)sp * npairs + pair) * 256 + e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+  // split-K reduction in-kernel: the last split block of this tile pair to finish sums the partials
+  // in split order (bit-reproducible) and writes the reduced tile; it also re-arms the counter
+  __threadfence();
+  __syncthreads();
+  if (e == 0) last = atomicAdd(count + pair, 1u) == (unsigned)(gridDim.y - 1) ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double g = 0.0;
+  for (int q = 0; q < (int)gridDim.y; ++q)
+    g += __hip_atomic_load(part + ((size_t)q * npairs + pair) * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  gram[(size_t)pair * 256 + e] = g;
+  if (e == 0) count[pair] = 0u;
 }
 
-extern "C" __global__ void __launch_bounds__(256) k_krum_rows(const double* part, int nsplit, int npairs, int T,
-                                                             const int* inbox, int n, int groupsize,
-                                                             double* scores) {
+extern "C" __global__ void __launch_bounds__(256) k_krum_rows(const double* gram, int T, const int* inbox, int n,
+                                                             int groupsize, double* scores) {
   __shared__ double row[256];
   __shared__ double kept[256];
   __shared__ double gdiag_a;
   const int i = blockIdx.x, v = blockIdx.y, t = threadIdx.x;
   const int* box = inbox + (size_t)v * n;
   const int a = box[i];
-  if (t == 0) gdiag_a = gram_at(part, nsplit, npairs, T, a, a);
+  if (t == 0) gdiag_a = gram_at(gram, T, a, a);
   __syncthreads();
   if (t < n) {
     const int b = box[t];
-    const double gab = gram_at(part, nsplit, npairs, T, a, b);
-    const double gbb = gram_at(part, nsplit, npairs, T, b, b);
+    const double gab = gram_at(gram, T, a, b);
+    const double gbb = gram_at(gram, T, b, b);
     row[t] = gdiag_a + gbb - 2.0 * gab;
   }
   __syncthreads();
@@ -539,31 +549,42 @@ extern "C" __global__ void __launch_bounds__(1024) k_krum_vote(const double* sco
                                                               int cap, int* acc, int* node) {
   __shared__ int sigs[1024];
   __shared__ int appr[1024];
+  __shared__ int lr[1024];
+  __shared__ double sv[4][256];
   const int t = threadIdx.x;
-  for (int w = t; w < U; w += 1024) sigs[w] = 0;
-  __syncthreads();
-  // per-verifier Multi-Krum selection: the n_accept lowest scores (index tie-break)
-  for (int e = t; e < V * n; e += 1024) {
-    const int v = e / n, i = e % n;
-    const double* sv = scores + (size_t)v * n;
-    const double s = sv[i];
-    int rank = 0;
-    for (int j = 0; j < n; ++j) rank += (sv[j] < s) || (sv[j] == s && j < i);
-    const int ok = rank < n_accept ? 1 : 0;
-    acc[e] = ok;
-    if (ok) atomicAdd(&sigs[inbox[e]], 1);
+  for (int w = t; w < U; w += 1024) {
+    sigs[w] = 0;
+    lr[w] = lead_rank[w];
+  }
+  // per-verifier Multi-Krum selection: the n_accept lowest scores (index tie-break); four verifiers
+  // at a time, their scores staged in LDS
+  for (int v0 = 0; v0 < V; v0 += 4) {
+    const int nv = min(4, V - v0);
+    __syncthreads();
+    for (int e = t; e < nv * n; e += 1024) sv[e / n][e % n] = scores[(size_t)(v0 + e / n) * n + e % n];
+    __syncthreads();
+    for (int e = t; e < nv * n; e += 1024) {
+      const int vv = e / n, i = e % n;
+      const double s = sv[vv][i];
+      int rank = 0;
+      for (int j = 0; j < n; ++j) rank += (sv[vv][j] < s) || (sv[vv][j] == s && j < i);
+      const int ok = rank < n_accept ? 1 : 0;
+      const size_t ge = (size_t)(v0 + vv) * n + i;
+      acc[ge] = ok;
+      if (ok) atomicAdd(&sigs[inbox[ge]], 1);
+    }
   }
   __syncthreads();
   // approval: >= need signatures among the submitted workers (lead_rank >= 0)
-  for (int w = t; w < U; w += 1024) appr[w] = (lead_rank[w] >= 0 && sigs[w] >= need) ? 1 : 0;
+  for (int w = t; w < U; w += 1024) appr[w] = (lr[w] >= 0 && sigs[w] >= need) ? 1 : 0;
   __syncthreads();
   // the leader's block: the first `cap` approved rows in leader arrival order (cap <= 0: all)
   for (int w = t; w < U; w += 1024) {
     int keep = appr[w];
     if (keep && cap > 0) {
       int before = 0;
-      const int r = lead_rank[w];
-      for (int x = 0; x < U; ++x) before += appr[x] && lead_rank[x] < r;
+      const int r = lr[w];
+      for (int x = 0; x < U; ++x) before += appr[x] && lr[x] < r;
       keep = before < cap;
     }
     node[w] = keep;
@@ -739,6 +760,83 @@ extern "C" __global__ void k_recover(const long long* ys, int nchunks, int npts,
 }
 
 // =====================================================================================
+// K12, fused form: share-value sums + exact recovery with precomputed integer weights.
+// For a fixed x-point layout (the contributing miners' parts) the inverse Vandermonde on the `poly`
+// basis nodes is A / Dn with integer A (host-computed exactly, |A| < 2^40, Dn = 2^s * Dodd), so
+// c_j = (sum_i A[j][i] y_{basis_i}) / Dn -- an int128 mat-vec and one exact division, done as a
+// shift plus a multiplication by Dodd^-1 mod 2^128 (no 128-bit divisions).  Every share is then
+// re-checked by Horner in int128 (status 0 -> the host's least squares, like the old kernel).
+// The miners' sums are fused in: agg[k][p] = sum over rows r with mask[r] of ys[r][k][ycols[p]]
+// (nrows = 1 and mask = null when ys already holds totals).  One block: 8 chunks.
+// =====================================================================================
+namespace {
+constexpr int RW_CPB = 8;     // chunks per block
+constexpr int RW_MAXP = 32;   // points per chunk
+constexpr int RW_MAXC = 16;   // coefficients per chunk
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(256) k_recover_w(
+    const long long* ys, int nrows, int nch, int T, const int* mask, const int* ycols, const int* xs, int npts,
+    const long long* A, const int* basis, int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi,
+    int d, const double* W, double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out) {
+  __shared__ long long agg[RW_CPB][RW_MAXP];
+  __shared__ __int128 cf[RW_CPB][RW_MAXC];
+  __shared__ int ok[RW_CPB];
+  const int t = threadIdx.x;
+  const int k0 = blockIdx.x * RW_CPB;
+  if (t < RW_CPB) ok[t] = 1;
+  // 1. the miners' share sums for this block's chunks
+  for (int e = t; e < RW_CPB * npts; e += 256) {
+    const int c = e / npts, p = e % npts, k = k0 + c;
+    if (k >= nch) continue;
+    long long s = 0;
+    const int col = ycols[p];
+    for (int r = 0; r < nrows; ++r)
+      if (mask == nullptr || mask[r]) s += ys[((size_t)r * nch + k) * T + col];
+    agg[c][p] = s;
+    agg_out[(size_t)k * npts + p] = s;
+  }
+  __syncthreads();
+  // 2. coefficients: int128 mat-vec, exact division by Dn = 2^shift * Dodd
+  const unsigned __int128 inv = ((unsigned __int128)inv_hi << 64) | inv_lo;
+  for (int e = t; e < RW_CPB * poly; e += 256) {
+    const int c = e / poly, j = e % poly;
+    if (k0 + c >= nch) continue;
+    __int128 n = 0;
+    for (int i = 0; i < poly; ++i) n += (__int128)A[j * poly + i] * (__int128)agg[c][basis[i]];
+    bool exact = (shift == 0) || ((n & ((((__int128)1) << shift) - 1)) == 0);
+    const __int128 q = (__int128)((unsigned __int128)(n >> shift) * inv);
+    // a true coefficient is tiny next to 2^100; an inexact division lands anywhere in 2^128
+    const __int128 lim = ((__int128)1) << 100;
+    exact = exact && q < lim && q > -lim;
+    cf[c][j] = q;
+    if (!exact) atomicAnd(&ok[c], 0);
+  }
+  __syncthreads();
+  // 3. every share must lie on the recovered polynomial (Horner, int128)
+  for (int e = t; e < RW_CPB * npts; e += 256) {
+    const int c = e / npts, p = e % npts;
+    if (k0 + c >= nch) continue;
+    __int128 acc = 0;
+    const __int128 x = xs[p];
+    for (int j = poly - 1; j >= 0; --j) acc = acc * x + cf[c][j];
+    if (acc != (__int128)agg[c][p]) atomicAnd(&ok[c], 0);
+  }
+  __syncthreads();
+  // 4. outputs: coefficients, dequantised model update
+  for (int e = t; e < RW_CPB * poly; e += 256) {
+    const int c = e / poly, j = e % poly, k = k0 + c;
+    if (k >= nch) continue;
+    const bool good = ok[c] != 0;
+    const long long v = good ? (long long)cf[c][j] : 0;
+    coeffs[(size_t)k * poly + j] = v;
+    if (j == 0) status[k] = good ? 1 : 0;
+    const int idx = k * poly + j;
+    if (idx < d) W_new[idx] = W[idx] + (double)v / qscale;
+  }
+}
+
+// =====================================================================================
 // Plain aggregation (non-secure-agg / FedSys): W_new = W + sum_r delta64[rows[r]] in fp64,
 // in row order (mat.Dense.Add sequence).
 // =====================================================================================
@@ -804,15 +902,17 @@ extern "C" int bsc_krum(const float* X, int n, int D, int ksplit, double* part, 
 // scores [V, n] f64; acc [V, n] int32; node [U] int32.
 extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, const int* inbox, int V, int n,
                                   int groupsize, int n_accept, int need, const int* lead_rank, int cap, double* part,
-                                  double* scores, int* acc, int* node, void* stream) {
+                                  double* gram, unsigned int* count, double* scores, int* acc, int* node,
+                                  void* stream) {
   if (U <= 0 || V <= 0 || n <= 0) return 0;
   if (U > 1024 || n > 256 || V > 64 || n > U || kchunk <= 0) return -1;
   const int T = (U + 15) / 16;
   const int npairs = T * (T + 1) / 2;
   const int nsplit = (D + kchunk - 1) / kchunk;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part);
-  hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, part, nsplit, npairs, T, inbox, n, groupsize, scores);
+  // count: npairs zeroed counters (re-armed by the kernel itself)
+  hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part, gram, count);
+  hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, gram, T, inbox, n, groupsize, scores);
   hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U, need, lead_rank, cap,
                      acc, node);
   return (int)hipGetLastError();
@@ -851,6 +951,18 @@ extern "C" int bsc_recover(const long long* ys, int nchunks, int npts, const int
   if (npts > 32 || poly > 16) return -1;
   hipLaunchKernelGGL(k_recover, dim3(nblk(nchunks, 64)), dim3(64), 0, (hipStream_t)stream, ys, nchunks, npts, xs,
                      poly, d, W, qscale, W_new, coeffs, status);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, const int* mask, const int* ycols,
+                             const int* xs, int npts, const long long* A, const int* basis, int poly, int shift,
+                             unsigned long long inv_lo, unsigned long long inv_hi, int d, const double* W, double qscale,
+                             double* W_new, long long* coeffs, int* status, long long* agg_out, void* stream) {
+  if (nch <= 0) return 0;
+  if (npts > RW_MAXP || poly > RW_MAXC || poly > npts || shift < 0 || shift > 100 || nrows <= 0) return -1;
+  hipLaunchKernelGGL(k_recover_w, dim3(nblk(nch, RW_CPB)), dim3(256), 0, (hipStream_t)stream, ys, nrows, nch, T, mask,
+                     ycols, xs, npts, A, basis, poly, shift, inv_lo, inv_hi, d, W, qscale, W_new, coeffs, status,
+                     agg_out);
   return (int)hipGetLastError();
 }
 

@@ -71,38 +71,37 @@ class MNISTCNNModel(_Flat):
 
 
 class LFWCNNModel(_Flat):
-    """lfw_cnn_model.py:8-47 -- two conv blocks + linear head for 62x47x3 faces, 12 classes."""
+    """lfw_cnn_model.py:8-28, layer for layer: conv3x3 3->18 (pad 1) + ReLU + maxpool 2, conv3x3
+    18->36 (pad 1) + ReLU + maxpool 2, fc 5940->2 on 62x47x3 faces (36 x 15 x 11 = 5940).
+    18,254 parameters -- the `get_num_params('lfw')` value of ML/Pytorch/datasets.py:22-23."""
 
-    def __init__(self, n_classes: int = 12):
+    def __init__(self, n_classes: int = 2):
         super().__init__()
-        self.conv1 = nn.Conv2d(3, 16, 5, padding=2)
-        self.conv2 = nn.Conv2d(16, 32, 5, padding=2)
-        self.fc = nn.Linear(32 * 15 * 11, n_classes)
+        self.conv1 = nn.Conv2d(3, 18, kernel_size=3, stride=1, padding=1)
+        self.conv2 = nn.Conv2d(18, 36, kernel_size=3, stride=1, padding=1)
+        self.fc1 = nn.Linear(5940, n_classes)
 
     def forward(self, x):
         x = x.reshape(x.shape[0], 3, 62, 47)
-        x = F.max_pool2d(F.relu(self.conv1(x)), 2)
-        x = F.max_pool2d(F.relu(self.conv2(x)), 2)
-        return self.fc(x.reshape(x.shape[0], -1))
+        x = F.max_pool2d(F.relu(self.conv1(x)), kernel_size=2, stride=2)
+        x = F.max_pool2d(F.relu(self.conv2(x)), kernel_size=2, stride=2)
+        return self.fc1(x.reshape(x.shape[0], -1))
 
 
 class CIFARCNNModel(_Flat):
-    """cifar_cnn_model.py:8-61 -- LeNet-style CNN for 32x32x3, 10 classes."""
+    """cifar_cnn_model.py:8-31, layer for layer: conv3x3 3->20 with padding 3 (32x32 -> 36x36) + ReLU
+    + maxpool(k=1, identity), fc 25920->10 (20 x 36 x 36 = 25920; the reference's ONE LAYER
+    variant).  259,770 parameters."""
 
-    def __init__(self):
+    def __init__(self, n_classes: int = 10):
         super().__init__()
-        self.conv1 = nn.Conv2d(3, 6, 5)
-        self.conv2 = nn.Conv2d(6, 16, 5)
-        self.fc1 = nn.Linear(16 * 5 * 5, 120)
-        self.fc2 = nn.Linear(120, 84)
-        self.fc3 = nn.Linear(84, 10)
+        self.conv1 = nn.Conv2d(3, 20, kernel_size=3, stride=1, padding=3)
+        self.fc1 = nn.Linear(25920, n_classes)
 
     def forward(self, x):
         x = x.reshape(x.shape[0], 3, 32, 32)
-        x = F.max_pool2d(F.relu(self.conv1(x)), 2)
-        x = F.max_pool2d(F.relu(self.conv2(x)), 2)
-        x = x.reshape(x.shape[0], -1)
-        return self.fc3(F.relu(self.fc2(F.relu(self.fc1(x)))))
+        x = F.max_pool2d(F.relu(self.conv1(x)), kernel_size=1, stride=1)
+        return self.fc1(x.reshape(x.shape[0], -1))
 
 
 def flatten_params(model: nn.Module) -> np.ndarray:

@@ -294,6 +294,20 @@ def _committee_host(X, inbox, groupsize, n_accept, need, lead_rank, cap):
     return acc, node
 
 
+_COUNTERS: dict = {}
+
+
+def _tile_counters(dev, n: int) -> torch.Tensor:
+    """Zeroed per-tile arrival counters of the in-kernel split-K reduction; the kernel re-arms them,
+    so one buffer per device serves every launch (stream-ordered on the round's main stream)."""
+    key = (str(dev), S.raw())
+    buf = _COUNTERS.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.zeros((max(n, 1024),), dtype=torch.int32, device=dev)
+        _COUNTERS[key] = buf
+    return buf
+
+
 def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lead_rank, cap: int,
                          kchunk: int = 512, on_accept=None):
     """Multi-Krum of a whole verifier committee in one pass (the reference runs Krum once per
@@ -322,12 +336,14 @@ def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lea
     nsplit = (D + kchunk - 1) // kchunk
     dev = X.device
     part = torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev)
+    gram = torch.empty((npairs, 256), dtype=torch.float64, device=dev)
+    count = _tile_counters(dev, npairs)
     scores = torch.empty((V, n), dtype=torch.float64, device=dev)
     out = torch.empty((V * n + U,), dtype=torch.int32, device=dev)
     acc, node = out[: V * n], out[V * n:]
     _check(hip().bsc_krum_committee(_p(X.contiguous()), U, D, kchunk, _p(inbox.contiguous()), V, n, groupsize, n_accept,
-                                    need, _p(lead_rank.contiguous()), cap, _p(part), _p(scores), _p(acc), _p(node),
-                                    _stream()), "krum_committee")
+                                    need, _p(lead_rank.contiguous()), cap, _p(part), _p(gram), _p(count), _p(scores),
+                                    _p(acc), _p(node), _stream()), "krum_committee")
     host = torch.empty(out.shape, dtype=torch.int32, pin_memory=True)
     host.copy_(out, non_blocking=True)
     ev = S.record()
@@ -418,6 +434,69 @@ def recover(agg_y, xs, poly: int, d: int, W, qscale=1e4):
                 Wn[i] = Wn[i] + float(r[j]) / qscale
     W_new.copy_(torch.from_numpy(Wn))
     return W_new, coeffs, status
+
+
+def recovery_weights(xs, poly: int) -> dict:
+    """Exact integer recovery weights for one x-point layout: the inverse Vandermonde of the `poly`
+    basis nodes of smallest |x| (kyber.go:809-857 solves the same system by QR) as A / Dn with
+    integer A, Dn = 2^shift * Dodd and Dodd^-1 mod 2^128 -- computed once per miner layout."""
+    from fractions import Fraction
+    from math import lcm
+
+    xs = [int(x) for x in xs]
+    order = sorted(range(len(xs)), key=lambda i: (abs(xs[i]), xs[i]))[:poly]
+    nodes = [xs[i] for i in order]
+    n = len(nodes)
+    M = [[Fraction(x) ** k for k in range(n)] for x in nodes]
+    inv = [[Fraction(int(i == j)) for j in range(n)] for i in range(n)]
+    for c in range(n):   # Gauss-Jordan over the rationals
+        p = next(r for r in range(c, n) if M[r][c] != 0)
+        M[c], M[p], inv[c], inv[p] = M[p], M[c], inv[p], inv[c]
+        f = M[c][c]
+        M[c] = [v / f for v in M[c]]
+        inv[c] = [v / f for v in inv[c]]
+        for r in range(n):
+            if r != c and M[r][c] != 0:
+                g = M[r][c]
+                M[r] = [a - g * b for a, b in zip(M[r], M[c])]
+                inv[r] = [a - g * b for a, b in zip(inv[r], inv[c])]
+    Dn = 1
+    for row in inv:
+        for v in row:
+            Dn = lcm(Dn, v.denominator)
+    A = [[int(v * Dn) for v in row] for row in inv]
+    assert max(abs(a) for r in A for a in r) < 2 ** 40, "recovery weights out of range"
+    shift = (Dn & -Dn).bit_length() - 1
+    odd = Dn >> shift
+    iv = pow(odd, -1, 1 << 128)
+    return {"A": np.asarray(A, dtype=np.int64), "basis": order, "shift": shift, "inv_lo": iv & (2 ** 64 - 1),
+            "inv_hi": iv >> 64, "Dn": Dn}
+
+
+def recover_rows(ys, mask, ycols, xs, weights: dict, A_dev, basis_dev, poly: int, d: int, W, qscale=1e4):
+    """Fused miner share sums + exact recovery + W update (GPU, k_recover_w).
+
+    ys int64 [R, nch, T] (R = 1 with mask None: already totals); mask int32 [R] or None; ycols /
+    xs int32 [npts] (the contributing miners' columns and x-points); weights from recovery_weights
+    with A_dev / basis_dev its device copies.  Returns (W_new fp64 [d], coeffs int64 [nch, poly],
+    status int32 [nch], agg int64 [nch, npts])."""
+    R, nch, T = ys.shape
+    npts = ycols.numel()
+    dev = ys.device
+    W_new = torch.empty_like(W)
+    coeffs = torch.empty((nch, poly), dtype=torch.int64, device=dev)
+    status = torch.empty((nch,), dtype=torch.int32, device=dev)
+    agg = torch.empty((nch, npts), dtype=torch.int64, device=dev)
+    if dev.type != "cuda":
+        rows = ys if mask is None else ys[mask.bool()]
+        agg.copy_(rows.sum(0).index_select(1, ycols.long()))
+        W_new, coeffs, status = recover(agg, xs, poly, d, W, qscale)
+        return W_new, coeffs, status, agg
+    assert ys.dtype == torch.int64 and ys.is_contiguous() and (mask is None or mask.numel() == R)
+    _check(hip().bsc_recover_w(_p(ys), R, nch, T, _p(mask), _p(ycols), _p(xs), npts, _p(A_dev), _p(basis_dev), poly,
+                               weights["shift"], weights["inv_lo"], weights["inv_hi"], d, _p(W), float(qscale),
+                               _p(W_new), _p(coeffs), _p(status), _p(agg), _stream()), "recover_w")
+    return W_new, coeffs, status, agg
 
 
 def add_rows(delta, rows, W):

@@ -51,7 +51,7 @@ class RunConfig:
     device: str | None = None       # "cpu" forces the CPU path
     log_every_peer: bool = False    # one Train Error line per local peer (reference style)
     deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
-    phase_sync: bool = True         # device sync at phase boundaries (accurate per-phase GPU times)
+    phase_sync: bool = False        # device sync at phase boundaries (diagnostics: per-phase GPU times)
     side_stream_skip_every: int = 4  # speculative-MSM stream leaves every Nth CU free (0: no CU mask)
     main_stream_exclusive: bool = False  # critical-path stream masked to exactly the CUs the MSM leaves free
     bg_stream_complement: bool = False  # background stream (commitments, witness sums) on the CUs the MSM
@@ -63,8 +63,12 @@ class RunConfig:
     comm_timeout_s: float = 300.0   # collective timeout: a dead rank fails the job instead of hanging it
     fail_at: int = -1               # fault injection: rank `fail_rank` dies right after committing this
     fail_rank: int = 0              #   iteration (the reference's FAIL_PROB crash, made deterministic)
-    spec_msm: bool = True           # share MSM of the whole inbox alongside verification (False: after Krum,
-    #                                 kept rows only -- half the MSM work, started later)
+    spec_msm: bool = True           # share MSM speculatively alongside verification, over the candidates most
+    #                                 likely to end in the block (False: after the committee's selection,
+    #                                 the block's rows only -- least work, started later)
+    spec_margin: float = 1.7        # speculative rows: the first ceil(margin * cap) + 2 candidates in leader
+    #                                 arrival order (the block takes the first `cap` approved of them;
+    #                                 a block row outside this prefix falls back to a top-up MSM)
     shared_inbox: bool = False      # all verifiers judge one inbox (round-1 model); default: each verifier
     #                                 collects its own first krum_thresh arrivals (krum.go:284-322)
     miner_cap: bool = True          # leader's block = first NUM_SAMPLES/2 approved arrivals (main.go:360)

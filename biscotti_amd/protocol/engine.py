@@ -482,8 +482,17 @@ class BiscottiEngine:
                         inboxes[v] = list(ib)
             row_of = {w: i for i, w in enumerate(local_workers)}
             spec = None
-            if self.gpu and cfg.secure_agg and local_workers:
+            cand = set()
+            if self.gpu and cfg.secure_agg:
+                # replicated on every rank: the rows (of all ranks) whose shares are computed up front
                 cand = self._block_candidates(plan, workers, inboxes)
+                cap = fsm.leader_cap_size()
+                if cfg.verification and cfg.spec_msm and cap > 0:
+                    # the block carries the first `cap` approved updates in leader arrival order, so the
+                    # speculative MSM covers a prefix of that order with margin for rejections
+                    k = min(len(cand), int(np.ceil(cfg.spec_margin * cap)) + 2)
+                    cand = set([w for w in fsm.leader_arrivals() if w in cand][:k])
+            if self.gpu and cfg.secure_agg and local_workers:
                 spec_workers = [w for w in local_workers if w in cand]
                 if spec_workers:
                     defer = cfg.verification and not cfg.spec_msm
@@ -493,7 +502,7 @@ class BiscottiEngine:
             # after Krum, so noise + Krum on the main stream do not queue behind them
             pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
-                    spec=spec)
+                    spec=spec, spec_cand=cand)
         # one rank, Multi-Krum: the noise and committee-Krum kernels (and, behind the selection, the
         # whole device-side aggregation) depend only on this head, so they can be queued now as well
         if (cfg.early_krum and self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.defense == "KRUM"
@@ -677,7 +686,13 @@ class BiscottiEngine:
                     acc_np = acc_t.numpy().astype(np.uint8)   # [len(vs), ni]
                     acc_row = {v: k for k, v in enumerate(vs)}
                     if box.get("sa") is not None:   # the rows the device aggregation kept
-                        box["sa"]["accepted"] = {w for w in workers if bool(node_t[xrow[w]])}
+                        kept = {w for w in workers if bool(node_t[xrow[w]])}
+                        # a block row outside the (replicated) speculative prefix was never computed:
+                        # the device aggregate is then incomplete and the host path tops it up
+                        if not kept <= head["spec_cand"]:
+                            kept = None
+                            self.stats["spec_misses"] = self.stats.get("spec_misses", 0) + 1
+                        box["sa"]["accepted"] = kept
                 else:
                     # RONI: each verifier judges with its own data, so only its rank can decide; the
                     # accept matrix [nv, ni] travels in one all_gather on several ranks
@@ -864,7 +879,9 @@ class BiscottiEngine:
         """Resident index tensors of one miner layout (a handful recur: the parts are a permutation of
         0..M-1): chunk-commitment columns, witness columns, the contributing miners' share columns and
         their x-points, uploaded once."""
-        key = (tuple(contributing), tuple(part[m] for m in contributing))
+        # the indices depend only on the sequence of parts (which miner holds which share slice), not
+        # on the miners' ids: M! layouts (6 for three miners) cover every round
+        key = tuple(part[m] for m in contributing)
         hit = self._agg_idx.get(key)
         if hit is None:
             spm, T, nch = self.pc.shares_per_miner, self.T, self.nchunks
@@ -873,10 +890,13 @@ class BiscottiEngine:
             wc = np.concatenate([(base[:, None] + spm * part[m] + np.arange(spm)[None, :]).reshape(-1)
                                  for m in contributing])
             assert wc.max() < nch * (T + 1) and ycols.max() < T
-            parts = [base + T, wc, ycols, ycols - 10]
+            wts = K.recovery_weights((ycols - 10).tolist(), self.cfg.poly_size)
+            parts = [base + T, wc, ycols, ycols - 10, np.asarray(wts["basis"])]
             idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
             offs = np.cumsum([0] + [len(x) for x in parts])
-            hit = ([idx[offs[i]:offs[i + 1]] for i in range(4)], (ycols - 10).tolist())
+            A_dev = h2d(wts["A"].reshape(-1), torch.int64, self.dev)
+            sl = [idx[offs[i]:offs[i + 1]] for i in range(5)]
+            hit = (sl[:4], (ycols - 10).tolist(), (wts, A_dev, sl[4]))
             if len(self._agg_idx) < 256:
                 self._agg_idx[key] = hit
         return hit
@@ -899,17 +919,27 @@ class BiscottiEngine:
         cfg, comm = self.cfg, self.comm
         T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
         audit = cfg.audit_aggregate
-        (ccols, wcols, ycols_t, xs_t), xs_list = self._agg_index(contributing, part)
+        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
         main = S.current() if self.gpu else None
         # ---- this rank's partial sums
+        single = comm.world == 1
         ys_part = torch.zeros((nch, T), dtype=torch.int64, device=self.dev)
+        ys_fused = mask_fused = None   # one rank, GPU: the share sums are fused into the recovery kernel
         cs_part = None
         if pts is not None and (not isinstance(rowsel, list) or rowsel):
             flat = pts.view(pts.shape[0], nch * (T + 1), pw)
             if self.gpu:
                 rows_t = None if not isinstance(rowsel, list) else h2d(rowsel, torch.int32, self.dev)
                 mask = rowsel if rows_t is None else None
-                if rows_t is None:
+                if single:
+                    ys_fused = ys
+                    if mask is not None:
+                        mask_fused = mask
+                    else:
+                        sel = np.zeros(ys.shape[0], np.int32)
+                        sel[np.asarray(rowsel)] = 1
+                        mask_fused = h2d(sel, torch.int32, self.dev)
+                elif rows_t is None:
                     ys_part = (ys * mask.view(-1, 1, 1)).sum(0)
                 else:
                     ys_part = ys.index_select(0, rows_t.long()).sum(0)
@@ -947,9 +977,14 @@ class BiscottiEngine:
         else:
             ys_tot = ys_part
             cs_tot = cs_part
-        agg = ys_tot.index_select(1, ycols_t.long() if not self.gpu else ycols_t).contiguous()   # [nch, npts]
-        W_new, coeffs, status = K.recover(agg, xs_t if self.gpu else xs_t.cpu(), cfg.poly_size, self.d, self.W,
-                                          10.0 ** cfg.precision)
+        if self.gpu:
+            src = ys_fused if ys_fused is not None else ys_tot.reshape(1, nch, T).contiguous()
+            W_new, coeffs, status, agg = K.recover_rows(src.contiguous(), mask_fused if ys_fused is not None else None,
+                                                        ycols_t, xs_t, wts, A_dev, basis_dev, cfg.poly_size, self.d,
+                                                        self.W, 10.0 ** cfg.precision)
+        else:
+            agg = ys_tot.index_select(1, ycols_t.long()).contiguous()   # [nch, npts]
+            W_new, coeffs, status = K.recover(agg, xs_t.cpu(), cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
         audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
         return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
                 "clock": clock, "now": now}

@@ -55,7 +55,8 @@ def _model(name: str, d_in: int, n_classes: int):
     from .models import zoo as Z
 
     return {"softmax": lambda: Z.SoftmaxModel(d_in, n_classes), "svm": lambda: Z.SVMModel(d_in, n_classes),
-            "mnist_cnn": Z.MNISTCNNModel, "lfw_cnn": lambda: Z.LFWCNNModel(n_classes),
+            "mnist_cnn": Z.MNISTCNNModel, "lfw_cnn": lambda: Z.LFWCNNModel(n_classes),   # the reference's head has 2 outputs; the
+            # synthetic LFW stand-in has 12 identities, so the head is sized to the data
             "cifar_cnn": Z.CIFARCNNModel}[name]()
 
 

@@ -110,6 +110,39 @@ def test_recover_exact(rt):
     np.testing.assert_array_equal(got3.cpu().numpy(), coeffs)
 
 
+@pytest.mark.parametrize("cols", [list(range(21)), list(range(0, 7)) + list(range(14, 21))])
+def test_recover_rows_fused_weights(cols):
+    """k_recover_w (share sums fused, precomputed exact weights) against the 128-bit Newton kernel's
+    contract: exact coefficients for consistent shares, status 0 for a tampered share, masked rows
+    left out of the sums."""
+    rng = np.random.default_rng(1)
+    R, nch, poly, T = 6, 785, 10, 21
+    per = rng.integers(-3 * 10**6, 3 * 10**6, size=(R, nch, poly))
+    xs_all = np.arange(-10, 11)
+    pw = xs_all[None, :] ** np.arange(poly)[:, None]             # [poly, 21]
+    ys = np.einsum("rkj,jx->rkx", per, pw).astype(np.int64)       # shares of every row
+    mask = np.array([1, 0, 1, 1, 0, 1], np.int32)
+    tot = per[mask.astype(bool)].sum(0)                           # [nch, poly]
+    xs = xs_all[cols]
+    w = K.recovery_weights(xs.tolist(), poly)
+    A = torch.from_numpy(w["A"].reshape(-1)).cuda()
+    basis = torch.tensor(w["basis"], dtype=torch.int32).cuda()
+    ys_t = torch.from_numpy(ys).cuda()
+    W = torch.zeros(7850, dtype=torch.float64).cuda()
+    ycols = torch.tensor(cols, dtype=torch.int32).cuda()
+    xs_t = torch.from_numpy(xs.astype(np.int32)).cuda()
+    Wn, got, st, agg = K.recover_rows(ys_t, torch.from_numpy(mask).cuda(), ycols, xs_t, w, A, basis, poly, 7850, W)
+    assert st.cpu().all()
+    np.testing.assert_array_equal(got.cpu().numpy(), tot)
+    np.testing.assert_array_equal(agg.cpu().numpy(), ys[mask.astype(bool)].sum(0)[:, cols])
+    np.testing.assert_allclose(Wn.cpu().numpy(), tot.reshape(-1)[:7850] / 1e4)
+    bad = ys.copy()
+    bad[2, 7, cols[3]] += 1
+    _, _, st2, _ = K.recover_rows(torch.from_numpy(bad).cuda(), torch.from_numpy(mask).cuda(), ycols, xs_t, w, A,
+                                  basis, poly, 7850, W)
+    assert st2.cpu()[7] == 0 and st2.cpu().sum() == nch - 1
+
+
 @pytest.mark.parametrize("early,spec_msm", [(False, True), (True, True), (False, False)])
 def test_engine_rounds_on_gpu(early, spec_msm):
     """Whole GPU round pipeline (speculative shares on the CU-masked stream, async commitments,

@@ -66,6 +66,24 @@ def test_sandbox_models_train_on_cpu():
         assert len(r["history"]) == 3
 
 
+def test_sandbox_cnn_architectures_match_reference():
+    """Layer shapes and parameter counts of lfw_cnn_model.py / cifar_cnn_model.py / mnist_cnn_model.py."""
+    import torch
+
+    from biscotti_amd.models import zoo as Z
+
+    lfw = Z.LFWCNNModel()
+    assert [tuple(p.shape) for p in lfw.parameters()] == [(18, 3, 3, 3), (18,), (36, 18, 3, 3), (36,), (2, 5940), (2,)]
+    assert sum(p.numel() for p in lfw.parameters()) == 18254          # datasets.get_num_params('lfw')
+    assert lfw(torch.zeros(2, 3 * 62 * 47)).shape == (2, 2)
+    cifar = Z.CIFARCNNModel()
+    assert [tuple(p.shape) for p in cifar.parameters()] == [(20, 3, 3, 3), (20,), (10, 25920), (10,)]
+    assert sum(p.numel() for p in cifar.parameters()) == 540 + 20 + 259200 + 10
+    assert cifar(torch.zeros(2, 3 * 32 * 32)).shape == (2, 10)
+    mnist = Z.MNISTCNNModel()
+    assert mnist(torch.zeros(2, 784)).shape == (2, 10)
+
+
 def test_native_selftest_under_asan_ubsan():
     """Host runtime under AddressSanitizer + UBSan, 6 threads (race/sanitizer coverage)."""
     r = subprocess.run([sys.executable, "-m", "biscotti_amd._build", "--sanitize"], cwd=ROOT, capture_output=True,
