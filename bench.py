@@ -62,6 +62,9 @@ PRESETS = {
     "credit50_fed50": ({"fedsys": True, "num_nodes": 50, "dataset": "creditcard", "poisoning": 0.5,
                         "perc_samples": 35}, None, 1 - 0.6310, {}, "nsdi-eval/credit/fed_50p"),
     "churn10": ({"churn": 0.1}, None, None, {}, "BASELINE.json config 5 (reference churn runs: 25-31 s/round)"),
+    # the long-parameter-vector ledger: LFW maleness softmax, d = 17486 (no reference number:
+    # the reference's lfw pipeline is inconsistent, see data.dataset_dims)
+    "lfw100": ({"dataset": "lfw"}, None, None, {}, "honest.go:211 'mnist/lfw for pytorch' (unpinned)"),
     "scale40": ({"num_nodes": 40}, 23.87, None, {}, "nsdi-eval/increments/results.log:2"),
     "scale60": ({"num_nodes": 60}, 34.05, None, {}, "nsdi-eval/increments/results.log:3"),
     "scale80": ({"num_nodes": 80}, 48.07, None, {}, "nsdi-eval/increments/results.log:4"),
@@ -227,10 +230,12 @@ def main() -> int:
             "baseline_source": ref_src,
             "rounds_total": eng.rounds_done if not fedsys else eng.iteration,
             "dtype": "fp32 model / fp64 ledger / exact BN256",
-            "data": ("synthetic: MNIST-shaped digits from sklearn's 8x8 real digits, augmented; zero-init model"
-                     if cfg.dataset == "mnist" else "creditcard.csv shipped with the reference"),
-            "config": {"name": a.config, "model": ("softmax regression 784x10 (7850 params, SoftmaxModel)"
-                                                   if cfg.dataset == "mnist" else "logistic regression (25)"),
+            "data": {"mnist": "synthetic: MNIST-shaped digits from sklearn's 8x8 real digits, augmented; zero-init model",
+                     "lfw": "synthetic: class-conditional 62x47x3 faces, maleness labels; zero-init model"}
+                    .get(cfg.dataset, "creditcard.csv shipped with the reference"),
+            "config": {"name": a.config, "model": {"mnist": "softmax regression 784x10 (7850 params, SoftmaxModel)",
+                                                   "lfw": "softmax regression 8742x2 (17486 params, SoftmaxModel)"}
+                       .get(cfg.dataset, "logistic regression (25)"),
                        "peers": cfg.num_nodes, "global_batch": cfg.num_nodes * cfg.batch_size, "seq_len": 1,
                        "parallelism": f"dp{comm.world} (virtual peers: {math.ceil(cfg.num_nodes / comm.world)}/GPU)",
                        "verifiers": cfg.num_verifiers, "aggregators": cfg.num_miners, "noisers": cfg.num_noisers,

@@ -54,7 +54,7 @@ __device__ __forceinline__ long long quantize(float v, double scale) {
 }  // namespace
 
 // =====================================================================================
-// K1: softmax regression local step.  D_IN <= 1024, D_OUT <= 16, B <= 16.
+// K1: softmax regression local step.  Any D_IN (K-tiled through LDS), D_OUT <= 16, B <= 16.
 // X: [Ntot, D_IN] fp32 (standardised pixels), y: [Ntot] int32.  Peer p trains on rows
 // [off[p], off[p] + ntrain[p]).  W: [D_OUT*D_IN + D_OUT] fp64 global model (W row-major, b).
 // Outputs: delta fp32 [P, nparam], qdelta int64 [P, nparam], loss fp32 [P].
@@ -95,25 +95,35 @@ extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
   }
   __syncthreads();
   const int Bq = min(B, n);
-  // 2. stage transformed rows (x - 0.5) / 0.5 (torchvision Normalize(0.5, 0.5)); zero padding
-  for (int i = tid; i < 16 * D_IN; i += SM_THREADS) {
-    const int s = i / D_IN, k = i % D_IN;
-    float v = 0.f;
-    if (s < Bq) v = (X[(off[p] + bidx[s]) * (long long)D_IN + k] - 0.5f) * 2.0f;
-    xs[s * SM_MAXK + k] = v;
-  }
-  __syncthreads();
-  // 3. logits via f32 MFMA 16x16x4: A[s][k] = xs, B[k][c] = W[c][k]; K split over the 4 waves
+  // 2-3. logits via f32 MFMA 16x16x4: A[s][k] = xs, B[k][c] = W[c][k].  The minibatch rows are staged
+  // through LDS in K tiles of SM_MAXK (one tile for MNIST's 784 features, nine for LFW's 8742);
+  // within a tile the 4 waves split K, each accumulating its share across tiles in registers.
+  const int ktiles = (D_IN + SM_MAXK - 1) / SM_MAXK;
+  auto stage = [&](int kt) {  // (x - 0.5) / 0.5 (torchvision Normalize(0.5, 0.5)); zero padding
+    const int k0 = kt * SM_MAXK, kw = min(SM_MAXK, D_IN - k0);
+    for (int i = tid; i < 16 * kw; i += SM_THREADS) {
+      const int s = i / kw, k = i % kw;
+      float v = 0.f;
+      if (s < Bq) v = (X[(off[p] + bidx[s]) * (long long)D_IN + k0 + k] - 0.5f) * 2.0f;
+      xs[s * SM_MAXK + k] = v;
+    }
+  };
   {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const int ksteps = (D_IN + 3) / 4;
-    const int per = (ksteps + 3) / 4;
     const int i = lane & 15, kk = lane >> 4;
-    for (int st = wid * per; st < min(ksteps, (wid + 1) * per); ++st) {
-      const int k = st * 4 + kk;
-      const float a = (k < D_IN) ? xs[i * SM_MAXK + k] : 0.f;
-      const float b = (k < D_IN && i < D_OUT) ? (float)W[i * D_IN + k] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    for (int kt = 0; kt < ktiles; ++kt) {
+      const int k0 = kt * SM_MAXK, kw = min(SM_MAXK, D_IN - k0);
+      if (kt > 0) __syncthreads();  // the previous tile has been consumed
+      stage(kt);
+      __syncthreads();
+      const int ksteps = (kw + 3) / 4;
+      const int per = (ksteps + 3) / 4;
+      for (int st = wid * per; st < min(ksteps, (wid + 1) * per); ++st) {
+        const int k = st * 4 + kk;
+        const float av = (k < kw) ? xs[i * SM_MAXK + k] : 0.f;
+        const float bv = (k < kw && i < D_OUT) ? (float)W[i * D_IN + k0 + k] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wid][(lane >> 4) * 4 + r][lane & 15] = acc[r];
@@ -145,28 +155,36 @@ extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
     for (int s = 0; s < Bq; ++s) l += red[0][s][0];
     loss[p] = l / (float)max(Bq, 1);
   }
-  // 5. dW[c][k] = sum_s G[s][c] xs[s][k] via f32 MFMA (M = classes, N = k tiles, K = samples)
+  // 5. dW[c][k] = sum_s G[s][c] xs[s][k] via f32 MFMA (M = classes, N = k tiles, K = samples); with
+  // several K tiles the rows are staged again (the last tile is still resident: it goes first)
   float* dst = delta + (size_t)p * nparam;
   float sq = 0.f;
-  {
-    const int ntiles = (D_IN + 15) / 16;
+  for (int q = 0; q < ktiles; ++q) {
+    const int kt = (ktiles - 1 + q) % ktiles;
+    const int k0 = kt * SM_MAXK, kw = min(SM_MAXK, D_IN - k0);
+    if (q > 0) {
+      __syncthreads();
+      stage(kt);
+      __syncthreads();
+    }
+    const int ntiles = (kw + 15) / 16;
     const int col = lane & 15, kk = lane >> 4;
     for (int t = wid; t < ntiles; t += 4) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int s = ks * 4 + kk;
-        const float a = G[s][col];  // A[c = col][s]
+        const float av = G[s][col];  // A[c = col][s]
         const int k = t * 16 + col;
-        const float b = (k < D_IN) ? xs[s * SM_MAXK + k] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        const float bv = (k < kw) ? xs[s * SM_MAXK + k] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
       }
       const int k = t * 16 + col;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = (lane >> 4) * 4 + r;
-        if (c < D_OUT && k < D_IN) {
-          dst[c * D_IN + k] = acc[r];
+        if (c < D_OUT && k < kw) {
+          dst[c * D_IN + k0 + k] = acc[r];
           sq += acc[r] * acc[r];
         }
       }
@@ -444,8 +462,12 @@ __device__ __forceinline__ double gram_at(const double* gram, int T, int a, int 
 }
 }  // namespace
 
+// rows [0, U1) of the Gram's operand come from X (row stride D), rows [U1, U) from X2 (row stride
+// stride2): the committee Krum's noise-aware form stacks the workers' deltas over the noisers'
+// pre-sampled vectors of this iteration (a strided view of the resident noise table)
 extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, int U, int D, int kchunk, int T,
-                                                              double* part, double* gram, unsigned int* count) {
+                                                              double* part, double* gram, unsigned int* count,
+                                                              const float* X2, int U1, long long stride2) {
   __shared__ double red[4][256];
   __shared__ unsigned int last;
   const int pair = blockIdx.x, sp = blockIdx.y;
@@ -460,8 +482,9 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = ti * 16 + (lane & 15), j = tj * 16 + (lane & 15), kk = lane >> 4;
   const bool va = i < U, vb = j < U;
-  const float* xa = X + (size_t)(va ? i : 0) * D;
-  const float* xb = X + (size_t)(vb ? j : 0) * D;
+  const int ia = va ? i : 0, jb = vb ? j : 0;
+  const float* xa = ia < U1 ? X + (size_t)ia * D : X2 + (size_t)(ia - U1) * stride2;
+  const float* xb = jb < U1 ? X + (size_t)jb * D : X2 + (size_t)(jb - U1) * stride2;
   // this block's K range, split into 4 wave ranges that are multiples of 4
   const int k0b = sp * kchunk, k1b = min(D, k0b + kchunk);
   const int per = (((k1b - k0b) + 15) / 16) * 4;
@@ -525,6 +548,62 @@ extern "C" __global__ void __launch_bounds__(256) k_krum_rows(const double* gram
     const double gab = gram_at(gram, T, a, b);
     const double gbb = gram_at(gram, T, b, b);
     row[t] = gdiag_a + gbb - 2.0 * gab;
+  }
+  __syncthreads();
+  if (t < n) {
+    const double val = row[t];
+    int rank = 0;
+    for (int k2 = 0; k2 < n; ++k2) {
+      const double u = row[k2];
+      rank += (u < val) || (u == val && k2 < t);
+    }
+    kept[t] = (rank >= 1 && rank < groupsize - 1) ? val : 0.0;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s += kept[j];
+    scores[(size_t)v * n + i] = s;
+  }
+}
+
+// KC2, noise-aware form: the candidate rows are x_a = delta_a + (1/nn) sum_s sc[a][s] t_{nz[a][s]}
+// (the noisers' pre-sampled vectors, main.go:1592-1660), and the Gram was taken over the stacked
+// [deltas; noise vectors] rows, so <x_a, x_b> expands into (1 + nn)^2 Gram entries -- the
+// d-dimensional work (the Gram) runs before the noisers are known (they come from the workers' VRF
+// outputs on the host); only this O(n^2 nn^2) assembly waits for them.
+namespace {
+__device__ __forceinline__ double xx_dot(const double* gram, int T, int U1, const int* nz, const float* sc, int nn,
+                                         int a, int b) {
+  double v = gram_at(gram, T, a, b);
+  const double inv = 1.0 / (double)nn;
+  for (int t = 0; t < nn; ++t) {
+    v += inv * (double)sc[b * nn + t] * gram_at(gram, T, a, U1 + nz[b * nn + t]);
+    v += inv * (double)sc[a * nn + t] * gram_at(gram, T, U1 + nz[a * nn + t], b);
+  }
+  for (int s2 = 0; s2 < nn; ++s2)
+    for (int t = 0; t < nn; ++t)
+      v += inv * inv * (double)sc[a * nn + s2] * (double)sc[b * nn + t] *
+           gram_at(gram, T, U1 + nz[a * nn + s2], U1 + nz[b * nn + t]);
+  return v;
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise(const double* gram, int T, int U1,
+                                                                   const int* nz, const float* sc, int nn,
+                                                                   const int* inbox, int n, int groupsize,
+                                                                   double* scores) {
+  __shared__ double row[256];
+  __shared__ double kept[256];
+  __shared__ double xaa;
+  const int i = blockIdx.x, v = blockIdx.y, t = threadIdx.x;
+  const int* box = inbox + (size_t)v * n;
+  const int a = box[i];
+  if (t == 0) xaa = xx_dot(gram, T, U1, nz, sc, nn, a, a);
+  __syncthreads();
+  if (t < n) {
+    const int b = box[t];
+    row[t] = xaa + xx_dot(gram, T, U1, nz, sc, nn, b, b) - 2.0 * xx_dot(gram, T, U1, nz, sc, nn, a, b);
   }
   __syncthreads();
   if (t < n) {
@@ -856,7 +935,7 @@ extern "C" int bsc_softmax_step(const float* X, const int* y, const long long* o
                                 const int* pid, const double* W, int D_IN, int D_OUT, int B, int P, unsigned long long seed,
                                 int iteration, float max_norm, double qscale, float* delta, long long* qdelta,
                                 float* loss, void* stream) {
-  if (D_IN > SM_MAXK || D_OUT > 16 || B > 16) return -1;
+  if (D_IN <= 0 || D_OUT > 16 || B > 16) return -1;
   if (P <= 0) return 0;
   hipLaunchKernelGGL(k_softmax_step, dim3(P), dim3(SM_THREADS), 0, (hipStream_t)stream, X, y, off, ntrain, pid, W, D_IN,
                      D_OUT, B, P, seed, iteration, max_norm, qscale, delta, qdelta, loss);
@@ -911,9 +990,42 @@ extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, cons
   const int nsplit = (D + kchunk - 1) / kchunk;
   hipStream_t s = (hipStream_t)stream;
   // count: npairs zeroed counters (re-armed by the kernel itself)
-  hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part, gram, count);
+  hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part, gram, count,
+                     (const float*)nullptr, U, 0ll);
   hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, gram, T, inbox, n, groupsize, scores);
   hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U, need, lead_rank, cap,
+                     acc, node);
+  return (int)hipGetLastError();
+}
+
+// Noise-aware committee Krum, phase 1 (before the noisers are known): Gram of the stacked rows
+// [X (U1 rows, stride D); X2 (U2 rows, stride stride2)] -> gram [npairs][256].
+extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
+                                double* part, double* gram, unsigned int* count, void* stream) {
+  const int U = U1 + U2;
+  if (U <= 0) return 0;
+  if (U > 1024 || kchunk <= 0) return -1;
+  const int T = (U + 15) / 16;
+  const int npairs = T * (T + 1) / 2;
+  const int nsplit = (D + kchunk - 1) / kchunk;
+  hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, (hipStream_t)stream, X, U, D, kchunk, T, part,
+                     gram, count, X2, U1, stride2);
+  return (int)hipGetLastError();
+}
+
+// phase 2 (once the noisers are known): scores of every verifier's inbox from the expanded Gram,
+// then the vote.  nz/sc: [U1][nn] noiser ids (rows U1 + id of the Gram) and scales.
+extern "C" int bsc_krum_committee_noise(const double* gram, int U1, int U, const int* nz, const float* sc, int nn,
+                                        const int* inbox, int V, int n, int groupsize, int n_accept, int need,
+                                        const int* lead_rank, int cap, double* scores, int* acc, int* node,
+                                        void* stream) {
+  if (U1 <= 0 || V <= 0 || n <= 0) return 0;
+  if (U > 1024 || U1 > 1024 || n > 256 || V > 64 || n > U1 || nn <= 0 || nn > 16) return -1;
+  const int T = (U + 15) / 16;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_krum_rows_noise, dim3(n, V), dim3(256), 0, s, gram, T, U1, nz, sc, nn, inbox, n, groupsize,
+                     scores);
+  hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U1, need, lead_rank, cap,
                      acc, node);
   return (int)hipGetLastError();
 }

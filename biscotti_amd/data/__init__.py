@@ -203,6 +203,43 @@ def synthetic_images(n: int, shape: tuple, n_classes: int, seed: int = 0, noise:
     return X.reshape(n, -1).numpy().astype(np.float32), y.numpy()
 
 
+# ------------------------------------------------------------------------------------ LFW
+LFW_SHAPE = (3, 62, 47)    # lfw_dataset.py: "batch shape for input x is (62, 47, 3)"
+LFW_CLASSES = 2            # parse_lfw_maleness.py labels maleness (1 male / 0 female)
+
+
+def lfw_federation(num_peers: int, seed: int = 1234, n_total: int = 5985) -> MnistFederation:
+    """LFW-maleness-shaped federation for the ledger path (the reference's lfw pipeline,
+    ML/Pytorch/data/lfw/parse_lfw_maleness.py + lfw_dataset.py).  The faces come from
+    sklearn.fetch_lfw_people, which needs the network, so the images are synthetic class-conditional
+    62x47x3 faces (synthetic_images) in [0, 1]; 75% train split into per-peer shards, the rest is
+    the test set.  The "attack" set is the test faces of class 1 (a 1 -> 0 label flip is the
+    binary analogue of the reference's 1 -> 7 poisoning); the poisoners' data is every class-1 train
+    face relabelled 0."""
+    X, y = synthetic_images(n_total, LFW_SHAPE, LFW_CLASSES, seed=seed, noise=0.9)
+    X = np.clip(0.5 + 0.25 * X, 0.0, 1.0).astype(np.float32)
+    cut = int(n_total * 0.75)
+    fed = MnistFederation(source="synthetic-lfw")
+    Xtr, ytr, Xte, yte = X[:cut], y[:cut], X[cut:], y[cut:]
+    rows = max(1, Xtr.shape[0] // num_peers)
+    for i in range(num_peers):
+        lo = (i * rows) % max(1, Xtr.shape[0] - rows + 1)
+        fed.shards_X.append(Xtr[lo:lo + rows])
+        fed.shards_y.append(ytr[lo:lo + rows].astype(np.int64))
+    fed.test_X, fed.test_y = Xte, yte.astype(np.int64)
+    ones = yte == 1
+    fed.attack_X, fed.attack_y = Xte[ones], yte[ones].astype(np.int64)
+    tr1 = ytr == 1
+    fed.bad_X, fed.bad_y = Xtr[tr1], np.zeros(int(tr1.sum()), np.int64)
+    return fed
+
+
 def dataset_dims(name: str) -> tuple[int, int, int]:
-    """(num_params, num_features, num_classes) -- ML/Pytorch/datasets.py:22-52."""
-    return {"mnist": (7850, 784, 10), "lfw": (18254, 8742, 12), "creditcard": (25, 25, 2)}[name]
+    """(num_params, num_features, num_classes) of the Biscotti model, SoftmaxModel(features, classes)
+    (client_obj.py:20-29 builds a SoftmaxModel for every torch dataset).  mnist 784x10 = 7850 as in
+    ML/Pytorch/datasets.py:22-52.  lfw: 8742 features x 2 maleness classes = 17486 -- the reference's
+    own lfw numbers are inconsistent (get_num_params 18254 is its LFW CNN's count, get_num_classes 12
+    does not match the maleness labels its partitioner writes), so the ledger runs the softmax on the
+    labels the data actually has."""
+    return {"mnist": (7850, 784, 10), "lfw": (8742 * LFW_CLASSES + LFW_CLASSES, 8742, LFW_CLASSES),
+            "creditcard": (25, 25, 2)}[name]

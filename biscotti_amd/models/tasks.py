@@ -22,7 +22,10 @@ class SoftmaxTask:
     d_in, d_out = 784, 10
 
     def __init__(self, peers: range, num_peers: int, device, seed: int, poisoned: set[int] | None = None,
-                 batch_size: int = 10, data_dir: str | None = None, federation: D.MnistFederation | None = None):
+                 batch_size: int = 10, data_dir: str | None = None, federation: D.MnistFederation | None = None,
+                 dims: tuple | None = None):
+        if dims is not None:
+            self.d_in, self.d_out = dims
         fed = federation or D.mnist_federation(num_peers, seed=seed, data_dir=data_dir)
         self.source = fed.source
         self.peers = list(peers)
@@ -53,6 +56,7 @@ class SoftmaxTask:
         self.eval_y = torch.cat([self.test_y, self.att_y]).contiguous()
         self.eval_split = int(self.test_X.shape[0])
         self._local_index = {p: i for i, p in enumerate(self.peers)}
+        self._sel_cache: dict = {}
 
     def noise_sigma(self, epsilon: float, delta: float = 1e-5) -> float:
         """client_obj.py:61: sigma = sqrt(2 ln(1.25/delta)) / epsilon (0 when epsilon == 0)."""
@@ -67,10 +71,15 @@ class SoftmaxTask:
         if not peers:
             z = torch.empty((0, self.nparam), device=self.device)
             return z.float(), z.long()
-        sel = h2d([self._local_index[p] for p in peers], torch.long, self.device)
-        pid = h2d(peers, torch.int32, self.device)
-        delta, qdelta, loss = K.softmax_step(self.X, self.y, self.off[sel].contiguous(),
-                                             self.ntrain[sel].contiguous(), pid, W, self.d_in, self.d_out,
+        key = tuple(peers)
+        hit = self._sel_cache.get(key)
+        if hit is None:   # per peer set (it changes only with churn): resident, uploaded once
+            sel = h2d([self._local_index[p] for p in peers], torch.long, self.device)
+            hit = (self.off[sel].contiguous(), self.ntrain[sel].contiguous(), h2d(peers, torch.int32, self.device))
+            if len(self._sel_cache) < 64:
+                self._sel_cache[key] = hit
+        off, ntr, pid = hit
+        delta, qdelta, loss = K.softmax_step(self.X, self.y, off, ntr, pid, W, self.d_in, self.d_out,
                                              self.batch, self.seed, iteration, 100.0, 1e4)
         self.last_loss = loss
         return delta, qdelta
@@ -179,6 +188,13 @@ def make_task(dataset: str, peers: range, num_peers: int, device, seed: int, **k
         kw.pop("epsilon", None)
         kw.pop("colluders", None)
         return SoftmaxTask(peers, num_peers, device, seed, **kw)
+    if dataset == "lfw":
+        kw.pop("epsilon", None)
+        kw.pop("colluders", None)
+        kw.pop("data_dir", None)
+        _, d_in, d_out = D.dataset_dims("lfw")
+        return SoftmaxTask(peers, num_peers, device, seed, federation=D.lfw_federation(num_peers, seed=seed),
+                           dims=(d_in, d_out), **kw)
     if dataset == "creditcard":
         kw.pop("data_dir", None)
         kw.pop("federation", None)

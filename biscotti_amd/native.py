@@ -37,7 +37,9 @@ def rt():
 
 
 def hip_library_path() -> Path:
-    return _PKG / "libbiscotti_hip.so"
+    # BISCOTTI_HIP_LIB: an alternative build of the same kernels (A/B experiments)
+    alt = os.environ.get("BISCOTTI_HIP_LIB")
+    return Path(alt) if alt else _PKG / "libbiscotti_hip.so"
 
 
 def hip():

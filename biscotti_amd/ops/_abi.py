@@ -34,6 +34,8 @@ SIGNATURES = {
     "bsc_dp_noise": [P, I, I, P, I, P, U64, I, P, P],
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],
     "bsc_krum_committee": [P, I, I, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, P],
+    "bsc_gram_stacked": [P, I, P, I, L, I, I, P, P, P, P],
+    "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_noise_table": [I, I, U64, P, P],
     "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P, P],

@@ -357,6 +357,61 @@ def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lea
     return result
 
 
+def gram_stacked_async(X, T_rows, kchunk: int = 512) -> dict:
+    """Noise-aware committee Krum, phase 1: f64 Gram of the stacked rows [X; T_rows] (GPU).
+
+    X fp32 [U1, d] (the workers' deltas, contiguous); T_rows fp32 [U2, d] with contiguous rows (a
+    strided view of the resident noise table at this iteration).  Runs before the noisers are known.
+    Returns the handle krum_committee_noise_async consumes."""
+    U1, D = X.shape
+    U2 = T_rows.shape[0]
+    assert X.is_contiguous() and T_rows.stride(1) == 1 and T_rows.shape[1] == D
+    assert X.dtype == torch.float32 and T_rows.dtype == torch.float32
+    U = U1 + U2
+    assert 0 < U <= 1024, "committee Krum size limits"
+    Tt = (U + 15) // 16
+    npairs = Tt * (Tt + 1) // 2
+    nsplit = (D + kchunk - 1) // kchunk
+    dev = X.device
+    part = torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev)
+    gram = torch.empty((npairs, 256), dtype=torch.float64, device=dev)
+    _check(hip().bsc_gram_stacked(_p(X), U1, T_rows.data_ptr(), U2, T_rows.stride(0), D, kchunk, _p(part), _p(gram),
+                                  _p(_tile_counters(dev, npairs)), _stream()), "gram_stacked")
+    return {"gram": gram, "U1": U1, "U": U, "keep": (X, T_rows, part)}
+
+
+def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accept: int, need: int, lead_rank,
+                               cap: int, on_accept=None):
+    """Noise-aware committee Krum, phase 2: the noised rows x_a = delta_a + mean_s sc[a, s] t_{nz[a, s]}
+    are never materialised -- their inner products are assembled from the phase-1 Gram.  nz int32 /
+    sc fp32 [U1, nn] (nz indexes the stacked noise rows); the rest as krum_committee_async."""
+    U1, U = pre["U1"], pre["U"]
+    V, n = inbox.shape
+    nn = nz.shape[1]
+    assert inbox.dtype == torch.int32 and lead_rank.dtype == torch.int32 and lead_rank.numel() == U1
+    assert nz.dtype == torch.int32 and sc.dtype == torch.float32 and tuple(nz.shape) == (U1, nn)
+    assert 0 < n <= 256 and 0 < V <= 64 and n <= U1 and 0 < nn <= 16
+    dev = pre["gram"].device
+    scores = torch.empty((V, n), dtype=torch.float64, device=dev)
+    out = torch.empty((V * n + U1,), dtype=torch.int32, device=dev)
+    acc, node = out[: V * n], out[V * n:]
+    _check(hip().bsc_krum_committee_noise(_p(pre["gram"]), U1, U, _p(nz.contiguous()), _p(sc.contiguous()), nn,
+                                          _p(inbox.contiguous()), V, n, groupsize, n_accept, need,
+                                          _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _stream()),
+           "krum_committee_noise")
+    host = torch.empty(out.shape, dtype=torch.int32, pin_memory=True)
+    host.copy_(out, non_blocking=True)
+    ev = S.record()
+    if on_accept is not None:
+        on_accept(node)
+
+    def result():
+        ev.synchronize()
+        h = host.bool()
+        return h[: V * n].view(V, n), h[V * n:]
+    return result
+
+
 # ---------------------------------------------------------------------------- K2 evaluation
 def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
     """Error rates of W on rows [0, split) and [split, N) of X from ONE kernel launch and one

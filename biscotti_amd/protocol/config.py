@@ -74,6 +74,8 @@ class RunConfig:
     miner_cap: bool = True          # leader's block = first NUM_SAMPLES/2 approved arrivals (main.go:360)
     noise_independent: bool = False  # ablation: each worker draws private noise instead of its noisers'
     #                                  shared pre-sampled vectors (client_obj.py:97-98); not the reference
+    krum_pregram: bool = True       # one rank, table noise: Krum's Gram over [deltas; noise vectors] runs
+    #                                 before the VRF outputs arrive; only an O(n^2) assembly waits for them
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
     #                                 (shortens the GPU chain; costs host time before the previous round ends)
 

@@ -195,9 +195,17 @@ class DeviceCrypto:
         stream = stream or main
         S.wait(stream, main)
         with S.use(stream):
-            rows = torch.arange(n, dtype=torch.int32, device=qdelta.device)
+            rows = self._arange(n, qdelta.device)
             jac = self.eng.commit_rows(qdelta.contiguous(), rows, check_rows=False)
-            host = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
+            # pinned landing buffers are reused round to round (two in flight: the round head is
+            # opened while the previous round's marshals may still be read)
+            self._pin_i = (getattr(self, "_pin_i", 0) + 1) % 2
+            key = (self._pin_i, tuple(jac.shape))
+            host = self._pins.get(key) if hasattr(self, "_pins") else None
+            if host is None:
+                if not hasattr(self, "_pins"):
+                    self._pins = {}
+                host = self._pins[key] = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
             host.copy_(jac, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
@@ -208,6 +216,11 @@ class DeviceCrypto:
 
     def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
         return self.commitments_async(qdelta).result()
+
+    def _arange(self, n: int, device) -> torch.Tensor:
+        if not hasattr(self, "_ar") or self._ar.numel() < n:
+            self._ar = torch.arange(max(n, 256), dtype=torch.int32, device=device)
+        return self._ar[:n]
 
     def shares(self, qdelta: torch.Tensor):
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
@@ -446,25 +459,16 @@ class BiscottiEngine:
         It depends only on the latest block, so it is opened as soon as that block is committed
         (overlapping the previous round's evaluation and logging) and consumed by run_round."""
         cfg, R, fsm = self.cfg, self.R, self.fsm
-        live = self._live_mask()
-        plan = fsm.begin_round(live)
+        with self.timer.phase("head.plan"):
+            live = self._live_mask()
+            plan = fsm.begin_round(live)
         head = {"live": live, "plan": plan}
         if plan.done:
             return head
         latest_hash = fsm.chain.latest().hash
         workers = [w for w in plan.workers if live[w]]
         local_workers = [w for w in workers if w in self.local]
-        # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  The host
-        # proofs run on native threads while the GPU does the local step and the commitments; the
-        # noise phase joins them.
-        seeds = [self.vrf_noise_seed[w] for w in local_workers]
-        fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads) if seeds else None
-        fut_roles = None
-        if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
-            fut_roles = R.vrf_prove_batch_async([self.vrf_roles_seed[p] for p in self.local if live[p]],
-                                                latest_hash, cfg.roles_vrf_threads, fut_noise)
-        head.update(workers=workers, local_workers=local_workers, stake=dict(fsm.stake), fut_noise=fut_noise,
-                    fut_roles=fut_roles)
+        head.update(workers=workers, local_workers=local_workers, stake=dict(fsm.stake))
         # the local step, the commitments and the speculative shares depend only on the new global
         # model too: queue them now, behind nothing but the block that produced it
         tm, it = self.timer, plan.iteration
@@ -501,19 +505,43 @@ class BiscottiEngine:
             # full-vector commitments on the background stream: their first consumer is the signing
             # after Krum, so noise + Krum on the main stream do not queue behind them
             pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
+        # one rank, Multi-Krum over table noise: the d-dimensional part of the committee's Krum (the
+        # Gram of the deltas stacked over the noisers' pre-sampled vectors of this iteration) depends
+        # only on this head, so it runs now, while the host computes the workers' VRF outputs; after
+        # the noisers are known only an O(n^2) assembly remains (ml.hip k_krum_rows_noise)
+        krum_pre = None
+        if (self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.verification and cfg.defense == "KRUM"
+                and inboxes and local_workers and cfg.noising and self.sigma > 0 and self.noise_tbl is not None
+                and not cfg.noise_independent and cfg.krum_pregram):
+            with tm.phase("verify.pregram"):
+                krum_pre = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
-                    spec=spec, spec_cand=cand)
+                    spec=spec, spec_cand=cand, krum_pre=krum_pre)
+        # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  The proofs run
+        # on native threads while the GPU works through the head queued above (the round's long
+        # kernels are launched first: their start, not the VRF's, bounds the round); the noise phase
+        # joins the outputs.
+        with self.timer.phase("head.vrf_submit"):
+            seeds = [self.vrf_noise_seed[w] for w in local_workers]
+            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads) if seeds else None
+            fut_roles = None
+            if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
+                fut_roles = R.vrf_prove_batch_async([self.vrf_roles_seed[p] for p in self.local if live[p]],
+                                                    latest_hash, cfg.roles_vrf_threads, fut_noise)
+        head.update(fut_noise=fut_noise, fut_roles=fut_roles)
         # one rank, Multi-Krum: the noise and committee-Krum kernels (and, behind the selection, the
         # whole device-side aggregation) depend only on this head, so they can be queued now as well
         if (cfg.early_krum and self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.defense == "KRUM"
                 and inboxes and spec is not None and cfg.noising and self.sigma > 0 and fut_noise is not None):
+            # (queued last: it waits for the VRF outputs on the host)
             with tm.phase("vrf_join"):
                 noisers = self._select_noisers(fut_noise, head["stake"], local_workers)
             with tm.phase("noise"):
-                noised = self._noise(delta, noisers, local_workers, it)
+                noised = None if krum_pre is not None else self._noise(delta, noisers, local_workers, it)
             with tm.phase("verify.launch"):
                 box: dict = {}
-                wait = self._launch_krum(noised, row_of, plan, live, inboxes, spec, box)
+                wait = self._launch_krum(noised, row_of, plan, live, inboxes, spec, box,
+                                         pre=krum_pre, noisers=noisers, local_workers=local_workers)
             head["early"] = {"noisers": noisers, "krum": wait, "box": box, "noised": noised}
         return head
 
@@ -557,15 +585,16 @@ class BiscottiEngine:
         nz = h2d(ids, torch.int32, self.dev)
         return K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl)
 
-    def _launch_krum(self, X, xrow, plan, live, inboxes, spec, box):
+    def _launch_krum(self, X, xrow, plan, live, inboxes, spec, box, pre=None, noisers=None, local_workers=None):
         """Queue the committee's Multi-Krum (one Gram over the candidate rows X, every live verifier's
         selection on its own inbox, the >= floor(nv/2) vote and the leader's arrival cap) and, behind
         it, the device-side follow-up of the selection (_on_accept).  xrow: worker -> row of X.
-        Returns the callable of krum_committee_async."""
+        pre: the phase-1 Gram of gram_stacked_async (X is then None: the noised rows are assembled
+        from it with the noisers' ids and scales).  Returns the callable giving (acc, node)."""
         cfg, fsm = self.cfg, self.fsm
         vs = [v for v in plan.verifiers if v in inboxes]
         n = len(inboxes[vs[0]])
-        U = X.shape[0]
+        U = X.shape[0] if X is not None else pre["U1"]
         inbox_t = h2d([[xrow[w] for w in inboxes[v]] for v in vs], torch.int32, self.dev)
         rank = np.full(U, -1, np.int32)
         for r, w in enumerate(fsm.leader_arrivals()):
@@ -575,8 +604,14 @@ class BiscottiEngine:
         need = len(plan.verifiers) // 2
         clip = fsm.krum_clip(n)
         on_accept = self._on_accept(spec, xrow, U, plan, live, box)
-        return K.krum_committee_async(X, inbox_t, n - clip, n - clip, need, h2d(rank, torch.int32, self.dev), cap,
-                                      on_accept=on_accept)
+        rank_t = h2d(rank, torch.int32, self.dev)
+        if pre is not None:
+            nz = h2d([noisers[w] for w in local_workers], torch.int32, self.dev)
+            sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma) for j in noisers[w]]
+                      for w in local_workers], torch.float32, self.dev)
+            return K.krum_committee_noise_async(pre, nz, sc, inbox_t, n - clip, n - clip, need, rank_t, cap,
+                                                on_accept=on_accept)
+        return K.krum_committee_async(X, inbox_t, n - clip, n - clip, need, rank_t, cap, on_accept=on_accept)
 
     def _on_accept(self, spec, xrow, U, plan, live, box):
         """Device-side follow-up of the committee's selection: this rank's share rows' flags become the
@@ -616,10 +651,13 @@ class BiscottiEngine:
             delta, qdelta, pending_commits = head["delta"], head["qdelta"], head["pending_commits"]
             inboxes, row_of, spec = head["inboxes"], head["row_of"], head["spec"]
         early = head.get("early")
+        krum_pre = head.get("krum_pre")
         with tm.phase("vrf_join"):
             noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake, local_workers)
         with tm.phase("noise"):
-            noised = early["noised"] if early else self._noise(delta, noisers, local_workers, it)
+            # with the phase-1 Gram the noised deltas are never materialised (only Krum reads them)
+            noised = early["noised"] if early else (None if krum_pre is not None else
+                                                    self._noise(delta, noisers, local_workers, it))
         # ---------------------------------------------------------------- verification
         with tm.phase("verify"):
             single = comm.world == 1
@@ -679,8 +717,9 @@ class BiscottiEngine:
                     # Multi-Krum is a pure function of the (gathered) noised deltas, so every rank
                     # evaluates the whole committee itself (identical inputs, deterministic kernels)
                     with tm.phase("verify.defense"):
-                        wait = early["krum"] if early else self._launch_krum(X, xrow, plan, live, inboxes, spec,
-                                                                             box)
+                        wait = early["krum"] if early else self._launch_krum(
+                            X, xrow, plan, live, inboxes, spec, box, pre=krum_pre, noisers=noisers,
+                            local_workers=local_workers)
                         with tm.phase("verify.krum_wait"):
                             acc_t, node_t = wait()
                     acc_np = acc_t.numpy().astype(np.uint8)   # [len(vs), ni]

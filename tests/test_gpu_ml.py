@@ -29,6 +29,49 @@ def test_softmax_step_matches_reference():
     assert (q_gpu.cpu() - q_ref).abs().max() <= 1
 
 
+@pytest.mark.parametrize("d_in,d_out", [(8742, 2), (2500, 12)])
+def test_softmax_step_k_tiled_matches_reference(d_in, d_out):
+    """K-tiled local step (features staged through LDS in 1024-wide tiles): LFW-sized 62x47x3 inputs."""
+    g = torch.Generator().manual_seed(d_in)
+    P, n = 6, 40
+    X = torch.rand((P * n, d_in), generator=g)
+    y = torch.randint(0, d_out, (P * n,), generator=g, dtype=torch.int32)
+    off = torch.arange(P, dtype=torch.int64) * n
+    nt = torch.full((P,), n, dtype=torch.int32)
+    pid = torch.arange(P, dtype=torch.int32) * 5 + 1
+    W = torch.randn(d_out * d_in + d_out, generator=g, dtype=torch.float64) * 0.01
+    d_ref, q_ref, l_ref = K.softmax_step(X, y, off, nt, pid, W, d_in, d_out, 10, 77, 3)
+    c = lambda t: t.cuda()
+    d_gpu, q_gpu, l_gpu = K.softmax_step(c(X), c(y), c(off), c(nt), c(pid), c(W), d_in, d_out, 10, 77, 3)
+    torch.testing.assert_close(d_gpu.cpu(), d_ref, rtol=5e-4, atol=5e-6)
+    torch.testing.assert_close(l_gpu.cpu(), l_ref, rtol=1e-4, atol=1e-5)
+    assert (q_gpu.cpu() - q_ref).abs().max() <= 1
+
+
+def test_lfw_ledger_rounds_on_gpu():
+    """The long-parameter-vector ledger (LFW maleness softmax, d = 17486, 1749 chunks): exact secure
+    aggregation and a valid chain."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    cfg = RunConfig(num_nodes=20, dataset="lfw", seed=4, max_iterations=100, deterministic_time=True)
+    eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
+    assert eng.d == 17486
+    res = []
+    for _ in range(3):
+        W0 = eng.W.clone()
+        r = eng.run_round()
+        res.append(r)
+        if not r.empty:
+            _, q = eng.task.step(W0, r.iteration, sorted(r.node_list))
+            torch.testing.assert_close(eng.W, W0 + q.sum(0).double() / 1e4, rtol=0, atol=1e-12)
+    ok, why = eng.fsm.chain.verify()
+    eng.close()
+    assert ok, why
+    assert sum(not r.empty for r in res) >= 2
+
+
 def test_softmax_step_clips_large_gradients():
     X, y, off, nt, pid, W = _fed(P=3)
     X = X * 1e3  # huge activations -> gradient norm far above 100
@@ -197,6 +240,33 @@ def test_krum_committee_matches_reference(U, n, V):
     for v in range(V):
         rows = inbox[v].long()
         assert not acc[v][torch.isin(rows, bad)].any()
+
+
+@pytest.mark.parametrize("U1,N,nn", [(94, 100, 2), (60, 64, 3)])
+def test_krum_committee_noise_aware_matches_explicit(U1, N, nn):
+    """Phase-1 Gram over [deltas; noise vectors] + phase-2 assembly gives the same committee decisions as
+    Krum over the explicitly noised rows (fp64 reference), incl. a colluding noiser (scale 0)."""
+    g = torch.Generator().manual_seed(U1 + N)
+    D = 7850
+    delta = (torch.randn((U1, D), generator=g) * 0.05).float()
+    bad = torch.arange(U1 - U1 // 4, U1)
+    delta[bad] += 0.3 * torch.randn((1, D), generator=g)
+    tbl = torch.randn((N, 100, D), generator=g).float()
+    it = 37
+    nz = torch.randint(0, N, (U1, nn), generator=g).int()
+    sc = torch.full((U1, nn), -0.76, dtype=torch.float32)
+    sc[5, 0] = 0.0
+    X64 = delta.double() + (sc.double()[:, :, None] * tbl[:, it].double()[nz.long()]).sum(1) / nn
+    n, V = min(70, U1 - 4), 3
+    inbox = torch.stack([torch.sort(torch.randperm(U1, generator=g)[:n]).values for _ in range(V)]).int()
+    rank = torch.randperm(U1, generator=g).int()
+    clip = n // 2
+    acc_ref, node_ref = K.krum_committee_async(X64, inbox, n - clip, n - clip, 1, rank, 20)()
+    pre = K.gram_stacked_async(delta.cuda(), tbl.cuda()[:, it, :])
+    acc, node = K.krum_committee_noise_async(pre, nz.cuda(), sc.cuda(), inbox.cuda(), n - clip, n - clip, 1,
+                                             rank.cuda(), 20)()
+    assert torch.equal(acc, acc_ref)
+    assert torch.equal(node, node_ref)
 
 
 def test_krum_committee_single_verifier_equals_krum():

@@ -59,3 +59,67 @@ def test_protocol_config_derivation(rt):
     assert pc.total_shares == 21                   # ceil(2 * poly / na) * na
     assert pc.shares_per_miner == 7
     assert pc.poisoning_index == 70                # ceil(N * (1 - po))
+
+
+def test_gob_blockdata_hand_derived_vector(rt):
+    """encoding/gob bytes of BlockData{Iteration: 3, GlobalW: [1.0], Deltas: [Update{SourceID: 2,
+    Iteration: 3, Commitment: [0xAB], Accepted: true}]} as a fresh Go process's Encoder writes them
+    (blockData.go:31-41), derived by hand from the encoding/gob wire spec -- not from our encoder.
+    Go is not available here, so parity with real Go output stays unpinned; this pins the spec.
+
+    Type ids: user ids start after firstUserId = 64 and are handed out while the type info is built:
+    BlockData 65 (struct, id set before its fields), []float64 66, Update 67 (the element gets its
+    id before the []Update slice does), [][]uint8 68, []main.Update 69.  Builtins: bool 1, int 2,
+    float 4, []byte 5.  Ints are zig-zag (x<<1, negative: ^x<<1|1); uints >= 128 are a negated byte
+    count then big-endian bytes; floats are the byte-reversed IEEE bits as a uint.  Messages are
+    uint(length) + payload; type definitions go depth-first in field order, each before its inner
+    types (Encoder.sendType), basic types and []byte are never described."""
+    def s(txt):  # string field value: uint(len) + bytes
+        return bytes([len(txt)]) + txt.encode()
+
+    def field(name, tid):  # fieldType{Name, Id}: 01 name 01 id 00
+        return b"\x01" + s(name) + b"\x01" + tid + b"\x00"
+
+    ID65, ID66, ID67, ID68, ID69 = b"\xff\x82", b"\xff\x84", b"\xff\x86", b"\xff\x88", b"\xff\x8a"
+    INT, FLOAT, BYTES, BOOL = b"\x04", b"\x08", b"\x0a", b"\x02"
+    # 1. BlockData: -65, wireType.StructT (delta 3), structType.CommonType (delta 1){Name, Id}, Field (delta 1)
+    m1 = (b"\xff\x81" + b"\x03" + b"\x01" + b"\x01" + s("BlockData") + b"\x01" + ID65 + b"\x00"
+          + b"\x01" + b"\x03" + field("Iteration", INT) + field("GlobalW", ID66) + field("Deltas", ID69)
+          + b"\x00" + b"\x00")
+    # 2. []float64: -66, wireType.SliceT (delta 2), sliceType.CommonType, sliceType.Elem = float
+    m2 = b"\xff\x83" + b"\x02" + b"\x01" + b"\x01" + s("[]float64") + b"\x01" + ID66 + b"\x00" + b"\x01" + FLOAT + \
+        b"\x00" + b"\x00"
+    # 3. []main.Update: -69, elem Update (67)
+    m3 = b"\xff\x89" + b"\x02" + b"\x01" + b"\x01" + s("[]main.Update") + b"\x01" + ID69 + b"\x00" + b"\x01" + ID67 + \
+        b"\x00" + b"\x00"
+    # 4. Update: -67, eight fields
+    m4 = (b"\xff\x85" + b"\x03" + b"\x01" + b"\x01" + s("Update") + b"\x01" + ID67 + b"\x00" + b"\x01" + b"\x08"
+          + field("SourceID", INT) + field("Iteration", INT) + field("Delta", ID66) + field("Commitment", BYTES)
+          + field("Noise", ID66) + field("NoisedDelta", ID66) + field("Accepted", BOOL)
+          + field("SignatureList", ID68) + b"\x00" + b"\x00")
+    # 5. [][]uint8: -68, elem []byte (5)
+    m5 = b"\xff\x87" + b"\x02" + b"\x01" + b"\x01" + s("[][]uint8") + b"\x01" + ID68 + b"\x00" + b"\x01" + BYTES + \
+        b"\x00" + b"\x00"
+    # 6. the value: type id 65, then the non-zero fields as (field-number delta, value), 0 terminator
+    upd = (b"\x01" + b"\x04"              # SourceID (field 0): int 2
+           + b"\x01" + b"\x06"            # Iteration (1): int 3
+           + b"\x02" + b"\x01\xab"        # Commitment (3, delta 2): []byte len 1, 0xAB
+           + b"\x03" + b"\x01"            # Accepted (6, delta 3): true
+           + b"\x00")
+    m6 = (ID65 + b"\x01" + b"\x06"        # Iteration (0): int 3
+          + b"\x01" + b"\x01" + b"\xfe\xf0\x3f"  # GlobalW (1): 1 element, 1.0 = bits 3ff0... reversed -> 0xf03f
+          + b"\x01" + b"\x01" + upd       # Deltas (2): 1 element
+          + b"\x00")
+
+    def msg(p):
+        n = len(p)
+        return (bytes([n]) if n < 128 else b"\xff" + bytes([n])) + p
+    expect = b"".join(msg(m) for m in (m1, m2, m3, m4, m5, m6))
+    assert [len(m) for m in (m1, m2, m3, m4, m5, m6)] == [62, 23, 28, 133, 23, 22]
+    d = rt.BlockData()
+    d.iteration = 3
+    d.global_w = [1.0]
+    u = rt.Update()
+    u.source_id, u.iteration, u.commitment, u.accepted = 2, 3, b"\xab", True
+    d.deltas = [u]
+    assert bytes(d.gob()) == expect
