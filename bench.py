@@ -62,6 +62,12 @@ PRESETS = {
     "credit50_fed50": ({"fedsys": True, "num_nodes": 50, "dataset": "creditcard", "poisoning": 0.5,
                         "perc_samples": 35}, None, 1 - 0.6310, {}, "nsdi-eval/credit/fed_50p"),
     "churn10": ({"churn": 0.1}, None, None, {}, "BASELINE.json config 5 (reference churn runs: 25-31 s/round)"),
+    # process churn with state loss + rejoin (eval/eval_FT/runEval.sh: a node killed every 60/rate s,
+    # restarted 5 s before the next kill), 50 MNIST peers as in nsdi-eval/churn
+    "churn_kill4": ({"num_nodes": 50, "churn_kill_per_min": 4.0}, 30.92, 1 - 0.121, {}, "nsdi-eval/churn/15s.log"),
+    "churn_kill2": ({"num_nodes": 50, "churn_kill_per_min": 2.0}, 26.27, 1 - 0.210, {}, "nsdi-eval/churn/30s.log"),
+    "churn_kill1": ({"num_nodes": 50, "churn_kill_per_min": 1.0}, 25.71, 1 - 0.138, {}, "nsdi-eval/churn/60s.log"),
+    "churn_kill05": ({"num_nodes": 50, "churn_kill_per_min": 0.5}, 25.44, 1 - 0.191, {}, "nsdi-eval/churn/120s.log"),
     # the long-parameter-vector ledger: LFW maleness softmax, d = 17486 (no reference number:
     # the reference's lfw pipeline is inconsistent, see data.dataset_dims)
     "lfw100": ({"dataset": "lfw"}, None, None, {}, "honest.go:211 'mnist/lfw for pytorch' (unpinned)"),

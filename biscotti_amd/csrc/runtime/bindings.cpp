@@ -715,6 +715,15 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         bool ok = c.verify(&why);
         return py::make_tuple(ok, why);
       })
+      .def("verify_range", [](const Blockchain& c, size_t from, size_t to) {
+        std::string why;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = c.verify_range(from, to, &why);
+        }
+        return py::make_tuple(ok, why);
+      })
       .def("print_chain", &Blockchain::print_chain)
       .def("truncate", [](Blockchain& c, size_t n) { if (n < c.blocks.size()) c.blocks.resize(n); });
   m.def("gob_uint", [](uint64_t x) { Bytes b; gob_put_uint(b, x); return P(b); });

@@ -74,6 +74,7 @@ struct Blockchain {
   int add_block(const Block& b);
   // chain validity: linkage + recomputed hashes
   bool verify(std::string* why = nullptr) const;
+  bool verify_range(size_t from, size_t to, std::string* why = nullptr) const;
   std::string print_chain() const;  // PrintChain (blockchain.go:43-54)
   // Persistence: append-only file of length-prefixed records (checkpoint/resume).
   static Bytes serialize_block(const Block& b);

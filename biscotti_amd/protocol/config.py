@@ -37,6 +37,9 @@ class RunConfig:
     # --- framework knobs
     seed: int = 0
     churn: float = 0.0              # fraction of peers offline per round (fault-tolerance runs)
+    churn_kill_per_min: float = 0.0  # process churn (eval/eval_FT): peers killed per minute, restarted after
+    #                                  60/rate - 5 s with fresh VRF keys, rejoining through chain sync
+    churn_round_s: float = 25.44    # seconds per reference round (maps churn seconds onto rounds)
     data_dir: str | None = None     # real MNIST .npy shards (reference layout), else synthetic
     commit_key: str | None = None   # commitKey.json (else generated: PK[i] = 2^i G1, s = 2)
     pkey_file: str | None = None    # pKeyG1.json (else derived from seed)
@@ -76,8 +79,49 @@ class RunConfig:
     #                                  shared pre-sampled vectors (client_obj.py:97-98); not the reference
     krum_pregram: bool = True       # one rank, table noise: Krum's Gram over [deltas; noise vectors] runs
     #                                 before the VRF outputs arrive; only an O(n^2) assembly waits for them
+    join_background: bool = False   # main stream waits for the background (witness-sum) work each round
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
     #                                 (shortens the GPU chain; costs host time before the previous round ends)
+
+    def validate(self) -> None:
+        """Reject configurations the kernels cannot run, up front (instead of a launch error in the
+        middle of a round).  Limits: committee Multi-Krum <= 1024 candidate rows, inbox <= 256,
+        <= 64 verifiers (ml.hip KC1-KC3); exact recovery <= 32 share points per chunk and poly <= 16
+        (k_recover_w); local step B <= 16 and <= 16 classes (k_softmax_step); <= 16 noisers."""
+        import math
+
+        err = []
+        if self.dataset not in ("mnist", "lfw", "creditcard"):
+            err.append(f"dataset {self.dataset!r}: expected mnist | lfw | creditcard")
+        if self.num_nodes < 2:
+            err.append("need at least 2 nodes")
+        committee = self.num_verifiers + self.num_miners
+        if self.num_nodes - committee < 1:
+            err.append(f"{self.num_nodes} nodes leave no worker beside {committee} committee members")
+        workers = max(0, self.num_nodes - min(committee, self.num_nodes))
+        if workers > 1024:
+            err.append(f"{workers} workers per round: committee Krum takes at most 1024 candidates")
+        thresh = min(int(self.num_nodes * self.perc_samples / 100.0), max(workers, 0))
+        if self.rand_sample:
+            thresh = max(workers, 0)
+        if self.verification and thresh > 256:
+            err.append(f"verifier inbox of {thresh} updates: committee Krum takes at most 256 per verifier")
+        if self.num_verifiers > 64:
+            err.append("at most 64 verifiers")
+        if self.num_miners <= 0 or self.num_verifiers < 0 or self.num_noisers < 0:
+            err.append("committee sizes must be non-negative (and >= 1 miner)")
+        elif math.ceil(2 * self.poly_size / self.num_miners) * self.num_miners > 32:
+            err.append("TOTAL_SHARES = ceil(2 POLY_SIZE / miners) * miners must be <= 32")
+        if not 2 <= self.poly_size <= 16:
+            err.append("POLY_SIZE must be in 2..16")
+        if self.dataset in ("mnist", "lfw") and not 1 <= self.batch_size <= 16:
+            err.append("softmax local step: batch size 1..16")
+        if self.num_noisers > 16 or (self.noising and self.num_noisers >= self.num_nodes):
+            err.append("noisers: at most 16 and fewer than the nodes")
+        if not 0.0 <= self.poisoning < 1.0 or not 0.0 <= self.churn < 1.0:
+            err.append("poisoning / churn fractions must be in [0, 1)")
+        if err:
+            raise ValueError("invalid RunConfig: " + "; ".join(err))
 
     def protocol(self, rt):
         pc = rt.ProtocolConfig()
@@ -137,6 +181,7 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--max-iterations", type=int, default=100)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--churn", type=float, default=0.0)
+    ap.add_argument("--churn-kill-per-min", type=float, default=0.0)
     ap.add_argument("--data-dir", default=None)
     ap.add_argument("--commit-key", default=None)
     ap.add_argument("--pkey-file", default=None)

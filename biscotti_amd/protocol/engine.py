@@ -256,6 +256,7 @@ class DeviceCrypto:
 
 class BiscottiEngine:
     def __init__(self, cfg: RunConfig, comm: Comm | None = None):
+        cfg.validate()
         self.cfg = cfg
         self.comm = comm or Comm()
         self.R = rt()
@@ -354,6 +355,9 @@ class BiscottiEngine:
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
+        self._churn = {"down": {}, "view": {}, "epoch": {}, "acc": 0.0, "kills": 0, "rejoins": 0,
+                       "synced_blocks": 0}
+        self.stats["churn"] = self._churn
         self.rounds_done = 0
         self._head = None
         import atexit
@@ -431,15 +435,64 @@ class BiscottiEngine:
         self.log.info("Resumed chain of %d blocks at iteration %d", len(chain), last.data.iteration)
 
     def _live_mask(self) -> list[int]:
-        if self.cfg.churn <= 0:
-            return [1] * self.N
-        seed = self.fsm.round_seed(7)
-        perm = self.R.seeded_permutation(self.N, seed)
-        k = int(round(self.cfg.churn * self.N))
         live = [1] * self.N
-        for p in perm[:k]:
-            live[p] = 0
+        if self.cfg.churn > 0:
+            # per-round availability churn: a seeded fraction of the peers is unreachable this round
+            seed = self.fsm.round_seed(7)
+            perm = self.R.seeded_permutation(self.N, seed)
+            k = int(round(self.cfg.churn * self.N))
+            for p in perm[:k]:
+                live[p] = 0
+        if self.cfg.churn_kill_per_min > 0:
+            self._crash_restart(live)
         return live
+
+    def _crash_restart(self, live: list) -> None:
+        """Process churn with state loss (eval/eval_FT/runEval.sh, DistSys/failAndRestartLocal.sh): every
+        60/rate seconds a random peer other than 0 is killed, stays down for 60/rate - 5 s and is
+        restarted.  Seconds map to rounds through cfg.churn_round_s (the reference's churn runs took
+        25-31 s per round).  A killed peer loses its state; the restarted process generates fresh
+        VRF keys (myVRF.init at start-up, vrf.go:16-32) and rejoins through RegisterPeer: it adopts
+        the longest chain it is offered after checking it (main.go:420-436,1000-1013,
+        honest.go:679-685) -- here the blocks it missed are re-hashed and link-checked
+        (Blockchain.verify_range) by the rank that hosts it.  Deterministic (round seed): every rank
+        replicates the schedule."""
+        cfg, fsm = self.cfg, self.fsm
+        st = self._churn
+        it = fsm.iteration + 1   # the round being opened
+        # restarts due this round
+        for p, back in list(st["down"].items()):
+            if it >= back:
+                del st["down"][p]
+                view = st["view"].get(p, 1)
+                height = len(fsm.chain)
+                st["epoch"][p] = st["epoch"].get(p, 0) + 1
+                st["rejoins"] += 1
+                if p in self.local:
+                    ok, why = fsm.chain.verify_range(max(0, view - 1), height)
+                    if not ok:
+                        raise RuntimeError(f"peer {p}: the chain offered at rejoin does not verify: {why}")
+                    e = st["epoch"][p]
+                    self.vrf_noise_seed[p] = _seed_bytes(cfg.seed, f"vrf-noise-e{e}", p)
+                    self.vrf_roles_seed[p] = _seed_bytes(cfg.seed, f"vrf-roles-e{e}", p)
+                    st["synced_blocks"] += height - view
+                    self.log.info("%d:Rejoined at iteration %d: adopted a chain of %d blocks (%d verified)", p, it,
+                                  height, height - view)
+        # kills due this round
+        st["acc"] += cfg.churn_kill_per_min * cfg.churn_round_s / 60.0
+        down_rounds = max(1, int(np.ceil((60.0 / cfg.churn_kill_per_min - 5.0) / cfg.churn_round_s)))
+        cand = [p for p in range(1, self.N) if p not in st["down"]]
+        perm = self.R.seeded_permutation(len(cand), fsm.round_seed(11)) if cand else []
+        j = 0
+        while st["acc"] >= 1.0 and j < len(cand):
+            p = cand[perm[j]]
+            j += 1
+            st["acc"] -= 1.0
+            st["down"][p] = it + down_rounds
+            st["view"][p] = len(fsm.chain)   # its chain at the moment it died
+            st["kills"] += 1
+        for p in st["down"]:
+            live[p] = 0
 
     def _rows_buffer(self, per_peer: dict, width: int, dtype) -> torch.Tensor:
         """[maxlocal, width] buffer whose row (peer - lo) holds that local peer's vector."""
@@ -1048,17 +1101,17 @@ class BiscottiEngine:
         if not self.gpu:
             ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
             return lambda: ok
+        # the check needs the recovered coefficients (main) and the commitment sums (side stream);
+        # by now the share MSM is done, so it runs on the main stream: high priority and every CU
+        # (the CU-masked side stream would leave a quarter of the GPU idle on the critical path)
         main = S.current()
-        st = self.side_stream
-        S.wait(st, main)
-        with S.use(st):
-            ok = self.crypto.check_aggregate(coeffs, csum)
-            host = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
-            host.copy_(ok, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(st)
-        coeffs.record_stream(st)
-        csum.record_stream(st)
+        if self.comm.world == 1:
+            S.wait(main, self.side_stream)
+        ok = self.crypto.check_aggregate(coeffs, csum)
+        host = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
+        host.copy_(ok, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(main)
 
         def result():
             ev.synchronize()
@@ -1066,10 +1119,14 @@ class BiscottiEngine:
         return result
 
     def _join_side_work(self) -> None:
+        # the background work (the miners' witness sums) has no consumer in the protocol: its inputs
+        # and outputs are stream-ordered on the background stream (record_stream), so the main stream
+        # does not wait for it -- it overlaps the next round's head instead of the audit
         if self._side_work:
-            main = S.current()
-            for ev, _ in self._side_work:
-                main.wait_event(ev)
+            if self.cfg.join_background:
+                main = S.current()
+                for ev, _ in self._side_work:
+                    main.wait_event(ev)
             self._side_work.clear()
 
     # ------------------------------------------------------------------ verification defences

@@ -105,3 +105,33 @@ def test_centralblock_prototype():
     assert cb.evaluate()["best_test_error"] < e0
     img = invert(np.arange(7840, dtype=np.float64))
     assert img.shape == (784,) and abs(img.max() - 2.55 * 1567 / 7839) < 1e-12
+
+
+def test_eval_plotters(tmp_path):
+    """The figure set of the reference's eval scripts from this framework's own traces / bench lines."""
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+    from biscotti_amd.protocol.fedsys import FedSysEngine
+    from biscotti_amd.utils import plots
+
+    tr, ftr = tmp_path / "b.jsonl", tmp_path / "f.jsonl"
+    kw = dict(num_nodes=6, dataset="creditcard", num_verifiers=1, num_miners=2, num_noisers=1, noising=False,
+              device="cpu", seed=2)
+    eng = BiscottiEngine(RunConfig(trace_file=str(tr), **kw))
+    for _ in range(4):
+        eng.run_round()
+    eng.close()
+    fed = FedSysEngine(RunConfig(trace_file=str(ftr), **kw))
+    for _ in range(4):
+        fed.run_round()
+    ref = os.path.join(ROOT, "profiles", "reference_curves.json")
+    outs = [plots.convergence(str(tr), str(ftr), str(tmp_path / "c.pdf"), ref),
+            plots.poisoning(str(tr), str(tmp_path / "p.pdf"), ref),
+            plots.breakdown(str(tr), str(tmp_path / "k.pdf"), skip=1)]
+    bl = []
+    for n in (4, 6):
+        f = tmp_path / f"bench{n}.txt"
+        f.write_text(json.dumps({"value": 0.001 * n, "n_gpus": 1, "config": {"peers": n}}) + "\n")
+        bl.append(str(f))
+    outs.append(plots.scaling(bl, "peers", str(tmp_path / "s.pdf")))
+    assert all(os.path.getsize(o) > 1000 for o in outs)
