@@ -146,6 +146,9 @@ def main() -> int:
         eng.run_round()
     comm.barrier()
     sync()
+    import resource
+
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     last = None
     phases: dict = {}
@@ -161,6 +164,9 @@ def main() -> int:
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    host_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)   # every thread of this rank
+    stats0 = {k: v for k, v in getattr(eng, "stats", {}).items() if isinstance(v, (int, float))}
     t = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
     if comm.world > 1:
         import torch.distributed as dist
@@ -230,6 +236,8 @@ def main() -> int:
             "final_test_acc_mean_std": ms(finals),
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
+            "host_cpu_ms_per_round": 1e3 * host_cpu / max(a.steps, 1),
+            "engine_stats": stats0,
             "table_gb": (eng.crypto.eng.table_bytes() / 1e9) if hasattr(getattr(eng, "crypto", None), "eng") else 0.0,
             "b0": getattr(getattr(getattr(eng, "crypto", None), "eng", None), "b0", None),
             "baseline_test_acc": ref_acc,

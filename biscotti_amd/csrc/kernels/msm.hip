@@ -187,23 +187,41 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
 // commitment) or S = 1 (commit_only: chunk commitments only).  out_y: int64 [nrows][nchunks][T].
 extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
-    int poly, int T, int B0, int NW, int commit_only, const int* alive, const int* compact, uint32_t* out_pts,
-    long long* out_y) {
+    int poly, int T, int B0, int NW, int commit_only, const int* alive, const int* compact, int group_rows,
+    uint32_t* out_pts, long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
   // compact (optional): [count, row...] -- only the listed rows are computed, packed densely over the
   // grid (a rejected row costs no SIMD lanes); the grid is sized for nrows, the surplus exits at once
   const int neff = compact != nullptr ? compact[0] : nrows;
   const long long total = (long long)neff * nchunks * S;
-  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  // group_rows G > 0: rows are taken G at a time in list order (the speculative rows arrive sorted
+  // by their arrival at the leader), chunk-major inside a group, and the XCD remap is applied per
+  // 64-block super-block -- so work proceeds through the row list in dispatch order (rows the
+  // selection drops later are skipped when reached) while each XCD still shares a chunk's table
+  // lines across the group's rows.  G = 0: one group of every row, remapped over the whole grid.
+  int lb;
+  if (group_rows > 0) {
+    const int SB = 64;
+    const int q = blockIdx.x / SB, j = blockIdx.x % SB;
+    const int sbn = min(SB, (int)gridDim.x - q * SB);
+    lb = q * SB + xcd_remap(j, sbn);
+  } else {
+    lb = xcd_remap(blockIdx.x, gridDim.x);
+  }
   const long long g = (long long)lb * blockDim.x + threadIdx.x;
   if (g >= total) return;
-  // chunk-major: consecutive groups share a chunk (and its table lines)
-  const int slot = (int)(g % S);
-  const long long grp = g / S;
-  const int pos = (int)(grp % neff);
+  const int G = group_rows > 0 ? min(group_rows, neff) : neff;
+  const long long per_group = (long long)G * nchunks * S;
+  const int gq = (int)(g / per_group);
+  const int r0 = gq * G, gr = min(G, neff - r0);
+  const long long gg = g - (long long)gq * per_group;
+  // chunk-major inside the group: consecutive groups of S lanes share a chunk (and its table lines)
+  const int slot = (int)(gg % S);
+  const long long grp = gg / S;
+  const int pos = r0 + (int)(grp % gr);
   const int r = compact != nullptr ? compact[1 + pos] : pos;
-  const int k = (int)(grp / neff);
+  const int k = (int)(grp / gr);
   // late cancellation of speculative work: rows the verifiers rejected (flag cleared by
   // k_set_alive on the critical-path stream while this kernel runs) are skipped from then on;
   // their outputs are never read.  A stale read only costs the work.
@@ -340,35 +358,48 @@ __device__ __forceinline__ bool jac_equal(const jac& p, const jac& q) {
   return fp_eq(fp_mul(p.y, fp_mul(z2s, q.z)), fp_mul(q.y, fp_mul(z1s, p.z)));
 }
 
+// One wave per chunk, one lane per (coefficient, window) digit: every lane issues its table fetch
+// up front (the fetches are independent; with one lane per coefficient the window loop exposed a
+// dependent HBM/TLB round trip per window -- the kernel sat on the critical path latency-bound),
+// then an LDS tree sums the <= 64 points and lane 0 compares with each miner's sum.
 extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* coeffs, int d, int poly,
                                                               const uint32_t* tbl_pk, int B0, int NW,
                                                               const uint32_t* csum, int nm, int nch, int* ok) {
   __shared__ uint32_t sh[64 * 24];
+  __shared__ int dig[16][9];   // signed digit of (coefficient j, window w); NW <= 9 (bsc_chunk_check)
   const int k = blockIdx.x, t = threadIdx.x;
   const int prev = k * poly, L = min(poly, d - prev);
   const int E0 = 1 << (B0 - 1);
   const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
-  jac acc = jac_inf();
-  if (t < L) {
-    const long long cj = coeffs[(size_t)k * poly + t];
-    const bool neg = cj < 0;
-    unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
-    const uint32_t* tb = tbl_pk + (size_t)(prev + t) * PB * 16;
-    int carry = 0;
-    for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
-      const int dg = recode(m, carry, win_bits(w, B0));
-      if (dg == 0) continue;
-      const int ad = dg < 0 ? -dg : dg;
-      aff q = ld_aff(tb + (size_t)win_entry(w, ad, E0) * 16);
-      if ((dg < 0) != neg) q = aff_neg(q);
-      acc = jac_add_aff(acc, q);
+  // 1. digits of every coefficient (cheap integer work, one lane per coefficient)
+  if (t < 16) {
+    for (int w = 0; w < 9; ++w) dig[t][w] = 0;
+    if (t < L) {
+      const long long cj = coeffs[(size_t)k * poly + t];
+      const bool neg = cj < 0;
+      unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
+      int carry = 0;
+      for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
+        const int dg = recode(m, carry, win_bits(w, B0));
+        dig[t][w] = neg ? -dg : dg;
+      }
     }
+  }
+  __syncthreads();
+  // 2. lane e -> (coefficient e / 9, window e % 9): its fetch issued before any addition
+  jac acc = jac_inf();
+  for (int e = t; e < L * 9; e += 64) {
+    const int j = e / 9, w = e % 9;
+    const int dg = w < NW ? dig[j][w] : 0;
+    if (dg == 0) continue;
+    const int ad = dg < 0 ? -dg : dg;
+    aff q = ld_aff(tbl_pk + ((size_t)(prev + j) * PB + win_entry(w, ad, E0)) * 16);
+    if (dg < 0) q = aff_neg(q);
+    acc = jac_add_aff(acc, q);
   }
   st_jac(sh + t * 24, acc);
   __syncthreads();
-  int top = 1;
-  while (top < L) top <<= 1;
-  for (int s = top >> 1; s > 0; s >>= 1) {
+  for (int s = 32; s > 0; s >>= 1) {
     if (t < s) st_jac(sh + t * 24, jac_add(ld_jac(sh + t * 24), ld_jac(sh + (t + s) * 24)));
     __syncthreads();
   }
@@ -399,17 +430,19 @@ extern "C" __global__ void __launch_bounds__(128) k_sum_rows(const uint32_t* pts
 extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
                                                              int nrows, const int* cols, int ncols,
                                                              const int* row_mask, uint32_t* out) {
-  __shared__ uint32_t sh[8][32][24];
-  const int cx = threadIdx.x & 31, ry = threadIdx.x >> 5;
-  const int i = blockIdx.x * 32 + cx;
+  // 16 columns x 16 row lanes per block: each lane's serial chain is nrows/16 additions, then a
+  // 4-level LDS tree (the sums sit on the round's critical path: latency, not throughput, matters)
+  __shared__ uint32_t sh[16][16][24];
+  const int cx = threadIdx.x & 15, ry = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + cx;
   jac acc = jac_inf();
   if (i < ncols && ry < nrows) {
     const int col = cols ? cols[i] : i;
-    // software pipeline: load row r + 8 while adding row r
+    // software pipeline: load row r + 16 while adding row r
     int row = rows ? rows[ry] : ry;
     jac cur = ld_jac(pts + 24 * ((size_t)row * ncols_in + col));
-    for (int r = ry; r < nrows; r += 8) {
-      const int rn = r + 8 < nrows ? r + 8 : r;
+    for (int r = ry; r < nrows; r += 16) {
+      const int rn = r + 16 < nrows ? r + 16 : r;
       const int rown = rows ? rows[rn] : rn;
       const jac nxt = ld_jac(pts + 24 * ((size_t)rown * ncols_in + col));
       if (row_mask == nullptr || row_mask[row] != 0) acc = jac_add(acc, cur);
@@ -419,8 +452,8 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
   }
   st_jac(&sh[ry][cx][0], acc);
   __syncthreads();
-  for (int s = 4; s > 0; s >>= 1) {
-    if (ry < s) st_jac(&sh[ry][cx][0], jac_add(ld_jac(&sh[ry][cx][0]), ld_jac(&sh[ry + s][cx][0])));
+  for (int s2 = 8; s2 > 0; s2 >>= 1) {
+    if (ry < s2) st_jac(&sh[ry][cx][0], jac_add(ld_jac(&sh[ry][cx][0]), ld_jac(&sh[ry + s2][cx][0])));
     __syncthreads();
   }
   if (ry == 0 && i < ncols) st_jac(out + 24 * (size_t)i, ld_jac(&sh[0][cx][0]));
@@ -517,15 +550,16 @@ extern "C" int bsc_fb_table(const uint32_t* bases, int bases_are_jac, int b0, in
 
 extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
                               const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
-                              const int* alive, const int* compact, uint32_t* out_pts, long long* out_y,
-                              void* stream) {
+                              const int* alive, const int* compact, int group_rows, uint32_t* out_pts,
+                              long long* out_y, void* stream) {
   if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;  // every int64 scalar must be covered
   const int nchunks = (d + poly - 1) / poly;
   const int S = commit_only ? 1 : T + 1;
   const long long n = (long long)nrows * nchunks * S;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_shares_msm, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows,
-                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, compact, out_pts, out_y);
+                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, compact, group_rows, out_pts,
+                     out_y);
   return (int)hipGetLastError();
 }
 
@@ -584,7 +618,7 @@ extern "C" int bsc_sum_rows(const uint32_t* pts, int ncols_in, const int* rows, 
 extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
                              int ncols, const int* row_mask, uint32_t* out, void* stream) {
   if (ncols <= 0) return 0;
-  hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 32)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
+  hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 16)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
                      rows, nrows, cols, ncols, row_mask, out);
   return (int)hipGetLastError();
 }
@@ -612,7 +646,7 @@ extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stri
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
                                const uint32_t* csum, int nm, int nch, int* ok, void* stream) {
   if (nch <= 0 || nm <= 0) return 0;
-  if (poly < 1 || poly > 64 || nm > 64 || B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;
+  if (poly < 1 || poly > 16 || nm > 64 || B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65 || NW > 9) return -1;
   if ((long long)nch * poly < d || (long long)(nch - 1) * poly >= d) return -1;
   hipLaunchKernelGGL(k_chunk_check, dim3(nch), dim3(64), 0, (hipStream_t)stream, coeffs, d, poly, tbl_pk, B0, NW,
                      csum, nm, nch, ok);

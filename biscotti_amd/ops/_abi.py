@@ -16,7 +16,7 @@ SIGNATURES = {
     "bsc_point_op": [P, P, P, P, I, I, P],
     "bsc_witness_bases": [P, I, I, I, P, P],
     "bsc_fb_table": [P, I, I, I, I, I, I, L, L, L, P, P, P],
-    "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, I, P, P, P, P, P],
+    "bsc_shares_msm": [P, I, P, I, P, P, I, I, I, I, I, P, P, I, P, P, P],
     "bsc_alive_compact": [P, I, P, P],
     "bsc_set_alive": [P, P, I, P, P],
     "bsc_sum_rows": [P, I, P, I, P, I, P, P],

@@ -119,7 +119,7 @@ class DeviceCommitEngine:
 
     # ---------------------------------------------------------------- per-round kernels
     def shares(self, coeffs: torch.Tensor, rows: torch.Tensor, commit_only: bool = False, check_rows: bool = True,
-               alive: torch.Tensor | None = None, compact: bool = False):
+               alive: torch.Tensor | None = None, compact: bool = False, group_rows: int = 0):
         """Fused chunk commitments (+ witnesses and share values unless commit_only).
 
         coeffs: int64 [P, d] quantized deltas; rows: int32 [n] rows of `coeffs` to process.
@@ -127,6 +127,8 @@ class DeviceCommitEngine:
         runs (set_alive) is skipped from then on and its outputs are left undefined.
         compact: the flags are final when the kernel starts -- the flagged rows are packed densely
         over the grid (a skipped row then costs no SIMD lanes, unlike the per-thread skip).
+        group_rows: process the rows G at a time in list order (late cancellation then saves the
+        rows not reached yet); 0 = all rows chunk-major at once.
         Returns (pts [n, nchunks, S, 24] Jacobian with S = 1 or T+1, ys [n, nchunks, T] or None).
         """
         assert coeffs.dtype == torch.int64 and coeffs.dim() == 2 and coeffs.shape[1] == self.d
@@ -145,7 +147,7 @@ class DeviceCommitEngine:
                 _check(hip().bsc_alive_compact(_ptr(alive), n, _ptr(cidx), _stream()), "alive_compact")
         _check(hip().bsc_shares_msm(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), _ptr(self.tbl_wb),
                                     self.poly, self.T, self.b0, self.nw, int(commit_only), _ptr(alive), _ptr(cidx),
-                                    _ptr(pts), _ptr(ys), _stream()),
+                                    int(group_rows), _ptr(pts), _ptr(ys), _stream()),
                "shares_msm")
         return pts, ys
 

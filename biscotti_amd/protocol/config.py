@@ -69,6 +69,8 @@ class RunConfig:
     spec_msm: bool = True           # share MSM speculatively alongside verification, over the candidates most
     #                                 likely to end in the block (False: after the committee's selection,
     #                                 the block's rows only -- least work, started later)
+    spec_group_rows: int = 8        # speculative MSM over EVERY candidate, G rows at a time in leader arrival
+    #                                 order; rows outside the block are skipped once the selection lands
     spec_margin: float = 1.7        # speculative rows: the first ceil(margin * cap) + 2 candidates in leader
     #                                 arrival order (the block takes the first `cap` approved of them;
     #                                 a block row outside this prefix falls back to a top-up MSM)

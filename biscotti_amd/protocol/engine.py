@@ -152,8 +152,9 @@ class _SpecShares:
     flag per row) is cleared for rows the verifiers reject; the MSM skips flagged rows, whether the
     flags were cleared before it started or while it runs.  Consumers wait on `ev`."""
 
-    def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream, deferred: bool = False):
+    def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream, deferred: bool = False, group_rows: int = 0):
         self.eng, self.qdelta, self.rows, self.stream = eng, qdelta, rows, stream
+        self.group_rows = 0 if deferred else group_rows
         self.alive = torch.ones((len(rows),), dtype=torch.int32, device=qdelta.device)
         self.pts = self.ys = self.ev = None
         # deferred: launched once the selection has set the flags -> only the kept rows are computed,
@@ -168,7 +169,7 @@ class _SpecShares:
         with S.use(self.stream):
             rows_t = h2d(self.rows, torch.int32, self.qdelta.device)
             self.pts, self.ys = self.eng.shares(self.qdelta, rows_t, check_rows=False, alive=self.alive,
-                                                compact=self.deferred)
+                                                compact=self.deferred, group_rows=self.group_rows)
             self.ev = torch.cuda.Event()
             self.ev.record(self.stream)
         for t in (self.qdelta, self.alive):
@@ -226,12 +227,13 @@ class DeviceCrypto:
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
         return self.eng.shares(qdelta, rows)
 
-    def shares_async(self, qdelta: torch.Tensor, rows: list, stream, launch: bool = True) -> "_SpecShares":
+    def shares_async(self, qdelta: torch.Tensor, rows: list, stream, launch: bool = True,
+                     group_rows: int = 0) -> "_SpecShares":
         """Shares + witnesses of qdelta[rows] on `stream` (the caller's work keeps flowing on its own
         stream).  launch=False prepares the per-row flags only; launch() then starts the MSM after
         everything queued so far on the caller's stream (e.g. Krum's selection), so rows already
         rejected cost nothing."""
-        sp = _SpecShares(self.eng, qdelta, rows, stream, deferred=not launch)
+        sp = _SpecShares(self.eng, qdelta, rows, stream, deferred=not launch, group_rows=group_rows)
         if launch:
             sp.launch()
         return sp
@@ -544,17 +546,23 @@ class BiscottiEngine:
                 # replicated on every rank: the rows (of all ranks) whose shares are computed up front
                 cand = self._block_candidates(plan, workers, inboxes)
                 cap = fsm.leader_cap_size()
-                if cfg.verification and cfg.spec_msm and cap > 0:
+                if cfg.verification and cfg.spec_msm and cap > 0 and cfg.spec_group_rows <= 0:
                     # the block carries the first `cap` approved updates in leader arrival order, so the
                     # speculative MSM covers a prefix of that order with margin for rejections
                     k = min(len(cand), int(np.ceil(cfg.spec_margin * cap)) + 2)
                     cand = set([w for w in fsm.leader_arrivals() if w in cand][:k])
             if self.gpu and cfg.secure_agg and local_workers:
-                spec_workers = [w for w in local_workers if w in cand]
+                # speculative rows in leader arrival order: with spec_group_rows the MSM works through
+                # them in that order, and once the committee's selection lands (set_alive) the rows
+                # outside the leader's block are skipped when reached -- the block's rows are the first
+                # approved arrivals, so by then most of them are done and no candidate is ever missing
+                lo_rank = {w: i for i, w in enumerate(fsm.leader_arrivals())}
+                spec_workers = sorted((w for w in local_workers if w in cand), key=lambda w: lo_rank.get(w, 1 << 30))
                 if spec_workers:
                     defer = cfg.verification and not cfg.spec_msm
                     spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
-                                                                   self.side_stream, launch=not defer))
+                                                                   self.side_stream, launch=not defer,
+                                                                   group_rows=cfg.spec_group_rows))
             # full-vector commitments on the background stream: their first consumer is the signing
             # after Krum, so noise + Krum on the main stream do not queue behind them
             pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
