@@ -7,7 +7,9 @@
 #include <atomic>
 #include <chrono>
 #include <future>
+#include <random>
 #include <thread>
+#include <unordered_map>
 
 #include "bn256.hpp"
 #include "hash.hpp"
@@ -196,6 +198,88 @@ static void run_sign_job(SignJob& j) {
     j.out[i] = schnorr_finish(j.msgs[i], j.keys[size_t(j.key_of[i])], vs[i], tm[i]);
   });
 }
+
+// ---------------------------------------------------------------- KZG audit helpers
+// r = splitmix64(seed + (idx + 1) * golden) | 1 -- the device kernel derives the same values
+static inline u64 kzg_r(u64 seed, u64 idx) {
+  u64 z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (z ^ (z >> 31)) | 1ull;
+}
+// signed 192-bit accumulator of r * y products (|sum| < 2^64 * 2^63 * npts)
+struct I192 {
+  u64 w[3] = {0, 0, 0};
+  void add_mul(u64 r, i64 y) {
+    const bool neg = y < 0;
+    const u64 m = neg ? u64(0) - u64(y) : u64(y);
+    const unsigned __int128 p = (unsigned __int128)r * m;
+    u64 t[3] = {u64(p), u64(p >> 64), 0};
+    if (neg) {  // two's complement of the 192-bit product
+      t[0] = ~t[0]; t[1] = ~t[1]; t[2] = ~t[2];
+      unsigned __int128 c = (unsigned __int128)t[0] + 1;
+      t[0] = u64(c);
+      c = (unsigned __int128)t[1] + u64(c >> 64);
+      t[1] = u64(c);
+      t[2] += u64(c >> 64);
+    }
+    unsigned __int128 c = (unsigned __int128)w[0] + t[0];
+    w[0] = u64(c);
+    c = (unsigned __int128)w[1] + t[1] + u64(c >> 64);
+    w[1] = u64(c);
+    w[2] = w[2] + t[2] + u64(c >> 64);
+  }
+  bool magnitude(U256& out) const {  // returns true if negative
+    const bool neg = w[2] >> 63;
+    u64 t[3] = {w[0], w[1], w[2]};
+    if (neg) {
+      t[0] = ~t[0]; t[1] = ~t[1]; t[2] = ~t[2];
+      unsigned __int128 c = (unsigned __int128)t[0] + 1;
+      t[0] = u64(c);
+      c = (unsigned __int128)t[1] + u64(c >> 64);
+      t[1] = u64(c);
+      t[2] += u64(c >> 64);
+    }
+    out = U256();
+    out.w[0] = t[0]; out.w[1] = t[1]; out.w[2] = t[2];
+    return neg;
+  }
+};
+static std::shared_ptr<G2Prepared> prepared_g2(const Bytes& marshal) {
+  static std::mutex mu;
+  static std::unordered_map<std::string, std::shared_ptr<G2Prepared>> cache;
+  const std::string key(marshal.begin(), marshal.end());
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  auto pr = std::make_shared<G2Prepared>(g2_prepare(G2::unmarshal(marshal)));
+  std::lock_guard<std::mutex> lk(mu);
+  return cache.emplace(key, pr).first->second;
+}
+// device Jacobian (8 LE 32-bit limbs per coordinate, Montgomery) -> host G1 (same representation)
+static G1 g1_from_dev_jac(const uint32_t* v) {
+  G1 g;
+  U256* c[3] = {&g.x, &g.y, &g.z};
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 4; ++k) c[i]->w[k] = u64(v[8 * i + 2 * k]) | (u64(v[8 * i + 2 * k + 1]) << 32);
+  if (g.z.is_zero()) return G1::infinity();
+  if (!g.on_curve()) fail("device point is not on the curve");
+  return g;
+}
+struct KzgJob {
+  G1 pts[3];
+  std::shared_ptr<G2Prepared> q0, q1, qg;
+  bool ok = false;
+  std::string error;
+  std::promise<void> done_p;
+  std::shared_future<void> done = done_p.get_future().share();
+  std::thread th;
+  ~KzgJob() {
+    if (th.joinable()) th.join();
+  }
+};
 
 struct CommitKey {
   std::vector<G1> pk;
@@ -479,6 +563,112 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     return r;
   }, py::arg("commits"), py::arg("witnesses"), py::arg("g2_0"), py::arg("g2_1"), py::arg("xs"), py::arg("ys"),
      py::arg("threads") = 1, py::arg("y_base") = py::none());
+
+  // ---------------------------------------------------------------- batched KZG audit (K13)
+  // verifySecret (kyber.go:650-673) over every (chunk k, share point j) of an aggregate at once:
+  // with random 64-bit r_kj the checks e(C_k - y_kj B_k, g2_0) == e(W_kj, g2_1 - x_j G2) collapse to
+  //   e(L1, g2_0) * e(-A, g2_1) * e(L2, G2) == 1,
+  //   L1 = sum_k (R_k C_k - Z_k B_k), R_k = sum_j r_kj, Z_k = sum_j r_kj y_kj,
+  //   A = sum r_kj W_kj,  L2 = sum x_j r_kj W_kj.
+  // The device computes the three points (kernels/kzg.hip); kzg_rlc_host is the CPU path and the
+  // test oracle.  r_kj = kzg_r(seed, k * npts + j) on both sides.
+  m.def("kzg_r", [](u64 seed, u64 idx) { return kzg_r(seed, idx); });
+  m.def("kzg_rlc_host", [](std::vector<py::bytes> commits, std::vector<py::bytes> wits,
+                           py::array_t<int64_t, py::array::c_style | py::array::forcecast> ys, std::vector<i64> xs,
+                           std::vector<py::bytes> bases, u64 seed, int threads) {
+    const size_t nch = commits.size(), npts = xs.size();
+    if (wits.size() != nch * npts || size_t(ys.size()) != nch * npts || (bases.size() != 1 && bases.size() != nch))
+      throw std::runtime_error("kzg_rlc_host: shape mismatch");
+    std::vector<G1> C, W, Bs;
+    for (auto& b : commits) C.push_back(G1::unmarshal(B(b)));
+    for (auto& b : wits) W.push_back(G1::unmarshal(B(b)));
+    for (auto& b : bases) Bs.push_back(G1::unmarshal(B(b)));
+    const int64_t* y = ys.data();
+    std::vector<G1> l1(nch), a(nch), l2(nch);
+    {
+      py::gil_scoped_release rel;
+      parallel_for(nch, threads, [&](size_t k) {
+        G1 acc_a = G1::infinity(), acc_l2 = G1::infinity();
+        unsigned __int128 R = 0;
+        I192 Z;
+        for (size_t j = 0; j < npts; ++j) {
+          const u64 r = kzg_r(seed, k * npts + j);
+          const G1 rw = W[k * npts + j].mul(U256::from_u64(r));
+          acc_a = acc_a.add(rw);
+          acc_l2 = acc_l2.add(rw.mul_i64(xs[j]));
+          R += r;
+          Z.add_mul(r, y[k * npts + j]);
+        }
+        U256 Ru;
+        Ru.w[0] = u64(R);
+        Ru.w[1] = u64(R >> 64);
+        U256 Zm;
+        const bool zneg = Z.magnitude(Zm);
+        const G1 zb = Bs[Bs.size() == 1 ? 0 : k].mul(Zm);
+        l1[k] = C[k].mul(Ru).add(zneg ? zb : zb.neg());
+        a[k] = acc_a;
+        l2[k] = acc_l2;
+      });
+    }
+    G1 L1 = G1::infinity(), A = G1::infinity(), L2 = G1::infinity();
+    for (size_t k = 0; k < nch; ++k) { L1 = L1.add(l1[k]); A = A.add(a[k]); L2 = L2.add(l2[k]); }
+    return py::make_tuple(P(L1.marshal()), P(A.marshal()), P(L2.marshal()));
+  }, py::arg("commits"), py::arg("witnesses"), py::arg("ys"), py::arg("xs"), py::arg("bases"), py::arg("seed"),
+     py::arg("threads") = 1);
+  m.def("kzg_check", [](py::bytes l1, py::bytes a, py::bytes l2, py::bytes g2_0, py::bytes g2_1) {
+    G1 L1 = G1::unmarshal(B(l1)), A = G1::unmarshal(B(a)), L2 = G1::unmarshal(B(l2));
+    auto q0 = prepared_g2(B(g2_0)), q1 = prepared_g2(B(g2_1)), qg = prepared_g2(G2::generator().marshal());
+    py::gil_scoped_release rel;
+    return multi_pairing_is_one({L1, A.neg(), L2}, {q0.get(), q1.get(), qg.get()});
+  });
+  // the device result: int32/uint32 [3, 24] Jacobian Montgomery (L1, A, L2); the pairing product
+  // runs on a native thread (result() joins) so it overlaps the next round
+  py::class_<KzgJob, std::shared_ptr<KzgJob>>(m, "KzgJob").def("result", [](KzgJob& j) {
+    {
+      py::gil_scoped_release rel;
+      j.done.wait();
+    }
+    if (!j.error.empty()) throw std::runtime_error(j.error);
+    return j.ok;
+  });
+  m.def("kzg_check_device_async", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> pts,
+                                     py::bytes g2_0, py::bytes g2_1) {
+    if (pts.size() != 72) throw std::runtime_error("kzg_check_device_async: expected [3, 24] limbs");
+    auto job = std::make_shared<KzgJob>();
+    for (int i = 0; i < 3; ++i) job->pts[i] = g1_from_dev_jac(pts.data() + 24 * i);
+    job->q0 = prepared_g2(B(g2_0));
+    job->q1 = prepared_g2(B(g2_1));
+    job->qg = prepared_g2(G2::generator().marshal());
+    KzgJob* jp = job.get();
+    jp->th = std::thread([jp] {
+      try {
+        jp->ok = multi_pairing_is_one({jp->pts[0], jp->pts[1].neg(), jp->pts[2]},
+                                      {jp->q0.get(), jp->q1.get(), jp->qg.get()});
+      } catch (const std::exception& e) {
+        jp->error = e.what();
+      }
+      jp->done_p.set_value();
+    });
+    return job;
+  });
+  m.def("g1_from_device_jac", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> v) {
+    if (v.size() != 24) throw std::runtime_error("g1_from_device_jac: expected 24 limbs");
+    return P(g1_from_dev_jac(v.data()).marshal());
+  });
+  m.def("final_exp_selftest", [](int n, u64 seed) {
+    // the u-chain hard part against the generic 760-bit exponent on Miller-loop outputs
+    std::mt19937_64 rng(seed);
+    for (int i = 0; i < n; ++i) {
+      U256 a, b;
+      for (int w = 0; w < 4; ++w) { a.w[w] = rng(); b.w[w] = rng(); }
+      a.w[3] >>= 3; b.w[3] >>= 3;
+      const G1 P1 = G1::generator().mul(a);
+      const G2Prepared q = g2_prepare(G2::generator().mul(b));
+      const Fp12 f = miller_prepared({P1}, {&q});
+      if (!(final_exp_u(f) == final_exp_generic(f))) return false;
+    }
+    return true;
+  });
 
   // ---------------------------------------------------------------- VRF
   m.def("vrf_public_key", [](py::bytes seed) { return P(VrfKey::from_seed(B(seed)).pk); });

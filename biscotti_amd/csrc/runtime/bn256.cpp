@@ -463,12 +463,27 @@ Fp2 Fp2::sub(const Fp2& o) const { Fp2 r; Fp().sub(r.x, x, o.x); Fp().sub(r.y, y
 Fp2 Fp2::neg() const { Fp2 r; Fp().neg(r.x, x); Fp().neg(r.y, y); return r; }
 Fp2 Fp2::mul(const Fp2& o) const {
   // (x i + y)(ox i + oy) = (x oy + y ox) i + (y oy - x ox)
+  // Karatsuba: x oy + y ox = (x + y)(ox + oy) - x ox - y oy  (3 products)
   const MontField& F = Fp();
-  U256 a, b, c, d;
-  F.mul(a, x, o.y); F.mul(b, y, o.x); F.mul(c, y, o.y); F.mul(d, x, o.x);
+  U256 c, d, s1, s2, m;
+  F.mul(c, y, o.y); F.mul(d, x, o.x);
+  F.add(s1, x, y); F.add(s2, o.x, o.y);
+  F.mul(m, s1, s2);
   Fp2 r;
-  F.add(r.x, a, b);
+  F.sub(m, m, c);
+  F.sub(r.x, m, d);
   F.sub(r.y, c, d);
+  return r;
+}
+Fp2 Fp2::sqr() const {
+  // (x i + y)^2 = 2xy i + (y + x)(y - x)  (2 products)
+  const MontField& F = Fp();
+  U256 a, b, t;
+  F.add(a, y, x); F.sub(b, y, x);
+  Fp2 r;
+  F.mul(r.y, a, b);
+  F.mul(t, x, y);
+  F.add(r.x, t, t);
   return r;
 }
 Fp2 Fp2::mul_fp(const U256& s) const { Fp2 r; Fp().mul(r.x, x, s); Fp().mul(r.y, y, s); return r; }

@@ -119,7 +119,7 @@ struct Fp2 {
   Fp2 sub(const Fp2& o) const;
   Fp2 neg() const;
   Fp2 mul(const Fp2& o) const;
-  Fp2 sqr() const { return mul(*this); }
+  Fp2 sqr() const;
   Fp2 mul_fp(const U256& s) const;
   Fp2 inv() const;
 };

@@ -129,7 +129,7 @@ Fp12 miller(const U256& xP, const U256& yP, const Fp2& xQ, const Fp2& yQ) {
   return f;
 }
 
-Fp12 final_exp(const Fp12& f) {
+Fp12 final_exp_slow(const Fp12& f) {
   Fp12 a = f.conj6().mul(f.inv());   // f^(p^6 - 1)
   a = a.frob().frob().mul(a);         // ^(p^2 + 1)
   Fp12 r = a;
@@ -219,10 +219,156 @@ Fp12 multi_pairing(const std::vector<G1>& Ps, const std::vector<G2>& Qs) {
     Qs[i].to_affine(xQ, yQ);
     f = f.mul(miller(xP, yP, xQ, yQ));
   }
-  return final_exp(f);
+  return final_exp_u(f);
 }
 
 Fp12 pairing(const G1& P, const G2& Q) { return multi_pairing({P}, {Q}); }
+
+Fp12 Fp12::sqr() const {
+  Fp2 acc[11];
+  for (int i = 0; i < 6; ++i) {
+    if (c[i].is_zero()) continue;
+    acc[2 * i] = acc[2 * i].add(c[i].sqr());
+    for (int j = i + 1; j < 6; ++j) {
+      if (c[j].is_zero()) continue;
+      const Fp2 t = c[i].mul(c[j]);
+      acc[i + j] = acc[i + j].add(t.add(t));
+    }
+  }
+  Fp12 r;
+  for (int k = 0; k < 6; ++k) r.c[k] = acc[k];
+  for (int k = 6; k < 11; ++k) r.c[k - 6] = r.c[k - 6].add(mul_xi(acc[k]));
+  return r;
+}
+
+namespace {
+// f * (c0 + c1 w + c3 w^3) with c0 in Fp: the shape of every Miller-loop line (18 products, not 36)
+Fp12 mul_line(const Fp12& f, const U256& c0, const Fp2& c1, const Fp2& c3) {
+  Fp2 acc[9];
+  for (int i = 0; i < 6; ++i) {
+    acc[i] = acc[i].add(f.c[i].mul_fp(c0));
+    acc[i + 1] = acc[i + 1].add(f.c[i].mul(c1));
+    acc[i + 3] = acc[i + 3].add(f.c[i].mul(c3));
+  }
+  Fp12 r;
+  for (int k = 0; k < 6; ++k) r.c[k] = acc[k];
+  for (int k = 6; k < 9; ++k) r.c[k - 6] = r.c[k - 6].add(mul_xi(acc[k]));
+  return r;
+}
+
+// x^u, u = 6518589491078791937 (the BN parameter; 63 bits)
+Fp12 pow_u(const Fp12& x) {
+  const u64 u = 6518589491078791937ull;
+  Fp12 r = x;
+  for (int b = 61; b >= 0; --b) {
+    r = r.sqr();
+    if ((u >> b) & 1) r = r.mul(x);
+  }
+  return r;
+}
+}  // namespace
+
+Fp12 final_exp_generic(const Fp12& f) { return final_exp_slow(f); }
+
+// f^((p^12 - 1) / n).  Easy part f^((p^6 - 1)(p^2 + 1)) leaves the cyclotomic subgroup, where the
+// inverse is the p^6 conjugate; the hard part (p^4 - p^2 + 1)/n = l3 p^3 + l2 p^2 + l1 p + l0 with
+// l3 = 1, l2 = 6u^2 + 1, l1 = -36u^3 - 18u^2 - 12u + 1, l0 = -36u^3 - 30u^2 - 18u - 2 is evaluated as
+// y0 y1^2 y2^6 y3^12 y4^18 y5^30 y6^36 (Scott, Benger, Charlemagne, Dominguez Perez, Kachisa 2009):
+// 3 exponentiations by u instead of a 760-bit square-and-multiply.
+Fp12 final_exp_u(const Fp12& f) {
+  Fp12 a = f.conj6().mul(f.inv());
+  a = a.frob().frob().mul(a);
+  const Fp12 fu = pow_u(a), fu2 = pow_u(fu), fu3 = pow_u(fu2);
+  const Fp12 ap = a.frob(), ap2 = ap.frob(), ap3 = ap2.frob();
+  const Fp12 y0 = ap.mul(ap2).mul(ap3);
+  const Fp12 y1 = a.conj6();
+  const Fp12 y2 = fu2.frob().frob();
+  const Fp12 y3 = fu.frob().conj6();
+  const Fp12 y4 = fu.mul(fu2.frob()).conj6();
+  const Fp12 y5 = fu2.conj6();
+  const Fp12 y6 = fu3.mul(fu3.frob()).conj6();
+  Fp12 t0 = y6.sqr().mul(y4).mul(y5);
+  Fp12 t1 = y3.mul(y5).mul(t0);
+  t0 = t0.mul(y2);
+  t1 = t1.sqr().mul(t0);
+  t1 = t1.sqr();
+  t0 = t1.mul(y1);
+  t1 = t1.mul(y0);
+  t0 = t0.sqr();
+  return t0.mul(t1);
+}
+
+G2Prepared g2_prepare(const G2& Q) {
+  G2Prepared pr;
+  if (Q.is_inf()) { pr.inf = true; return pr; }
+  const Consts& k = K();
+  Fp2 xQ, yQ;
+  Q.to_affine(xQ, yQ);
+  Fp2 xT = xQ, yT = yQ;
+  auto add_step = [&](const Fp2& xR, const Fp2& yR) {
+    const Fp2 dx = xR.sub(xT);
+    if (dx.is_zero()) {   // vertical line (T = -R): a subfield element, dropped like in miller()
+      pr.lines.push_back({Fp2::zero(), Fp2::zero(), true});
+      xT = Fp2::zero();
+      yT = Fp2::zero();
+      return;
+    }
+    const Fp2 lam = yR.sub(yT).mul(dx.inv());
+    pr.lines.push_back({lam, lam.mul(xT).sub(yT), false});
+    const Fp2 x3 = lam.sqr().sub(xT).sub(xR);
+    yT = lam.mul(xT.sub(x3)).sub(yT);
+    xT = x3;
+  };
+  for (size_t i = 1; i < k.loop_bits.size(); ++i) {
+    const Fp2 x2 = xT.sqr();
+    const Fp2 lam = x2.add(x2).add(x2).mul(yT.add(yT).inv());
+    pr.lines.push_back({lam, lam.mul(xT).sub(yT), false});
+    const Fp2 x3 = lam.sqr().sub(xT).sub(xT);
+    yT = lam.mul(xT.sub(x3)).sub(yT);
+    xT = x3;
+    if (k.loop_bits[i]) add_step(xQ, yQ);
+  }
+  const Fp2 x1 = conj(xQ).mul(k.xi_pow[2]), y1 = conj(yQ).mul(k.xi_pow[3]);
+  const Fp2 x2 = conj(x1).mul(k.xi_pow[2]), y2 = conj(y1).mul(k.xi_pow[3]).neg();
+  add_step(x1, y1);
+  add_step(x2, y2);
+  return pr;
+}
+
+Fp12 miller_prepared(const std::vector<G1>& Ps, const std::vector<const G2Prepared*>& Qs) {
+  if (Ps.size() != Qs.size()) fail("miller_prepared: size mismatch");
+  const Consts& k = K();
+  struct Pair { U256 xP, yP; const G2Prepared* q; };
+  std::vector<Pair> pairs;
+  for (size_t i = 0; i < Ps.size(); ++i) {
+    if (Ps[i].is_inf() || Qs[i]->inf) continue;
+    Pair p;
+    Ps[i].to_affine(p.xP, p.yP);
+    p.q = Qs[i];
+    pairs.push_back(p);
+  }
+  Fp12 f = Fp12::one();
+  size_t li = 0;
+  auto apply = [&](size_t idx) {
+    for (const Pair& p : pairs) {
+      const auto& L = p.q->lines[idx];
+      if (L.skip) continue;
+      f = mul_line(f, p.yP, L.lam.mul_fp(p.xP).neg(), L.mu);
+    }
+  };
+  for (size_t i = 1; i < k.loop_bits.size(); ++i) {
+    if (i > 1) f = f.sqr();
+    apply(li++);
+    if (k.loop_bits[i]) apply(li++);
+  }
+  apply(li++);
+  apply(li++);
+  return f;
+}
+
+bool multi_pairing_is_one(const std::vector<G1>& Ps, const std::vector<const G2Prepared*>& Qs) {
+  return final_exp_u(miller_prepared(Ps, Qs)).is_one();
+}
 
 bool verify_secret(const G1& commitment, const G1& witness, const G2& g2_0, const G2& g2_1, i64 x, i64 y,
                    const G1& y_base) {

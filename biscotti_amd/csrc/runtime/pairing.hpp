@@ -22,7 +22,7 @@ struct Fp12 {
   bool is_one() const;
   bool operator==(const Fp12& o) const;
   Fp12 mul(const Fp12& o) const;
-  Fp12 sqr() const { return mul(*this); }
+  Fp12 sqr() const;           // 21 Fp2 products (symmetric schoolbook) instead of 36
   Fp12 inv() const;
   Fp12 frob() const;          // x -> x^p
   Fp12 conj6() const;         // x -> x^(p^6)
@@ -33,6 +33,22 @@ struct Fp12 {
 Fp12 pairing(const G1& P, const G2& Q);
 // prod_i e(P_i, Q_i) with one shared final exponentiation
 Fp12 multi_pairing(const std::vector<G1>& Ps, const std::vector<G2>& Qs);
+// Fixed G2 point with its Miller-loop line coefficients precomputed once (affine, so every
+// inversion happens here): the loop over a prepared point is one Fp12 squaring per bit plus a sparse
+// line product per step -- no inversions and no G2 arithmetic.  The KZG audit pairs against the three
+// fixed points G2, s*G2 and g2key[0], so they are prepared once per run.
+struct G2Prepared {
+  struct Line { Fp2 lam, mu; bool skip; };   // l(P) = yP - lam xP w + mu w^3,  mu = lam xT - yT
+  std::vector<Line> lines;
+  bool inf = false;
+};
+G2Prepared g2_prepare(const G2& Q);
+// prod_i e(P_i, Q_i) == 1 over prepared points: shared Fp12 squarings across the pairs and the
+// final exponentiation's hard part by the BN parameter u (Scott et al., 3 exponentiations by u).
+bool multi_pairing_is_one(const std::vector<G1>& Ps, const std::vector<const G2Prepared*>& Qs);
+Fp12 final_exp_u(const Fp12& f);     // exposed for the equality test against the generic exponent
+Fp12 final_exp_generic(const Fp12& f);
+Fp12 miller_prepared(const std::vector<G1>& Ps, const std::vector<const G2Prepared*>& Qs);
 // kyber.go:650-673 -- commitment C = f(s) G1, witness W = q(s) G1 with q = (f - y)/(X - x),
 // g2key[0] = G2, g2key[1] = s G2:   e(C, G2) == e(W, sG2 - xG2) * e(y_base, G2)^y.
 // The reference uses y_base = minerG1key[0] = G1, which is only consistent for chunk 0: chunk k is

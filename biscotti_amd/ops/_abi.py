@@ -28,6 +28,9 @@ SIGNATURES = {
     "bsc_marshal": [P, I, P, P],
     "bsc_to_affine": [P, I, P, P],
     "bsc_chunk_check": [P, I, I, P, I, I, P, I, I, P, P],
+    # kzg.hip
+    "bsc_kzg_blocks": [I, I],
+    "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, U64, P, P, P],
     # ml.hip
     "bsc_softmax_step": [P, P, P, P, P, P, I, I, I, I, U64, I, F, D, P, P, P, P],
     "bsc_logreg_step": [P, P, P, P, P, P, I, I, I, U64, P, D, D, P, D, P, P, P],

@@ -180,6 +180,33 @@ class DeviceCommitEngine:
                                      nm, self.nchunks, _ptr(ok), _stream()), "chunk_check")
         return ok
 
+    def kzg_rlc(self, csum: torch.Tensor, wsum: torch.Tensor, ys: torch.Tensor, xs: torch.Tensor, spm: int,
+                literal: bool, seed: int) -> torch.Tensor:
+        """G1 side of the batched verifySecret audit (kzg.hip): (L1, A, L2) Jacobian int32 [3, 24] with
+        e(L1, g2_0) e(-A, g2_1) e(L2, G2) == 1 iff (whp) every (chunk, share point) check holds.
+
+        csum [nch, 24] chunk commitments; wsum [(npts/spm) * nch * spm, 24] witnesses (miner-major,
+        chunk, share slot); ys int64 [nch, npts] share values at xs int32 [npts]; literal: pair y
+        against G1 for every chunk (the reference's verifySecret, quirk Q9) instead of PK[poly*k]."""
+        nch, npts = ys.shape
+        assert csum.dtype == torch.int32 and tuple(csum.shape) == (nch, 24) and nch == self.nchunks
+        assert wsum.dtype == torch.int32 and tuple(wsum.shape) == (nch * npts, 24)
+        assert ys.dtype == torch.int64 and xs.dtype == torch.int32 and xs.numel() == npts
+        assert spm > 0 and npts % spm == 0
+        if literal:
+            if getattr(self, "_g1_aff", None) is None:
+                self._g1_aff = u32_tensor(rt().g1_affine_mont_u32(rt().g1_generator()), self.device)
+            bases, stride = self._g1_aff, 0
+        else:
+            bases, stride = self.pk_aff, self.poly
+        lib = hip()
+        partial = torch.empty((lib.bsc_kzg_blocks(nch, npts), 72), dtype=torch.int32, device=self.device)
+        out = torch.empty((3, 24), dtype=torch.int32, device=self.device)
+        _check(lib.bsc_kzg_rlc(_ptr(csum.contiguous()), _ptr(wsum.contiguous()), _ptr(ys.contiguous()),
+                               _ptr(xs.contiguous()), nch, npts, int(spm), _ptr(bases), stride,
+                               int(seed) & ((1 << 64) - 1), _ptr(partial), _ptr(out), _stream()), "kzg_rlc")
+        return out
+
     def commitments(self, pts: torch.Tensor) -> torch.Tensor:
         """Full-vector commitment per row = sum of its chunk commitments. Returns Jacobian [n, 24]."""
         n, nch, S, _ = pts.shape

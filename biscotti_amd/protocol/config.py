@@ -82,6 +82,11 @@ class RunConfig:
     krum_pregram: bool = True       # one rank, table noise: Krum's Gram over [deltas; noise vectors] runs
     #                                 before the VRF outputs arrive; only an O(n^2) assembly waits for them
     join_background: bool = False   # main stream waits for the background (witness-sum) work each round
+    kzg_audit: str = "off"          # batched verifySecret (kyber.go:650-673) over every (chunk, share point) of
+    #                                 the aggregate: off | consistent (y against PK[poly*k]) | literal (y
+    #                                 against G1: the reference's formula, which only chunk 0 satisfies, Q9).
+    #                                 Device RLC sums (kzg.hip) + one host 3-pairing product per round,
+    #                                 joined lazily; failures are counted and logged, never block the chain
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
     #                                 (shortens the GPU chain; costs host time before the previous round ends)
 
@@ -122,6 +127,8 @@ class RunConfig:
             err.append("noisers: at most 16 and fewer than the nodes")
         if not 0.0 <= self.poisoning < 1.0 or not 0.0 <= self.churn < 1.0:
             err.append("poisoning / churn fractions must be in [0, 1)")
+        if self.kzg_audit not in ("off", "consistent", "literal"):
+            err.append(f"kzg_audit {self.kzg_audit!r}: expected off | consistent | literal")
         if err:
             raise ValueError("invalid RunConfig: " + "; ".join(err))
 
@@ -200,6 +207,8 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--no-phase-sync", dest="phase_sync", action="store_false")
     ap.add_argument("--no-audit-aggregate", dest="audit_aggregate", action="store_false")
     ap.add_argument("--no-noise-table", dest="noise_table", action="store_false")
+    ap.add_argument("--kzg-audit", default="off", choices=["off", "consistent", "literal"],
+                    help="batched verifySecret over each round's aggregate (K13)")
     ap.add_argument("--comm-timeout", dest="comm_timeout_s", type=float, default=300.0)
     ap.add_argument("--fail-at", type=int, default=-1, help="fault injection: die after committing this iteration")
     ap.add_argument("--fail-rank", type=int, default=0)

@@ -357,6 +357,12 @@ class BiscottiEngine:
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
+        # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
+        self._kzg_pending: list = []
+        if cfg.kzg_audit != "off":
+            self.stats.update(kzg_checks=0, kzg_failures=0)
+            self._kzg_g2 = (self.R.g2_generator(), self._commit_key_g2_1(cfg.commit_key))
+            self._kzg_rng = np.random.default_rng([cfg.seed, self.comm.rank, 0x6B7A67])
         self._churn = {"down": {}, "view": {}, "epoch": {}, "acc": 0.0, "kills": 0, "rejoins": 0,
                        "synced_blocks": 0}
         self.stats["churn"] = self._churn
@@ -374,8 +380,71 @@ class BiscottiEngine:
         gc.freeze()
 
     # ------------------------------------------------------------------ lifecycle
+    def _commit_key_g2_1(self, path):
+        """s G2 -- commitKey.json's Skey of Id 1 (publicKey.go:26-61), or 2 G2 for the generated key."""
+        if path:
+            import base64
+            import json
+            with open(path) as f:
+                for ln in f:
+                    if ln.strip():
+                        rec = json.loads(ln)
+                        if rec.get("Id") == 1:
+                            return base64.b64decode(rec["Skey"])
+            raise ValueError(f"{path}: no commit key record with Id 1")
+        return self.R.g2_mul(self.R.g2_generator(), 2)
+
+    def _kzg_queue(self, csum, wsum, ys, xs_t, it) -> None:
+        """Queue the device RLC sums of this round's aggregate on the current stream; their read-back
+        and the host pairing product run later (_kzg_poll), off the round's critical path."""
+        spm = self.pc.shares_per_miner
+        seed = int(self._kzg_rng.integers(0, 2**63))
+        pts = self.crypto.eng.kzg_rlc(csum, wsum, ys, xs_t, spm, self.cfg.kzg_audit == "literal", seed)
+        host = torch.empty((3, 24), dtype=torch.int32, pin_memory=True)
+        host.copy_(pts, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(S.current())
+        self._kzg_pending.append({"it": it, "ev": ev, "host": host, "job": None})
+
+    def _kzg_host(self, cs, ws, ys, xs, it) -> None:
+        """CPU path: the same random linear combination on the host (native threads)."""
+        nch, npts = ys.shape
+        spm = self.pc.shares_per_miner
+        C = [bytes(c) for c in cs.numpy()]
+        Wm = [bytes(w) for w in ws.numpy()]
+        W = [Wm[(j // spm) * nch * spm + k * spm + j % spm] for k in range(nch) for j in range(npts)]
+        bases = [self.R.g1_generator()] if self.cfg.kzg_audit == "literal" else \
+            [self.crypto.key.point(self.cfg.poly_size * k) for k in range(nch)]
+        pts = self.R.kzg_rlc_host(C, W, ys.numpy().reshape(-1), list(xs), bases,
+                                  int(self._kzg_rng.integers(0, 2**63)), self.cfg.host_threads)
+        self._kzg_pending.append({"it": it, "ok": self.R.kzg_check(*pts, *self._kzg_g2)})
+
+    def _kzg_poll(self, final: bool = False) -> None:
+        """Start the pairing products whose device sums are ready and collect finished ones (all of
+        them when final, or when more than 4 are outstanding)."""
+        keep = []
+        for i, e in enumerate(self._kzg_pending):
+            must = final or len(self._kzg_pending) - i > 4
+            if "ok" not in e and e["job"] is None and (must or e["ev"].query()):
+                e["ev"].synchronize()
+                e["job"] = self.R.kzg_check_device_async(e["host"].numpy().view(np.uint32), *self._kzg_g2)
+            if "ok" not in e and e["job"] is not None and must:
+                e["ok"] = e["job"].result()
+            if "ok" in e:
+                self.stats["kzg_checks"] += 1
+                if not e["ok"]:
+                    self.stats["kzg_failures"] += 1
+                    self.log.info("KZG audit (verifySecret, %s) failed for the aggregate of iteration %d",
+                                  self.cfg.kzg_audit, e["it"])
+            else:
+                keep.append(e)
+        self._kzg_pending = keep
+
     def drain(self) -> None:
-        """Join host work that belongs to rounds already returned (the last roles-VRF batch)."""
+        """Join host work that belongs to rounds already returned (the last roles-VRF batch, the
+        outstanding KZG audits)."""
+        if self._kzg_pending:
+            self._kzg_poll(final=True)
         futs, self._pending_roles = getattr(self, "_pending_roles", None), None
         for fut in futs or ():
             if fut is not None:
@@ -1019,7 +1088,9 @@ class BiscottiEngine:
         cfg, comm = self.cfg, self.comm
         T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
         audit = cfg.audit_aggregate
+        kzg = cfg.kzg_audit != "off"
         (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
+        kzg_in = None   # this rank's (commitment sums, witness sums, share sums) for the KZG audit
         main = S.current() if self.gpu else None
         # ---- this rank's partial sums
         single = comm.world == 1
@@ -1043,22 +1114,31 @@ class BiscottiEngine:
                     ys_part = (ys * mask.view(-1, 1, 1)).sum(0)
                 else:
                     ys_part = ys.index_select(0, rows_t.long()).sum(0)
-                if audit:
+                ws_part = None
+                if audit or kzg:
                     st = self.side_stream if comm.world == 1 else main
                     if st is not main:
                         S.wait(st, main)
                     with S.use(st):
                         cs_part = B.sum_rows(flat, rows_t, ccols, check=False, row_mask=mask)
+                        if kzg:   # the witness sums get a consumer: the audit's RLC
+                            ws_part = B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask)
                     if st is not main:
-                        for t in (pts, ccols) + ((mask,) if mask is not None else (rows_t,)):
+                        for t in (pts, ccols, wcols) + ((mask,) if mask is not None else (rows_t,)):
                             t.record_stream(st)
-                self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
-                                 flat, wcols, mask if mask is not None else rows_t)
+                if not kzg:
+                    self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
+                                     flat, wcols, mask if mask is not None else rows_t)
+                else:
+                    kzg_in = (cs_part, ws_part, None if single else ys_part.index_select(1, ycols_t.long()))
             else:
                 rows_l = list(rowsel)
                 ys_part = ys[rows_l].sum(0)
-                if audit:
+                if audit or kzg:
                     cs_part = self.crypto.sum_rows(flat[rows_l][:, ccols.long()])
+                if kzg:
+                    kzg_in = (cs_part, self.crypto.sum_rows(flat[rows_l][:, wcols.long()]),
+                              ys_part.index_select(1, ycols_t.long()))
         if audit and cs_part is None:   # no local rows: the neutral element (point at infinity)
             cs_part = torch.zeros((nch, pw), dtype=pdt, device=self.dev)
         # ---- combine over ranks: ONE all_gather (share sums, commitment sums, clock)
@@ -1086,6 +1166,21 @@ class BiscottiEngine:
             agg = ys_tot.index_select(1, ycols_t.long()).contiguous()   # [nch, npts]
             W_new, coeffs, status = K.recover(agg, xs_t.cpu(), cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
         audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
+        if kzg_in is not None:
+            # each rank audits its own partial aggregate: verifySecret is linear in (C, W, y), so the
+            # partial sums of honest shares satisfy it exactly like the total does
+            cs_k, ws_k, y_k = kzg_in
+            if self.gpu:
+                y_k = agg if y_k is None else y_k
+                bg = self.bg_stream
+                S.wait(bg, main)
+                S.wait(bg, self.side_stream)
+                with S.use(bg):
+                    self._kzg_queue(cs_k, ws_k, y_k, xs_t, self.fsm.iteration)
+                for t in (cs_k, ws_k, y_k, xs_t):
+                    t.record_stream(bg)
+            else:
+                self._kzg_host(cs_k, ws_k, y_k, xs_list, self.fsm.iteration)
         return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
                 "clock": clock, "now": now}
 
@@ -1247,6 +1342,8 @@ class BiscottiEngine:
                               int((ok == 0).sum()), plan.iteration)
                 return None
         self._last_nodes = node_list
+        if self._kzg_pending:
+            self._kzg_poll()
         return block
 
     # ------------------------------------------------------------------ plain aggregation path

@@ -319,3 +319,30 @@ def test_vrf_two_phase_outputs_match_full_proofs(rt):
     assert betas == [b for b, _ in full]
     for s, (b, pi) in zip(seeds, full):
         assert (b, pi) == tuple(rt.vrf_prove(s, alpha))
+
+
+def test_batched_kzg_check_host(rt):
+    """K13 on the host: the u-chain final exponentiation equals the generic exponent; the random
+    linear combination of every (chunk, point) verifySecret accepts exactly when each check does."""
+    import numpy as np
+
+    assert rt.final_exp_selftest(2, 11)
+    s = 3
+    key = rt.CommitKey.generate(35, s)
+    coeffs = np.random.default_rng(5).integers(-10**5, 10**5, size=35)
+    _, cc, ys, wits = key.make_shares(coeffs, 10, 21)
+    g2 = rt.g2_generator()
+    g2s = rt.g2_mul(g2, s)
+    xs = [t - 10 for t in range(21)]
+    bases = [key.point(10 * k) for k in range(len(cc))]
+    pts = rt.kzg_rlc_host(cc, wits, ys.reshape(-1), xs, bases, 42, 2)
+    assert rt.kzg_check(*pts, g2, g2s)
+    bad = list(wits)
+    bad[30] = wits[31]
+    assert not rt.kzg_check(*rt.kzg_rlc_host(cc, bad, ys.reshape(-1), xs, bases, 42, 2), g2, g2s)
+    y2 = ys.copy()
+    y2[2, 7] -= 1
+    assert not rt.kzg_check(*rt.kzg_rlc_host(cc, wits, y2.reshape(-1), xs, bases, 42, 2), g2, g2s)
+    # literal form (y against G1): chunk 0 only
+    assert rt.kzg_check(*rt.kzg_rlc_host(cc[:1], wits[:21], ys[:1].reshape(-1), xs, [rt.g1_generator()], 7, 1), g2, g2s)
+    assert not rt.kzg_check(*rt.kzg_rlc_host(cc, wits, ys.reshape(-1), xs, [rt.g1_generator()], 7, 1), g2, g2s)

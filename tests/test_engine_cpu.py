@@ -121,3 +121,19 @@ def test_process_churn_rejoin_with_chain_sync():
     ok, why = eng.fsm.chain.verify()
     assert ok, why
     assert sum(not r.empty for r in res) >= 5
+
+
+@pytest.mark.parametrize("mode", ["consistent", "literal"])
+def test_kzg_audit_rounds(mode):
+    """Batched verifySecret over each round's aggregate (K13): the consistent check passes every
+    round; the reference's literal formula (y against G1) fails as soon as there is a second chunk
+    (creditcard: d = 25, 3 chunks) -- quirk Q9.  Failures are reported, the chain is unaffected."""
+    eng = BiscottiEngine(_cfg(num_nodes=6, kzg_audit=mode))
+    res = [eng.run_round() for _ in range(4)]
+    eng.drain()
+    blocks = sum(1 for r in res if not r.empty)
+    assert blocks >= 3
+    assert eng.stats["kzg_checks"] == blocks
+    assert eng.stats["kzg_failures"] == (0 if mode == "consistent" else blocks)
+    assert eng.fsm.chain.verify()[0]
+    eng.close()
