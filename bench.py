@@ -71,6 +71,8 @@ PRESETS = {
     # the long-parameter-vector ledger: LFW maleness softmax, d = 17486 (no reference number:
     # the reference's lfw pipeline is inconsistent, see data.dataset_dims)
     "lfw100": ({"dataset": "lfw"}, None, None, {}, "honest.go:211 'mnist/lfw for pytorch' (unpinned)"),
+    # headline + the batched verifySecret audit of every aggregate (K13; not on the reference's path)
+    "kzg_audit": ({"kzg_audit": "consistent"}, 29.83, 0.877, {}, "nsdi-eval/scaleup/bis_baseline_100 + K13 audit"),
     "scale40": ({"num_nodes": 40}, 23.87, None, {}, "nsdi-eval/increments/results.log:2"),
     "scale60": ({"num_nodes": 60}, 34.05, None, {}, "nsdi-eval/increments/results.log:3"),
     "scale80": ({"num_nodes": 80}, 48.07, None, {}, "nsdi-eval/increments/results.log:4"),

@@ -1,0 +1,637 @@
+// ECVRF-EDWARDS25519-SHA512-TAI proofs (RFC 9381) on gfx950 -- the VRF proofs the protocol
+// computes but never consumes: the roles proof of getVRFRoles (quirk Q7) and the proof half of every
+// worker's noiser VRF (vrf.go:54-100; the lottery reads only the 64-byte output, which the host
+// computes on the critical path).  The host runtime (runtime/vrf.cpp) is the bit-exact oracle.
+//
+// One thread per proof, everything on the device: SHA-512 (try-and-increment hash to curve, nonce,
+// challenge), GF(2^255 - 19) arithmetic, point decompression, x*H and k*H over ONE signed radix-16
+// table of H (the two variable-base multiplications share it), k*B over a resident fixed-base
+// table (64 windows x 8 multiples, uploaded once), one field inversion for the three point
+// encodings, and the scalar arithmetic mod L.
+//
+// Field elements: 10 unsigned 32-bit limbs in radix 2^25.5 (26, 25, 26, ... bits).  A product is
+// 100 32x32->64 multiply-adds (v_mad_u64_u32) into 64-bit column sums, then one carry chain; the
+// wrap-around 2^255 = 19 is folded into the multiplicands (19 g_j), and the odd-odd products carry
+// an extra factor 2 (2^26 * 2^25 = 2^51 = 2 * 2^50.5...).  Limbs stay non-negative: subtraction adds
+// 4p first.  Bounds: carried limbs are < 2^26 + 2^9, so a column sum is < 2^62.
+//
+// The batch is a whole round's (or several rounds') proofs: ~200-800 threads, a few waves; the
+// kernel runs on a low-priority stream while the protocol's critical path owns the rest of the GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__constant__ static const unsigned long long K512[80] = {
+    0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
+    0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
+    0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
+    0x72be5d74f27b896full, 0x80deb1fe3b1696b1ull, 0x9bdc06a725c71235ull, 0xc19bf174cf692694ull,
+    0xe49b69c19ef14ad2ull, 0xefbe4786384f25e3ull, 0x0fc19dc68b8cd5b5ull, 0x240ca1cc77ac9c65ull,
+    0x2de92c6f592b0275ull, 0x4a7484aa6ea6e483ull, 0x5cb0a9dcbd41fbd4ull, 0x76f988da831153b5ull,
+    0x983e5152ee66dfabull, 0xa831c66d2db43210ull, 0xb00327c898fb213full, 0xbf597fc7beef0ee4ull,
+    0xc6e00bf33da88fc2ull, 0xd5a79147930aa725ull, 0x06ca6351e003826full, 0x142929670a0e6e70ull,
+    0x27b70a8546d22ffcull, 0x2e1b21385c26c926ull, 0x4d2c6dfc5ac42aedull, 0x53380d139d95b3dfull,
+    0x650a73548baf63deull, 0x766a0abb3c77b2a8ull, 0x81c2c92e47edaee6ull, 0x92722c851482353bull,
+    0xa2bfe8a14cf10364ull, 0xa81a664bbc423001ull, 0xc24b8b70d0f89791ull, 0xc76c51a30654be30ull,
+    0xd192e819d6ef5218ull, 0xd69906245565a910ull, 0xf40e35855771202aull, 0x106aa07032bbd1b8ull,
+    0x19a4c116b8d2d0c8ull, 0x1e376c085141ab53ull, 0x2748774cdf8eeb99ull, 0x34b0bcb5e19b48a8ull,
+    0x391c0cb3c5c95a63ull, 0x4ed8aa4ae3418acbull, 0x5b9cca4f7763e373ull, 0x682e6ff3d6b2b8a3ull,
+    0x748f82ee5defb2fcull, 0x78a5636f43172f60ull, 0x84c87814a1f0ab72ull, 0x8cc702081a6439ecull,
+    0x90befffa23631e28ull, 0xa4506cebde82bde9ull, 0xbef9a3f7b2c67915ull, 0xc67178f2e372532bull,
+    0xca273eceea26619cull, 0xd186b8c721c0c207ull, 0xeada7dd6cde0eb1eull, 0xf57d4f7fee6ed178ull,
+    0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
+    0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
+    0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull,
+};
+__constant__ static const unsigned long long H512[8] = {
+    0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
+    0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull,
+};
+
+__device__ __forceinline__ unsigned long long rotr64(unsigned long long x, int n) { return (x >> n) | (x << (64 - n)); }
+
+struct Sha512 {
+  unsigned long long h[8];
+  uint8_t buf[128];
+  int blen;
+  unsigned long long total;
+};
+
+__device__ void sha_compress(Sha512& s) {
+  unsigned long long w[80];
+  for (int i = 0; i < 16; ++i) {
+    unsigned long long v = 0;
+    for (int b = 0; b < 8; ++b) v = (v << 8) | s.buf[8 * i + b];
+    w[i] = v;
+  }
+  for (int i = 16; i < 80; ++i) {
+    const unsigned long long s0 = rotr64(w[i - 15], 1) ^ rotr64(w[i - 15], 8) ^ (w[i - 15] >> 7);
+    const unsigned long long s1 = rotr64(w[i - 2], 19) ^ rotr64(w[i - 2], 61) ^ (w[i - 2] >> 6);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  unsigned long long a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+  for (int i = 0; i < 80; ++i) {
+    const unsigned long long S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    const unsigned long long ch = (e & f) ^ (~e & g);
+    const unsigned long long t1 = h + S1 + ch + K512[i] + w[i];
+    const unsigned long long S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    const unsigned long long mj = (a & b) ^ (a & c) ^ (b & c);
+    const unsigned long long t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d; s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+__device__ void sha_init(Sha512& s) {
+  for (int i = 0; i < 8; ++i) s.h[i] = H512[i];
+  s.blen = 0;
+  s.total = 0;
+}
+__device__ void sha_byte(Sha512& s, uint8_t v) {
+  s.buf[s.blen++] = v;
+  s.total += 1;
+  if (s.blen == 128) {
+    sha_compress(s);
+    s.blen = 0;
+  }
+}
+__device__ void sha_bytes(Sha512& s, const uint8_t* p, int n) {
+  for (int i = 0; i < n; ++i) sha_byte(s, p[i]);
+}
+__device__ void sha_words(Sha512& s, const uint32_t* w, int nw) {   // little-endian words as bytes
+  for (int i = 0; i < nw; ++i)
+    for (int b = 0; b < 4; ++b) sha_byte(s, (uint8_t)(w[i] >> (8 * b)));
+}
+__device__ void sha_final(Sha512& s, uint8_t out[64]) {
+  const unsigned long long bits = s.total * 8;
+  sha_byte(s, 0x80);
+  while (s.blen != 112) sha_byte(s, 0);
+  for (int b = 0; b < 8; ++b) sha_byte(s, 0);          // high 64 bits of the 128-bit length
+  for (int b = 7; b >= 0; --b) sha_byte(s, (uint8_t)(bits >> (8 * b)));
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 8; ++b) out[8 * i + b] = (uint8_t)(s.h[i] >> (56 - 8 * b));
+}
+
+// ---------------------------------------------------------------- GF(2^255 - 19)
+struct fe { uint32_t v[10]; };
+__device__ __forceinline__ constexpr int fw(int i) { return (i & 1) ? 25 : 26; }
+
+__device__ __forceinline__ fe fe_small(uint32_t a) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.v[i] = 0;
+  r.v[0] = a;
+  return r;
+}
+__device__ __forceinline__ void fe_carry(fe& r) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t c = r.v[i] >> fw(i);
+    r.v[i] &= (1u << fw(i)) - 1;
+    if (i < 9) r.v[i + 1] += c;
+    else r.v[0] += 19 * c;
+  }
+}
+__device__ __forceinline__ fe fe_add(const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] + b.v[i];
+  fe_carry(r);
+  return r;
+}
+__device__ __forceinline__ fe fe_sub(const fe& a, const fe& b) {
+  fe r;   // a + 4p - b
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t p4 = i == 0 ? 0x0FFFFFB4u : ((i & 1) ? 0x07FFFFFCu : 0x0FFFFFFCu);
+    r.v[i] = a.v[i] + p4 - b.v[i];
+  }
+  fe_carry(r);
+  return r;
+}
+__device__ __forceinline__ fe fe_neg(const fe& a) { return fe_sub(fe_small(0), a); }
+
+__device__ fe fe_mul(const fe& f, const fe& g) {
+  uint32_t g19[10], f2[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    g19[i] = 19 * g.v[i];
+    f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
+  }
+  unsigned long long h[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      const uint32_t b = (i + j >= 10) ? g19[j] : g.v[j];
+      h[(i + j) % 10] += (unsigned long long)a * b;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned long long c = h[i] >> fw(i);
+    h[i] &= (1ull << fw(i)) - 1;
+    if (i < 9) h[i + 1] += c;
+    else h[0] += 19 * c;
+  }
+  const unsigned long long c = h[0] >> 26;
+  h[0] &= (1ull << 26) - 1;
+  h[1] += c;
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.v[i] = (uint32_t)h[i];
+  return r;
+}
+__device__ __forceinline__ fe fe_sq(const fe& a) { return fe_mul(a, a); }
+__device__ fe fe_sqn(fe a, int n) {
+  for (int i = 0; i < n; ++i) a = fe_sq(a);
+  return a;
+}
+
+// canonical little-endian 255-bit value as 8 words
+__device__ void fe_tobytes(uint32_t out[8], fe a) {
+  fe_carry(a);
+  fe_carry(a);
+  uint32_t q = (a.v[0] + 19) >> 26;
+#pragma unroll
+  for (int i = 1; i < 10; ++i) q = (a.v[i] + q) >> fw(i);
+  a.v[0] += 19 * q;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint32_t c = a.v[i] >> fw(i);
+    a.v[i] &= (1u << fw(i)) - 1;
+    a.v[i + 1] += c;
+  }
+  a.v[9] &= (1u << 25) - 1;
+  unsigned long long acc = 0;
+  int bits = 0, o = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    acc |= (unsigned long long)a.v[i] << bits;
+    bits += fw(i);
+    if (bits >= 32) {
+      out[o++] = (uint32_t)acc;
+      acc >>= 32;
+      bits -= 32;
+    }
+  }
+  out[7] = (uint32_t)acc;
+}
+__device__ fe fe_frombytes(const uint32_t w[8]) {   // bit 255 ignored
+  fe r;
+  int off = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const int wi = off >> 5, sh = off & 31;
+    const unsigned long long lo = w[wi], hi = wi + 1 < 8 ? w[wi + 1] : 0u;
+    r.v[i] = (uint32_t)(((hi << 32) | lo) >> sh) & ((1u << fw(i)) - 1);
+    off += fw(i);
+  }
+  return r;
+}
+__device__ bool fe_eq(const fe& a, const fe& b) {
+  uint32_t x[8], y[8];
+  fe_tobytes(x, a);
+  fe_tobytes(y, b);
+  uint32_t o = 0;
+  for (int i = 0; i < 8; ++i) o |= x[i] ^ y[i];
+  return o == 0;
+}
+__device__ bool fe_isneg(const fe& a) {
+  uint32_t x[8];
+  fe_tobytes(x, a);
+  return x[0] & 1;
+}
+__device__ bool fe_iszero(const fe& a) { return fe_eq(a, fe_small(0)); }
+__device__ fe fe_invert(const fe& z) {   // z^(p-2)
+  fe t0 = fe_sq(z);
+  fe t1 = fe_sqn(t0, 2);
+  t1 = fe_mul(z, t1);
+  t0 = fe_mul(t0, t1);
+  fe t2 = fe_sq(t0);
+  t1 = fe_mul(t1, t2);
+  t2 = fe_sqn(t1, 5);
+  t1 = fe_mul(t2, t1);
+  t2 = fe_sqn(t1, 10);
+  t2 = fe_mul(t2, t1);
+  fe t3 = fe_sqn(t2, 20);
+  t2 = fe_mul(t3, t2);
+  t2 = fe_sqn(t2, 10);
+  t1 = fe_mul(t2, t1);
+  t2 = fe_sqn(t1, 50);
+  t2 = fe_mul(t2, t1);
+  t3 = fe_sqn(t2, 100);
+  t2 = fe_mul(t3, t2);
+  t2 = fe_sqn(t2, 50);
+  t1 = fe_mul(t2, t1);
+  t1 = fe_sqn(t1, 5);
+  return fe_mul(t1, t0);
+}
+__device__ fe fe_pow22523(const fe& z) {   // z^((p-5)/8)
+  fe t0 = fe_sq(z);
+  fe t1 = fe_sqn(t0, 2);
+  t1 = fe_mul(z, t1);
+  t0 = fe_mul(t0, t1);
+  t0 = fe_sq(t0);
+  t0 = fe_mul(t1, t0);
+  t1 = fe_sqn(t0, 5);
+  t0 = fe_mul(t1, t0);
+  t1 = fe_sqn(t0, 10);
+  t1 = fe_mul(t1, t0);
+  fe t2 = fe_sqn(t1, 20);
+  t1 = fe_mul(t2, t1);
+  t1 = fe_sqn(t1, 10);
+  t0 = fe_mul(t1, t0);
+  t1 = fe_sqn(t0, 50);
+  t1 = fe_mul(t1, t0);
+  t2 = fe_sqn(t1, 100);
+  t1 = fe_mul(t2, t1);
+  t1 = fe_sqn(t1, 50);
+  t0 = fe_mul(t1, t0);
+  t0 = fe_sqn(t0, 2);
+  return fe_mul(t0, z);
+}
+
+__constant__ static const uint32_t C_D[8] = {0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du,
+                                             0x7779e898u, 0x8cc74079u, 0x2b6ffe73u, 0x52036ceeu};
+__constant__ static const uint32_t C_D2[8] = {0x26b2f159u, 0xebd69b94u, 0x8283b156u, 0x00e0149au,
+                                              0xeef3d130u, 0x198e80f2u, 0x56dffce7u, 0x2406d9dcu};
+__constant__ static const uint32_t C_SQRTM1[8] = {0x4a0ea0b0u, 0xc4ee1b27u, 0xad2fe478u, 0x2f431806u,
+                                                  0x3dfbd7a7u, 0x2b4d0099u, 0x4fc1df0bu, 0x2b832480u};
+__device__ __forceinline__ fe fe_const(const uint32_t* c) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i) w[i] = c[i];
+  return fe_frombytes(w);
+}
+
+// ---------------------------------------------------------------- edwards25519 points
+struct ge { fe X, Y, Z, T; };
+struct gc { fe YpX, YmX, Z2, T2d; };   // cached form: an addition is 8 products
+
+__device__ ge ge_identity() { return ge{fe_small(0), fe_small(1), fe_small(1), fe_small(0)}; }
+__device__ gc ge_cache(const ge& p, const fe& d2) {
+  return gc{fe_add(p.Y, p.X), fe_sub(p.Y, p.X), fe_add(p.Z, p.Z), fe_mul(p.T, d2)};
+}
+__device__ ge ge_add_cached(const ge& p, const gc& q) {
+  const fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
+  const fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
+  const fe C = fe_mul(p.T, q.T2d);
+  const fe D = fe_mul(p.Z, q.Z2);
+  const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), fe_mul(E, H)};
+}
+__device__ ge ge_dbl(const ge& p, bool withT) {   // dbl-2008-hwcd, a = -1
+  const fe A = fe_sq(p.X), B = fe_sq(p.Y);
+  const fe zz = fe_sq(p.Z);
+  const fe C = fe_add(zz, zz);
+  const fe D = fe_neg(A);
+  const fe E = fe_sub(fe_sub(fe_sq(fe_add(p.X, p.Y)), A), B);
+  const fe G = fe_add(D, B), F = fe_sub(G, C), H = fe_sub(D, B);
+  return ge{fe_mul(E, F), fe_mul(G, H), fe_mul(F, G), withT ? fe_mul(E, H) : fe_small(0)};
+}
+__device__ gc gc_neg(const gc& c) { return gc{c.YmX, c.YpX, c.Z2, fe_neg(c.T2d)}; }
+
+__device__ void st_fe(uint32_t* p, const fe& a) {
+  for (int i = 0; i < 10; ++i) p[i] = a.v[i];
+}
+__device__ fe ld_fe(const uint32_t* p) {
+  fe r;
+  for (int i = 0; i < 10; ++i) r.v[i] = p[i];
+  return r;
+}
+__device__ void st_gc(uint32_t* p, const gc& c) {
+  st_fe(p, c.YpX); st_fe(p + 10, c.YmX); st_fe(p + 20, c.Z2); st_fe(p + 30, c.T2d);
+}
+__device__ gc ld_gc(const uint32_t* p) { return gc{ld_fe(p), ld_fe(p + 10), ld_fe(p + 20), ld_fe(p + 30)}; }
+
+// scalar (8 LE words, < 2^255) -> 64 signed radix-16 digits in [-8, 8)
+__device__ void signed_digits(int8_t e[64], const uint32_t k[8]) {
+  for (int i = 0; i < 64; ++i) e[i] = (int8_t)((k[i >> 3] >> (4 * (i & 7))) & 15);
+  int carry = 0;
+  for (int i = 0; i < 63; ++i) {
+    e[i] = (int8_t)(e[i] + carry);
+    carry = (e[i] + 8) >> 4;
+    e[i] = (int8_t)(e[i] - (carry << 4));
+  }
+  e[63] = (int8_t)(e[63] + carry);
+}
+// k * P with P's table (1P..8P, cached) already in `tbl` (global scratch of this thread)
+__device__ ge ge_mul_tbl(const uint32_t* tbl, const uint32_t k[8]) {
+  int8_t e[64];
+  signed_digits(e, k);
+  ge r = ge_identity();
+  for (int w = 63; w >= 0; --w) {
+    if (w != 63) {
+      r = ge_dbl(r, false);
+      r = ge_dbl(r, false);
+      r = ge_dbl(r, false);
+      r = ge_dbl(r, true);
+    }
+    const int d = e[w];
+    if (d > 0) r = ge_add_cached(r, ld_gc(tbl + (d - 1) * 40));
+    else if (d < 0) r = ge_add_cached(r, gc_neg(ld_gc(tbl + (-d - 1) * 40)));
+  }
+  return r;
+}
+// fixed base: btab[w * 8 + d - 1] = d * 16^w * B in cached form, 4 canonical fe encodings (32 words)
+__device__ gc ld_btab(const uint32_t* btab, int idx) {
+  const uint32_t* p = btab + idx * 32;
+  uint32_t w[8];
+  gc c;
+  for (int i = 0; i < 8; ++i) w[i] = p[i];
+  c.YpX = fe_frombytes(w);
+  for (int i = 0; i < 8; ++i) w[i] = p[8 + i];
+  c.YmX = fe_frombytes(w);
+  for (int i = 0; i < 8; ++i) w[i] = p[16 + i];
+  c.Z2 = fe_frombytes(w);
+  for (int i = 0; i < 8; ++i) w[i] = p[24 + i];
+  c.T2d = fe_frombytes(w);
+  return c;
+}
+__device__ ge ge_mul_base(const uint32_t* btab, const uint32_t k[8]) {
+  int8_t e[64];
+  signed_digits(e, k);
+  ge r = ge_identity();
+  for (int w = 0; w < 64; ++w) {
+    const int d = e[w];
+    if (d > 0) r = ge_add_cached(r, ld_btab(btab, w * 8 + d - 1));
+    else if (d < 0) r = ge_add_cached(r, gc_neg(ld_btab(btab, w * 8 - d - 1)));
+  }
+  return r;
+}
+// RFC 8032 5.1.3 decoding (non-canonical y rejected)
+__device__ bool ge_frombytes(ge& out, const uint8_t in[32], const fe& d) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; ++i)
+    w[i] = (uint32_t)in[4 * i] | ((uint32_t)in[4 * i + 1] << 8) | ((uint32_t)in[4 * i + 2] << 16) |
+           ((uint32_t)in[4 * i + 3] << 24);
+  const int sign = w[7] >> 31;
+  w[7] &= 0x7fffffffu;
+  const fe y = fe_frombytes(w);
+  uint32_t chk[8];
+  fe_tobytes(chk, y);
+  uint32_t o = 0;
+  for (int i = 0; i < 8; ++i) o |= chk[i] ^ w[i];
+  if (o) return false;
+  const fe y2 = fe_sq(y);
+  const fe u = fe_sub(y2, fe_small(1));
+  const fe v = fe_add(fe_mul(d, y2), fe_small(1));
+  const fe v3 = fe_mul(fe_sq(v), v);
+  const fe v7 = fe_mul(fe_sq(v3), v);
+  fe x = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
+  const fe vx2 = fe_mul(v, fe_sq(x));
+  if (!fe_eq(vx2, u)) {
+    if (fe_eq(vx2, fe_neg(u))) x = fe_mul(x, fe_const(C_SQRTM1));
+    else return false;
+  }
+  if (fe_iszero(x) && sign) return false;
+  if ((int)fe_isneg(x) != sign) x = fe_neg(x);
+  out = ge{x, y, fe_small(1), fe_mul(x, y)};
+  return true;
+}
+__device__ void enc_affine(uint32_t out[8], const fe& x, const fe& y) {
+  fe_tobytes(out, y);
+  if (fe_isneg(x)) out[7] |= 0x80000000u;
+}
+
+// ---------------------------------------------------------------- scalars mod L
+__constant__ static const unsigned long long C_L[4] = {0x5812631a5cf5d3edull, 0x14def9dea2f79cd6ull, 0ull,
+                                                       0x1000000000000000ull};
+// r = (little-endian byte string of `nbits` bits, given as 32-bit words) mod L, bitwise
+__device__ void sc_reduce_words(uint32_t out[8], const uint32_t* in, int nbits) {
+  unsigned long long r[4] = {0, 0, 0, 0};
+  for (int bi = nbits - 1; bi >= 0; --bi) {
+    unsigned long long c = (in[bi >> 5] >> (bi & 31)) & 1u;
+    for (int i = 0; i < 4; ++i) {
+      const unsigned long long nc = r[i] >> 63;
+      r[i] = (r[i] << 1) | c;
+      c = nc;
+    }
+    bool ge_l = true;
+    for (int i = 3; i >= 0; --i) {
+      if (r[i] != C_L[i]) {
+        ge_l = r[i] > C_L[i];
+        break;
+      }
+    }
+    if (ge_l) {
+      unsigned long long br = 0;
+      for (int i = 0; i < 4; ++i) {
+        const unsigned long long li = C_L[i] + br;
+        const unsigned long long nb = (li < br) || (r[i] < li);
+        r[i] -= li;
+        br = nb;
+      }
+    }
+  }
+  for (int i = 0; i < 4; ++i) {
+    out[2 * i] = (uint32_t)r[i];
+    out[2 * i + 1] = (uint32_t)(r[i] >> 32);
+  }
+}
+
+constexpr uint8_t SUITE = 0x03;
+
+}  // namespace
+
+// keys: [nkeys][24] words = x (clamped secret, 8 LE words), prefix (8), pk encoding (8);
+// key_idx / alpha_idx: [n]; alphas: [nalpha][alpha_len] bytes; btab: [512][32] words;
+// scratch: [n][320] words (the per-thread table of H); pi: [n][80] bytes; beta: [n][64] or null.
+extern "C" __global__ void __launch_bounds__(64) k_vrf_prove(const uint32_t* __restrict__ keys,
+                                                            const int* __restrict__ key_idx,
+                                                            const uint8_t* __restrict__ alphas,
+                                                            const int* __restrict__ alpha_idx, int alpha_len, int n,
+                                                            const uint32_t* __restrict__ btab, uint32_t* scratch,
+                                                            uint8_t* __restrict__ pi, uint8_t* __restrict__ beta) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t* key = keys + (long long)key_idx[t] * 24;
+  const uint8_t* alpha = alphas + (long long)alpha_idx[t] * alpha_len;
+  uint32_t x[8], prefix[8], pk[8];
+  for (int i = 0; i < 8; ++i) {
+    x[i] = key[i];
+    prefix[i] = key[8 + i];
+    pk[i] = key[16 + i];
+  }
+  const fe d = fe_const(C_D), d2 = fe_const(C_D2);
+  // ---- H = encode_to_curve_try_and_increment(pk, alpha)
+  ge H;
+  bool found = false;
+  for (int ctr = 0; ctr < 256 && !found; ++ctr) {
+    Sha512 s;
+    sha_init(s);
+    sha_byte(s, SUITE);
+    sha_byte(s, 0x01);
+    sha_words(s, pk, 8);
+    sha_bytes(s, alpha, alpha_len);
+    sha_byte(s, (uint8_t)ctr);
+    sha_byte(s, 0x00);
+    uint8_t dig[64];
+    sha_final(s, dig);
+    found = ge_frombytes(H, dig, d);
+  }
+  if (!found) return;   // probability 2^-256: the host marks an all-zero proof as failed
+  H = ge_dbl(ge_dbl(ge_dbl(H, false), false), true);   // cofactor 8
+  // ---- one table of H for x*H and k*H
+  uint32_t* tbl = scratch + (long long)t * 320;
+  {
+    const gc c1 = ge_cache(H, d2);
+    st_gc(tbl, c1);
+    ge acc = ge_dbl(H, true);
+    st_gc(tbl + 40, ge_cache(acc, d2));
+    for (int i = 2; i < 8; ++i) {
+      acc = ge_add_cached(acc, c1);
+      st_gc(tbl + 40 * i, ge_cache(acc, d2));
+    }
+  }
+  const ge Gamma = ge_mul_tbl(tbl, x);
+  // ---- hstr = encode(H); nonce k = SHA512(prefix || hstr) mod L
+  const fe hzi = fe_invert(H.Z);
+  uint32_t hstr[8];
+  enc_affine(hstr, fe_mul(H.X, hzi), fe_mul(H.Y, hzi));
+  uint32_t k[8];
+  {
+    Sha512 s;
+    sha_init(s);
+    sha_words(s, prefix, 8);
+    sha_words(s, hstr, 8);
+    uint8_t dig[64];
+    sha_final(s, dig);
+    uint32_t dw[16];
+    for (int i = 0; i < 16; ++i)
+      dw[i] = (uint32_t)dig[4 * i] | ((uint32_t)dig[4 * i + 1] << 8) | ((uint32_t)dig[4 * i + 2] << 16) |
+              ((uint32_t)dig[4 * i + 3] << 24);
+    sc_reduce_words(k, dw, 512);
+  }
+  const ge U = ge_mul_base(btab, k);
+  const ge V = ge_mul_tbl(tbl, k);
+  // ---- encodings of Gamma, U, V with one inversion
+  const fe zgu = fe_mul(Gamma.Z, U.Z);
+  const fe inv = fe_invert(fe_mul(zgu, V.Z));
+  const fe ziV = fe_mul(inv, zgu);
+  const fe inv2 = fe_mul(inv, V.Z);          // 1 / (Zg Zu)
+  const fe ziU = fe_mul(inv2, Gamma.Z);
+  const fe ziG = fe_mul(inv2, U.Z);
+  uint32_t eg[8], eu[8], ev[8];
+  enc_affine(eg, fe_mul(Gamma.X, ziG), fe_mul(Gamma.Y, ziG));
+  enc_affine(eu, fe_mul(U.X, ziU), fe_mul(U.Y, ziU));
+  enc_affine(ev, fe_mul(V.X, ziV), fe_mul(V.Y, ziV));
+  // ---- c = SHA512(suite || 0x02 || Y || H || Gamma || U || V || 0x00)[0..16]
+  uint8_t cdig[64];
+  {
+    Sha512 s;
+    sha_init(s);
+    sha_byte(s, SUITE);
+    sha_byte(s, 0x02);
+    sha_words(s, pk, 8);
+    sha_words(s, hstr, 8);
+    sha_words(s, eg, 8);
+    sha_words(s, eu, 8);
+    sha_words(s, ev, 8);
+    sha_byte(s, 0x00);
+    sha_final(s, cdig);
+  }
+  // ---- s = (k + c x) mod L: 128 x 256-bit product plus k, reduced bitwise
+  uint32_t cw[4];
+  for (int i = 0; i < 4; ++i)
+    cw[i] = (uint32_t)cdig[4 * i] | ((uint32_t)cdig[4 * i + 1] << 8) | ((uint32_t)cdig[4 * i + 2] << 16) |
+            ((uint32_t)cdig[4 * i + 3] << 24);
+  uint32_t prod[13];
+  for (int i = 0; i < 13; ++i) prod[i] = 0;
+  for (int i = 0; i < 4; ++i) {
+    unsigned long long carry = 0;
+    for (int j = 0; j < 8; ++j) {
+      const unsigned long long v = (unsigned long long)cw[i] * x[j] + prod[i + j] + carry;
+      prod[i + j] = (uint32_t)v;
+      carry = v >> 32;
+    }
+    for (int j = i + 8; carry && j < 13; ++j) {
+      const unsigned long long v = (unsigned long long)prod[j] + carry;
+      prod[j] = (uint32_t)v;
+      carry = v >> 32;
+    }
+  }
+  {
+    unsigned long long carry = 0;
+    for (int i = 0; i < 13; ++i) {
+      const unsigned long long v = (unsigned long long)prod[i] + (i < 8 ? k[i] : 0u) + carry;
+      prod[i] = (uint32_t)v;
+      carry = v >> 32;
+    }
+  }
+  uint32_t sc[8];
+  sc_reduce_words(sc, prod, 13 * 32);
+  // ---- pi = Gamma (32) || c (16) || s (32)
+  uint8_t* o = pi + (long long)t * 80;
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 4; ++b) o[4 * i + b] = (uint8_t)(eg[i] >> (8 * b));
+  for (int i = 0; i < 16; ++i) o[32 + i] = cdig[i];
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 4; ++b) o[48 + 4 * i + b] = (uint8_t)(sc[i] >> (8 * b));
+  if (beta != nullptr) {   // beta = SHA512(suite || 0x03 || encode(8 Gamma) || 0x00)
+    const ge G8 = ge_dbl(ge_dbl(ge_dbl(Gamma, false), false), true);
+    const fe zi = fe_invert(G8.Z);
+    uint32_t e8[8];
+    enc_affine(e8, fe_mul(G8.X, zi), fe_mul(G8.Y, zi));
+    Sha512 s;
+    sha_init(s);
+    sha_byte(s, SUITE);
+    sha_byte(s, 0x03);
+    sha_words(s, e8, 8);
+    sha_byte(s, 0x00);
+    sha_final(s, beta + (long long)t * 64);
+  }
+}
+
+extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
+                             int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
+                             void* stream) {
+  if (n <= 0) return 0;
+  if (alpha_len < 0 || alpha_len > 1024) return -1;
+  hipLaunchKernelGGL(k_vrf_prove, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, keys, key_idx, alphas,
+                     alpha_idx, alpha_len, n, btab, scratch, pi, beta);
+  return (int)hipGetLastError();
+}

@@ -139,6 +139,7 @@ struct VrfJob {
   std::promise<void> done_p;
   std::shared_future<void> done = done_p.get_future().share();
   std::shared_ptr<VrfJob> after;  // run only once this job has finished (keeps the pool to one job)
+  bool outputs_only = false;      // betas only: the proofs are left empty (computed on the device)
   std::thread th;
   std::chrono::steady_clock::time_point t_submit, t_start, t_end;
   ~VrfJob() {
@@ -732,9 +733,20 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         for (auto& o : j.out) r.append(P(o.first));
         return r;
       });
+  m.def("vrf_key_material", [](py::bytes seed) {
+    // x (clamped secret) || nonce prefix || encoded public key: the device prover's key row
+    const VrfKey& k = VrfKey::cached(B(seed));
+    Bytes out(k.x, k.x + 32);
+    out.insert(out.end(), k.prefix, k.prefix + 32);
+    out.insert(out.end(), k.pk.begin(), k.pk.end());
+    return P(out);
+  });
+  m.def("vrf_base_table", [] { return P(vrf_base_table_bytes()); });
+  m.def("vrf_beta", [](py::bytes seed, py::bytes alpha) { return P(vrf_beta(VrfKey::cached(B(seed)), B(alpha))); });
   m.def("vrf_prove_batch_async", [](std::vector<py::bytes> seeds, py::bytes alpha, int threads,
-                                    std::shared_ptr<VrfJob> after) {
+                                    std::shared_ptr<VrfJob> after, bool outputs_only) {
     auto job = std::make_shared<VrfJob>();
+    job->outputs_only = outputs_only;
     job->after = std::move(after);
     for (auto& s : seeds) job->seeds.push_back(B(s));
     job->alpha = B(alpha);
@@ -747,13 +759,20 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       jp->t_start = std::chrono::steady_clock::now();
       bool beta_set = false;
       try {
-        // pass 1: every output (H, Gamma = x*H, beta); pass 2: the proofs (k*B, k*H, c, s)
-        parallel_for(jp->seeds.size(), threads, [&](size_t i) {
-          jp->out[i].first = vrf_output(VrfKey::cached(jp->seeds[i]), jp->alpha, &jp->stages[i]);
-        });
+        // pass 1: every output (H, Gamma = x*H, beta); pass 2: the proofs (k*B, k*H, c, s) unless
+        // they are produced elsewhere (outputs_only: the device prover, kernels/vrf.hip)
+        if (jp->outputs_only) {
+          parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+            jp->out[i].first = vrf_beta(VrfKey::cached(jp->seeds[i]), jp->alpha);
+          });
+        } else {
+          parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+            jp->out[i].first = vrf_output(VrfKey::cached(jp->seeds[i]), jp->alpha, &jp->stages[i]);
+          });
+        }
         jp->beta_p.set_value();
         beta_set = true;
-        parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+        if (!jp->outputs_only) parallel_for(jp->seeds.size(), threads, [&](size_t i) {
           jp->out[i].second = vrf_finish(VrfKey::cached(jp->seeds[i]), jp->stages[i]);
           jp->stages[i].st.reset();
         });
@@ -768,7 +787,8 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       jp->done_p.set_value();
     });
     return job;
-  }, py::arg("seeds"), py::arg("alpha"), py::arg("threads"), py::arg("after") = nullptr);
+  }, py::arg("seeds"), py::arg("alpha"), py::arg("threads"), py::arg("after") = nullptr,
+     py::arg("outputs_only") = false);
 
   // ---------------------------------------------------------------- keys
   py::class_<CommitKey>(m, "CommitKey")

@@ -335,9 +335,13 @@ struct BaseTable {
     }
   }
 };
+const BaseTable& base_table() {
+  static const BaseTable bt;
+  return bt;
+}
 // no doublings at all: one cached addition per non-zero digit
 Ge ge_mul_base(const u8 k[32]) {
-  static const BaseTable bt;
+  const BaseTable& bt = base_table();
   int8_t e[64];
   signed_digits(e, k);
   Ge r = ge_identity();
@@ -590,6 +594,31 @@ Bytes vrf_output(const VrfKey& key, const Bytes& alpha, VrfStage* stage) {
   bh.final(beta.data());
   stage->st = st;
   return beta;
+}
+
+Bytes vrf_beta(const VrfKey& key, const Bytes& alpha) {
+  const Ge H = encode_to_curve(key.pk, alpha);
+  const Ge G8 = ge_dbl(ge_dbl(ge_dbl(ge_mul(H, key.x))));
+  Sha512 bh;
+  u8 pre[2] = {SUITE, 0x03};
+  bh.update(pre, 2);
+  bh.update(ge_tobytes(G8));
+  u8 z = 0;
+  bh.update(&z, 1);
+  Bytes beta(64);
+  bh.final(beta.data());
+  return beta;
+}
+
+Bytes vrf_base_table_bytes() {
+  const BaseTable& bt = base_table();
+  Bytes out(bt.t.size() * 128);
+  for (size_t i = 0; i < bt.t.size(); ++i) {
+    const GeCached& c = bt.t[i];
+    const Fe* f[4] = {&c.YpX, &c.YmX, &c.Z2, &c.T2d};
+    for (int j = 0; j < 4; ++j) fe_tobytes(out.data() + 128 * i + 32 * j, *f[j]);
+  }
+  return out;
 }
 
 Bytes vrf_finish(const VrfKey& key, const VrfStage& stage) {

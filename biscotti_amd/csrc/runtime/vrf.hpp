@@ -35,6 +35,12 @@ struct VrfStage {
 };
 Bytes vrf_output(const VrfKey& key, const Bytes& alpha, VrfStage* stage);
 Bytes vrf_finish(const VrfKey& key, const VrfStage& stage);
+// The output alone (no proof, no encoding of H): the noiser lottery's input when the proofs are
+// produced elsewhere (kernels/vrf.hip).
+Bytes vrf_beta(const VrfKey& key, const Bytes& alpha);
+// The fixed-base table of B (64 signed radix-16 windows x 8 multiples, cached form) as 512 x 4
+// canonical 32-byte field encodings (Y+X, Y-X, 2Z, 2dT): the device prover's k*B table.
+Bytes vrf_base_table_bytes();
 // Returns true and fills beta on success.
 bool vrf_verify(const Bytes& pk, const Bytes& alpha, const Bytes& pi, Bytes* beta);
 Bytes vrf_proof_to_hash(const Bytes& pi);

@@ -28,6 +28,8 @@ SIGNATURES = {
     "bsc_marshal": [P, I, P, P],
     "bsc_to_affine": [P, I, P, P],
     "bsc_chunk_check": [P, I, I, P, I, I, P, I, I, P, P],
+    # vrf.hip
+    "bsc_vrf_prove": [P, P, P, P, I, I, P, P, P, P, P],
     # kzg.hip
     "bsc_kzg_blocks": [I, I],
     "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, U64, P, P, P],

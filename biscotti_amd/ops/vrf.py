@@ -1,0 +1,96 @@
+"""Device ECVRF prover (kernels/vrf.hip): RFC 9381 ECVRF-EDWARDS25519-SHA512-TAI proofs on gfx950.
+
+The protocol computes two VRF proofs per peer per round that nothing reads (the roles proof of
+getVRFRoles, quirk Q7, and the proof half of every worker's noiser VRF, vrf.go:54-100 -- only the
+64-byte output feeds the lottery).  Round 1 spent ~37 ms of host CPU per round on them; here the
+host computes the outputs the lottery needs (VrfJob outputs_only) and the proofs are queued for the
+device, a few rounds per launch on a low-priority stream.  Bit-exact with runtime/vrf.cpp
+(tests/test_gpu_vrf.py), which is itself pinned to the RFC's example vector.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..native import hip, rt
+from ..utils import streams as S
+
+
+def _i32(b: bytes) -> np.ndarray:
+    return np.frombuffer(b, np.uint8).view(np.int32)
+
+
+class DeviceVrfProver:
+    ALPHA_LEN = 32
+
+    def __init__(self, device, batch_rounds: int = 4):
+        self.device = torch.device(device)
+        self.btab = torch.from_numpy(_i32(rt().vrf_base_table()).copy()).to(self.device)   # [512 * 32]
+        self.batch_rounds = max(1, int(batch_rounds))
+        self._row: dict[bytes, int] = {}
+        self._keys: list[np.ndarray] = []
+        self._keys_dev = None
+        self._queue: list[tuple[list[int], bytes]] = []
+        self._inflight: list = []
+        self.proofs = 0
+
+    def _rows(self, seeds) -> list[int]:
+        out = []
+        for s in seeds:
+            r = self._row.get(s)
+            if r is None:
+                r = self._row[s] = len(self._keys)
+                self._keys.append(_i32(rt().vrf_key_material(s)))
+                self._keys_dev = None
+            out.append(r)
+        return out
+
+    def prove(self, seeds, alphas, beta: bool = False):
+        """Proofs of seeds[i] over alphas[i] (32-byte messages) on the current stream: (pi uint8
+        [n, 80], beta uint8 [n, 64] or None).  Asynchronous: read the tensors after a sync."""
+        n = len(seeds)
+        assert len(alphas) == n and all(len(a) == self.ALPHA_LEN for a in alphas)
+        rows = self._rows(seeds)
+        if self._keys_dev is None:
+            self._keys_dev = torch.from_numpy(np.concatenate(self._keys)).to(self.device)
+        uniq = {a: i for i, a in enumerate(dict.fromkeys(alphas))}
+        al = torch.from_numpy(np.frombuffer(b"".join(uniq), np.uint8).copy()).to(self.device)
+        idx = torch.from_numpy(np.asarray(rows + [uniq[a] for a in alphas], np.int32)).to(self.device)
+        scratch = torch.empty((max(n, 1), 320), dtype=torch.int32, device=self.device)
+        pi = torch.empty((n, 80), dtype=torch.uint8, device=self.device)
+        bt = torch.empty((n, 64), dtype=torch.uint8, device=self.device) if beta else None
+        err = hip().bsc_vrf_prove(self._keys_dev.data_ptr(), idx.data_ptr(), al.data_ptr(), idx[n:].data_ptr(),
+                                  self.ALPHA_LEN, n, self.btab.data_ptr(), scratch.data_ptr(), pi.data_ptr(),
+                                  bt.data_ptr() if bt is not None else None, S.raw())
+        if err != 0:
+            raise RuntimeError(f"HIP launch of vrf_prove failed with hipError {err}")
+        self.proofs += n
+        return pi, bt
+
+    # ---- round-batched queue: the engine submits each round's proofs, one launch per batch_rounds
+    def submit(self, seeds, alpha: bytes, stream) -> None:
+        if seeds:
+            self._queue.append((list(seeds), bytes(alpha)))
+        if len(self._queue) >= self.batch_rounds:
+            self.flush(stream)
+
+    def flush(self, stream) -> None:
+        if not self._queue:
+            return
+        seeds = [s for ss, _ in self._queue for s in ss]
+        alphas = [a for ss, a in self._queue for _ in ss]
+        self._queue = []
+        main = S.current()
+        S.wait(stream, main)   # key/alpha uploads above are ordered on the current stream
+        with S.use(stream):
+            pi, _ = self.prove(seeds, alphas)
+            ev = S.record(stream)
+        self._inflight.append((ev, pi))
+        # keep the last few batches alive until their kernels finished (the proofs are discarded)
+        self._inflight = [x for x in self._inflight if not x[0].query()] if len(self._inflight) > 2 else self._inflight
+
+    def drain(self, stream) -> None:
+        self.flush(stream)
+        for ev, _ in self._inflight:
+            ev.synchronize()
+        self._inflight = []

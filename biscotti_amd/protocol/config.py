@@ -82,6 +82,10 @@ class RunConfig:
     krum_pregram: bool = True       # one rank, table noise: Krum's Gram over [deltas; noise vectors] runs
     #                                 before the VRF outputs arrive; only an O(n^2) assembly waits for them
     join_background: bool = False   # main stream waits for the background (witness-sum) work each round
+    vrf_device: bool = True         # GPU: the VRF proofs nothing reads (roles proof Q7, the noiser proofs)
+    #                                 run on the device (kernels/vrf.hip); the host computes only the
+    #                                 64-byte outputs the lottery consumes
+    vrf_device_batch_rounds: int = 4  # rounds of proofs per device launch
     kzg_audit: str = "off"          # batched verifySecret (kyber.go:650-673) over every (chunk, share point) of
     #                                 the aggregate: off | consistent (y against PK[poly*k]) | literal (y
     #                                 against G1: the reference's formula, which only chunk 0 satisfies, Q9).
@@ -207,6 +211,8 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--no-phase-sync", dest="phase_sync", action="store_false")
     ap.add_argument("--no-audit-aggregate", dest="audit_aggregate", action="store_false")
     ap.add_argument("--no-noise-table", dest="noise_table", action="store_false")
+    ap.add_argument("--no-vrf-device", dest="vrf_device", action="store_false",
+                    help="compute every VRF proof on host threads")
     ap.add_argument("--kzg-audit", default="off", choices=["off", "consistent", "literal"],
                     help="batched verifySecret over each round's aggregate (K13)")
     ap.add_argument("--comm-timeout", dest="comm_timeout_s", type=float, default=300.0)

@@ -353,6 +353,10 @@ class BiscottiEngine:
         self.noise_tbl = None
         if self.gpu and cfg.noising and cfg.noise_table and self.sigma > 0 and self.N * 100 * self.d * 4 <= (8 << 30):
             self.noise_tbl = K.noise_table(self.N, self.d, cfg.seed, self.dev)
+        self.vrf_dev = None
+        if self.gpu and cfg.vrf_device:
+            from ..ops.vrf import DeviceVrfProver
+            self.vrf_dev = DeviceVrfProver(self.dev, cfg.vrf_device_batch_rounds)
         self._side_work: list = []   # (event, tensors) of off-critical-path device work of this round
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
@@ -440,11 +444,15 @@ class BiscottiEngine:
                 keep.append(e)
         self._kzg_pending = keep
 
-    def drain(self) -> None:
-        """Join host work that belongs to rounds already returned (the last roles-VRF batch, the
-        outstanding KZG audits)."""
-        if self._kzg_pending:
-            self._kzg_poll(final=True)
+    def drain(self, final: bool = True) -> None:
+        """Join work that belongs to rounds already returned: the last host VRF batch and, when
+        final, the outstanding KZG audits and the device VRF proofs still queued or in flight."""
+        if final:
+            if self._kzg_pending:
+                self._kzg_poll(final=True)
+            if self.vrf_dev is not None and getattr(self, "bg_stream", None) is not None:
+                self.vrf_dev.drain(self.bg_stream)
+                self.stats["vrf_device_proofs"] = self.vrf_dev.proofs
         futs, self._pending_roles = getattr(self, "_pending_roles", None), None
         for fut in futs or ():
             if fut is not None:
@@ -653,11 +661,16 @@ class BiscottiEngine:
         # joins the outputs.
         with self.timer.phase("head.vrf_submit"):
             seeds = [self.vrf_noise_seed[w] for w in local_workers]
-            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads) if seeds else None
+            dev = self.vrf_dev is not None
+            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads, None, dev) if seeds else None
             fut_roles = None
-            if cfg.roles_vrf_proof:  # getVRFRoles proves with the roles key too (result unused, Q7)
-                fut_roles = R.vrf_prove_batch_async([self.vrf_roles_seed[p] for p in self.local if live[p]],
-                                                    latest_hash, cfg.roles_vrf_threads, fut_noise)
+            roles = [self.vrf_roles_seed[p] for p in self.local if live[p]] if cfg.roles_vrf_proof else []
+            if roles and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
+                fut_roles = R.vrf_prove_batch_async(roles, latest_hash, cfg.roles_vrf_threads, fut_noise)
+            if dev:
+                # the proofs nobody reads -- every noiser proof and the roles proofs -- on the device,
+                # several rounds per launch on the background stream
+                self.vrf_dev.submit(seeds + roles, latest_hash, self.bg_stream)
         head.update(fut_noise=fut_noise, fut_roles=fut_roles)
         # one rank, Multi-Krum: the noise and committee-Krum kernels (and, behind the selection, the
         # whole device-side aggregation) depend only on this head, so they can be queued now as well
@@ -965,7 +978,7 @@ class BiscottiEngine:
             # the VRF outputs) and the discarded roles proofs (Q7) finish on the native threads;
             # they are joined one round later (drain() joins the last ones), so the round does not
             # wait for them
-            self.drain()
+            self.drain(final=False)
             self._pending_roles = (fut_noise, fut_roles)
         with tm.phase("side_join"):
             self._join_side_work()
