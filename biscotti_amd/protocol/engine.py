@@ -332,6 +332,9 @@ class BiscottiEngine:
                 self.bg_stream, self.bg_cus = B.cu_masked_stream(self.dev, -cfg.side_stream_skip_every)
             else:
                 self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
+            # the device VRF proofs (kernels/vrf.hip, ~5 ms launches nothing waits for) get a stream of
+            # their own: on the background stream they would hold up the next round's commitments
+            self.vrf_stream = torch.cuda.Stream(device=self.dev, priority=lo) if cfg.vrf_device else None
             torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
             torch.cuda.set_stream(self.main_stream)
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
@@ -450,8 +453,8 @@ class BiscottiEngine:
         if final:
             if self._kzg_pending:
                 self._kzg_poll(final=True)
-            if self.vrf_dev is not None and getattr(self, "bg_stream", None) is not None:
-                self.vrf_dev.drain(self.bg_stream)
+            if self.vrf_dev is not None and getattr(self, "vrf_stream", None) is not None:
+                self.vrf_dev.drain(self.vrf_stream)
                 self.stats["vrf_device_proofs"] = self.vrf_dev.proofs
         futs, self._pending_roles = getattr(self, "_pending_roles", None), None
         for fut in futs or ():
@@ -669,8 +672,8 @@ class BiscottiEngine:
                 fut_roles = R.vrf_prove_batch_async(roles, latest_hash, cfg.roles_vrf_threads, fut_noise)
             if dev:
                 # the proofs nobody reads -- every noiser proof and the roles proofs -- on the device,
-                # several rounds per launch on the background stream
-                self.vrf_dev.submit(seeds + roles, latest_hash, self.bg_stream)
+                # several rounds per launch on their own low-priority stream
+                self.vrf_dev.submit(seeds + roles, latest_hash, self.vrf_stream)
         head.update(fut_noise=fut_noise, fut_roles=fut_roles)
         # one rank, Multi-Krum: the noise and committee-Krum kernels (and, behind the selection, the
         # whole device-side aggregation) depend only on this head, so they can be queued now as well
