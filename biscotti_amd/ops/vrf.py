@@ -52,10 +52,10 @@ class DeviceVrfProver:
         assert len(alphas) == n and all(len(a) == self.ALPHA_LEN for a in alphas)
         rows = self._rows(seeds)
         if self._keys_dev is None:
-            self._keys_dev = torch.from_numpy(np.concatenate(self._keys)).to(self.device)
+            self._keys_dev = self._upload(np.concatenate(self._keys))
         uniq = {a: i for i, a in enumerate(dict.fromkeys(alphas))}
-        al = torch.from_numpy(np.frombuffer(b"".join(uniq), np.uint8).copy()).to(self.device)
-        idx = torch.from_numpy(np.asarray(rows + [uniq[a] for a in alphas], np.int32)).to(self.device)
+        al = self._upload(np.frombuffer(b"".join(uniq), np.uint8))
+        idx = self._upload(np.asarray(rows + [uniq[a] for a in alphas], np.int32))
         scratch = torch.empty((max(n, 1), 320), dtype=torch.int32, device=self.device)
         pi = torch.empty((n, 80), dtype=torch.uint8, device=self.device)
         bt = torch.empty((n, 64), dtype=torch.uint8, device=self.device) if beta else None
@@ -66,6 +66,12 @@ class DeviceVrfProver:
             raise RuntimeError(f"HIP launch of vrf_prove failed with hipError {err}")
         self.proofs += n
         return pi, bt
+
+    def _upload(self, a: np.ndarray) -> torch.Tensor:
+        # pinned staging + a stream-ordered copy: a pageable .to(device) is a blocking copy that can
+        # stall the host behind the round's queued kernels
+        h = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+        return h.to(self.device, non_blocking=True)
 
     # ---- round-batched queue: the engine submits each round's proofs, one launch per batch_rounds
     def submit(self, seeds, alpha: bytes, stream) -> None:
@@ -80,9 +86,7 @@ class DeviceVrfProver:
         seeds = [s for ss, _ in self._queue for s in ss]
         alphas = [a for ss, a in self._queue for _ in ss]
         self._queue = []
-        main = S.current()
-        S.wait(stream, main)   # key/alpha uploads above are ordered on the current stream
-        with S.use(stream):
+        with S.use(stream):   # uploads, scratch and the launch all on the prover's stream
             pi, _ = self.prove(seeds, alphas)
             ev = S.record(stream)
         self._inflight.append((ev, pi))

@@ -85,7 +85,7 @@ class RunConfig:
     vrf_device: bool = True         # GPU: the VRF proofs nothing reads (roles proof Q7, the noiser proofs)
     #                                 run on the device (kernels/vrf.hip); the host computes only the
     #                                 64-byte outputs the lottery consumes
-    vrf_device_batch_rounds: int = 8  # rounds of proofs per device launch (a launch takes ~5 ms whatever its size)
+    vrf_device_batch_rounds: int = 16  # rounds of proofs per device launch (a launch takes ~5 ms whatever its size)
     kzg_audit: str = "off"          # batched verifySecret (kyber.go:650-673) over every (chunk, share point) of
     #                                 the aggregate: off | consistent (y against PK[poly*k]) | literal (y
     #                                 against G1: the reference's formula, which only chunk 0 satisfies, Q9).

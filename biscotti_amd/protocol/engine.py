@@ -604,6 +604,21 @@ class BiscottiEngine:
         workers = [w for w in plan.workers if live[w]]
         local_workers = [w for w in workers if w in self.local]
         head.update(workers=workers, local_workers=local_workers, stake=dict(fsm.stake))
+        # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  Only the
+        # 64-byte outputs gate the round (the noiser lottery -> noise -> Krum -> the selection that
+        # cancels speculative MSM rows), and they need nothing but the plan and the block hash: they
+        # start first, on host_threads - 1 native threads (the launching thread keeps a core); the
+        # proofs nothing reads run on the device (vrf_device) or after the outputs on the host.
+        with self.timer.phase("head.vrf_submit"):
+            seeds = [self.vrf_noise_seed[w] for w in local_workers]
+            dev = self.vrf_dev is not None
+            nthr = max(1, cfg.host_threads - 1) if self.gpu else cfg.host_threads
+            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, nthr, None, dev) if seeds else None
+            fut_roles = None
+            roles = [self.vrf_roles_seed[p] for p in self.local if live[p]] if cfg.roles_vrf_proof else []
+            if roles and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
+                fut_roles = R.vrf_prove_batch_async(roles, latest_hash, cfg.roles_vrf_threads, fut_noise)
+        head.update(fut_noise=fut_noise, fut_roles=fut_roles)
         # the local step, the commitments and the speculative shares depend only on the new global
         # model too: queue them now, behind nothing but the block that produced it
         tm, it = self.timer, plan.iteration
@@ -658,23 +673,10 @@ class BiscottiEngine:
                 krum_pre = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
                     spec=spec, spec_cand=cand, krum_pre=krum_pre)
-        # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  The proofs run
-        # on native threads while the GPU works through the head queued above (the round's long
-        # kernels are launched first: their start, not the VRF's, bounds the round); the noise phase
-        # joins the outputs.
-        with self.timer.phase("head.vrf_submit"):
-            seeds = [self.vrf_noise_seed[w] for w in local_workers]
-            dev = self.vrf_dev is not None
-            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, cfg.host_threads, None, dev) if seeds else None
-            fut_roles = None
-            roles = [self.vrf_roles_seed[p] for p in self.local if live[p]] if cfg.roles_vrf_proof else []
-            if roles and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
-                fut_roles = R.vrf_prove_batch_async(roles, latest_hash, cfg.roles_vrf_threads, fut_noise)
-            if dev:
-                # the proofs nobody reads -- every noiser proof and the roles proofs -- on the device,
-                # several rounds per launch on their own low-priority stream
-                self.vrf_dev.submit(seeds + roles, latest_hash, self.vrf_stream)
-        head.update(fut_noise=fut_noise, fut_roles=fut_roles)
+        if self.vrf_dev is not None:
+            # the proofs nobody reads -- every noiser proof and the roles proofs -- on the device,
+            # several rounds per launch on their own low-priority stream
+            self.vrf_dev.submit(seeds + roles, latest_hash, self.vrf_stream)
         # one rank, Multi-Krum: the noise and committee-Krum kernels (and, behind the selection, the
         # whole device-side aggregation) depend only on this head, so they can be queued now as well
         if (cfg.early_krum and self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.defense == "KRUM"
