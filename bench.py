@@ -76,6 +76,8 @@ PRESETS = {
     "scale40": ({"num_nodes": 40}, 23.87, None, {}, "nsdi-eval/increments/results.log:2"),
     "scale60": ({"num_nodes": 60}, 34.05, None, {}, "nsdi-eval/increments/results.log:3"),
     "scale80": ({"num_nodes": 80}, 48.07, None, {}, "nsdi-eval/increments/results.log:4"),
+    # 200 peers (eval/eval_FedSys_scale runs FedSys up to 200; Krum inboxes of 140 updates)
+    "scale200": ({"num_nodes": 200}, None, None, {}, "eval/eval_FedSys_scale (Biscotti at 200 peers: unpinned)"),
     "secagg_off": ({"secure_agg": False}, 50.63, None, {}, "nsdi-eval/increments/results.log:10"),
     "verification_off": ({"verification": False}, 19.95, None, {}, "nsdi-eval/increments/results.log:15"),
     "noising_off": ({"noising": False}, 53.10, None, {}, "nsdi-eval/increments/results.log:20"),

@@ -91,6 +91,7 @@ class RunConfig:
     #                                 against G1: the reference's formula, which only chunk 0 satisfies, Q9).
     #                                 Device RLC sums (kzg.hip) + one host 3-pairing product per round,
     #                                 joined lazily; failures are counted and logged, never block the chain
+    kzg_batch_rounds: int = 16      # rounds whose audits share one pairing product (sums of independent RLCs)
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
     #                                 (shortens the GPU chain; costs host time before the previous round ends)
 

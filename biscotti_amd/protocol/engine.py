@@ -366,6 +366,8 @@ class BiscottiEngine:
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
         self._kzg_pending: list = []
+        self._kzg_jobs: list = []
+        self._kzg_batch = None
         if cfg.kzg_audit != "off":
             self.stats.update(kzg_checks=0, kzg_failures=0)
             self._kzg_g2 = (self.R.g2_generator(), self._commit_key_g2_1(cfg.commit_key))
@@ -427,31 +429,49 @@ class BiscottiEngine:
         self._kzg_pending.append({"it": it, "ok": self.R.kzg_check(*pts, *self._kzg_g2)})
 
     def _kzg_poll(self, final: bool = False) -> None:
-        """Start the pairing products whose device sums are ready and collect finished ones (all of
-        them when final, or when more than 4 are outstanding)."""
+        """Fold the rounds whose device sums are ready into the open batch; every kzg_batch_rounds
+        rounds (and at the end) one pairing product checks the whole batch on a native thread.  A
+        failed batch is re-checked round by round to name the failing iterations."""
         keep = []
-        for i, e in enumerate(self._kzg_pending):
-            must = final or len(self._kzg_pending) - i > 4
-            if "ok" not in e and e["job"] is None and (must or e["ev"].query()):
+        for e in self._kzg_pending:
+            if "ok" in e:                      # CPU path: checked synchronously
+                self._kzg_record([e["it"]], [e["ok"]])
+            elif final or e["ev"].query():
                 e["ev"].synchronize()
-                e["job"] = self.R.kzg_check_device_async(e["host"].numpy().view(np.uint32), *self._kzg_g2)
-            if "ok" not in e and e["job"] is not None and must:
-                e["ok"] = e["job"].result()
-            if "ok" in e:
-                self.stats["kzg_checks"] += 1
-                if not e["ok"]:
-                    self.stats["kzg_failures"] += 1
-                    self.log.info("KZG audit (verifySecret, %s) failed for the aggregate of iteration %d",
-                                  self.cfg.kzg_audit, e["it"])
+                if self._kzg_batch is None:
+                    self._kzg_batch, self._kzg_its = self.R.KzgBatch(), []
+                self._kzg_batch.add(e["host"].numpy().view(np.uint32))
+                self._kzg_its.append(e["it"])
             else:
                 keep.append(e)
         self._kzg_pending = keep
+        if self._kzg_batch is not None and (len(self._kzg_its) >= self.cfg.kzg_batch_rounds or final):
+            self._kzg_jobs.append((self._kzg_batch.check_async(*self._kzg_g2), self._kzg_batch, self._kzg_its))
+            self._kzg_batch = None
+        jobs = []
+        for job, batch, its in self._kzg_jobs:
+            if final or len(self._kzg_jobs) - len(jobs) > 2:
+                if job.result():
+                    self._kzg_record(its, [True] * len(its))
+                else:
+                    self._kzg_record(its, batch.check_each(*self._kzg_g2))
+            else:
+                jobs.append((job, batch, its))
+        self._kzg_jobs = jobs
+
+    def _kzg_record(self, its, oks) -> None:
+        for it, ok in zip(its, oks):
+            self.stats["kzg_checks"] += 1
+            if not ok:
+                self.stats["kzg_failures"] += 1
+                self.log.info("KZG audit (verifySecret, %s) failed for the aggregate of iteration %d",
+                              self.cfg.kzg_audit, it)
 
     def drain(self, final: bool = True) -> None:
         """Join work that belongs to rounds already returned: the last host VRF batch and, when
         final, the outstanding KZG audits and the device VRF proofs still queued or in flight."""
         if final:
-            if self._kzg_pending:
+            if self._kzg_pending or self._kzg_jobs or self._kzg_batch is not None:
                 self._kzg_poll(final=True)
             if self.vrf_dev is not None and getattr(self, "vrf_stream", None) is not None:
                 self.vrf_dev.drain(self.vrf_stream)
@@ -1041,6 +1061,8 @@ class BiscottiEngine:
                 part[m] = k
                 k += 1
         contributing = [plan.leader] + [m for m in plan.miners if m != plan.leader and live[m]]
+        if self.pc.shares_per_miner * len(contributing) < self.cfg.poly_size:
+            return None   # too few live miners for a quorum (leader_view): the round's block is empty
         return contributing, part
 
     def _spec_aggregate(self, spec, pred, node) -> dict:
@@ -1360,7 +1382,7 @@ class BiscottiEngine:
                               int((ok == 0).sum()), plan.iteration)
                 return None
         self._last_nodes = node_list
-        if self._kzg_pending:
+        if self._kzg_pending or self._kzg_jobs:
             self._kzg_poll()
         return block
 

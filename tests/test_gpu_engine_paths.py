@@ -60,6 +60,16 @@ def test_churn_on_gpu():
     assert len(res) == 5
 
 
+def test_heavy_churn_without_miner_quorum():
+    """Rounds where too few miners are live for a quorum (shares_per_miner x live miners < POLY_SIZE)
+    end in empty blocks; the device-side aggregation is not queued for them (it would have fewer
+    share points than coefficients)."""
+    eng = _engine(num_nodes=20, churn=0.6)
+    res = _run_exact(eng, 25)
+    assert len(res) == 25 and any(r.empty for r in res) and any(not r.empty for r in res)
+    assert eng.fsm.chain.verify()[0]
+
+
 def test_poisoners_on_gpu():
     eng = _engine(num_nodes=20, poisoning=0.3)
     pois = {p for p in range(20) if eng.fsm.is_poisoner(p)}
