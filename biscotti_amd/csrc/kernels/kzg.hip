@@ -36,8 +36,26 @@ __device__ __forceinline__ unsigned long long kzg_r(unsigned long long seed, uns
   return (z ^ (z >> 31)) | 1ull;
 }
 
+// dbl-2009-l, force-inlined here (bn::jac_dbl is a call: its frame would live in scratch)
+__device__ __forceinline__ jac kz_dbl(const jac& p) {
+  fp A = fp_sqr(p.x);
+  fp B = fp_sqr(p.y);
+  fp C = fp_sqr(B);
+  fp t = fp_sqr(fp_add(p.x, B));
+  t = fp_sub(fp_sub(t, A), C);
+  fp D = fp_dbl(t);
+  fp E = fp_add(fp_dbl(A), A);
+  fp F = fp_sqr(E);
+  jac r;
+  r.x = fp_sub(F, fp_dbl(D));
+  fp c8 = fp_dbl(fp_dbl(fp_dbl(C)));
+  r.y = fp_sub(fp_mul(E, fp_sub(D, r.x)), c8);
+  r.z = fp_dbl(fp_mul(p.y, p.z));
+  return r;   // infinity (z = 0) stays infinity: z' = 2 y z = 0
+}
+
 // k * P for a 192-bit unsigned k = (k2:k1:k0), left to right over its bit length
-__device__ jac jac_mul_192(const jac& p, unsigned long long k0, unsigned long long k1, unsigned long long k2) {
+__device__ __forceinline__ jac jac_mul_192(const jac& p, unsigned long long k0, unsigned long long k1, unsigned long long k2) {
   int nbits;
   if (k2) nbits = 192 - __clzll(k2);
   else if (k1) nbits = 128 - __clzll(k1);
@@ -54,7 +72,7 @@ __device__ jac jac_mul_192(const jac& p, unsigned long long k0, unsigned long lo
   jac acc = p;   // the top bit
   k2 = (k2 << 1) | (k1 >> 63); k1 = (k1 << 1) | (k0 >> 63); k0 <<= 1;
   for (int b = 1; b < nbits; ++b) {
-    acc = jac_dbl(acc);
+    acc = kz_dbl(acc);
     if (k2 >> 63) acc = jac_add(acc, p);
     k2 = (k2 << 1) | (k1 >> 63); k1 = (k1 << 1) | (k0 >> 63); k0 <<= 1;
   }
@@ -62,7 +80,7 @@ __device__ jac jac_mul_192(const jac& p, unsigned long long k0, unsigned long lo
 }
 
 // same with an affine base (mixed additions: 11 products instead of 16)
-__device__ jac aff_mul_192(const aff& q, unsigned long long k0, unsigned long long k1, unsigned long long k2) {
+__device__ __forceinline__ jac aff_mul_192(const aff& q, unsigned long long k0, unsigned long long k1, unsigned long long k2) {
   if (aff_is_inf(q)) return jac_inf();
   int nbits;
   if (k2) nbits = 192 - __clzll(k2);
@@ -82,7 +100,7 @@ __device__ jac aff_mul_192(const aff& q, unsigned long long k0, unsigned long lo
   acc.z = fp_one();
   k2 = (k2 << 1) | (k1 >> 63); k1 = (k1 << 1) | (k0 >> 63); k0 <<= 1;
   for (int b = 1; b < nbits; ++b) {
-    acc = jac_dbl(acc);
+    acc = kz_dbl(acc);
     if (k2 >> 63) acc = jac_add_aff(acc, q);
     k2 = (k2 << 1) | (k1 >> 63); k1 = (k1 << 1) | (k0 >> 63); k0 <<= 1;
   }
@@ -90,7 +108,7 @@ __device__ jac aff_mul_192(const aff& q, unsigned long long k0, unsigned long lo
 }
 
 // sum of one Jacobian point per lane of the block, result valid in lane 0
-__device__ jac block_sum(jac v, uint32_t* lds) {
+__device__ __forceinline__ jac block_sum(jac v, uint32_t* lds) {
   const int t = threadIdx.x;
   for (int s = KZ_THREADS / 2; s > 0; s >>= 1) {
     if (t >= s && t < 2 * s) st_jac(lds + (t - s) * 24, v);
@@ -111,7 +129,7 @@ __device__ jac block_sum(jac v, uint32_t* lds) {
 extern "C" __global__ void __launch_bounds__(KZ_THREADS) k_kzg_rlc(
     const uint32_t* __restrict__ csum, const uint32_t* __restrict__ wsum, const long long* __restrict__ ys,
     const int* __restrict__ xs, int nch, int npts, int spm, const uint32_t* __restrict__ bases, int base_stride,
-    unsigned long long seed, uint32_t* __restrict__ partial) {
+    int nch_round, unsigned long long seed, uint32_t* __restrict__ partial) {
   __shared__ uint32_t lds[KZ_THREADS * 24];
   const long long g = (long long)blockIdx.x * KZ_THREADS + threadIdx.x;
   const long long nw = (long long)nch * npts;
@@ -122,7 +140,7 @@ extern "C" __global__ void __launch_bounds__(KZ_THREADS) k_kzg_rlc(
     const long long row = (long long)(j / spm) * nch * spm + (long long)k * spm + j % spm;
     const jac w = ld_jac(wsum + row * 24);
     a = jac_mul_192(w, r, 0, 0);
-    const int x = xs[j];
+    const int x = xs[(long long)(k / nch_round) * npts + j];
     const unsigned ax = x < 0 ? unsigned(-x) : unsigned(x);
     l2 = jac_mul_192(a, ax, 0, 0);
     if (x < 0) l2 = jac_neg(l2);
@@ -167,7 +185,7 @@ extern "C" __global__ void __launch_bounds__(KZ_THREADS) k_kzg_rlc(
       z1 += c0;
       z2 += (c0 && z1 == 0);
     }
-    const aff b = ld_aff(bases + (long long)k * base_stride * 16);
+    const aff b = ld_aff(bases + (long long)(k % nch_round) * base_stride * 16);
     l1 = aff_mul_192(b, z0, z1, z2);
     if (!neg) l1 = jac_neg(l1);   // the term is -Z_k B_k
   }
@@ -194,8 +212,11 @@ extern "C" __global__ void __launch_bounds__(KZ_THREADS) k_kzg_reduce(const uint
   }
 }
 
-// csum [nch][24], wsum [nch*npts][24] (layout above), ys int64 [nch][npts], xs int32 [npts],
-// bases affine [*][16] read at k * base_stride (0: one base for every chunk, the literal check),
+// csum [nch][24], wsum [nch*npts][24] (layout above), ys int64 [nch][npts], xs int32 [nch/nch_round][npts],
+// bases affine [*][16] read at (k % nch_round) * base_stride (0: one base for every chunk, the
+// literal check).  Several rounds' aggregates stack as nch = rounds * nch_round chunks (witness
+// sums pre-permuted to (chunk, point) order, spm = npts): the sums then cover all of them,
+// one random weight per (round, chunk, point), and one launch serves the whole batch;
 // partial scratch [blocks][72] (blocks = bsc_kzg_blocks), out [3][24] = (L1, A, L2).
 extern "C" int bsc_kzg_blocks(int nch, int npts) {
   const long long n = (long long)nch * npts + 2LL * nch;
@@ -203,13 +224,14 @@ extern "C" int bsc_kzg_blocks(int nch, int npts) {
 }
 
 extern "C" int bsc_kzg_rlc(const uint32_t* csum, const uint32_t* wsum, const long long* ys, const int* xs, int nch,
-                           int npts, int spm, const uint32_t* bases, int base_stride, unsigned long long seed,
-                           uint32_t* partial, uint32_t* out, void* stream) {
+                           int npts, int spm, const uint32_t* bases, int base_stride, int nch_round,
+                           unsigned long long seed, uint32_t* partial, uint32_t* out, void* stream) {
   if (nch <= 0 || npts <= 0) return 0;
-  if (spm <= 0 || npts % spm != 0 || base_stride < 0 || npts > 4096) return -1;
+  if (spm <= 0 || npts % spm != 0 || base_stride < 0 || npts > 4096 || nch_round <= 0 || nch % nch_round != 0)
+    return -1;
   const int nb = bsc_kzg_blocks(nch, npts);
   hipLaunchKernelGGL(k_kzg_rlc, dim3(nb), dim3(KZ_THREADS), 0, (hipStream_t)stream, csum, wsum, ys, xs, nch, npts, spm,
-                     bases, base_stride, seed, partial);
+                     bases, base_stride, nch_round, seed, partial);
   hipLaunchKernelGGL(k_kzg_reduce, dim3(1), dim3(KZ_THREADS), 0, (hipStream_t)stream, partial, nb, out);
   return (int)hipGetLastError();
 }

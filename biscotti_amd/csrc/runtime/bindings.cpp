@@ -270,10 +270,6 @@ static G1 g1_from_dev_jac(const uint32_t* v) {
   if (!g.on_curve()) fail("device point is not on the curve");
   return g;
 }
-struct KzgBatch {
-  G1 acc[3] = {G1::infinity(), G1::infinity(), G1::infinity()};
-  std::vector<std::array<G1, 3>> items;
-};
 struct KzgJob {
   G1 pts[3];
   std::shared_ptr<G2Prepared> q0, q1, qg;
@@ -657,48 +653,6 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     });
     return job;
   });
-  // Several rounds' audits in ONE pairing product: every round's (L1, A, L2) is already a random
-  // combination with independent weights, so their sums are a valid combination of all of them.
-  // check_each() re-checks the rounds one by one (attribution after a failed batch).
-  py::class_<KzgBatch, std::shared_ptr<KzgBatch>>(m, "KzgBatch")
-      .def(py::init<>())
-      .def("add", [](KzgBatch& b, py::array_t<uint32_t, py::array::c_style | py::array::forcecast> pts) {
-        if (pts.size() != 72) throw std::runtime_error("KzgBatch.add: expected [3, 24] limbs");
-        std::array<G1, 3> it;
-        for (int i = 0; i < 3; ++i) {
-          it[size_t(i)] = g1_from_dev_jac(pts.data() + 24 * i);
-          b.acc[i] = b.acc[i].add(it[size_t(i)]);
-        }
-        b.items.push_back(it);
-      })
-      .def("__len__", [](const KzgBatch& b) { return b.items.size(); })
-      .def("check_async", [](std::shared_ptr<KzgBatch> b, py::bytes g2_0, py::bytes g2_1) {
-        auto job = std::make_shared<KzgJob>();
-        for (int i = 0; i < 3; ++i) job->pts[i] = b->acc[i];
-        job->q0 = prepared_g2(B(g2_0));
-        job->q1 = prepared_g2(B(g2_1));
-        job->qg = prepared_g2(G2::generator().marshal());
-        KzgJob* jp = job.get();
-        jp->th = std::thread([jp] {
-          try {
-            jp->ok = multi_pairing_is_one({jp->pts[0], jp->pts[1].neg(), jp->pts[2]},
-                                          {jp->q0.get(), jp->q1.get(), jp->qg.get()});
-          } catch (const std::exception& e) {
-            jp->error = e.what();
-          }
-          jp->done_p.set_value();
-        });
-        return job;
-      })
-      .def("check_each", [](const KzgBatch& b, py::bytes g2_0, py::bytes g2_1) {
-        auto q0 = prepared_g2(B(g2_0)), q1 = prepared_g2(B(g2_1)), qg = prepared_g2(G2::generator().marshal());
-        std::vector<bool> ok(b.items.size());
-        py::gil_scoped_release rel;
-        for (size_t i = 0; i < b.items.size(); ++i)
-          ok[i] = multi_pairing_is_one({b.items[i][0], b.items[i][1].neg(), b.items[i][2]},
-                                       {q0.get(), q1.get(), qg.get()});
-        return ok;
-      });
   m.def("g1_from_device_jac", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> v) {
     if (v.size() != 24) throw std::runtime_error("g1_from_device_jac: expected 24 limbs");
     return P(g1_from_dev_jac(v.data()).marshal());

@@ -32,7 +32,7 @@ SIGNATURES = {
     "bsc_vrf_prove": [P, P, P, P, I, I, P, P, P, P, P],
     # kzg.hip
     "bsc_kzg_blocks": [I, I],
-    "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, U64, P, P, P],
+    "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, I, U64, P, P, P],
     # ml.hip
     "bsc_softmax_step": [P, P, P, P, P, P, I, I, I, I, U64, I, F, D, P, P, P, P],
     "bsc_logreg_step": [P, P, P, P, P, P, I, I, I, U64, P, D, D, P, D, P, P, P],

@@ -187,12 +187,14 @@ class DeviceCommitEngine:
 
         csum [nch, 24] chunk commitments; wsum [(npts/spm) * nch * spm, 24] witnesses (miner-major,
         chunk, share slot); ys int64 [nch, npts] share values at xs int32 [npts]; literal: pair y
-        against G1 for every chunk (the reference's verifySecret, quirk Q9) instead of PK[poly*k]."""
+        against G1 for every chunk (the reference's verifySecret, quirk Q9) instead of PK[poly*k].
+        Several rounds: nch = rounds * nchunks stacked chunks, xs [rounds, npts], wsum in (chunk,
+        point) order with spm = npts (kzg_order() gives that permutation of one round's sums)."""
         nch, npts = ys.shape
-        assert csum.dtype == torch.int32 and tuple(csum.shape) == (nch, 24) and nch == self.nchunks
+        assert csum.dtype == torch.int32 and tuple(csum.shape) == (nch, 24) and nch % self.nchunks == 0
         assert wsum.dtype == torch.int32 and tuple(wsum.shape) == (nch * npts, 24)
-        assert ys.dtype == torch.int64 and xs.dtype == torch.int32 and xs.numel() == npts
-        assert spm > 0 and npts % spm == 0
+        assert ys.dtype == torch.int64 and xs.dtype == torch.int32 and xs.numel() == npts * (nch // self.nchunks)
+        assert spm > 0 and npts % spm == 0 and (nch == self.nchunks or spm == npts)
         if literal:
             if getattr(self, "_g1_aff", None) is None:
                 self._g1_aff = u32_tensor(rt().g1_affine_mont_u32(rt().g1_generator()), self.device)
@@ -203,9 +205,21 @@ class DeviceCommitEngine:
         partial = torch.empty((lib.bsc_kzg_blocks(nch, npts), 72), dtype=torch.int32, device=self.device)
         out = torch.empty((3, 24), dtype=torch.int32, device=self.device)
         _check(lib.bsc_kzg_rlc(_ptr(csum.contiguous()), _ptr(wsum.contiguous()), _ptr(ys.contiguous()),
-                               _ptr(xs.contiguous()), nch, npts, int(spm), _ptr(bases), stride,
+                               _ptr(xs.contiguous()), nch, npts, int(spm), _ptr(bases), stride, self.nchunks,
                                int(seed) & ((1 << 64) - 1), _ptr(partial), _ptr(out), _stream()), "kzg_rlc")
         return out
+
+    def kzg_order(self, npts: int, spm: int) -> torch.Tensor:
+        """Row permutation taking one round's witness sums from (miner, chunk, slot) to (chunk, point)
+        order (int64 [nchunks * npts], cached): the layout several stacked rounds share."""
+        key = (npts, spm)
+        cache = self.__dict__.setdefault("_kzg_perm", {})
+        if key not in cache:
+            k = np.arange(self.nchunks)[:, None]
+            j = np.arange(npts)[None, :]
+            rows = (j // spm) * self.nchunks * spm + k * spm + j % spm
+            cache[key] = torch.from_numpy(rows.reshape(-1).astype(np.int64)).to(self.device)
+        return cache[key]
 
     def commitments(self, pts: torch.Tensor) -> torch.Tensor:
         """Full-vector commitment per row = sum of its chunk commitments. Returns Jacobian [n, 24]."""

@@ -332,9 +332,11 @@ class BiscottiEngine:
                 self.bg_stream, self.bg_cus = B.cu_masked_stream(self.dev, -cfg.side_stream_skip_every)
             else:
                 self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
-            # the device VRF proofs (kernels/vrf.hip, ~5 ms launches nothing waits for) get a stream of
-            # their own: on the background stream they would hold up the next round's commitments
-            self.vrf_stream = torch.cuda.Stream(device=self.dev, priority=lo) if cfg.vrf_device else None
+            # long device work nothing in a round waits for -- the VRF proofs (kernels/vrf.hip) and the
+            # KZG audit sums (kernels/kzg.hip), ~5 ms launches -- gets a stream of its own: on the
+            # background stream it would hold up the next round's commitments
+            self.vrf_stream = torch.cuda.Stream(device=self.dev, priority=lo) \
+                if cfg.vrf_device or cfg.kzg_audit != "off" else None
             torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
             torch.cuda.set_stream(self.main_stream)
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
@@ -365,9 +367,8 @@ class BiscottiEngine:
         self._W_next = None          # device copy of the model a block under construction carries
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
-        self._kzg_pending: list = []
-        self._kzg_jobs: list = []
-        self._kzg_batch = None
+        self._kzg_pending: list = []   # launched audits (device) or checked ones (CPU)
+        self._kzg_stage: list = []     # rounds waiting for the next device launch
         if cfg.kzg_audit != "off":
             self.stats.update(kzg_checks=0, kzg_failures=0)
             self._kzg_g2 = (self.R.g2_generator(), self._commit_key_g2_1(cfg.commit_key))
@@ -404,16 +405,33 @@ class BiscottiEngine:
         return self.R.g2_mul(self.R.g2_generator(), 2)
 
     def _kzg_queue(self, csum, wsum, ys, xs_t, it) -> None:
-        """Queue the device RLC sums of this round's aggregate on the current stream; their read-back
-        and the host pairing product run later (_kzg_poll), off the round's critical path."""
+        """Stage this round's aggregate for the device RLC sums (on the audit stream, current here);
+        kzg_batch_rounds rounds with the same share-point layout go into ONE launch and one pairing
+        product, read back and checked later (_kzg_poll), off the round's critical path."""
+        npts = ys.shape[1]
         spm = self.pc.shares_per_miner
-        seed = int(self._kzg_rng.integers(0, 2**63))
-        pts = self.crypto.eng.kzg_rlc(csum, wsum, ys, xs_t, spm, self.cfg.kzg_audit == "literal", seed)
-        host = torch.empty((3, 24), dtype=torch.int32, pin_memory=True)
-        host.copy_(pts, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(S.current())
-        self._kzg_pending.append({"it": it, "ev": ev, "host": host, "job": None})
+        if self._kzg_stage and self._kzg_stage[0]["npts"] != npts:
+            self._kzg_launch()
+        wperm = wsum.index_select(0, self.crypto.eng.kzg_order(npts, spm))   # (chunk, point) order
+        self._kzg_stage.append({"cs": csum, "ws": wperm, "ys": ys, "xs": xs_t, "npts": npts, "it": it})
+        if len(self._kzg_stage) >= self.cfg.kzg_batch_rounds:
+            self._kzg_launch()
+
+    def _kzg_launch(self) -> None:
+        st, self._kzg_stage = self._kzg_stage, []
+        if not st:
+            return
+        with S.use(self.vrf_stream):
+            cat = lambda k: torch.cat([e[k] for e in st]) if len(st) > 1 else st[0][k]
+            npts = st[0]["npts"]
+            pts = self.crypto.eng.kzg_rlc(cat("cs"), cat("ws"), cat("ys"), torch.stack([e["xs"] for e in st]),
+                                          npts, self.cfg.kzg_audit == "literal",
+                                          int(self._kzg_rng.integers(0, 2**63)))
+            host = torch.empty((3, 24), dtype=torch.int32, pin_memory=True)
+            host.copy_(pts, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.vrf_stream)
+        self._kzg_pending.append({"its": [e["it"] for e in st], "ev": ev, "host": host, "job": None})
 
     def _kzg_host(self, cs, ws, ys, xs, it) -> None:
         """CPU path: the same random linear combination on the host (native threads)."""
@@ -426,52 +444,36 @@ class BiscottiEngine:
             [self.crypto.key.point(self.cfg.poly_size * k) for k in range(nch)]
         pts = self.R.kzg_rlc_host(C, W, ys.numpy().reshape(-1), list(xs), bases,
                                   int(self._kzg_rng.integers(0, 2**63)), self.cfg.host_threads)
-        self._kzg_pending.append({"it": it, "ok": self.R.kzg_check(*pts, *self._kzg_g2)})
+        self._kzg_pending.append({"its": [it], "ok": self.R.kzg_check(*pts, *self._kzg_g2)})
 
     def _kzg_poll(self, final: bool = False) -> None:
-        """Fold the rounds whose device sums are ready into the open batch; every kzg_batch_rounds
-        rounds (and at the end) one pairing product checks the whole batch on a native thread.  A
-        failed batch is re-checked round by round to name the failing iterations."""
+        """Start the pairing products of launches whose sums are back, and collect finished ones (all
+        of them when final, the oldest when more than two are outstanding)."""
+        if final and self._kzg_stage:
+            self._kzg_launch()
         keep = []
-        for e in self._kzg_pending:
-            if "ok" in e:                      # CPU path: checked synchronously
-                self._kzg_record([e["it"]], [e["ok"]])
-            elif final or e["ev"].query():
+        for i, e in enumerate(self._kzg_pending):
+            must = final or len(self._kzg_pending) - i > 2
+            if "ok" not in e and e["job"] is None and (must or e["ev"].query()):
                 e["ev"].synchronize()
-                if self._kzg_batch is None:
-                    self._kzg_batch, self._kzg_its = self.R.KzgBatch(), []
-                self._kzg_batch.add(e["host"].numpy().view(np.uint32))
-                self._kzg_its.append(e["it"])
+                e["job"] = self.R.kzg_check_device_async(e["host"].numpy().view(np.uint32), *self._kzg_g2)
+            if "ok" not in e and e["job"] is not None and must:
+                e["ok"] = e["job"].result()
+            if "ok" in e:
+                self.stats["kzg_checks"] += len(e["its"])
+                if not e["ok"]:
+                    self.stats["kzg_failures"] += len(e["its"])
+                    self.log.info("KZG audit (verifySecret, %s) failed for the aggregates of iterations %s",
+                                  self.cfg.kzg_audit, e["its"])
             else:
                 keep.append(e)
         self._kzg_pending = keep
-        if self._kzg_batch is not None and (len(self._kzg_its) >= self.cfg.kzg_batch_rounds or final):
-            self._kzg_jobs.append((self._kzg_batch.check_async(*self._kzg_g2), self._kzg_batch, self._kzg_its))
-            self._kzg_batch = None
-        jobs = []
-        for job, batch, its in self._kzg_jobs:
-            if final or len(self._kzg_jobs) - len(jobs) > 2:
-                if job.result():
-                    self._kzg_record(its, [True] * len(its))
-                else:
-                    self._kzg_record(its, batch.check_each(*self._kzg_g2))
-            else:
-                jobs.append((job, batch, its))
-        self._kzg_jobs = jobs
-
-    def _kzg_record(self, its, oks) -> None:
-        for it, ok in zip(its, oks):
-            self.stats["kzg_checks"] += 1
-            if not ok:
-                self.stats["kzg_failures"] += 1
-                self.log.info("KZG audit (verifySecret, %s) failed for the aggregate of iteration %d",
-                              self.cfg.kzg_audit, it)
 
     def drain(self, final: bool = True) -> None:
         """Join work that belongs to rounds already returned: the last host VRF batch and, when
         final, the outstanding KZG audits and the device VRF proofs still queued or in flight."""
         if final:
-            if self._kzg_pending or self._kzg_jobs or self._kzg_batch is not None:
+            if self._kzg_pending or self._kzg_stage:
                 self._kzg_poll(final=True)
             if self.vrf_dev is not None and getattr(self, "vrf_stream", None) is not None:
                 self.vrf_dev.drain(self.vrf_stream)
@@ -1161,15 +1163,14 @@ class BiscottiEngine:
                         S.wait(st, main)
                     with S.use(st):
                         cs_part = B.sum_rows(flat, rows_t, ccols, check=False, row_mask=mask)
-                        if kzg:   # the witness sums get a consumer: the audit's RLC
-                            ws_part = B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask)
                     if st is not main:
-                        for t in (pts, ccols, wcols) + ((mask,) if mask is not None else (rows_t,)):
+                        for t in (pts, ccols) + ((mask,) if mask is not None else (rows_t,)):
                             t.record_stream(st)
-                if not kzg:
-                    self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
-                                     flat, wcols, mask if mask is not None else rows_t)
-                else:
+                # the miners' witness sums: no consumer on the protocol path (background stream); the
+                # KZG audit, when on, reads them from there
+                ws_part = self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
+                                           flat, wcols, mask if mask is not None else rows_t)
+                if kzg:
                     kzg_in = (cs_part, ws_part, None if single else ys_part.index_select(1, ycols_t.long()))
             else:
                 rows_l = list(rowsel)
@@ -1212,9 +1213,10 @@ class BiscottiEngine:
             cs_k, ws_k, y_k = kzg_in
             if self.gpu:
                 y_k = agg if y_k is None else y_k
-                bg = self.bg_stream
+                bg = self.vrf_stream
                 S.wait(bg, main)
                 S.wait(bg, self.side_stream)
+                S.wait(bg, self.bg_stream)
                 with S.use(bg):
                     self._kzg_queue(cs_k, ws_k, y_k, xs_t, self.fsm.iteration)
                 for t in (cs_k, ws_k, y_k, xs_t):
@@ -1382,7 +1384,7 @@ class BiscottiEngine:
                               int((ok == 0).sum()), plan.iteration)
                 return None
         self._last_nodes = node_list
-        if self._kzg_pending or self._kzg_jobs:
+        if self._kzg_pending:
             self._kzg_poll()
         return block
 
