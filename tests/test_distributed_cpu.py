@@ -30,25 +30,37 @@ def _worker(rank, world, port, kw, rounds, q):
     count = kw.pop("_count_collectives", False)
     comm = Comm.init(device="cpu")
     eng = BiscottiEngine(RunConfig(**kw), comm)
-    calls = []
+    calls, reads = [], []
     if count:
         import torch.distributed as dist
 
-        real = dist.all_gather_into_tensor
+        def wrap(name):
+            real = getattr(dist, name)
 
-        def counting(*a, **k):
-            calls.append(1)
-            return real(*a, **k)
-        dist.all_gather_into_tensor = counting
+            def counting(*a, **k):
+                calls.append(name)
+                return real(*a, **k)
+            setattr(dist, name, counting)
+        for name in ("all_gather_into_tensor", "all_gather", "all_reduce", "broadcast", "all_to_all_single",
+                     "all_to_all", "reduce_scatter_tensor", "gather", "scatter", "all_gather_object",
+                     "broadcast_object_list", "reduce"):
+            wrap(name)
+        real_d2h = eng._d2h
+
+        def counting_d2h(*ts):
+            reads.append(len(ts))
+            return real_d2h(*ts)
+        eng._d2h = counting_d2h
     per_round = []
     for _ in range(rounds):
-        n0 = len(calls)
+        n0, r0 = len(calls), len(reads)
         r = eng.run_round()
-        per_round.append((len(calls) - n0, r.empty))
+        per_round.append((len(calls) - n0, len(reads) - r0, r.empty))
     if count:
-        # every non-empty secure round: verification gather + aggregation gather
-        assert all(c == 2 for c, empty in per_round if not empty), per_round
-        assert any(not empty for _, empty in per_round)
+        # every non-empty secure round: the verification gather + the aggregation gather, and one
+        # batched read-back of the recovered model (+ clocks); nothing else crosses ranks
+        assert all(c == 2 and rd <= 2 for c, rd, empty in per_round if not empty), per_round
+        assert any(not empty for *_, empty in per_round)
     q.put((rank, [bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))]))
     comm.barrier()
     comm.shutdown()
@@ -104,13 +116,15 @@ def test_three_ranks_uneven_packing():
     assert multi[0] == single
 
 
-def test_collectives_per_round():
-    """A secure-aggregation round with Multi-Krum issues exactly two collectives on several ranks
-    (the verification all_gather and the aggregation all_gather): no accept-mask, signature or
-    block traffic (every rank replicates the committee and the recovery)."""
-    kw = dict(KW, num_nodes=8, seed=3)
-    out = _run(2, dict(kw, _count_collectives=True), 3)
-    assert out[0] == out[1]
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_collectives_per_round(world):
+    """A secure-aggregation round with Multi-Krum issues exactly two collectives of any kind on
+    2-4 ranks (the verification all_gather and the aggregation all_gather) and at most two batched
+    read-backs: no accept-mask, share, signature or block traffic (every rank replicates the
+    committee and the recovery)."""
+    kw = dict(KW, num_nodes=9, seed=3)
+    out = _run(world, dict(kw, _count_collectives=True), 3)
+    assert all(out[r] == out[0] for r in range(world))
 
 
 def test_peer_processes_localtest_oracle():
