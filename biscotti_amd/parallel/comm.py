@@ -56,7 +56,9 @@ class Comm:
             be = backend or ("nccl" if dev.type == "cuda" else "gloo")
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
             be = os.environ.get("BISCOTTI_BACKEND", be)
-            if be == "nccl" and torch.cuda.device_count() < local_world:
+            if be == "nccl" and torch.cuda.device_count() < local_world and not os.environ.get("NCCL_HOSTID"):
+                # (with a distinct NCCL_HOSTID per rank RCCL treats the ranks as separate hosts and
+                # connects them over its socket transport: the RCCL path rehearsed on one GPU)
                 # several ranks share one device (rehearsals on a 1-GPU box): RCCL refuses
                 # duplicate devices, gloo moves the same device tensors through host memory.  Said
                 # out loud: a multi-GPU run must never end up on gloo by accident.

@@ -1,0 +1,726 @@
+// EXPERIMENT (not built): msm.hip with the 29-bit-limb loops of bn29_experiment.h; see that file.
+// Batched fixed-base multi-scalar multiplication on BN256 G1 for Biscotti's secure aggregation.
+//
+// Reference hot loop: createCommitment / createShareAndWitness (DistSys/kyber.go:533-646),
+// ~180k Go big.Int double-and-add scalar multiplications per worker per round.
+//
+// MI355X design:
+//  * Commitment-key points PK[i] and witness bases B_{j,x} (B_1=PK[0], B_{j+1}=x*B_j+PK[j]) are
+//    fixed for the run, so each gets a signed-window table resident in HBM:
+//        T[base][w][k-1] = k * 2^(8w) * base,  k = 1..128, w = 0..NW-1     (affine, Montgomery)
+//    A scalar |c| < 2^64 is recoded into signed 8-bit digits (d in [-127, 128]); every non-zero
+//    digit costs one mixed (Jacobian + affine) addition and one 64-byte table read.
+//  * One thread per output point.  Threads of one (worker, chunk) group -- 21 witness lanes and
+//    the chunk-commitment lane -- consume the SAME scalar c_j at step j, so digit control flow is
+//    uniform inside a group, and the 21 witness lanes read 21 adjacent table points (1344 B
+//    contiguous, table layout [chunk][j][w][k][x][16]).
+//  * The share values y = p(x) (kyber.go:598-605, exact int64 Horner) are fused into the same
+//    kernel.  Full-vector commitment = sum of chunk commitments (PK slices are consecutive).
+//  * Blocks are remapped XCD-contiguously (chunk-major order), so one chunk's table lines are
+//    pulled into a single XCD's L2.
+#include <hip/hip_ext.h>
+
+#include <vector>
+
+#include "bn256_dev.h"
+#include "bn29_experiment.h"
+
+using namespace bn;
+
+namespace {
+
+constexpr int TBL_ENTRIES = 128;  // entries of an 8-bit signed window
+
+// Window plan of every fixed-base table: window 0 is B0 bits wide (2^(B0-1) entries: signed digits
+// |d| <= 2^(B0-1)), windows 1..NW-1 are 8 bits (128 entries).  Per base the entries are laid out
+// window 0 first, then 128 per further window; entry (w, |d|) of a base is entry index
+//   w == 0 ? |d| - 1 : E0 + (w - 1) * 128 + |d| - 1,   E0 = 2^(B0-1).
+// A wide first window turns the typical quantised update coefficient (|q| < 2^13) into ONE mixed
+// addition instead of two: HBM is spent (tens of GB of tables) to halve the MSM arithmetic.
+__device__ __forceinline__ int win_bits(int w, int B0) { return w ? 8 : B0; }
+__device__ __forceinline__ int win_entry(int w, int ad, int E0) { return (w ? E0 + (w - 1) * TBL_ENTRIES : 0) + ad - 1; }
+// next signed digit of width `bits` from (m, carry); digits lie in (-2^(bits-1), 2^(bits-1)]
+__device__ __forceinline__ int recode(unsigned long long& m, int& carry, int bits) {
+  int dg = (int)(m & ((1ull << bits) - 1)) + carry;
+  m >>= bits;
+  if (dg > (1 << (bits - 1))) {
+    dg -= 1 << bits;
+    carry = 1;
+  } else {
+    carry = 0;
+  }
+  return dg;
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  // bijective: blocks that share an XCD (bid % 8) get a contiguous logical range
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + idx;
+}
+
+// A table entry for the 29-bit-limb accumulation loops: tables hold canonical R29 coordinates
+// (k_fb_table), so the load is an unpack; negation of a canonical y is p - y.
+__device__ __forceinline__ bool ld_tbl29(const uint32_t* p, bool negate, bn29::aff29& q) {
+  q = bn29::ld_aff29(p);
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) z |= q.y.v[i];
+  if (z == 0) return false;   // infinity
+  if (negate) q.y = bn29::f29_neg_canon(q.y);
+  return true;
+}
+// R256 affine (canonical Montgomery) -> canonical R29 coordinates, packed (infinity stays (0, 0))
+__device__ __forceinline__ void st_aff_r29(uint32_t* dst, const aff& o) {
+  if (aff_is_inf(o)) {
+    st_aff(dst, o);
+    return;
+  }
+  fp x, y;
+  bn29::f29_pack(x.v, bn29::f29_canon(bn29::from_r256(o.x)));
+  bn29::f29_pack(y.v, bn29::f29_canon(bn29::from_r256(o.y)));
+  st_fp(dst, x);
+  st_fp(dst + 8, y);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ test kernels
+extern "C" __global__ void __launch_bounds__(256) k_fp_mul(const uint32_t* a, const uint32_t* b, uint32_t* out, int n, int op) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fp x = ld_fp(a + 8 * i), y = ld_fp(b + 8 * i), r;
+  switch (op) {
+    case 0: r = fp_mul(x, y); break;
+    case 1: r = fp_add(x, y); break;
+    case 2: r = fp_sub(x, y); break;
+    case 3: r = fp_inv(x); break;
+    default: r = fp_from_mont(x); break;
+  }
+  st_fp(out + 8 * i, r);
+}
+
+// op 0: jac(a)+jac(b) ; 1: jac(a)+aff(b) ; 2: dbl(jac(a)) ; 3: small mul a*k
+extern "C" __global__ void __launch_bounds__(256) k_point_op(const uint32_t* a_aff, const uint32_t* b_aff, const int* ks, uint32_t* out,
+                                      int n, int op) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  aff A = ld_aff(a_aff + 16 * i), Bq = ld_aff(b_aff + 16 * i);
+  jac a = jac_inf();
+  if (!aff_is_inf(A)) { a.x = A.x; a.y = A.y; a.z = fp_one(); }
+  jac b = jac_inf();
+  if (!aff_is_inf(Bq)) { b.x = Bq.x; b.y = Bq.y; b.z = fp_one(); }
+  jac r;
+  switch (op) {
+    case 0: r = jac_add(jac_dbl(a), b); break;  // non-trivial Z on the left operand
+    case 1: r = jac_add_aff(jac_dbl(a), Bq); break;
+    case 2: r = jac_dbl(a); break;
+    default: r = jac_mul_small(a, ks[i]); break;
+  }
+  st_jac(out + 24 * i, r);
+}
+
+// ------------------------------------------------------------------ witness bases
+// out: Jacobian [nchunks][J][T][24], J = poly-1.  Short chunks leave trailing bases = infinity.
+extern "C" __global__ void __launch_bounds__(128) k_witness_bases(const uint32_t* pk_aff, int d, int poly, int T, uint32_t* out) {
+  const int nchunks = (d + poly - 1) / poly;
+  const int J = poly - 1;
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nchunks * T) return;
+  const int k = g / T, s = g % T;
+  const int prev = k * poly;
+  const int L = min(poly, d - prev);
+  const int x = s - 10;  // kyber.go:588
+  jac b = jac_inf();
+  for (int j = 1; j <= J; ++j) {
+    if (j < L) {
+      aff pk = ld_aff(pk_aff + 16 * (prev + j - 1));
+      if (j == 1) {
+        b = jac_add_aff(jac_inf(), pk);
+      } else {
+        b = jac_add_aff(jac_mul_small(b, x), pk);
+      }
+      st_jac(out + 24 * (((size_t)k * J + (j - 1)) * T + s), b);
+    } else {
+      st_jac(out + 24 * (((size_t)k * J + (j - 1)) * T + s), jac_inf());
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fixed-base tables
+// Thread per (base b, run): a run is 128 consecutive entries of one window -- window 0 has
+// E0/128 runs, every 8-bit window one.  Run r of window w holds (128 r + k) * 2^shift_w * base,
+// k = 1..128, shift_0 = 0, shift_w = B0 + 8 (w - 1).  Base index b = outer * inner + in; entry e
+// of base b is stored at table + 16 * (outer * s_outer + e * s_e + in * s_in).
+// scratch: per thread 128 x 32 u32 (Jacobian + exclusive prefix product of the Z's).
+extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb,
+                                                           int inner, int B0, int NW, long long s_outer,
+                                                           long long s_e, long long s_in, uint32_t* table,
+                                                           uint32_t* scratch) {
+  const int E0 = 1 << (B0 - 1);
+  const int R0 = E0 / TBL_ENTRIES;
+  const int runs = R0 + NW - 1;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long long)nb * runs) return;
+  const int bl = (int)(g / runs), run = (int)(g % runs);
+  const int b = b0 + bl;
+  const int w = run < R0 ? 0 : run - R0 + 1;
+  const int r = run < R0 ? run : 0;
+  const int shift = w ? B0 + 8 * (w - 1) : 0;
+  const int e0 = w ? E0 + (w - 1) * TBL_ENTRIES : r * TBL_ENTRIES;
+  jac P;
+  if (bases_are_jac) {
+    P = ld_jac(bases + 24 * (size_t)b);
+  } else {
+    aff a = ld_aff(bases + 16 * (size_t)b);
+    P = jac_add_aff(jac_inf(), a);
+  }
+  for (int i = 0; i < shift; ++i) P = jac_dbl(P);
+  uint32_t* sc = scratch + (size_t)g * TBL_ENTRIES * 32;
+  jac acc = r ? jac_mul_small(P, r * TBL_ENTRIES + 1) : P;
+  fp prod = fp_one();
+  for (int k = 0; k < TBL_ENTRIES; ++k) {
+    st_jac(sc + 32 * k, acc);
+    st_fp(sc + 32 * k + 24, prod);  // exclusive prefix product of the non-zero Z's before k
+    if (!jac_is_inf(acc)) prod = fp_mul(prod, acc.z);
+    acc = jac_add(acc, P);
+  }
+  fp inv = fp_inv(prod);  // Montgomery's trick: one inversion per run
+  const int outer = b / inner, in = b % inner;
+  uint32_t* dst0 = table + 16 * ((long long)outer * s_outer + (long long)e0 * s_e + (long long)in * s_in);
+  for (int k = TBL_ENTRIES - 1; k >= 0; --k) {
+    jac pt = ld_jac(sc + 32 * k);
+    aff o;
+    if (jac_is_inf(pt)) {
+      o.x = fp_zero();
+      o.y = fp_zero();
+    } else {
+      fp zi = fp_mul(inv, ld_fp(sc + 32 * k + 24));  // 1 / z_k
+      inv = fp_mul(inv, pt.z);
+      fp zi2 = fp_sqr(zi);
+      o.x = fp_mul(pt.x, zi2);
+      o.y = fp_mul(pt.y, fp_mul(zi2, zi));
+    }
+    st_aff_r29(dst0 + 16 * ((long long)k * s_e), o);   // the MSM loops read R29 coordinates
+  }
+}
+
+// ------------------------------------------------------------------ fused shares + commitments
+// coeffs: int64 [*, d] (row stride d); rows: worker rows to process.
+// tbl_pk: [d][PB][16]; tbl_wb: [nchunks][J][PB][T][16]; PB = E0 + (NW-1)*128 entries per base.
+// out_pts: Jacobian [nrows][nchunks][S][24] with S = T+1 (slots 0..T-1 witnesses, slot T the chunk
+// commitment) or S = 1 (commit_only: chunk commitments only).  out_y: int64 [nrows][nchunks][T].
+extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
+    const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
+    int poly, int T, int B0, int NW, int commit_only, const int* alive, const int* compact, int group_rows,
+    uint32_t* out_pts, long long* out_y) {
+  const int nchunks = (d + poly - 1) / poly;
+  const int S = commit_only ? 1 : T + 1;
+  // compact (optional): [count, row...] -- only the listed rows are computed, packed densely over the
+  // grid (a rejected row costs no SIMD lanes); the grid is sized for nrows, the surplus exits at once
+  const int neff = compact != nullptr ? compact[0] : nrows;
+  const long long total = (long long)neff * nchunks * S;
+  // group_rows G > 0: rows are taken G at a time in list order (the speculative rows arrive sorted
+  // by their arrival at the leader), chunk-major inside a group, and the XCD remap is applied per
+  // 64-block super-block -- so work proceeds through the row list in dispatch order (rows the
+  // selection drops later are skipped when reached) while each XCD still shares a chunk's table
+  // lines across the group's rows.  G = 0: one group of every row, remapped over the whole grid.
+  int lb;
+  if (group_rows > 0) {
+    const int SB = 64;
+    const int q = blockIdx.x / SB, j = blockIdx.x % SB;
+    const int sbn = min(SB, (int)gridDim.x - q * SB);
+    lb = q * SB + xcd_remap(j, sbn);
+  } else {
+    lb = xcd_remap(blockIdx.x, gridDim.x);
+  }
+  const long long g = (long long)lb * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  const int G = group_rows > 0 ? min(group_rows, neff) : neff;
+  const long long per_group = (long long)G * nchunks * S;
+  const int gq = (int)(g / per_group);
+  const int r0 = gq * G, gr = min(G, neff - r0);
+  const long long gg = g - (long long)gq * per_group;
+  // chunk-major inside the group: consecutive groups of S lanes share a chunk (and its table lines)
+  const int slot = (int)(gg % S);
+  const long long grp = gg / S;
+  const int pos = r0 + (int)(grp % gr);
+  const int r = compact != nullptr ? compact[1 + pos] : pos;
+  const int k = (int)(grp / gr);
+  // late cancellation of speculative work: rows the verifiers rejected (flag cleared by
+  // k_set_alive on the critical-path stream while this kernel runs) are skipped from then on;
+  // their outputs are never read.  A stale read only costs the work.
+  if (alive != nullptr && __hip_atomic_load(alive + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  const int row = rows[r];
+  const int prev = k * poly;
+  const int L = min(poly, d - prev);
+  const bool is_commit = commit_only || slot == T;
+  const int J = poly - 1;
+  const long long* c = coeffs + (size_t)row * d + prev;
+
+  const int E0 = 1 << (B0 - 1);
+  const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
+  const size_t pk_base_stride = PB * 16;
+  const size_t wb_j_stride = PB * T * 16;
+  const uint32_t* wb_chunk = tbl_wb + (size_t)k * J * wb_j_stride;
+
+  bn29::jac29 acc = bn29::jac29_inf();
+  // commitment uses c_0..c_{L-1} on PK[prev..]; witness uses c_1..c_{L-1} on B_{1..L-1, x}
+  for (int j = is_commit ? 0 : 1; j < L; ++j) {
+    const long long cj = c[j];
+    if (cj == 0) continue;
+    const bool neg = cj < 0;
+    unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
+    const uint32_t* tb;
+    size_t estride;
+    if (is_commit) {
+      tb = tbl_pk + (size_t)(prev + j) * pk_base_stride;
+      estride = 16;
+    } else {
+      tb = wb_chunk + (size_t)(j - 1) * wb_j_stride + (size_t)slot * 16;
+      estride = (size_t)T * 16;
+    }
+    int carry = 0;
+    for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
+      const int dg = recode(m, carry, win_bits(w, B0));
+      if (dg == 0) continue;
+      const int ad = dg < 0 ? -dg : dg;
+      bn29::aff29 q;
+      if (ld_tbl29(tb + (size_t)win_entry(w, ad, E0) * estride, (dg < 0) != neg, q)) acc = bn29::jac29_add_aff(acc, q);
+    }
+  }
+  const size_t o = ((size_t)r * nchunks + k) * S + slot;
+  st_jac(out_pts + 24 * o, bn29::to_jac256(acc));
+  if (!is_commit && out_y != nullptr) {
+    // y = p(x) exact int64 Horner (kyber.go:598-605 evaluates the same value in float64)
+    const long long x = slot - 10;
+    unsigned long long y = 0;
+    for (int j = L - 1; j >= 0; --j) y = y * (unsigned long long)x + (unsigned long long)c[j];
+    out_y[((size_t)r * nchunks + k) * T + slot] = (long long)y;
+  }
+}
+
+// ------------------------------------------------------------------ full-vector commitments
+// C_row = sum_i c_i PK[i] for whole rows (the commit phase: commitUpdate, kyber.go:533-559).
+// One 256-thread block per (row, 1024-coefficient slab):
+//   1. signed 8-bit digit decomposition of the slab into an LDS work list of NONZERO digits
+//      (table entry index | sign bit) -- lanes holding different coefficients would otherwise
+//      diverge on their different digit counts;
+//   2. every lane consumes the list round-robin (uniform mixed additions, no divergence);
+//   3. LDS tree over the 256 partial sums (the list's LDS is reused).
+// out_partial: Jacobian [nrows][nslab][24]; bsc_commit_rows finishes with a per-row segment sum.
+#define COMMIT_CB 1024
+extern "C" __global__ void __launch_bounds__(256) k_commit_rows(const long long* coeffs, int d, const int* rows,
+                                                               int nrows, const uint32_t* tbl_pk, int B0, int NW,
+                                                               uint32_t* out_partial) {
+  __shared__ uint32_t lds[9 * COMMIT_CB];  // >= 256 * 24 for the reduction
+  __shared__ int cnt;
+  const int nslab = (d + COMMIT_CB - 1) / COMMIT_CB;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int r = b / nslab, slab = b % nslab;
+  if (r >= nrows) return;  // uniform per block
+  const long long* c = coeffs + (size_t)rows[r] * d;
+  const int c0 = slab * COMMIT_CB, c1 = min(d, c0 + COMMIT_CB);
+  const int E0 = 1 << (B0 - 1);
+  const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  for (int i = c0 + (int)threadIdx.x; i < c1; i += 256) {
+    const long long cj = c[i];
+    if (cj == 0) continue;
+    const bool neg = cj < 0;
+    unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
+    int carry = 0;
+    for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
+      const int dg = recode(m, carry, win_bits(w, B0));
+      if (dg == 0) continue;
+      const int ad = dg < 0 ? -dg : dg;
+      uint32_t e = (uint32_t)((size_t)i * PB + win_entry(w, ad, E0));
+      if ((dg < 0) != neg) e |= 0x80000000u;
+      lds[atomicAdd(&cnt, 1)] = e;
+    }
+  }
+  __syncthreads();
+  const int n = cnt;
+  bn29::jac29 acc = bn29::jac29_inf();
+  // software pipeline: the next table point is in flight while the current one is added
+  int k = threadIdx.x;
+  uint32_t e = k < n ? lds[k] : 0u;
+  aff q = ld_aff(tbl_pk + (size_t)(e & 0x7FFFFFFFu) * 16);
+  while (k < n) {
+    const int kn = k + 256;
+    const uint32_t en = kn < n ? lds[kn] : 0u;
+    const aff qn = ld_aff(tbl_pk + (size_t)(en & 0x7FFFFFFFu) * 16);
+    bn29::aff29 q29;
+    q29.x = bn29::f29_unpack(q.x.v);
+    q29.y = bn29::f29_unpack(q.y.v);
+    if (!aff_is_inf(q)) {
+      if (e >> 31) q29.y = bn29::f29_neg_canon(q29.y);
+      acc = bn29::jac29_add_aff(acc, q29);
+    }
+    k = kn;
+    e = en;
+    q = qn;
+  }
+  __syncthreads();
+  st_jac(lds + threadIdx.x * 24, bn29::to_jac256(acc));
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      st_jac(lds + threadIdx.x * 24, jac_add(ld_jac(lds + threadIdx.x * 24), ld_jac(lds + (threadIdx.x + s) * 24)));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) st_jac(out_partial + 24 * (size_t)b, ld_jac(lds));
+}
+
+// ------------------------------------------------------------------ aggregate commitment audit
+// verifyCommitment (kyber.go:564-577) applied to the secure aggregate: by additive homomorphism
+// the miners' summed chunk commitments sum_w C_k(q_w) must equal the commitment of the recovered
+// chunk C_k(sum_w q_w).  One 64-lane block per chunk: lane j < L adds c_j * PK[prev + j] from the
+// fixed-base tables, an LDS tree sums the lanes, then lane m compares the result projectively
+// (X1 Z2^2 == X2 Z1^2, Y1 Z2^3 == Y2 Z1^3: no inversion) with miner m's sum.
+// coeffs: int64 [nch][poly] (recovered); csum: Jacobian [nm][nch][24]; ok: int32 [nm][nch].
+__device__ __forceinline__ bool jac_equal(const jac& p, const jac& q) {
+  const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  const fp z1s = fp_sqr(p.z), z2s = fp_sqr(q.z);
+  if (!fp_eq(fp_mul(p.x, z2s), fp_mul(q.x, z1s))) return false;
+  return fp_eq(fp_mul(p.y, fp_mul(z2s, q.z)), fp_mul(q.y, fp_mul(z1s, p.z)));
+}
+
+// One wave per chunk, one lane per (coefficient, window) digit: every lane issues its table fetch
+// up front (the fetches are independent; with one lane per coefficient the window loop exposed a
+// dependent HBM/TLB round trip per window -- the kernel sat on the critical path latency-bound),
+// then an LDS tree sums the <= 64 points and lane 0 compares with each miner's sum.
+extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* coeffs, int d, int poly,
+                                                              const uint32_t* tbl_pk, int B0, int NW,
+                                                              const uint32_t* csum, int nm, int nch, int* ok) {
+  __shared__ uint32_t sh[64 * 24];
+  __shared__ int dig[16][9];   // signed digit of (coefficient j, window w); NW <= 9 (bsc_chunk_check)
+  const int k = blockIdx.x, t = threadIdx.x;
+  const int prev = k * poly, L = min(poly, d - prev);
+  const int E0 = 1 << (B0 - 1);
+  const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
+  // 1. digits of every coefficient (cheap integer work, one lane per coefficient)
+  if (t < 16) {
+    for (int w = 0; w < 9; ++w) dig[t][w] = 0;
+    if (t < L) {
+      const long long cj = coeffs[(size_t)k * poly + t];
+      const bool neg = cj < 0;
+      unsigned long long m = neg ? 0ull - (unsigned long long)cj : (unsigned long long)cj;
+      int carry = 0;
+      for (int w = 0; w < NW && (m != 0 || carry != 0); ++w) {
+        const int dg = recode(m, carry, win_bits(w, B0));
+        dig[t][w] = neg ? -dg : dg;
+      }
+    }
+  }
+  __syncthreads();
+  // 2. lane e -> (coefficient e / 9, window e % 9): its fetch issued before any addition
+  bn29::jac29 acc = bn29::jac29_inf();
+  for (int e = t; e < L * 9; e += 64) {
+    const int j = e / 9, w = e % 9;
+    const int dg = w < NW ? dig[j][w] : 0;
+    if (dg == 0) continue;
+    const int ad = dg < 0 ? -dg : dg;
+    bn29::aff29 q;
+    if (ld_tbl29(tbl_pk + ((size_t)(prev + j) * PB + win_entry(w, ad, E0)) * 16, dg < 0, q))
+      acc = bn29::jac29_add_aff(acc, q);
+  }
+  st_jac(sh + t * 24, bn29::to_jac256(acc));
+  __syncthreads();
+  for (int s = 32; s > 0; s >>= 1) {
+    if (t < s) st_jac(sh + t * 24, jac_add(ld_jac(sh + t * 24), ld_jac(sh + (t + s) * 24)));
+    __syncthreads();
+  }
+  if (t < nm) ok[(size_t)t * nch + k] = jac_equal(ld_jac(sh), ld_jac(csum + 24 * ((size_t)t * nch + k))) ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ reductions
+// out[i] = sum_{r < nrows} pts[(rows[r] * ncols_in + cols[i]) * 24]   (cols == nullptr: cols[i] = i)
+// One thread per output column; used for miner-side share aggregation (aggregateSecret).
+extern "C" __global__ void __launch_bounds__(128) k_sum_rows(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
+                                      int ncols, uint32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncols) return;
+  const int col = cols ? cols[i] : i;
+  jac acc = jac_inf();
+  for (int r = 0; r < nrows; ++r) {
+    const int row = rows ? rows[r] : r;
+    acc = jac_add(acc, ld_jac(pts + 24 * ((size_t)row * ncols_in + col)));
+  }
+  st_jac(out + 24 * (size_t)i, acc);
+}
+
+// Two-level version: block = 32 columns x 8 row groups; each thread sums every 8th row of its
+// column, then an LDS tree over the 8 partials.  8x the parallelism of k_sum_rows, and the column
+// list may concatenate several miners' slots (one launch per rank).
+// row_mask (optional, indexed by input row): rows whose flag is 0 are left out -- the device-side
+// selection of the approved workers' shares, decided by the verification kernels on the GPU.
+extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
+                                                             int nrows, const int* cols, int ncols,
+                                                             const int* row_mask, uint32_t* out) {
+  // 16 columns x 16 row lanes per block: each lane's serial chain is nrows/16 additions, then a
+  // 4-level LDS tree (the sums sit on the round's critical path: latency, not throughput, matters)
+  __shared__ uint32_t sh[16][16][24];
+  const int cx = threadIdx.x & 15, ry = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + cx;
+  jac acc = jac_inf();
+  if (i < ncols && ry < nrows) {
+    const int col = cols ? cols[i] : i;
+    // software pipeline: load row r + 16 while adding row r
+    int row = rows ? rows[ry] : ry;
+    jac cur = ld_jac(pts + 24 * ((size_t)row * ncols_in + col));
+    for (int r = ry; r < nrows; r += 16) {
+      const int rn = r + 16 < nrows ? r + 16 : r;
+      const int rown = rows ? rows[rn] : rn;
+      const jac nxt = ld_jac(pts + 24 * ((size_t)rown * ncols_in + col));
+      if (row_mask == nullptr || row_mask[row] != 0) acc = jac_add(acc, cur);
+      cur = nxt;
+      row = rown;
+    }
+  }
+  st_jac(&sh[ry][cx][0], acc);
+  __syncthreads();
+  for (int s2 = 8; s2 > 0; s2 >>= 1) {
+    if (ry < s2) st_jac(&sh[ry][cx][0], jac_add(ld_jac(&sh[ry][cx][0]), ld_jac(&sh[ry + s2][cx][0])));
+    __syncthreads();
+  }
+  if (ry == 0 && i < ncols) st_jac(out + 24 * (size_t)i, ld_jac(&sh[0][cx][0]));
+}
+
+// Sum of a strided segment per group: out[g] = sum_{k<n} pts[(g*n + k)*stride + off], one block
+// per group, LDS tree.  Used for the full commitment = sum of chunk commitments.
+extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* pts, int n, int stride, int off,
+                                                               uint32_t* out) {
+  __shared__ uint32_t sh[256 * 24];
+  const int g = blockIdx.x;
+  jac acc = jac_inf();
+  for (int k = threadIdx.x; k < n; k += blockDim.x)
+    acc = jac_add(acc, ld_jac(pts + 24 * ((size_t)(g * (size_t)n + k) * stride + off)));
+  st_jac(sh + threadIdx.x * 24, acc);
+  __syncthreads();
+  // tree only over the lanes that hold partial sums (n is typically 8 slabs: 3 levels, not 8)
+  int top = 1;
+  while (top < n && top < (int)blockDim.x) top <<= 1;
+  for (int s = top / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      jac a = ld_jac(sh + threadIdx.x * 24), b = ld_jac(sh + (threadIdx.x + s) * 24);
+      st_jac(sh + threadIdx.x * 24, jac_add(a, b));
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) st_jac(out + 24 * (size_t)g, ld_jac(sh));
+}
+
+// Jacobian -> kyber marshal (64 B: big-endian affine x || y, Montgomery-decoded; infinity = 0s)
+extern "C" __global__ void __launch_bounds__(64) k_marshal(const uint32_t* pts, int n, uint8_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  aff a = jac_to_aff(ld_jac(pts + 24 * (size_t)i));
+  uint8_t* o = out + 64 * (size_t)i;
+  if (aff_is_inf(a)) {
+    for (int t = 0; t < 64; ++t) o[t] = 0;
+    return;
+  }
+  fp x = fp_from_mont(a.x), y = fp_from_mont(a.y);
+  for (int l = 0; l < 8; ++l) {
+    const uint32_t vx = x.v[7 - l], vy = y.v[7 - l];
+    for (int b = 0; b < 4; ++b) {
+      o[4 * l + b] = (uint8_t)(vx >> (24 - 8 * b));
+      o[32 + 4 * l + b] = (uint8_t)(vy >> (24 - 8 * b));
+    }
+  }
+}
+
+// Jacobian -> affine (Montgomery) [n][16]
+extern "C" __global__ void __launch_bounds__(64) k_to_affine(const uint32_t* pts, int n, uint32_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st_aff(out + 16 * (size_t)i, jac_to_aff(ld_jac(pts + 24 * (size_t)i)));
+}
+
+// ------------------------------------------------------------------ C ABI launchers
+// (same translation unit as the kernels: no relocatable device code needed)
+static inline int blocks_for(long long n, int bs) { return (int)((n + bs - 1) / bs); }
+
+extern "C" int bsc_fp_op(const uint32_t* a, const uint32_t* b, uint32_t* out, int n, int op, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_fp_mul, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, a, b, out, n, op);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_point_op(const uint32_t* a, const uint32_t* b, const int* ks, uint32_t* out, int n, int op,
+                            void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_point_op, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, a, b, ks, out, n, op);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_witness_bases(const uint32_t* pk_aff, int d, int poly, int T, uint32_t* out, void* stream) {
+  const int nchunks = (d + poly - 1) / poly;
+  const long long n = (long long)nchunks * T;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_witness_bases, dim3(blocks_for(n, 128)), dim3(128), 0, (hipStream_t)stream, pk_aff, d, poly,
+                     T, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_fb_table(const uint32_t* bases, int bases_are_jac, int b0, int nb, int inner, int B0, int NW,
+                            long long s_outer, long long s_e, long long s_in, uint32_t* table, uint32_t* scratch,
+                            void* stream) {
+  if (B0 < 8 || B0 > 20 || NW < 1) return -1;
+  const long long runs = (1ll << (B0 - 1)) / TBL_ENTRIES + NW - 1;
+  const long long n = (long long)nb * runs;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_fb_table, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, bases, bases_are_jac, b0,
+                     nb, inner, B0, NW, s_outer, s_e, s_in, table, scratch);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
+                              const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
+                              const int* alive, const int* compact, int group_rows, uint32_t* out_pts,
+                              long long* out_y, void* stream) {
+  if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;  // every int64 scalar must be covered
+  const int nchunks = (d + poly - 1) / poly;
+  const int S = commit_only ? 1 : T + 1;
+  const long long n = (long long)nrows * nchunks * S;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_shares_msm, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows,
+                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, compact, group_rows, out_pts,
+                     out_y);
+  return (int)hipGetLastError();
+}
+
+// compact = [count, r0, r1, ...]: the rows r with alive[r] != 0, ascending (one block, n <= 4096)
+extern "C" __global__ void __launch_bounds__(1024) k_alive_compact(const int* alive, int n, int* compact) {
+  __shared__ int cnt[1024];
+  const int t = threadIdx.x;
+  const int per = (n + 1023) / 1024;
+  const int lo = t * per, hi = min(n, lo + per);
+  int c = 0;
+  for (int r = lo; r < hi; ++r) c += alive[r] != 0;
+  cnt[t] = c;
+  __syncthreads();
+  // inclusive scan over the 1024 per-thread counts (Hillis-Steele)
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = t >= o ? cnt[t - o] : 0;
+    __syncthreads();
+    cnt[t] += v;
+    __syncthreads();
+  }
+  int w = cnt[t] - c;
+  for (int r = lo; r < hi; ++r)
+    if (alive[r] != 0) compact[1 + w++] = r;
+  if (t == 1023) compact[0] = cnt[1023];
+}
+
+extern "C" int bsc_alive_compact(const int* alive, int n, int* compact, void* stream) {
+  if (n < 0 || n > 4096) return -1;
+  hipLaunchKernelGGL(k_alive_compact, dim3(1), dim3(1024), 0, (hipStream_t)stream, alive, n, compact);
+  return (int)hipGetLastError();
+}
+
+// alive[map[j]] = accept[j] for every verified update j with a speculative row (map[j] >= 0):
+// agent-scope stores, read by a k_shares_msm still running on another stream.
+extern "C" __global__ void k_set_alive(const int* accept, const int* map, int n, int* alive) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int r = map[j];
+  if (r >= 0) __hip_atomic_store(alive + r, accept[j] ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+extern "C" int bsc_set_alive(const int* accept, const int* map, int n, int* alive, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_set_alive, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, accept, map, n, alive);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_sum_rows(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols, int ncols,
+                            uint32_t* out, void* stream) {
+  if (ncols <= 0) return 0;
+  hipLaunchKernelGGL(k_sum_rows, dim3(blocks_for(ncols, 128)), dim3(128), 0, (hipStream_t)stream, pts, ncols_in,
+                     rows, nrows, cols, ncols, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
+                             int ncols, const int* row_mask, uint32_t* out, void* stream) {
+  if (ncols <= 0) return 0;
+  hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 16)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
+                     rows, nrows, cols, ncols, row_mask, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
+                               int B0, int NW, uint32_t* partial, uint32_t* out, void* stream) {
+  if (nrows <= 0) return 0;
+  if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65 || NW > 9) return -1;
+  const long long PB = (1ll << (B0 - 1)) + (long long)(NW - 1) * TBL_ENTRIES;
+  if ((long long)d * PB >= (1ll << 31)) return -1;
+  const int nslab = (d + COMMIT_CB - 1) / COMMIT_CB;
+  hipLaunchKernelGGL(k_commit_rows, dim3(nrows * nslab), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows, nrows,
+                     tbl_pk, B0, NW, partial);
+  hipLaunchKernelGGL(k_segment_sum, dim3(nrows), dim3(256), 0, (hipStream_t)stream, partial, nslab, 1, 0, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
+                               void* stream) {
+  if (ngroups <= 0) return 0;
+  hipLaunchKernelGGL(k_segment_sum, dim3(ngroups), dim3(256), 0, (hipStream_t)stream, pts, n, stride, off, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
+                               const uint32_t* csum, int nm, int nch, int* ok, void* stream) {
+  if (nch <= 0 || nm <= 0) return 0;
+  if (poly < 1 || poly > 16 || nm > 64 || B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65 || NW > 9) return -1;
+  if ((long long)nch * poly < d || (long long)(nch - 1) * poly >= d) return -1;
+  hipLaunchKernelGGL(k_chunk_check, dim3(nch), dim3(64), 0, (hipStream_t)stream, coeffs, d, poly, tbl_pk, B0, NW,
+                     csum, nm, nch, ok);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_marshal(const uint32_t* pts, int n, uint8_t* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_marshal, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, pts, n, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int bsc_to_affine(const uint32_t* pts, int n, uint32_t* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_to_affine, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, pts, n, out);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------ streams
+// A stream restricted to a subset of the CUs: the speculative share/commitment MSMs run there so
+// the protocol's critical-path kernels (noise, Krum, aggregation) always find idle CUs -- HIP
+// stream priorities only order dispatch, they do not preempt the MSM's long-lived waves.
+// `skip_every` = 4 leaves every 4th CU (spread over all XCDs / shader engines) out of the mask.
+extern "C" void* bsc_stream_create_cumask(int skip_every, int* ncu_used) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return nullptr;
+  const int ncu = prop.multiProcessorCount;
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  int used = 0;
+  // skip_every < 0: the complement -- ONLY the CUs a stream created with -skip_every leaves free
+  const int k = skip_every < 0 ? -skip_every : skip_every;
+  for (int c = 0; c < ncu; ++c) {
+    const bool skipped = k > 0 && c % k == k - 1;
+    if (skip_every < 0 ? !skipped : skipped) continue;
+    mask[c / 32] |= 1u << (c % 32);
+    ++used;
+  }
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
+  if (ncu_used) *ncu_used = used;
+  return (void*)st;
+}
+
+extern "C" int bsc_stream_destroy(void* st) { return (int)hipStreamDestroy((hipStream_t)st); }

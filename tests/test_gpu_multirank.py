@@ -1,5 +1,6 @@
-"""Multi-rank engine on the GPU: 2 and 4 ranks share cuda:0 over the gloo backend (RCCL cannot put
-two ranks on one device), which runs every device-side multi-rank path -- the all_gather of
+"""Multi-rank engine on the GPU: 2 and 4 ranks share cuda:0 over the gloo backend, and 2 ranks over
+RCCL (distinct NCCL_HOSTIDs: RCCL's socket transport on loopback), which runs every device-side
+multi-rank path -- the all_gather of
 commitments + noised deltas, the replicated committee Krum, per-rank partial share sums and their
 all_gather, replicated exact recovery -- and must reproduce the single-process GPU chain byte for
 byte (deterministic timestamps), also with poisoners and churn."""
@@ -16,9 +17,14 @@ from test_distributed_cpu import ROOT, _free_port
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, kw, rounds, q):
+def _worker(rank, world, port, kw, rounds, q, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", BSC_TABLE_B0="10")
+    if backend == "nccl":
+        # RCCL refuses two ranks on one device within a host; a distinct host id per rank makes it
+        # connect them through its socket transport on loopback -- RCCL's init, proxy threads and
+        # collective kernels all run, on cuda:0 for both ranks
+        os.environ.update(NCCL_HOSTID=f"biscotti-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     sys.path.insert(0, ROOT)
     import torch
 
@@ -26,8 +32,9 @@ def _worker(rank, world, port, kw, rounds, q):
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
-    comm = Comm.init(backend="gloo") if world > 1 else Comm(device=torch.device("cuda", 0))
+    comm = Comm.init(backend=backend) if world > 1 else Comm(device=torch.device("cuda", 0))
     assert comm.device.type == "cuda"
+    assert world == 1 or comm.backend == backend, (comm.backend, backend)
     eng = BiscottiEngine(RunConfig(**kw), comm)
     for _ in range(rounds):
         eng.run_round()
@@ -37,11 +44,11 @@ def _worker(rank, world, port, kw, rounds, q):
     comm.shutdown()
 
 
-def _run(world, kw, rounds):
+def _run(world, kw, rounds, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, kw, rounds, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kw, rounds, q, backend)) for r in range(world)]
     for p in ps:
         p.start()
     out, deadline = {}, time.time() + 400
@@ -79,4 +86,14 @@ def test_gpu_four_ranks_poisoning_and_churn_match_single_process():
     single = _run(1, kw, 4)[0]
     multi = _run(4, kw, 4)
     assert multi[0] == multi[1] == multi[2] == multi[3]
+    assert multi[0] == single
+
+
+def test_gpu_two_ranks_over_rccl_match_single_process():
+    """The same round over the RCCL ("nccl") backend: both collectives of a secure round (the
+    packed all_gathers) run through RCCL and the chain equals the single-process GPU chain."""
+    kw = dict(num_nodes=12, dataset="mnist", seed=5, deterministic_time=True, max_iterations=100)
+    single = _run(1, kw, 3)[0]
+    multi = _run(2, kw, 3, backend="nccl")
+    assert multi[0] == multi[1]
     assert multi[0] == single
