@@ -13,7 +13,10 @@ import numpy as np
 import torch
 
 from ..native import hip, rt
+from ..utils import h2d
 from ..utils import streams as S
+
+_TORCH_OF = {np.dtype(np.int32): torch.int32, np.dtype(np.uint8): torch.uint8}
 
 
 def _i32(b: bytes) -> np.ndarray:
@@ -48,14 +51,17 @@ class DeviceVrfProver:
     def prove(self, seeds, alphas, beta: bool = False):
         """Proofs of seeds[i] over alphas[i] (32-byte messages) on the current stream: (pi uint8
         [n, 80], beta uint8 [n, 64] or None).  Asynchronous: read the tensors after a sync."""
-        n = len(seeds)
-        assert len(alphas) == n and all(len(a) == self.ALPHA_LEN for a in alphas)
-        rows = self._rows(seeds)
+        assert len(alphas) == len(seeds) and all(len(a) == self.ALPHA_LEN for a in alphas)
+        uniq = {a: i for i, a in enumerate(dict.fromkeys(alphas))}
+        return self._launch(np.asarray(self._rows(seeds), np.int32), list(uniq),
+                            np.asarray([uniq[a] for a in alphas], np.int32), beta)
+
+    def _launch(self, rows: np.ndarray, alphas: list, alpha_idx: np.ndarray, beta: bool = False):
+        n = int(rows.size)
         if self._keys_dev is None:
             self._keys_dev = self._upload(np.concatenate(self._keys))
-        uniq = {a: i for i, a in enumerate(dict.fromkeys(alphas))}
-        al = self._upload(np.frombuffer(b"".join(uniq), np.uint8))
-        idx = self._upload(np.asarray(rows + [uniq[a] for a in alphas], np.int32))
+        al = self._upload(np.frombuffer(b"".join(alphas), np.uint8))
+        idx = self._upload(np.concatenate([rows, alpha_idx]))
         scratch = torch.empty((max(n, 1), 320), dtype=torch.int32, device=self.device)
         pi = torch.empty((n, 80), dtype=torch.uint8, device=self.device)
         bt = torch.empty((n, 64), dtype=torch.uint8, device=self.device) if beta else None
@@ -68,26 +74,26 @@ class DeviceVrfProver:
         return pi, bt
 
     def _upload(self, a: np.ndarray) -> torch.Tensor:
-        # pinned staging + a stream-ordered copy: a pageable .to(device) is a blocking copy that can
-        # stall the host behind the round's queued kernels
-        h = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
-        return h.to(self.device, non_blocking=True)
+        # through the pinned staging ring (utils.h2d), stream-ordered: a pageable .to(device) blocks
+        # behind the round's queued kernels, and a fresh pin_memory() costs ~1 ms of host time
+        return h2d(np.ascontiguousarray(a), _TORCH_OF[a.dtype], self.device)
 
     # ---- round-batched queue: the engine submits each round's proofs, one launch per batch_rounds
     def submit(self, seeds, alpha: bytes, stream) -> None:
         if seeds:
-            self._queue.append((list(seeds), bytes(alpha)))
+            # key rows resolved now (a few dict lookups per round), so a flush only concatenates
+            self._queue.append((np.asarray(self._rows(seeds), np.int32), bytes(alpha)))
         if len(self._queue) >= self.batch_rounds:
             self.flush(stream)
 
     def flush(self, stream) -> None:
         if not self._queue:
             return
-        seeds = [s for ss, _ in self._queue for s in ss]
-        alphas = [a for ss, a in self._queue for _ in ss]
-        self._queue = []
+        q, self._queue = self._queue, []
+        rows = np.concatenate([r for r, _ in q])
+        alpha_idx = np.repeat(np.arange(len(q), dtype=np.int32), [r.size for r, _ in q])
         with S.use(stream):   # uploads, scratch and the launch all on the prover's stream
-            pi, _ = self.prove(seeds, alphas)
+            pi, _ = self._launch(rows, [a for _, a in q], alpha_idx)
             ev = S.record(stream)
         self._inflight.append((ev, pi))
         # keep the last few batches alive until their kernels finished (the proofs are discarded)

@@ -895,7 +895,8 @@ class BiscottiEngine:
                     acc_np = acc_t.numpy().astype(np.uint8)   # [len(vs), ni]
                     acc_row = {v: k for k, v in enumerate(vs)}
                     if box.get("sa") is not None:   # the rows the device aggregation kept
-                        kept = {w for w in workers if bool(node_t[xrow[w]])}
+                        node_np = node_t.numpy()
+                        kept = {w for w in workers if node_np[xrow[w]]}
                         # a block row outside the (replicated) speculative prefix was never computed:
                         # the device aggregate is then incomplete and the host path tops it up
                         if not kept <= head["spec_cand"]:
