@@ -53,6 +53,13 @@ class Comm:
         else:
             dev = torch.device("cpu")
         if world > 1 and not dist.is_initialized():
+            if os.environ.get("BISCOTTI_RCCL_SHARED_DEVICE") == "1":
+                # rehearsal of the RCCL path with several ranks on one GPU: a distinct host id per rank
+                # makes RCCL connect them through its socket transport instead of refusing the
+                # duplicate device (test_gpu_multirank.py, scripts/gpu_rccl_bench.sh)
+                os.environ.setdefault("NCCL_HOSTID", f"biscotti-rank{rank}")
+                os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+                os.environ.setdefault("NCCL_IB_DISABLE", "1")
             be = backend or ("nccl" if dev.type == "cuda" else "gloo")
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
             be = os.environ.get("BISCOTTI_BACKEND", be)

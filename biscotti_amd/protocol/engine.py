@@ -351,8 +351,10 @@ class BiscottiEngine:
             for i in range(self.N):
                 s, p = self.R.client_key_from_entropy(_seed_bytes(cfg.seed, "client", i))
                 self.sk[i], self.pk[i] = s, p
-        self.vrf_noise_seed = {i: _seed_bytes(cfg.seed, "vrf-noise", i) for i in self.local}
-        self.vrf_roles_seed = {i: _seed_bytes(cfg.seed, "vrf-roles", i) for i in self.local}
+        # every peer's VRF seeds (the multi-rank noise-aware Krum replicates the noiser lottery, whose
+        # outputs are publicly verifiable, on every rank); churn epochs are replicated too
+        self.vrf_noise_seed = {i: _seed_bytes(cfg.seed, "vrf-noise", i) for i in range(self.N)}
+        self.vrf_roles_seed = {i: _seed_bytes(cfg.seed, "vrf-roles", i) for i in range(self.N)}
         self.sigma = self.task.noise_sigma(cfg.epsilon)
         # every noiser's 100 pre-sampled noise vectors resident in HBM (314 MB for MNIST x 100 peers)
         self.noise_tbl = None
@@ -572,13 +574,13 @@ class BiscottiEngine:
                 height = len(fsm.chain)
                 st["epoch"][p] = st["epoch"].get(p, 0) + 1
                 st["rejoins"] += 1
+                e = st["epoch"][p]
+                self.vrf_noise_seed[p] = _seed_bytes(cfg.seed, f"vrf-noise-e{e}", p)
+                self.vrf_roles_seed[p] = _seed_bytes(cfg.seed, f"vrf-roles-e{e}", p)
                 if p in self.local:
                     ok, why = fsm.chain.verify_range(max(0, view - 1), height)
                     if not ok:
                         raise RuntimeError(f"peer {p}: the chain offered at rejoin does not verify: {why}")
-                    e = st["epoch"][p]
-                    self.vrf_noise_seed[p] = _seed_bytes(cfg.seed, f"vrf-noise-e{e}", p)
-                    self.vrf_roles_seed[p] = _seed_bytes(cfg.seed, f"vrf-roles-e{e}", p)
                     st["synced_blocks"] += height - view
                     self.log.info("%d:Rejoined at iteration %d: adopted a chain of %d blocks (%d verified)", p, it,
                                   height, height - view)
@@ -631,11 +633,20 @@ class BiscottiEngine:
         # cancels speculative MSM rows), and they need nothing but the plan and the block hash: they
         # start first, on host_threads - 1 native threads (the launching thread keeps a core); the
         # proofs nothing reads run on the device (vrf_device) or after the outputs on the host.
+        # Several ranks with the noise-aware Krum: every rank evaluates the committee over every
+        # worker, so it needs every worker's noisers -- each rank replicates the (publicly verifiable)
+        # VRF outputs instead of a gather after them; only the local proofs are produced here.
+        mr_pre = (self.gpu and self.comm.world > 1 and cfg.secure_agg and cfg.verification and cfg.defense == "KRUM"
+                  and cfg.noising and self.sigma > 0 and self.noise_tbl is not None and not cfg.noise_independent
+                  and cfg.krum_pregram)
+        vrf_workers = workers if mr_pre else local_workers
+        head["vrf_workers"] = vrf_workers
         with self.timer.phase("head.vrf_submit"):
             seeds = [self.vrf_noise_seed[w] for w in local_workers]
             dev = self.vrf_dev is not None
             nthr = max(1, cfg.host_threads - 1) if self.gpu else cfg.host_threads
-            fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, nthr, None, dev) if seeds else None
+            vseeds = seeds if vrf_workers is local_workers else [self.vrf_noise_seed[w] for w in vrf_workers]
+            fut_noise = R.vrf_prove_batch_async(vseeds, latest_hash, nthr, None, dev) if vseeds else None
             fut_roles = None
             roles = [self.vrf_roles_seed[p] for p in self.local if live[p]] if cfg.roles_vrf_proof else []
             if roles and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
@@ -693,6 +704,18 @@ class BiscottiEngine:
                 and not cfg.noise_independent and cfg.krum_pregram):
             with tm.phase("verify.pregram"):
                 krum_pre = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
+        elif mr_pre and inboxes and workers:
+            # several ranks: ONE all_gather of the deltas right here (the first collective of the round),
+            # then every rank runs the same phase-1 Gram over [every worker's delta; noise rows] while
+            # the VRF outputs are computed -- the commitments travel later, off Krum's path
+            with tm.phase("verify.pregram"):
+                buf = torch.zeros((self.maxlocal, self.d), dtype=torch.float32, device=self.dev)
+                if local_workers:
+                    buf.index_copy_(0, h2d([w - self.lo for w in local_workers], torch.long, self.dev), delta)
+                g = self.comm.all_gather(buf).reshape(-1, self.d)
+                Xw = g.index_select(0, h2d([self.flat[w] for w in workers], torch.long, self.dev)).contiguous()
+                krum_pre = K.gram_stacked_async(Xw, self.noise_tbl[:, it % 100, :])
+                krum_pre["xrow"] = {w: i for i, w in enumerate(workers)}
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
                     spec=spec, spec_cand=cand, krum_pre=krum_pre)
         if self.vrf_dev is not None:
@@ -823,7 +846,8 @@ class BiscottiEngine:
         early = head.get("early")
         krum_pre = head.get("krum_pre")
         with tm.phase("vrf_join"):
-            noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake, local_workers)
+            noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake,
+                                                                           head.get("vrf_workers", local_workers))
         with tm.phase("noise"):
             # with the phase-1 Gram the noised deltas are never materialised (only Krum reads them)
             noised = early["noised"] if early else (None if krum_pre is not None else
@@ -846,7 +870,8 @@ class BiscottiEngine:
                     sel = h2d([self.flat[w] for w in workers], torch.long, self.dev)
                     cl = self.crypto.marshal_rows(g_commit.index_select(0, sel))
                     commit_of.update({w: cl[i].tobytes() for i, w in enumerate(workers)})
-            if not single:
+            mr_pre = not single and krum_pre is not None and "xrow" in krum_pre
+            if not single and not mr_pre:
                 # ONE all_gather carries every rank's commitments (device Jacobian rows), noised
                 # deltas (the verifiers' input) and, on the plain path, deltas (the block payload)
                 cr = self.crypto
@@ -883,13 +908,23 @@ class BiscottiEngine:
                 nv = len(plan.verifiers)
                 ni = len(inboxes[vs[0]])
                 X, xrow = (noised, row_of) if single else (g_noised, self.flat)
+                if mr_pre:
+                    X, xrow = None, krum_pre["xrow"]
                 if cfg.defense == "KRUM":
                     # Multi-Krum is a pure function of the (gathered) noised deltas, so every rank
                     # evaluates the whole committee itself (identical inputs, deterministic kernels)
                     with tm.phase("verify.defense"):
                         wait = early["krum"] if early else self._launch_krum(
                             X, xrow, plan, live, inboxes, spec, box, pre=krum_pre, noisers=noisers,
-                            local_workers=local_workers)
+                            local_workers=workers if mr_pre else local_workers)
+                        if mr_pre:
+                            # the commitments' all_gather, queued behind Krum and its aggregation
+                            cr = self.crypto
+                            part = torch.zeros((self.maxlocal, cr.point_width), dtype=cr.point_dtype, device=self.dev)
+                            if local_workers:
+                                lidx = h2d([w - self.lo for w in local_workers], torch.long, self.dev)
+                                part.index_copy_(0, lidx, cr.commit_rows_tensor(pending_commits).to(self.dev))
+                            g_commit = comm.all_gather(part).reshape(-1, cr.point_width)
                         with tm.phase("verify.krum_wait"):
                             acc_t, node_t = wait()
                     acc_np = acc_t.numpy().astype(np.uint8)   # [len(vs), ni]
