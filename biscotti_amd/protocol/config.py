@@ -40,6 +40,9 @@ class RunConfig:
     churn_kill_per_min: float = 0.0  # process churn (eval/eval_FT): peers killed per minute, restarted after
     #                                  60/rate - 5 s with fresh VRF keys, rejoining through chain sync
     churn_round_s: float = 25.44    # seconds per reference round (maps churn seconds onto rounds)
+    partition: str = ""             # network partition injection (DistSys/blockNode.sh drops one peer's port
+    #                                 for 30 s): "peer:first_iteration:rounds[,...]" -- the peer is
+    #                                 unreachable (and unreaching) for those rounds
     data_dir: str | None = None     # real MNIST .npy shards (reference layout), else synthetic
     commit_key: str | None = None   # commitKey.json (else generated: PK[i] = 2^i G1, s = 2)
     pkey_file: str | None = None    # pKeyG1.json (else derived from seed)
@@ -132,10 +135,24 @@ class RunConfig:
             err.append("noisers: at most 16 and fewer than the nodes")
         if not 0.0 <= self.poisoning < 1.0 or not 0.0 <= self.churn < 1.0:
             err.append("poisoning / churn fractions must be in [0, 1)")
+        try:
+            for peer, first, rounds in self.partitions():
+                if not (0 <= peer < self.num_nodes) or rounds < 1:
+                    err.append(f"partition {peer}:{first}:{rounds}: peer out of range or no rounds")
+        except ValueError:
+            err.append(f"partition {self.partition!r}: expected peer:first_iteration:rounds[,...]")
         if self.kzg_audit not in ("off", "consistent", "literal"):
             err.append(f"kzg_audit {self.kzg_audit!r}: expected off | consistent | literal")
         if err:
             raise ValueError("invalid RunConfig: " + "; ".join(err))
+
+    def partitions(self) -> list[tuple[int, int, int]]:
+        """The partition schedule as (peer, first iteration, rounds) triples."""
+        out = []
+        for item in filter(None, (x.strip() for x in self.partition.split(","))):
+            peer, first, rounds = (int(v) for v in item.split(":"))
+            out.append((peer, first, rounds))
+        return out
 
     def protocol(self, rt):
         pc = rt.ProtocolConfig()
@@ -196,6 +213,7 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--churn", type=float, default=0.0)
     ap.add_argument("--churn-kill-per-min", type=float, default=0.0)
+    ap.add_argument("--partition", default="", help="peer:first_iteration:rounds[,...] unreachable (blockNode.sh)")
     ap.add_argument("--data-dir", default=None)
     ap.add_argument("--commit-key", default=None)
     ap.add_argument("--pkey-file", default=None)

@@ -379,6 +379,7 @@ class BiscottiEngine:
                        "synced_blocks": 0}
         self.stats["churn"] = self._churn
         self.rounds_done = 0
+        self._partitions = cfg.partitions()
         self._head = None
         import atexit
         import weakref
@@ -551,6 +552,13 @@ class BiscottiEngine:
                 live[p] = 0
         if self.cfg.churn_kill_per_min > 0:
             self._crash_restart(live)
+        if self._partitions:
+            # DistSys/blockNode.sh: iptables drops the peer's port both ways for 30 s -- it neither
+            # receives nor sends, i.e. it is offline for those rounds (and keeps its state)
+            it = self.fsm.iteration + 1   # the round being opened (as in _crash_restart)
+            for peer, first, rounds in self._partitions:
+                if first <= it < first + rounds:
+                    live[peer] = 0
         return live
 
     def _crash_restart(self, live: list) -> None:

@@ -7,6 +7,8 @@
   breakdown     stacked per-phase time per round (usenix-eval/generateResults.py,
                 nsdi-eval/increments -> eval_cost_breakdown.pdf)
   scaling       seconds per round vs peers or vs GPUs (nsdi-eval/increments/plot_incremental.py)
+  heatmap       attack rate over poisoner fraction x % of updates collected
+                (eval/eval_poison_nsamples/plotHeatMap.py)
 
 Inputs are what this framework writes: peer logs in the reference's line format (parsed with
 utils.logparse), the engine's JSONL trace (``--trace-file``: per-round error, attack rate, wall time
@@ -159,6 +161,44 @@ def scaling(bench_files: list[str], x: str = "peers", out: str = "eval_scaling.p
     return out
 
 
+def heatmap(bench_jsonl: list[str], out: str = "eval_poison_nsamples.pdf", metric: str = "attack_rate_last10_mean",
+            rows: str = "poisoning", cols: str = "ns_percent") -> str:
+    """Attack rate (or any bench metric) over poisoner fraction x % of updates collected, from bench
+    result lines (eval/eval_poison_nsamples/plotHeatMap.py: 10-50 % poisoners x -ns 20/40/70)."""
+    import numpy as np
+
+    plt = _plt()
+    cells = {}
+    for f in bench_jsonl:
+        with open(f) as fh:
+            for ln in fh:
+                if ln.startswith("{"):
+                    b = json.loads(ln)
+                    c = b.get("config")
+                    if isinstance(c, dict) and metric in b and rows in c and cols in c:
+                        cells[(c[rows], c[cols])] = b[metric]
+    rv = sorted({k[0] for k in cells}, reverse=True)
+    cv = sorted({k[1] for k in cells})
+    grid = np.full((len(rv), len(cv)), np.nan)
+    for (r, c), v in cells.items():
+        grid[rv.index(r), cv.index(c)] = v
+    fig, ax = plt.subplots(figsize=(7, 4.5))
+    im = ax.imshow(grid, cmap="Greys", aspect="auto")
+    for i in range(len(rv)):
+        for j in range(len(cv)):
+            if not np.isnan(grid[i, j]):
+                ax.text(j, i, f"{grid[i, j]:.2f}", ha="center", va="center",
+                        color="white" if grid[i, j] > 0.5 * np.nanmax(grid) else "black", fontsize=12)
+    ax.set_xticks(range(len(cv)), [f"{c}%" for c in cv])
+    ax.set_yticks(range(len(rv)), [f"{100 * r:.0f}%" for r in rv])
+    ax.set_xlabel("Number (%) of received updates", fontsize=13)
+    ax.set_ylabel("Percent of poisoners", fontsize=13)
+    fig.colorbar(im, ax=ax, label=metric)
+    fig.tight_layout()
+    fig.savefig(out)
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -180,6 +220,10 @@ def main(argv=None) -> int:
     s.add_argument("--bench", nargs="+", required=True)
     s.add_argument("--x", default="peers", choices=["peers", "gpus"])
     s.add_argument("-o", "--out", default="eval_scaling.pdf")
+    h = sub.add_parser("heatmap")
+    h.add_argument("--bench", nargs="+", required=True, help="bench JSON lines (files)")
+    h.add_argument("--metric", default="attack_rate_last10_mean")
+    h.add_argument("-o", "--out", default="eval_poison_nsamples.pdf")
     a = ap.parse_args(argv)
     if a.cmd == "convergence":
         print(convergence(a.trace, a.fedsys_trace, a.out, a.reference))
@@ -187,6 +231,8 @@ def main(argv=None) -> int:
         print(poisoning(a.trace, a.out, a.reference, a.fedsys_trace))
     elif a.cmd == "breakdown":
         print(breakdown(a.trace, a.out, a.skip))
+    elif a.cmd == "heatmap":
+        print(heatmap(a.bench, a.out, a.metric))
     else:
         print(scaling(a.bench, a.x, a.out))
     return 0

@@ -137,3 +137,22 @@ def test_kzg_audit_rounds(mode):
     assert eng.stats["kzg_failures"] == (0 if mode == "consistent" else blocks)
     assert eng.fsm.chain.verify()[0]
     eng.close()
+
+
+def test_partition_injection_blocknode():
+    """DistSys/blockNode.sh: one peer's port is dropped both ways for a while -- the peer sends no
+    update and none of its updates lands in a block in those rounds (the VRF may still draw it into
+    a committee: it then simply does not answer, like the reference's unreachable node), and it
+    is back afterwards."""
+    eng = BiscottiEngine(_cfg(num_nodes=6, partition="3:2:3"))
+    res = [eng.run_round() for _ in range(7)]
+    for r in res:
+        if 2 <= r.iteration < 5:
+            assert 3 not in r.node_list and 3 not in r.approved, r.iteration
+            if 3 in r.miners and 3 == max(r.miners):   # an unreachable leader: empty block
+                assert r.empty
+    assert any(3 in r.node_list for r in res if not 2 <= r.iteration < 5)
+    assert eng.fsm.chain.verify()[0]
+    with pytest.raises(ValueError):
+        from biscotti_amd.protocol.config import RunConfig
+        RunConfig(num_nodes=6, partition="9:1:1").validate()

@@ -134,4 +134,29 @@ def test_eval_plotters(tmp_path):
         f.write_text(json.dumps({"value": 0.001 * n, "n_gpus": 1, "config": {"peers": n}}) + "\n")
         bl.append(str(f))
     outs.append(plots.scaling(bl, "peers", str(tmp_path / "s.pdf")))
+    hm = tmp_path / "poison_ns.jsonl"
+    hm.write_text("".join(json.dumps({"attack_rate_last10_mean": 0.1 * i + 0.01 * j,
+                                      "config": {"poisoning": po, "ns_percent": ns}}) + "\n"
+                          for i, po in enumerate((0.1, 0.3, 0.5)) for j, ns in enumerate((20, 40, 70))))
+    outs.append(plots.heatmap([str(hm)], str(tmp_path / "h.pdf")))
     assert all(os.path.getsize(o) > 1000 for o in outs)
+
+
+def test_vrf_security_models_and_lottery(tmp_path):
+    """eval_vrf_security / eval_privacy_noise_attack models; the capture probability of this
+    framework's own lottery (distinct stake-weighted picks) matches the hypergeometric model."""
+    from biscotti_amd.native import rt
+    from biscotti_amd.utils import vrf_security as V
+
+    assert abs(V.majority_capture_prob(3, 0.5) - 0.5) < 1e-12
+    assert V.min_committee_size(0.1, 0.001) == 8      # binomial tail (even sizes need a strict majority of c/2 + 1)
+    assert V.noise_attack_prob_reference(0.3, 2, 3) == 0.3 ** 2 * (1 - 0.3 ** 3)
+    trials = 1500
+    emp = V.simulate_verifier_capture(rt(), 30, 30, 3, trials)
+    model = V.majority_capture_prob_distinct(30, 9, 3)
+    sd = (model * (1 - model) / trials) ** 0.5
+    assert abs(emp - model) < 4 * sd + 0.01, (emp, model)
+    assert (tmp_path / "c.pdf").exists() is False
+    V.plot_committee(str(tmp_path / "c.pdf"))
+    V.plot_noise(str(tmp_path / "n.pdf"))
+    assert (tmp_path / "c.pdf").stat().st_size > 0 and (tmp_path / "n.pdf").stat().st_size > 0
