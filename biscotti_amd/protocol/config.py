@@ -60,8 +60,6 @@ class RunConfig:
     phase_sync: bool = False        # device sync at phase boundaries (diagnostics: per-phase GPU times)
     side_stream_skip_every: int = 4  # speculative-MSM stream leaves every Nth CU free (0: no CU mask)
     main_stream_exclusive: bool = False  # critical-path stream masked to exactly the CUs the MSM leaves free
-    bg_stream_complement: bool = False  # background stream (commitments, witness sums) on the CUs the MSM
-    #                                     leaves free, so it never takes SIMDs from the share MSM
     audit_aggregate: bool = True    # check the recovered aggregate against the miners' summed chunk
     #                                 commitments (verifyCommitment on the aggregate; not in the reference)
     noise_table: bool = True        # GPU: every noiser's 100 noise vectors resident in HBM (pre-sampled

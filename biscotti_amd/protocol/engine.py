@@ -327,11 +327,8 @@ class BiscottiEngine:
             self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, cfg.side_stream_skip_every) \
                 if cfg.side_stream_skip_every > 0 else (torch.cuda.Stream(device=self.dev, priority=lo), 0)
             # work no consumer in the round waits for (the miners' witness sums) runs here
-            self.bg_cus = 0
-            if cfg.bg_stream_complement and cfg.side_stream_skip_every > 0:
-                self.bg_stream, self.bg_cus = B.cu_masked_stream(self.dev, -cfg.side_stream_skip_every)
-            else:
-                self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
+            # (a CU mask complementing the MSM's was measured slower and removed: docs/PERF.md)
+            self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
             # long device work nothing in a round waits for -- the VRF proofs (kernels/vrf.hip) and the
             # KZG audit sums (kernels/kzg.hip), ~5 ms launches -- gets a stream of its own: on the
             # background stream it would hold up the next round's commitments
@@ -519,9 +516,6 @@ class BiscottiEngine:
             if getattr(self, "main_cus", 0):
                 B.hip().bsc_stream_destroy(self.main_stream.cuda_stream)
                 self.main_cus = 0
-            if getattr(self, "bg_cus", 0):
-                B.hip().bsc_stream_destroy(self.bg_stream.cuda_stream)
-                self.bg_cus = 0
             self.side_stream = None
 
     # ------------------------------------------------------------------ helpers
