@@ -1244,6 +1244,9 @@ class BiscottiEngine:
         else:
             agg = ys_tot.index_select(1, ycols_t.long()).contiguous()   # [nch, npts]
             W_new, coeffs, status = K.recover(agg, xs_t.cpu(), cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
+        # the recovered model (and the clocks) are read back right behind the recovery, AHEAD of the
+        # audit queued next on the same stream: the block is built while the audit still runs
+        readback = self._d2h_async(status, W_new, *((clock,) if clock is not None else ()))
         audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
         if kzg_in is not None:
             # each rank audits its own partial aggregate: verifySecret is linear in (C, W, y), so the
@@ -1262,20 +1265,29 @@ class BiscottiEngine:
             else:
                 self._kzg_host(cs_k, ws_k, y_k, xs_list, self.fsm.iteration)
         return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
-                "clock": clock, "now": now}
+                "clock": clock, "now": now, "readback": readback}
 
     def _d2h(self, *ts: torch.Tensor) -> list:
         """Several device tensors to host numpy arrays with ONE wait (pinned, stream-ordered copies)."""
+        return self._d2h_async(*ts)()
+
+    def _d2h_async(self, *ts: torch.Tensor):
+        """Queue the copies now (on the current stream, behind what produced the tensors and ahead of
+        anything queued later); the returned callable waits for them and gives numpy arrays."""
         if not self.gpu:
-            return [t.numpy() for t in ts]
+            out = [t.numpy() for t in ts]
+            return lambda: out
         hs = []
         for t in ts:
             h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             h.copy_(t, non_blocking=True)
             hs.append(h)
         ev = S.record()
-        ev.synchronize()
-        return [h.numpy() for h in hs]
+
+        def wait():
+            ev.synchronize()
+            return [h.numpy() for h in hs]
+        return wait
 
     def _audit(self, coeffs: torch.Tensor, csum: torch.Tensor):
         """Queue the aggregate audit (recovered chunks vs the miners' summed chunk commitments);
@@ -1390,11 +1402,11 @@ class BiscottiEngine:
         cfg, R, fsm, tm = self.cfg, self.R, self.fsm, self.timer
         W_new, status, agg, xs, audit_ok = h["W_new"], h["status"], h["agg"], h["xs"], h["audit_ok"]
         with tm.phase("recover.readback"):
+            got = h["readback"]()
+            st, W_np = got[0], got[1]
             if h["clock"] is not None:
-                st, W_np, clk = self._d2h(status, W_new, h["clock"])
-                now = int(clk[self.comm.owner(plan.leader, self.N)])   # the leader's clock stamps the block
+                now = int(got[2][self.comm.owner(plan.leader, self.N)])   # the leader's clock stamps the block
             else:
-                st, W_np = self._d2h(status, W_new)
                 now = h["now"]
         if not st.all():  # inconsistent shares: the reference's float64 least squares
             aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()

@@ -45,12 +45,12 @@ def _worker(rank, world, port, kw, rounds, q):
                      "all_to_all", "reduce_scatter_tensor", "gather", "scatter", "all_gather_object",
                      "broadcast_object_list", "reduce"):
             wrap(name)
-        real_d2h = eng._d2h
+        real_d2h = eng._d2h_async
 
         def counting_d2h(*ts):
             reads.append(len(ts))
             return real_d2h(*ts)
-        eng._d2h = counting_d2h
+        eng._d2h_async = counting_d2h
     per_round = []
     for _ in range(rounds):
         n0, r0 = len(calls), len(reads)
