@@ -358,20 +358,48 @@ __device__ __forceinline__ bool jac_equal(const jac& p, const jac& q) {
   return fp_eq(fp_mul(p.y, fp_mul(z2s, q.z)), fp_mul(q.y, fp_mul(z1s, p.z)));
 }
 
-// One wave per chunk, one lane per (coefficient, window) digit: every lane issues its table fetch
-// up front (the fetches are independent; with one lane per coefficient the window loop exposed a
-// dependent HBM/TLB round trip per window -- the kernel sat on the critical path latency-bound),
-// then an LDS tree sums the <= 64 points and lane 0 compares with each miner's sum.
+// affine + affine -> Jacobian (mmadd-2007-bl, Z1 = Z2 = 1: 4M + 2S), complete for the special cases
+__device__ __forceinline__ jac aff_add_aff(const aff& p, const aff& q) {
+  if (aff_is_inf(p)) return jac_add_aff(jac_inf(), q);
+  if (aff_is_inf(q)) return jac_add_aff(jac_inf(), p);
+  const fp h = fp_sub(q.x, p.x);
+  fp r = fp_sub(q.y, p.y);
+  if (fp_is_zero(h)) {
+    if (fp_is_zero(r)) return jac_dbl(jac_add_aff(jac_inf(), p));
+    return jac_inf();
+  }
+  const fp hh = fp_sqr(h);
+  const fp i = fp_dbl(fp_dbl(hh));
+  const fp j = fp_mul(h, i);
+  r = fp_dbl(r);
+  const fp v = fp_mul(p.x, i);
+  jac o;
+  o.x = fp_sub(fp_sub(fp_sub(fp_sqr(r), j), v), v);
+  o.y = fp_sub(fp_mul(r, fp_sub(v, o.x)), fp_dbl(fp_mul(p.y, j)));
+  o.z = fp_dbl(h);
+  return o;
+}
+
+// One wave per chunk.  The check sits on the round's critical path (the host commits the block only
+// after it), and it is a latency chain, so it is built to be short:
+//   1. signed digits of every coefficient (one lane per coefficient);
+//   2. the NONZERO digits (typically one per coefficient with the 14-bit first window) are compacted
+//      into an LDS list, so ~10 points, not 64 lanes, enter the sum;
+//   3. lane i adds points 2i and 2i+1 affine + affine (6 products instead of a Jacobian addition's
+//      16), then a tree over the ceil(n/2) partial sums (log2 levels, not 6);
+//   4. lane m < nm compares the total projectively with miner m's sum.
 extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* coeffs, int d, int poly,
                                                               const uint32_t* tbl_pk, int B0, int NW,
                                                               const uint32_t* csum, int nm, int nch, int* ok) {
   __shared__ uint32_t sh[64 * 24];
-  __shared__ int dig[16][9];   // signed digit of (coefficient j, window w); NW <= 9 (bsc_chunk_check)
+  __shared__ int dig[16][9];      // signed digit of (coefficient j, window w); NW <= 9 (bsc_chunk_check)
+  __shared__ uint32_t items[16 * 9];   // nonzero digits: table entry | sign bit
+  __shared__ int cnt;
   const int k = blockIdx.x, t = threadIdx.x;
   const int prev = k * poly, L = min(poly, d - prev);
   const int E0 = 1 << (B0 - 1);
   const size_t PB = (size_t)E0 + (size_t)(NW - 1) * TBL_ENTRIES;
-  // 1. digits of every coefficient (cheap integer work, one lane per coefficient)
+  if (t == 0) cnt = 0;
   if (t < 16) {
     for (int w = 0; w < 9; ++w) dig[t][w] = 0;
     if (t < L) {
@@ -386,20 +414,35 @@ extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* 
     }
   }
   __syncthreads();
-  // 2. lane e -> (coefficient e / 9, window e % 9): its fetch issued before any addition
-  jac acc = jac_inf();
   for (int e = t; e < L * 9; e += 64) {
     const int j = e / 9, w = e % 9;
     const int dg = w < NW ? dig[j][w] : 0;
     if (dg == 0) continue;
     const int ad = dg < 0 ? -dg : dg;
-    aff q = ld_aff(tbl_pk + ((size_t)(prev + j) * PB + win_entry(w, ad, E0)) * 16);
-    if (dg < 0) q = aff_neg(q);
-    acc = jac_add_aff(acc, q);
+    const uint32_t ent = (uint32_t)((size_t)(prev + j) * PB + win_entry(w, ad, E0));
+    items[atomicAdd(&cnt, 1)] = ent | (dg < 0 ? 0x80000000u : 0u);
   }
-  st_jac(sh + t * 24, acc);
   __syncthreads();
-  for (int s = 32; s > 0; s >>= 1) {
+  const int n = cnt, m = (n + 1) / 2;
+  jac v = jac_inf();
+  if (t < m) {
+    const uint32_t e1 = items[2 * t];
+    aff q1 = ld_aff(tbl_pk + (size_t)(e1 & 0x7FFFFFFFu) * 16);
+    if (e1 >> 31) q1 = aff_neg(q1);
+    if (2 * t + 1 < n) {
+      const uint32_t e2 = items[2 * t + 1];
+      aff q2 = ld_aff(tbl_pk + (size_t)(e2 & 0x7FFFFFFFu) * 16);
+      if (e2 >> 31) q2 = aff_neg(q2);
+      v = aff_add_aff(q1, q2);
+    } else {
+      v = jac_add_aff(jac_inf(), q1);
+    }
+  }
+  st_jac(sh + t * 24, v);
+  __syncthreads();
+  int p2 = 1;
+  while (p2 < m) p2 <<= 1;
+  for (int s = p2 >> 1; s > 0; s >>= 1) {
     if (t < s) st_jac(sh + t * 24, jac_add(ld_jac(sh + t * 24), ld_jac(sh + (t + s) * 24)));
     __syncthreads();
   }

@@ -1,11 +1,11 @@
-# bench + rocprofv3 kernel trace (CSV) of the headline config; summaries land in gpurun_out/
+# bench + rocprofv3 kernel trace (CSV) of the headline config (SETS: extra bench args); summaries land in gpurun_out/
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
 mkdir -p "$R/gpurun_out/prof"
-timeout -k 10 400 python bench.py > "$R/gpurun_out/bench.txt" 2>&1 || { echo BENCH FAILED; tail -20 "$R/gpurun_out/bench.txt"; exit 1; }
+timeout -k 10 400 python bench.py $SETS > "$R/gpurun_out/bench.txt" 2>&1 || { echo BENCH FAILED; tail -20 "$R/gpurun_out/bench.txt"; exit 1; }
 tail -1 "$R/gpurun_out/bench.txt"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 40 --warmup 3 > "$R/gpurun_out/prof_bench.txt" 2>&1 || { echo PROF FAILED; tail -20 "$R/gpurun_out/prof_bench.txt"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 40 --warmup 3 $SETS > "$R/gpurun_out/prof_bench.txt" 2>&1 || { echo PROF FAILED; tail -20 "$R/gpurun_out/prof_bench.txt"; exit 1; }
 cd "$R"
 T=$(find gpurun_out/prof -name '*kernel_trace.csv' | head -1)
 S=$(find gpurun_out/prof -name '*kernel_stats.csv' | head -1)
