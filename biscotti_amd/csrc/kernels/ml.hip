@@ -65,7 +65,7 @@ constexpr int SM_THREADS = 256;
 extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
     const float* X, const int* y, const long long* off, const int* ntrain, const int* pid, const double* W, int D_IN,
     int D_OUT, int B, int P, unsigned long long seed, int iteration, float max_norm, double qscale, float* delta,
-    long long* qdelta, float* loss) {
+    long long* qdelta, float* loss, int lo) {
   __shared__ float xs[16 * SM_MAXK];  // minibatch rows, transformed; rows >= B are zero
   __shared__ float red[4][16][16];    // per-wave partial logits
   __shared__ float G[16][16];         // (softmax - onehot) / B
@@ -76,7 +76,11 @@ extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
   if (p >= P) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nparam = D_OUT * D_IN + D_OUT;
-  const int n = ntrain[p];
+  // lo >= 0: off / ntrain are indexed by local peer (pid - lo), resident for every local peer, so a
+  // round uploads only the peer ids; lo < 0: per-row arrays
+  const int li = lo >= 0 ? pid[p] - lo : p;
+  const long long offp = off[li];
+  const int n = ntrain[li];
   // 1. draw B distinct minibatch indices (DataLoader(shuffle=True) takes the first batch)
   if (tid == 0) {
     int cnt = 0;
@@ -104,7 +108,7 @@ extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
     for (int i = tid; i < 16 * kw; i += SM_THREADS) {
       const int s = i / kw, k = i % kw;
       float v = 0.f;
-      if (s < Bq) v = (X[(off[p] + bidx[s]) * (long long)D_IN + k0 + k] - 0.5f) * 2.0f;
+      if (s < Bq) v = (X[(offp + bidx[s]) * (long long)D_IN + k0 + k] - 0.5f) * 2.0f;
       xs[s * SM_MAXK + k] = v;
     }
   };
@@ -141,7 +145,7 @@ extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
       }
       float se = 0.f;
       for (int c = 0; c < D_OUT; ++c) se += expf(lg[c] - mx);
-      const int lab = y[off[p] + bidx[s]];
+      const int lab = y[offp + bidx[s]];
       for (int c = 0; c < D_OUT; ++c) G[s][c] = (expf(lg[c] - mx) / se - (c == lab ? 1.f : 0.f)) / (float)Bq;
       for (int c = D_OUT; c < 16; ++c) G[s][c] = 0.f;
       red[0][s][0] = (mx + logf(se)) - lg[lab];  // per-row CE (red no longer needed)
@@ -934,11 +938,11 @@ static inline int nblk(long long n, int bs) { return (int)((n + bs - 1) / bs); }
 extern "C" int bsc_softmax_step(const float* X, const int* y, const long long* off, const int* ntrain,
                                 const int* pid, const double* W, int D_IN, int D_OUT, int B, int P, unsigned long long seed,
                                 int iteration, float max_norm, double qscale, float* delta, long long* qdelta,
-                                float* loss, void* stream) {
+                                float* loss, int lo, void* stream) {
   if (D_IN <= 0 || D_OUT > 16 || B > 16) return -1;
   if (P <= 0) return 0;
   hipLaunchKernelGGL(k_softmax_step, dim3(P), dim3(SM_THREADS), 0, (hipStream_t)stream, X, y, off, ntrain, pid, W, D_IN,
-                     D_OUT, B, P, seed, iteration, max_norm, qscale, delta, qdelta, loss);
+                     D_OUT, B, P, seed, iteration, max_norm, qscale, delta, qdelta, loss, lo);
   return (int)hipGetLastError();
 }
 

@@ -55,6 +55,7 @@ class SoftmaxTask:
         self.eval_X = torch.cat([self.test_X, self.att_X]).contiguous()
         self.eval_y = torch.cat([self.test_y, self.att_y]).contiguous()
         self.eval_split = int(self.test_X.shape[0])
+        assert self.peers == list(range(self.peers[0], self.peers[0] + len(self.peers))), "local peers are contiguous"
         self._local_index = {p: i for i, p in enumerate(self.peers)}
         self._sel_cache: dict = {}
 
@@ -72,15 +73,13 @@ class SoftmaxTask:
             z = torch.empty((0, self.nparam), device=self.device)
             return z.float(), z.long()
         key = tuple(peers)
-        hit = self._sel_cache.get(key)
-        if hit is None:   # per peer set (it changes only with churn): resident, uploaded once
-            sel = h2d([self._local_index[p] for p in peers], torch.long, self.device)
-            hit = (self.off[sel].contiguous(), self.ntrain[sel].contiguous(), h2d(peers, torch.int32, self.device))
+        pid = self._sel_cache.get(key)
+        if pid is None:   # only the peer ids travel; off / ntrain stay resident over all local peers
+            pid = h2d(peers, torch.int32, self.device)
             if len(self._sel_cache) < 64:
-                self._sel_cache[key] = hit
-        off, ntr, pid = hit
-        delta, qdelta, loss = K.softmax_step(self.X, self.y, off, ntr, pid, W, self.d_in, self.d_out,
-                                             self.batch, self.seed, iteration, 100.0, 1e4)
+                self._sel_cache[key] = pid
+        delta, qdelta, loss = K.softmax_step(self.X, self.y, self.off, self.ntrain, pid, W, self.d_in, self.d_out,
+                                             self.batch, self.seed, iteration, 100.0, 1e4, lo=self.peers[0])
         self.last_loss = loss
         return delta, qdelta
 
@@ -147,6 +146,7 @@ class LogisticTask:
         self.yv = torch.from_numpy(cd.yvalid).to(self.device)
         self.Xt = torch.from_numpy(cd.X).to(self.device)
         self.yt = torch.from_numpy(cd.y).to(self.device)
+        assert self.peers == list(range(self.peers[0], self.peers[0] + len(self.peers))), "local peers are contiguous"
         self._local_index = {p: i for i, p in enumerate(self.peers)}
 
     def noise_sigma(self, epsilon: float, delta: float = 1e-5) -> float:

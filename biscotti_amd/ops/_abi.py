@@ -34,7 +34,7 @@ SIGNATURES = {
     "bsc_kzg_blocks": [I, I],
     "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, I, U64, P, P, P],
     # ml.hip
-    "bsc_softmax_step": [P, P, P, P, P, P, I, I, I, I, U64, I, F, D, P, P, P, P],
+    "bsc_softmax_step": [P, P, P, P, P, P, I, I, I, I, U64, I, F, D, P, P, P, I, P],
     "bsc_logreg_step": [P, P, P, P, P, P, I, I, I, U64, P, D, D, P, D, P, P, P],
     "bsc_dp_noise": [P, I, I, P, I, P, U64, I, P, P],
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],

@@ -81,14 +81,15 @@ def minibatch_indices(p: int, iteration: int, n: int, B: int, seed: int, tag: in
 
 
 # ---------------------------------------------------------------------------- K1 softmax step
-def softmax_step(X, y, off, ntrain, pid, W, d_in, d_out, B, seed, iteration, max_norm=100.0, qscale=1e4):
+def softmax_step(X, y, off, ntrain, pid, W, d_in, d_out, B, seed, iteration, max_norm=100.0, qscale=1e4, lo=-1):
     """Batched local SGD step of SoftmaxModel for every local peer.
 
     X fp32 [Ntot, d_in]; y int32 [Ntot]; off int64 [P]; ntrain int32 [P]; pid int32 [P] global peer
-    ids (key of each peer's minibatch stream); W fp64 [nparam].
+    ids (key of each peer's minibatch stream); W fp64 [nparam].  lo >= 0: off / ntrain are indexed by
+    local peer id pid - lo (resident arrays over all local peers) instead of by row.
     Returns (delta fp32 [P, nparam] = -clip(grad), qdelta int64 [P, nparam], loss fp32 [P]).
     """
-    P = off.numel()
+    P = pid.numel()
     nparam = d_out * d_in + d_out
     dev = X.device
     delta = torch.empty((P, nparam), dtype=torch.float32, device=dev)
@@ -97,14 +98,19 @@ def softmax_step(X, y, off, ntrain, pid, W, d_in, d_out, B, seed, iteration, max
     if dev.type == "cuda":
         assert X.dtype == torch.float32 and y.dtype == torch.int32 and W.dtype == torch.float64
         assert off.dtype == torch.int64 and ntrain.dtype == torch.int32 and W.numel() == nparam
-        assert pid.dtype == torch.int32 and pid.numel() == P
+        assert pid.dtype == torch.int32 and (lo >= 0 or off.numel() == P)
         _check(hip().bsc_softmax_step(_p(X), _p(y), _p(off), _p(ntrain), _p(pid), _p(W), d_in, d_out, B, P, seed & (2**64 - 1),
                                       iteration, float(max_norm), float(qscale), _p(delta), _p(qdelta), _p(loss),
-                                      _stream()), "softmax_step")
+                                      int(lo), _stream()), "softmax_step")
         return delta, qdelta, loss
     Wm = W.to(torch.float32)
     Wt, bt = Wm[: d_out * d_in].view(d_out, d_in), Wm[d_out * d_in:]
-    offs, ns, pids = off.tolist(), ntrain.tolist(), pid.tolist()
+    pids = pid.tolist()
+    if lo >= 0:
+        offs = [int(off[q - lo]) for q in pids]
+        ns = [int(ntrain[q - lo]) for q in pids]
+    else:
+        offs, ns = off.tolist(), ntrain.tolist()
     for p in range(P):
         idx = minibatch_indices(pids[p], iteration, ns[p], B, seed)
         rows = torch.tensor([offs[p] + i for i in idx], dtype=torch.long)

@@ -29,6 +29,20 @@ def test_softmax_step_matches_reference():
     assert (q_gpu.cpu() - q_ref).abs().max() <= 1
 
 
+def test_softmax_step_resident_indexing_matches_row_indexing():
+    """lo >= 0: off / ntrain indexed by pid - lo over all local peers (a subset, out of order)."""
+    X, y, off, nt, _, W = _fed()
+    lo = 40
+    pid_all = torch.arange(lo, lo + off.numel(), dtype=torch.int32)
+    sel = torch.tensor([3, 0, 5, 2], dtype=torch.long)
+    c = lambda t: t.cuda()
+    d_row, q_row, l_row = K.softmax_step(c(X), c(y), c(off[sel]), c(nt[sel]), c(pid_all[sel]), c(W), 784, 10, 10, 99, 2)
+    d_res, q_res, l_res = K.softmax_step(c(X), c(y), c(off), c(nt), c(pid_all[sel]), c(W), 784, 10, 10, 99, 2, lo=lo)
+    assert torch.equal(d_row, d_res) and torch.equal(q_row, q_res) and torch.equal(l_row, l_res)
+    d_cpu, _, _ = K.softmax_step(X, y, off, nt, pid_all[sel], W, 784, 10, 10, 99, 2, lo=lo)
+    torch.testing.assert_close(d_res.cpu(), d_cpu, rtol=2e-4, atol=2e-6)
+
+
 @pytest.mark.parametrize("d_in,d_out", [(8742, 2), (2500, 12)])
 def test_softmax_step_k_tiled_matches_reference(d_in, d_out):
     """K-tiled local step (features staged through LDS in 1024-wide tiles): LFW-sized 62x47x3 inputs."""
