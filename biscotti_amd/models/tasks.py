@@ -20,6 +20,7 @@ from ..utils import h2d
 
 class SoftmaxTask:
     d_in, d_out = 784, 10
+    stateless_step = True   # step() of a peer depends only on (W, peer, iteration): it can run ahead
 
     def __init__(self, peers: range, num_peers: int, device, seed: int, poisoned: set[int] | None = None,
                  batch_size: int = 10, data_dir: str | None = None, federation: D.MnistFederation | None = None,

@@ -94,6 +94,10 @@ class RunConfig:
     #                                 joined lazily; failures are counted and logged, never block the chain
     kzg_batch_rounds: int = 16      # rounds whose audits share one pairing product (sums of independent RLCs)
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
+    pre_step: bool = True           # one rank, GPU: the next round's local step (every local peer) and its
+    #                                 commitments are queued right behind this round's recovery, before the
+    #                                 host builds the block; the head adopts them if the block carries that
+    #                                 model (stateless local steps only: Philox minibatches keyed by peer, round)
     #                                 (shortens the GPU chain; costs host time before the previous round ends)
 
     def validate(self) -> None:

@@ -364,6 +364,7 @@ class BiscottiEngine:
         self._side_work: list = []   # (event, tensors) of off-critical-path device work of this round
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
+        self._pre = None             # next round's local step + commitments, queued behind the recovery
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
         self._kzg_pending: list = []   # launched audits (device) or checked ones (CPU)
@@ -657,8 +658,20 @@ class BiscottiEngine:
         # the local step, the commitments and the speculative shares depend only on the new global
         # model too: queue them now, behind nothing but the block that produced it
         tm, it = self.timer, plan.iteration
+        # the local step (and the commitments) may already be in flight: queued behind the recovery of
+        # the model this head starts from (_queue_pre_step), for every local peer
+        pre, self._pre = self._pre, None
+        use_pre = pre is not None and pre["it"] == it and pre["W"] is self.W and bool(local_workers)
         with tm.phase("local_step"):
-            delta, qdelta = self.task.step(self.W, it, local_workers)
+            if use_pre:
+                self.stats["pre_steps"] = self.stats.get("pre_steps", 0) + 1
+                qdelta, qrow = pre["qdelta"], {w: w - self.lo for w in local_workers}
+                delta = pre["delta"]
+                if len(local_workers) != delta.shape[0]:
+                    delta = delta.index_select(0, h2d([w - self.lo for w in local_workers], torch.long, self.dev))
+            else:
+                delta, qdelta = self.task.step(self.W, it, local_workers)
+                qrow = None
         with tm.phase("commit"):
             # every live verifier collects its own first krum_thresh arrivals (krum.go:284-322); only
             # updates that can end in the leader's block secret-share: the MSM runs on the CU-masked
@@ -669,7 +682,8 @@ class BiscottiEngine:
                 for v, ib in zip(plan.verifiers, fsm.verifier_inboxes(workers)):
                     if live[v]:
                         inboxes[v] = list(ib)
-            row_of = {w: i for i, w in enumerate(local_workers)}
+            row_of = {w: i for i, w in enumerate(local_workers)}   # rows of delta (Krum, noise)
+            qrow = qrow or row_of                                   # rows of qdelta (MSMs, commitments)
             spec = None
             cand = set()
             if self.gpu and cfg.secure_agg:
@@ -690,12 +704,13 @@ class BiscottiEngine:
                 spec_workers = sorted((w for w in local_workers if w in cand), key=lambda w: lo_rank.get(w, 1 << 30))
                 if spec_workers:
                     defer = cfg.verification and not cfg.spec_msm
-                    spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
+                    spec = (spec_workers, self.crypto.shares_async(qdelta, [qrow[w] for w in spec_workers],
                                                                    self.side_stream, launch=not defer,
                                                                    group_rows=cfg.spec_group_rows))
             # full-vector commitments on the background stream: their first consumer is the signing
             # after Krum, so noise + Krum on the main stream do not queue behind them
-            pending_commits = self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
+            pending_commits = pre["commits"] if use_pre else \
+                self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
         # one rank, Multi-Krum over table noise: the d-dimensional part of the committee's Krum (the
         # Gram of the deltas stacked over the noisers' pre-sampled vectors of this iteration) depends
         # only on this head, so it runs now, while the host computes the workers' VRF outputs; after
@@ -719,7 +734,7 @@ class BiscottiEngine:
                 krum_pre = K.gram_stacked_async(Xw, self.noise_tbl[:, it % 100, :])
                 krum_pre["xrow"] = {w: i for i, w in enumerate(workers)}
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
-                    spec=spec, spec_cand=cand, krum_pre=krum_pre)
+                    qrow=qrow, spec=spec, spec_cand=cand, krum_pre=krum_pre)
         if self.vrf_dev is not None:
             # the proofs nobody reads -- every noiser proof and the roles proofs -- on the device,
             # several rounds per launch on their own low-priority stream
@@ -845,6 +860,7 @@ class BiscottiEngine:
             fut_noise, fut_roles = head["fut_noise"], head["fut_roles"]
             delta, qdelta, pending_commits = head["delta"], head["qdelta"], head["pending_commits"]
             inboxes, row_of, spec = head["inboxes"], head["row_of"], head["spec"]
+            qrow = head["qrow"]
         early = head.get("early")
         krum_pre = head.get("krum_pre")
         with tm.phase("vrf_join"):
@@ -867,7 +883,7 @@ class BiscottiEngine:
                 if single:
                     if local_workers:
                         cl = pending_commits.result()
-                        commit_of.update({w: cl[row_of[w]].tobytes() for w in local_workers})
+                        commit_of.update({w: cl[qrow[w]].tobytes() for w in local_workers})
                 elif workers:   # every worker's commitment: one batched marshal of the gathered rows
                     sel = h2d([self.flat[w] for w in workers], torch.long, self.dev)
                     cl = self.crypto.marshal_rows(g_commit.index_select(0, sel))
@@ -1012,7 +1028,7 @@ class BiscottiEngine:
         # must come at the same point on every rank)
         self._idle_work = pending_signatures
         if cfg.secure_agg:
-            block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, row_of,
+            block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, qrow,
                                              commit_of, signatures, spec, box.get("sa") if cfg.verification else None)
         else:
             block = self._plain_aggregation(plan, live, approved, delta, noised, local_workers, commit_of,
@@ -1248,6 +1264,8 @@ class BiscottiEngine:
         # audit queued next on the same stream: the block is built while the audit still runs
         readback = self._d2h_async(status, W_new, *((clock,) if clock is not None else ()))
         audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
+        if self.gpu and single and cfg.pre_step and getattr(self.task, "stateless_step", False):
+            self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)   # fsm: the round being aggregated
         if kzg_in is not None:
             # each rank audits its own partial aggregate: verifySecret is linear in (C, W, y), so the
             # partial sums of honest shares satisfy it exactly like the total does
@@ -1266,6 +1284,15 @@ class BiscottiEngine:
                 self._kzg_host(cs_k, ws_k, y_k, xs_list, self.fsm.iteration)
         return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
                 "clock": clock, "now": now, "readback": readback}
+
+    def _queue_pre_step(self, W: torch.Tensor, it: int) -> dict:
+        """The next round's local step for EVERY local peer (its workers are not known before the next
+        block's roles) and their commitments (background stream), queued right behind the recovery
+        of W -- the GPU runs them while the host reads W back, builds and commits the block; the next
+        head adopts them if that block carries W (same device tensor) and discards them otherwise."""
+        delta, qdelta = self.task.step(W, it, list(self.local))
+        return {"W": W, "it": it, "delta": delta, "qdelta": qdelta,
+                "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
 
     def _d2h(self, *ts: torch.Tensor) -> list:
         """Several device tensors to host numpy arrays with ONE wait (pinned, stream-ordered copies)."""

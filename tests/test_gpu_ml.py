@@ -200,8 +200,9 @@ def test_recover_rows_fused_weights(cols):
     assert st2.cpu()[7] == 0 and st2.cpu().sum() == nch - 1
 
 
-@pytest.mark.parametrize("early,spec_msm", [(False, True), (True, True), (False, False)])
-def test_engine_rounds_on_gpu(early, spec_msm):
+@pytest.mark.parametrize("early,spec_msm,pre_step", [(False, True, True), (True, True, True), (False, False, True),
+                                                   (False, True, False)])
+def test_engine_rounds_on_gpu(early, spec_msm, pre_step):
     """Whole GPU round pipeline (speculative shares on the CU-masked stream, async commitments,
     pipelined round heads): each block's model is EXACTLY the old model plus the sum of the
     included workers' quantised updates, recomputed independently through the Philox step."""
@@ -209,7 +210,8 @@ def test_engine_rounds_on_gpu(early, spec_msm):
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
-    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, early_krum=early, spec_msm=spec_msm)
+    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, early_krum=early, spec_msm=spec_msm,
+                    pre_step=pre_step)
     eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
     res = []
     for _ in range(5):
@@ -229,6 +231,9 @@ def test_engine_rounds_on_gpu(early, spec_msm):
     # the device-side aggregation queued behind Krum was adopted (and matched the exact sums above)
     assert eng.stats.get("device_aggregations", 0) >= 3
     assert eng.stats["audit_failures"] == 0
+    # the next round's local step queued behind the recovery was adopted (and the blocks above match
+    # the independently recomputed step)
+    assert (eng.stats.get("pre_steps", 0) >= 1) if pre_step else "pre_steps" not in eng.stats
     eng.close()
 
 
