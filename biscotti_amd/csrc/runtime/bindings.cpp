@@ -1,4 +1,5 @@
 // pybind11 module `_biscotti_rt`: the native host runtime of biscotti_amd.
+#include <cstring>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -180,6 +181,48 @@ static std::shared_ptr<SignJob> make_sign_job(std::vector<py::bytes>& msgs, std:
   job->out.resize(n);
   (void)gen_table();
   return job;
+}
+
+static void run_sign_job(SignJob& j);
+
+// messages as rows of one uint8 table (the round's commitments, [n, width]): no bytes object per message
+static std::shared_ptr<SignJob> make_sign_job_rows(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> table,
+                                                   std::vector<int>& rows, std::vector<py::bytes>& sks,
+                                                   std::vector<int>& key_of, std::vector<py::bytes>& nonce_base,
+                                                   std::vector<int>& nonce_ids, int threads) {
+  if (table.ndim() != 2) throw std::runtime_error("schnorr_sign_rows: table must be [n, width]");
+  const size_t nt = size_t(table.shape(0)), wd = size_t(table.shape(1));
+  const size_t n = rows.size();
+  if (key_of.size() != n || nonce_ids.size() != n || nonce_base.size() != sks.size())
+    throw std::runtime_error("schnorr_sign_rows: length mismatch");
+  auto job = std::make_shared<SignJob>();
+  const uint8_t* t = table.data();
+  job->msgs.reserve(n);
+  for (int r : rows) {
+    if (r < 0 || size_t(r) >= nt) throw std::runtime_error("schnorr_sign_rows: bad row");
+    job->msgs.emplace_back(t + size_t(r) * wd, t + (size_t(r) + 1) * wd);
+  }
+  for (auto& x : sks) job->keys.push_back(Scalar::from_be(B(x)));
+  for (auto& x : nonce_base) job->bases.push_back(B(x));
+  for (int k : key_of)
+    if (k < 0 || size_t(k) >= job->keys.size()) throw std::runtime_error("schnorr_sign_rows: bad key index");
+  job->key_of = key_of;
+  job->ids = nonce_ids;
+  job->threads = threads;
+  job->out.resize(n);
+  (void)gen_table();
+  return job;
+}
+
+static void start_sign_job(SignJob* jp) {
+  jp->th = std::thread([jp] {
+    try {
+      run_sign_job(*jp);
+    } catch (const std::exception& e) {
+      jp->error = e.what();
+    }
+    jp->done_p.set_value();
+  });
 }
 
 static void run_sign_job(SignJob& j) {
@@ -465,16 +508,32 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   // All signatures of a round in one call: message i signed with sks[key_of[i]], nonce entropy
   // nonce_base[key_of[i]] || le32(nonce_ids[i]).  _async returns a job that signs on native
   // threads right away (result() joins) so the work overlaps the GPU share computation.
-  py::class_<SignJob, std::shared_ptr<SignJob>>(m, "SignJob").def("result", [](SignJob& j) {
-    {
-      py::gil_scoped_release rel;
-      j.done.wait();
-    }
-    if (!j.error.empty()) throw std::runtime_error(j.error);
-    std::vector<py::bytes> r;
-    for (auto& o : j.out) r.push_back(P(o));
-    return r;
-  });
+  py::class_<SignJob, std::shared_ptr<SignJob>>(m, "SignJob")
+      .def("result", [](SignJob& j) {
+        {
+          py::gil_scoped_release rel;
+          j.done.wait();
+        }
+        if (!j.error.empty()) throw std::runtime_error(j.error);
+        std::vector<py::bytes> r;
+        for (auto& o : j.out) r.push_back(P(o));
+        return r;
+      })
+      // every signature as one uint8 [n, 64] array (one allocation instead of n bytes objects)
+      .def("result_array", [](SignJob& j) {
+        {
+          py::gil_scoped_release rel;
+          j.done.wait();
+        }
+        if (!j.error.empty()) throw std::runtime_error(j.error);
+        py::array_t<uint8_t> a({py::ssize_t(j.out.size()), py::ssize_t(64)});
+        uint8_t* o = a.mutable_data();
+        for (size_t i = 0; i < j.out.size(); ++i) {
+          if (j.out[i].size() != 64) throw std::runtime_error("signature is not 64 bytes");
+          std::memcpy(o + 64 * i, j.out[i].data(), 64);
+        }
+        return a;
+      });
   m.def("schnorr_sign_multi", [](std::vector<py::bytes> msgs, std::vector<py::bytes> sks, std::vector<int> key_of,
                                  std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads) {
     auto job = make_sign_job(msgs, sks, key_of, nonce_base, nonce_ids, threads);
@@ -490,15 +549,15 @@ PYBIND11_MODULE(_biscotti_rt, m) {
                                        std::vector<int> key_of, std::vector<py::bytes> nonce_base,
                                        std::vector<int> nonce_ids, int threads) {
     auto job = make_sign_job(msgs, sks, key_of, nonce_base, nonce_ids, threads);
-    SignJob* jp = job.get();
-    jp->th = std::thread([jp] {
-      try {
-        run_sign_job(*jp);
-      } catch (const std::exception& e) {
-        jp->error = e.what();
-      }
-      jp->done_p.set_value();
-    });
+    start_sign_job(job.get());
+    return job;
+  });
+  // same, message i = table[rows[i]] (e.g. the marshalled commitments of the round, uint8 [n, 64])
+  m.def("schnorr_sign_rows_async", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> table,
+                                      std::vector<int> rows, std::vector<py::bytes> sks, std::vector<int> key_of,
+                                      std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads) {
+    auto job = make_sign_job_rows(table, rows, sks, key_of, nonce_base, nonce_ids, threads);
+    start_sign_job(job.get());
     return job;
   });
   m.def("client_key_from_entropy", [](py::bytes e) {

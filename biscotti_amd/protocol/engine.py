@@ -147,6 +147,22 @@ class HostCrypto:
         return ok
 
 
+class _CommitTable(dict):
+    """worker -> marshalled commitment (64 bytes), read from the round's uint8 [n, 64] table on first
+    use: the signing reads the table rows natively, only the block's rows become bytes objects."""
+
+    def __init__(self):
+        super().__init__()
+        self.table, self.row = None, {}
+
+    def fill(self, table: np.ndarray, row: dict) -> None:
+        self.table, self.row = table, row
+
+    def __missing__(self, w):
+        v = self[w] = self.table[self.row[w]].tobytes()
+        return v
+
+
 class _SpecShares:
     """Speculative share/witness MSM of some workers' rows on a side stream.  `alive` (int32, one
     flag per row) is cleared for rows the verifiers reject; the MSM skips flagged rows, whether the
@@ -776,6 +792,15 @@ class BiscottiEngine:
         sel = self.R.select_noisers_batch(stake, betas, local_workers, self.cfg.num_noisers, self.N) if betas else []
         return dict(zip(local_workers, sel))
 
+    def _noise_scales(self, noisers: dict, ws: list) -> np.ndarray:
+        """float32 [len(ws), nn]: each noiser's vector weight (getNoise's -sigma/sqrt(B)); 0 for
+        colluding noisers (isCollusionAttack, main.go:1026-1057)."""
+        ids = np.asarray([noisers[w] for w in ws], np.int64).reshape(len(ws), -1)
+        sc = np.full(ids.shape, self.task.noise_scale(self.sigma), np.float32)
+        if self.colluders:
+            sc[np.isin(ids, np.fromiter(self.colluders, np.int64))] = 0.0
+        return sc
+
     def _noise(self, delta, noisers, local_workers, it):
         """Noised deltas of the local workers (requestNoise + NoisedDelta, main.go:1513-1660): each
         worker's noisers' pre-sampled vectors averaged and added (HBM-resident table on the GPU)."""
@@ -784,8 +809,7 @@ class BiscottiEngine:
             return delta
         ids = [noisers[w] for w in local_workers]
         assert all(0 <= j < self.N for row in ids for j in row), "noiser id out of range"
-        sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma) for j in noisers[w]]
-                  for w in local_workers], torch.float32, self.dev)
+        sc = h2d(self._noise_scales(noisers, local_workers), torch.float32, self.dev)
         if cfg.noise_independent:
             # ablation (not the reference): every (worker, noiser slot) draws its own vector, so no two
             # workers share noise -- isolates the effect of the noisers' shared pre-sampled vectors
@@ -817,8 +841,7 @@ class BiscottiEngine:
         rank_t = h2d(rank, torch.int32, self.dev)
         if pre is not None:
             nz = h2d([noisers[w] for w in local_workers], torch.int32, self.dev)
-            sc = h2d([[0.0 if j in self.colluders else self.task.noise_scale(self.sigma) for j in noisers[w]]
-                      for w in local_workers], torch.float32, self.dev)
+            sc = h2d(self._noise_scales(noisers, local_workers), torch.float32, self.dev)
             return K.krum_committee_noise_async(pre, nz, sc, inbox_t, n - clip, n - clip, need, rank_t, cap,
                                                 on_accept=on_accept)
         return K.krum_committee_async(X, inbox_t, n - clip, n - clip, need, rank_t, cap, on_accept=on_accept)
@@ -873,21 +896,20 @@ class BiscottiEngine:
         # ---------------------------------------------------------------- verification
         with tm.phase("verify"):
             single = comm.world == 1
-            commit_of: dict = {}
+            commit_of = _CommitTable()
             g_commit = g_noised = g_delta = g_ts = None
             need_X = cfg.verification and bool(inboxes)
 
             def _materialize_commits():  # first use comes after the Krum kernels are queued
-                if commit_of:
+                if commit_of.table is not None:
                     return
                 if single:
                     if local_workers:
-                        cl = pending_commits.result()
-                        commit_of.update({w: cl[qrow[w]].tobytes() for w in local_workers})
+                        commit_of.fill(pending_commits.result(), qrow)
                 elif workers:   # every worker's commitment: one batched marshal of the gathered rows
                     sel = h2d([self.flat[w] for w in workers], torch.long, self.dev)
-                    cl = self.crypto.marshal_rows(g_commit.index_select(0, sel))
-                    commit_of.update({w: cl[i].tobytes() for i, w in enumerate(workers)})
+                    commit_of.fill(self.crypto.marshal_rows(g_commit.index_select(0, sel)),
+                                   {w: i for i, w in enumerate(workers)})
             mr_pre = not single and krum_pre is not None and "xrow" in krum_pre
             if not single and not mr_pre:
                 # ONE all_gather carries every rank's commitments (device Jacobian rows), noised
@@ -978,32 +1000,40 @@ class BiscottiEngine:
                 # the local verifiers sign their accepted commitments on native threads while the GPU
                 # computes shares (main.go:1120-1140); joined where first needed (plain blocks carry
                 # them, --verify-signatures checks them) or at the end of the round
-                msgs, key_of, ids, slots, sks, bases = [], [], [], [], [], []
+                # message i = row rows[i] of the commitment table, signed with sks[key_of[i]], nonce id =
+                # the worker; (sl_v, sl_j) = its (verifier, inbox slot) in the signature matrix
+                rows, key_of, ids, sks, bases, sl_v, sl_j = [], [], [], [], [], [], []
                 local_vs = [v for v in vs if v in self.local]
                 if local_vs:
                     _materialize_commits()
+                vidx = {v: i for i, v in enumerate(plan.verifiers)}
                 for v in local_vs:
+                    js = np.flatnonzero(acc_np[acc_row[v]]).tolist()
+                    ib, k = inboxes[v], len(sks)
                     sks.append(self.sk[v])
                     bases.append(_seed_bytes(cfg.seed, f"nonce-{it}", v))
-                    for j, (w, a_) in enumerate(zip(inboxes[v], acc_np[acc_row[v]])):
-                        if a_:
-                            msgs.append(commit_of[w])
-                            key_of.append(len(sks) - 1)
-                            ids.append(w)
-                            slots.append((plan.verifiers.index(v), j))
-                sign_job = R.schnorr_sign_multi_async(msgs, sks, key_of, bases, ids, cfg.host_threads) \
-                    if msgs else None
+                    ws = [ib[j] for j in js]
+                    rows.extend([commit_of.row[w] for w in ws])
+                    key_of.extend([k] * len(ws))
+                    ids.extend(ws)
+                    sl_v.extend([vidx[v]] * len(ws))
+                    sl_j.extend(js)
+                sign_job = R.schnorr_sign_rows_async(commit_of.table, rows, sks, key_of, bases, ids,
+                                                     cfg.host_threads) if rows else None
                 sig_np = np.zeros((nv, ni, 64), np.uint8)
 
-                def _join_signatures(sign_job=sign_job, slots=slots, sig_np=sig_np, vs=vs):
+                def _join_signatures(sign_job=sign_job, sl_v=sl_v, sl_j=sl_j, sig_np=sig_np, vs=vs):
                     with tm.phase("verify.sign_join"):
-                        sigs = sign_job.result() if sign_job is not None else []
-                        for (vi, j), sg in zip(slots, sigs):
-                            sig_np[vi, j] = np.frombuffer(sg, np.uint8)
+                        if sign_job is not None:
+                            sig_np[sl_v, sl_j] = sign_job.result_array()
+                        self.last_signatures = sig_np   # [nv, ni, 64]: this rank's verifiers' signatures
                         # the signatures travel to the workers (and on to the miners) only where a
                         # consumer reads them: plain blocks carry them, --verify-signatures checks them;
-                        # on the secure path each rank keeps the ones its verifiers produced (Q5)
-                        gather = not single and (not cfg.secure_agg or cfg.verify_signatures)
+                        # on the secure path each rank keeps the ones its verifiers produced (Q5) -- as
+                        # this matrix, with no per-signature objects
+                        if cfg.secure_agg and not cfg.verify_signatures:
+                            return
+                        gather = not single
                         sig_all = comm.all_gather(torch.from_numpy(sig_np).to(self.dev)).cpu().numpy() if gather \
                             else sig_np[None]
                         for v in vs:

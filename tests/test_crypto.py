@@ -255,11 +255,34 @@ def test_schnorr_sign_multi_batch(rt):
     assert rt.schnorr_sign(msgs[7], keys[key_of[7]][0], ent) == sigs[7]
 
 
+def test_schnorr_sign_rows_matches_message_list(rt):
+    """Table-row signing (messages = rows of a uint8 [n, 64] table) equals the list API, and the
+    array result equals the bytes result."""
+    import os
+
+    import numpy as np
+
+    keys = [rt.client_key_from_entropy(os.urandom(32)) for _ in range(2)]
+    table = np.frombuffer(os.urandom(64 * 12), np.uint8).reshape(12, 64)
+    rows = [5, 0, 11, 5, 3]
+    key_of = [0, 1, 1, 0, 1]
+    bases = [os.urandom(32) for _ in range(2)]
+    ids = [7, 8, 9, 10, 11]
+    want = rt.schnorr_sign_multi([table[r].tobytes() for r in rows], [k[0] for k in keys], key_of, bases, ids, 2)
+    job = rt.schnorr_sign_rows_async(table, rows, [k[0] for k in keys], key_of, bases, ids, 3)
+    arr = job.result_array()
+    assert arr.shape == (5, 64) and [a.tobytes() for a in arr] == want
+    with pytest.raises(RuntimeError):
+        rt.schnorr_sign_rows_async(table, [12], [keys[0][0]], [0], bases[:1], [1], 1).result_array()
+
+
 def test_concurrent_native_jobs_share_the_pool(rt):
     """VRF and signing jobs running at once (and a foreground batch) give the serial results."""
     import os
 
     seeds = [os.urandom(32) for _ in range(40)]
+    import numpy as np
+
     keys = [rt.client_key_from_entropy(os.urandom(32)) for _ in range(2)]
     msgs = [os.urandom(64) for _ in range(60)]
     key_of = [i % 2 for i in range(60)]

@@ -156,3 +156,29 @@ def test_partition_injection_blocknode():
     with pytest.raises(ValueError):
         from biscotti_amd.protocol.config import RunConfig
         RunConfig(num_nodes=6, partition="9:1:1").validate()
+
+
+def test_verifier_signatures_kept_and_valid_on_secure_path():
+    """Secure path without --verify-signatures: the local verifiers' signatures stay in one
+    [nv, inbox, 64] matrix (no per-signature objects); every accepted slot verifies against the
+    worker's commitment in the block under the verifier's key, empty slots stay zero."""
+    eng = BiscottiEngine(_cfg(num_nodes=6, num_verifiers=3, num_miners=2))
+    for _ in range(3):
+        r = eng.run_round()
+        eng.drain()
+        sig = eng.last_signatures
+        assert sig.shape[0] == len(r.verifiers)
+        blk = eng.fsm.chain.latest()
+        # secure-agg blocks list the commitments in node_list order
+        commits = {w: bytes(u.commitment) for w, u in zip(r.node_list, blk.data.deltas)} if not r.empty else {}
+        n_ok = 0
+        for vi, v in enumerate(r.verifiers):
+            for j, w in enumerate(r.inboxes.get(v, [])):
+                s_ = sig[vi, j].tobytes()
+                if any(s_):
+                    if w in commits:
+                        assert eng.R.schnorr_verify(commits[w], eng.pk[v], s_)
+                        n_ok += 1
+                else:
+                    assert w not in r.approved_by_krum or v not in eng.local
+        assert r.empty or n_ok > 0
