@@ -4,6 +4,7 @@
 #include <charconv>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 
 #include "bn256.hpp"
@@ -114,9 +115,35 @@ static const Bytes& gob_type_prefix() {
   return pre;
 }
 
+// A float64 travels as the uint of its byte-reversed bits (gob_put_float); for a model vector that is
+// ~9 bytes per value.  One reservation, raw writes: block hashing sits on the round's host path
+// (each round's block is encoded to be hashed).
+static inline u8* gob_uint_raw(u8* o, u64 x) {
+  if (x < 128) {
+    *o++ = u8(x);
+    return o;
+  }
+  const int n = 8 - (__builtin_clzll(x) >> 3);   // bytes of x without leading zeros
+  *o++ = u8(256 - n);
+  // the n low bytes of x, big-endian, as ONE 8-byte store (the caller reserves 9 bytes per value,
+  // so the bytes past the n valid ones land in space the next value overwrites or the final resize
+  // drops)
+  const u64 be = __builtin_bswap64(x << (8 * (8 - n)));
+  memcpy(o, &be, 8);
+  return o + n;
+}
+
 static void put_f64s(Bytes& p, const std::vector<double>& v) {
   gob_put_uint(p, v.size());
-  for (double x : v) gob_put_float(p, x);
+  const size_t at = p.size();
+  p.resize(at + 9 * v.size());
+  u8* o = p.data() + at;
+  for (double x : v) {
+    u64 bits;
+    memcpy(&bits, &x, 8);
+    o = gob_uint_raw(o, __builtin_bswap64(bits));
+  }
+  p.resize(size_t(o - p.data()));
 }
 
 static void encode_update(Bytes& p, const Update& u) {
@@ -140,6 +167,12 @@ static void encode_update(Bytes& p, const Update& u) {
 Bytes gob_encode_blockdata(const BlockData& d) {
   Bytes out = gob_type_prefix();
   Bytes p;
+  size_t est = 16 + 9 * d.global_w.size();
+  for (auto& u : d.deltas)
+    est += 48 + u.commitment.size() + 9 * (u.delta.size() + u.noise.size() + u.noised_delta.size()) +
+           80 * u.signatures.size();
+  p.reserve(est);
+  out.reserve(out.size() + est + 10);
   gob_put_int(p, T_BLOCKDATA);
   int last = -1;
   auto field = [&](int idx) { gob_put_uint(p, u64(idx - last)); last = idx; };

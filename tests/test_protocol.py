@@ -136,3 +136,27 @@ def test_runconfig_rejects_unsupported_shapes():
                 dict(batch_size=32), dict(dataset="cifar"), dict(num_nodes=5, num_verifiers=3, num_miners=2)):
         with _pt.raises(ValueError):
             RunConfig(**bad).validate()
+
+
+def test_gob_float_vector_matches_scalar_encoder(rt):
+    """The block's model vector goes through the raw-pointer vector encoder: its bytes equal the
+    per-value gob float encoding (byte-reversed IEEE bits as a uint) for edge values and random ones."""
+    import struct
+
+    import numpy as np
+
+    vals = [0.0, -0.0, 1.0, -1.0, 0.5, 2.0 ** -1074, 1e308, -1e-300, float("inf"), float("-inf"), 3.0, 1.0 / 3]
+    vals += np.random.default_rng(5).standard_normal(500).tolist()
+    d = rt.BlockData()
+    d.global_w = vals
+    enc = d.gob()
+    body = b"".join(rt.gob_float(v) for v in vals)
+    assert body in enc
+
+    def slow(v):   # the wire spec, in Python
+        rev = int.from_bytes(struct.pack("<d", v), "big")
+        if rev < 128:
+            return bytes([rev])
+        raw = rev.to_bytes(8, "big").lstrip(b"\x00")
+        return bytes([256 - len(raw)]) + raw
+    assert all(rt.gob_float(v) == slow(v) for v in vals)
