@@ -87,6 +87,22 @@ PRESETS = {
 }
 
 
+def _host_threads() -> int:
+    """Native crypto pool per rank: the CPUs this job may use (cgroup quota, else the affinity mask)
+    shared by the node's local ranks, 4..16 (16 = one rank on a 16-CPU share of the 1-GPU box)."""
+    import os
+
+    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 16)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            cpus = min(cpus, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return max(4, min(16, cpus // max(1, local)))
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,7 +136,7 @@ def main() -> int:
         # cgroup CPU quota from the native crypto pool
         torch.set_num_threads(min(4, torch.get_num_threads()))
     kw = dict(num_nodes=100, dataset="mnist", seed=a.seed, max_iterations=10**9, trace_file=a.trace,
-              host_threads=16, phase_sync=a.phase_sync)
+              host_threads=_host_threads(), phase_sync=a.phase_sync)
     kw.update(over)
     if a.peers:
         kw["num_nodes"] = a.peers

@@ -495,17 +495,23 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
   int k = k0b + wid * per;
   const int kend = min(k1b, k + per);
   f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  // 32 k per step: lane (r, kk) reads k + 16h + 4kk .. +3 of its row as ONE 16-byte load per half h
+  // (4 vector loads per step instead of 16 dword loads); MFMA step (h, c) then sums the elements
+  // k + 16h + 4kk + c over kk -- the same k set for A and B, only the summation order differs
+  typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
   for (; k + 32 <= kend; k += 32) {
-    float a[8], b[8];
+    const f32x4u a0 = *(const f32x4u*)(xa + k + 4 * kk), a1 = *(const f32x4u*)(xa + k + 16 + 4 * kk);
+    const f32x4u b0 = *(const f32x4u*)(xb + k + 4 * kk), b1 = *(const f32x4u*)(xb + k + 16 + 4 * kk);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      a[u] = xa[k + 4 * u + kk];
-      b[u] = xb[k + 4 * u + kk];
+    for (int c = 0; c < 4; c += 2) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a0[c] : 0.0, vb ? (double)b0[c] : 0.0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a0[c + 1] : 0.0, vb ? (double)b0[c + 1] : 0.0, acc1,
+                                                  0, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < 8; u += 2) {
-      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a[u] : 0.0, vb ? (double)b[u] : 0.0, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a[u + 1] : 0.0, vb ? (double)b[u + 1] : 0.0, acc1,
+    for (int c = 0; c < 4; c += 2) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a1[c] : 0.0, vb ? (double)b1[c] : 0.0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? (double)a1[c + 1] : 0.0, vb ? (double)b1[c + 1] : 0.0, acc1,
                                                   0, 0, 0);
     }
   }

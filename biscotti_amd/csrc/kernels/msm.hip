@@ -736,3 +736,9 @@ extern "C" void* bsc_stream_create_cumask(int skip_every, int* ncu_used) {
 }
 
 extern "C" int bsc_stream_destroy(void* st) { return (int)hipStreamDestroy((hipStream_t)st); }
+
+// Small host -> device upload from pinned staging memory (utils.h2d): the bare runtime call,
+// without the per-copy event bookkeeping a framework-level pinned copy adds on the host.
+extern "C" int bsc_h2d_async(void* dst, const void* src, long long nbytes, void* stream) {
+  return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+}

@@ -94,7 +94,11 @@ class RunConfig:
     #                                 joined lazily; failures are counted and logged, never block the chain
     kzg_batch_rounds: int = 16      # rounds whose audits share one pairing product (sums of independent RLCs)
     early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
-    pre_step: bool = True           # one rank, GPU: the next round's local step (every local peer) and its
+    early_vrf: bool = True          # GPU: the next round's noiser VRF outputs start as soon as the block that
+    #                                 seeds them is built (before its audit is read and it is committed)
+    pre_gram: bool = True           # GPU, one rank: the noise-aware Krum Gram over [every local peer's delta;
+    #                                 noise rows] is queued with the pre-step, behind the recovery
+    pre_step: bool = True           # GPU (any world size): the next round's local step (every local peer) and its
     #                                 commitments are queued right behind this round's recovery, before the
     #                                 host builds the block; the head adopts them if the block carries that
     #                                 model (stateless local steps only: Philox minibatches keyed by peer, round)

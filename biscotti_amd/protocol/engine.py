@@ -38,7 +38,7 @@ from ..native import rt
 from ..ops import bn256 as B
 from ..ops import ml as K
 from ..parallel.comm import Comm
-from ..utils import JsonlWriter, PhaseTimer, flush_logs, get_logger, h2d
+from ..utils import JsonlWriter, PhaseTimer, flush_logs, get_logger, h2d, h2d_many
 from ..utils import streams as S
 from .config import RunConfig
 
@@ -350,6 +350,9 @@ class BiscottiEngine:
             # background stream it would hold up the next round's commitments
             self.vrf_stream = torch.cuda.Stream(device=self.dev, priority=lo) \
                 if cfg.vrf_device or cfg.kzg_audit != "off" else None
+            # the pre-step's Krum Gram (_queue_pre_step): beside the main stream, so the evaluation and
+            # the audit queued there do not wait for it
+            self.gram_stream = torch.cuda.Stream(device=self.dev, priority=lo)
             torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
             torch.cuda.set_stream(self.main_stream)
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
@@ -381,6 +384,7 @@ class BiscottiEngine:
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
         self._pre = None             # next round's local step + commitments, queued behind the recovery
+        self._early_vrf = None       # next round's VRF outputs, started as soon as the block hash exists
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
         self._kzg_pending: list = []   # launched audits (device) or checked ones (CPU)
@@ -665,7 +669,18 @@ class BiscottiEngine:
             dev = self.vrf_dev is not None
             nthr = max(1, cfg.host_threads - 1) if self.gpu else cfg.host_threads
             vseeds = seeds if vrf_workers is local_workers else [self.vrf_noise_seed[w] for w in vrf_workers]
-            fut_noise = R.vrf_prove_batch_async(vseeds, latest_hash, nthr, None, dev) if vseeds else None
+            early, self._early_vrf = self._early_vrf, None
+            fut_noise = None
+            if early is not None and vseeds and early["hash"] == bytes(latest_hash):
+                # the outputs started when the block was built (_early_vrf_submit): adopt them if they
+                # cover these workers with the same keys
+                pos = early["pos"]
+                if all(w in pos and early["seeds"][pos[w]] == self.vrf_noise_seed[w] for w in vrf_workers):
+                    fut_noise = early["job"]
+                    head["vrf_index"] = [pos[w] for w in vrf_workers]
+                    self.stats["early_vrf"] = self.stats.get("early_vrf", 0) + 1
+            if fut_noise is None:
+                fut_noise = R.vrf_prove_batch_async(vseeds, latest_hash, nthr, None, dev) if vseeds else None
             fut_roles = None
             roles = [self.vrf_roles_seed[p] for p in self.local if live[p]] if cfg.roles_vrf_proof else []
             if roles and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
@@ -683,7 +698,11 @@ class BiscottiEngine:
                 self.stats["pre_steps"] = self.stats.get("pre_steps", 0) + 1
                 qdelta, qrow = pre["qdelta"], {w: w - self.lo for w in local_workers}
                 delta = pre["delta"]
-                if len(local_workers) != delta.shape[0]:
+                # with the pre-step's Krum Gram (rows = every local peer) nothing reads the workers'
+                # delta rows alone; otherwise they are selected once here
+                if len(local_workers) != delta.shape[0] and not (
+                        pre.get("gram") is not None and self.comm.world == 1 and self._noise_krum()
+                        and cfg.verification):
                     delta = delta.index_select(0, h2d([w - self.lo for w in local_workers], torch.long, self.dev))
             else:
                 delta, qdelta = self.task.step(self.W, it, local_workers)
@@ -698,7 +717,9 @@ class BiscottiEngine:
                 for v, ib in zip(plan.verifiers, fsm.verifier_inboxes(workers)):
                     if live[v]:
                         inboxes[v] = list(ib)
-            row_of = {w: i for i, w in enumerate(local_workers)}   # rows of delta (Krum, noise)
+            # rows of delta (Krum, noise): the workers in order, or every local peer (unselected pre-step)
+            row_of = {w: i for i, w in enumerate(local_workers)} if delta.shape[0] == len(local_workers) else \
+                {w: w - self.lo for w in local_workers}
             qrow = qrow or row_of                                   # rows of qdelta (MSMs, commitments)
             spec = None
             cand = set()
@@ -732,11 +753,12 @@ class BiscottiEngine:
         # only on this head, so it runs now, while the host computes the workers' VRF outputs; after
         # the noisers are known only an O(n^2) assembly remains (ml.hip k_krum_rows_noise)
         krum_pre = None
-        if (self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.verification and cfg.defense == "KRUM"
-                and inboxes and local_workers and cfg.noising and self.sigma > 0 and self.noise_tbl is not None
-                and not cfg.noise_independent and cfg.krum_pregram):
+        if self.comm.world == 1 and self._noise_krum() and inboxes and local_workers:
             with tm.phase("verify.pregram"):
-                krum_pre = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
+                # adopted from the pre-step (rows = every local peer) or launched now (rows = workers)
+                krum_pre = pre.get("gram") if use_pre else None
+                if krum_pre is None:
+                    krum_pre = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
         elif mr_pre and inboxes and workers:
             # several ranks: ONE all_gather of the deltas right here (the first collective of the round),
             # then every rank runs the same phase-1 Gram over [every worker's delta; noise rows] while
@@ -761,13 +783,15 @@ class BiscottiEngine:
                 and inboxes and spec is not None and cfg.noising and self.sigma > 0 and fut_noise is not None):
             # (queued last: it waits for the VRF outputs on the host)
             with tm.phase("vrf_join"):
-                noisers = self._select_noisers(fut_noise, head["stake"], local_workers)
+                noisers = self._select_noisers(fut_noise, head["stake"], local_workers, head.get("vrf_index"))
             with tm.phase("noise"):
                 noised = None if krum_pre is not None else self._noise(delta, noisers, local_workers, it)
             with tm.phase("verify.launch"):
                 box: dict = {}
-                wait = self._launch_krum(noised, row_of, plan, live, inboxes, spec, box,
-                                         pre=krum_pre, noisers=noisers, local_workers=local_workers)
+                pg = krum_pre is not None and "row_peers" in krum_pre   # the pre-step's Gram: rows = local peers
+                wait = self._launch_krum(noised, krum_pre["xrow"] if pg else row_of, plan, live, inboxes, spec, box,
+                                         pre=krum_pre, noisers=noisers,
+                                         local_workers=krum_pre["row_peers"] if pg else local_workers)
             head["early"] = {"noisers": noisers, "krum": wait, "box": box, "noised": noised}
         return head
 
@@ -785,10 +809,13 @@ class BiscottiEngine:
             out.update(ib)
         return out
 
-    def _select_noisers(self, fut_noise, stake, local_workers) -> dict:
+    def _select_noisers(self, fut_noise, stake, local_workers, index=None) -> dict:
         """Each worker's noisers from its own VRF output (getVRFNoisers, vrf.go:54-100).  Waits for
-        the outputs only; the proofs finish on the native threads and are joined at round end."""
+        the outputs only; the proofs finish on the native threads and are joined at round end.
+        index: positions of local_workers in the job's output list (an early job covers more peers)."""
         betas = fut_noise.betas() if fut_noise is not None else []
+        if index is not None and betas:
+            betas = [betas[i] for i in index]
         sel = self.R.select_noisers_batch(stake, betas, local_workers, self.cfg.num_noisers, self.N) if betas else []
         return dict(zip(local_workers, sel))
 
@@ -829,7 +856,7 @@ class BiscottiEngine:
         vs = [v for v in plan.verifiers if v in inboxes]
         n = len(inboxes[vs[0]])
         U = X.shape[0] if X is not None else pre["U1"]
-        inbox_t = h2d([[xrow[w] for w in inboxes[v]] for v in vs], torch.int32, self.dev)
+        inbox_np = np.asarray([[xrow[w] for w in inboxes[v]] for v in vs], np.int32)
         rank = np.full(U, -1, np.int32)
         for r, w in enumerate(fsm.leader_arrivals()):
             if live[w] and w in xrow:
@@ -837,27 +864,48 @@ class BiscottiEngine:
         cap = fsm.leader_cap_size()
         need = len(plan.verifiers) // 2
         clip = fsm.krum_clip(n)
-        on_accept = self._on_accept(spec, xrow, U, plan, live, box)
-        rank_t = h2d(rank, torch.int32, self.dev)
-        if pre is not None:
-            nz = h2d([noisers[w] for w in local_workers], torch.int32, self.dev)
-            sc = h2d(self._noise_scales(noisers, local_workers), torch.float32, self.dev)
-            return K.krum_committee_noise_async(pre, nz, sc, inbox_t, n - clip, n - clip, need, rank_t, cap,
-                                                on_accept=on_accept)
-        return K.krum_committee_async(X, inbox_t, n - clip, n - clip, need, rank_t, cap, on_accept=on_accept)
-
-    def _on_accept(self, spec, xrow, U, plan, live, box):
-        """Device-side follow-up of the committee's selection: this rank's share rows' flags become the
-        leader's block mask (rows outside it are cancelled, or never computed when the MSM was
-        deferred) and the aggregation of the kept rows is queued -- on EVERY rank, with or without
-        local rows, so the aggregation's collective lines up; its handle lands in box['sa']."""
-        amap_t = sp = None
+        ups = [(inbox_np, torch.int32), (rank, torch.int32)]
+        amap = None
         if spec is not None:
             amap = np.full(U, -1, np.int32)
             for i, w in enumerate(spec[0]):
                 amap[xrow[w]] = i
-            amap_t = h2d(amap, torch.int32, self.dev)
-            sp = spec[1]
+            ups.append((amap, torch.int32))
+        if pre is not None:
+            # one (noisers, scales) row per Gram row; rows of peers that are not workers this round
+            # (the pre-step's Gram covers every local peer) are never in an inbox: zero weights
+            ws = [w for w in local_workers if w in noisers]
+            if len(ws) == len(local_workers):
+                nz_np = np.asarray([noisers[w] for w in local_workers], np.int32)
+                sc_np = self._noise_scales(noisers, local_workers)
+            else:
+                nn_ = len(noisers[ws[0]]) if ws else 1
+                nz_np = np.zeros((len(local_workers), nn_), np.int32)
+                sc_np = np.zeros((len(local_workers), nn_), np.float32)
+                if ws:
+                    at = np.asarray([i for i, w in enumerate(local_workers) if w in noisers])
+                    nz_np[at] = np.asarray([noisers[w] for w in ws], np.int32)
+                    sc_np[at] = self._noise_scales(noisers, ws)
+            ups += [(nz_np, torch.int32), (sc_np, torch.float32)]
+        # every index table of the launch in ONE upload
+        got = h2d_many(ups, self.dev)
+        inbox_t, rank_t = got[0], got[1]
+        on_accept = self._on_accept(spec, got[2] if amap is not None else None, plan, live, box)
+        if pre is not None:
+            nz, sc = got[-2], got[-1]
+            if "ev" in pre:   # produced on the Gram stream
+                S.current().wait_event(pre["ev"])
+            return K.krum_committee_noise_async(pre, nz, sc, inbox_t, n - clip, n - clip, need, rank_t, cap,
+                                                on_accept=on_accept)
+        return K.krum_committee_async(X, inbox_t, n - clip, n - clip, need, rank_t, cap, on_accept=on_accept)
+
+    def _on_accept(self, spec, amap_t, plan, live, box):
+        """Device-side follow-up of the committee's selection: this rank's share rows' flags become the
+        leader's block mask (rows outside it are cancelled, or never computed when the MSM was
+        deferred) and the aggregation of the kept rows is queued -- on EVERY rank, with or without
+        local rows, so the aggregation's collective lines up; its handle lands in box['sa'].
+        amap_t: device int32 [U], Krum row -> row of the speculative MSM (-1: none)."""
+        sp = spec[1] if spec is not None else None
         pred = self._predict_miners(plan, live) if self.gpu and self.cfg.secure_agg else None
 
         def on_accept(node):
@@ -888,7 +936,8 @@ class BiscottiEngine:
         krum_pre = head.get("krum_pre")
         with tm.phase("vrf_join"):
             noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake,
-                                                                           head.get("vrf_workers", local_workers))
+                                                                           head.get("vrf_workers", local_workers),
+                                                                           head.get("vrf_index"))
         with tm.phase("noise"):
             # with the phase-1 Gram the noised deltas are never materialised (only Krum reads them)
             noised = early["noised"] if early else (None if krum_pre is not None else
@@ -924,7 +973,7 @@ class BiscottiEngine:
                     parts.append(torch.full((self.maxlocal, 1), self._now(it), dtype=torch.int64, device=self.dev))
                 if local_workers:
                     lidx = h2d([w - self.lo for w in local_workers], torch.long, self.dev)
-                    parts[0].index_copy_(0, lidx, cr.commit_rows_tensor(pending_commits).to(self.dev))
+                    parts[0].index_copy_(0, lidx, self._local_commit_rows(pending_commits, local_workers, qrow))
                     if len(parts) > 1:
                         parts[1].index_copy_(0, lidx, noised)
                     if len(parts) > 2:
@@ -948,7 +997,7 @@ class BiscottiEngine:
                 nv = len(plan.verifiers)
                 ni = len(inboxes[vs[0]])
                 X, xrow = (noised, row_of) if single else (g_noised, self.flat)
-                if mr_pre:
+                if krum_pre is not None and "xrow" in krum_pre:
                     X, xrow = None, krum_pre["xrow"]
                 if cfg.defense == "KRUM":
                     # Multi-Krum is a pure function of the (gathered) noised deltas, so every rank
@@ -956,14 +1005,16 @@ class BiscottiEngine:
                     with tm.phase("verify.defense"):
                         wait = early["krum"] if early else self._launch_krum(
                             X, xrow, plan, live, inboxes, spec, box, pre=krum_pre, noisers=noisers,
-                            local_workers=workers if mr_pre else local_workers)
+                            local_workers=krum_pre.get("row_peers", workers) if mr_pre or (
+                                krum_pre is not None and "row_peers" in krum_pre) else local_workers)
                         if mr_pre:
                             # the commitments' all_gather, queued behind Krum and its aggregation
                             cr = self.crypto
                             part = torch.zeros((self.maxlocal, cr.point_width), dtype=cr.point_dtype, device=self.dev)
                             if local_workers:
                                 lidx = h2d([w - self.lo for w in local_workers], torch.long, self.dev)
-                                part.index_copy_(0, lidx, cr.commit_rows_tensor(pending_commits).to(self.dev))
+                                part.index_copy_(0, lidx, self._local_commit_rows(pending_commits, local_workers,
+                                                                                   qrow))
                             g_commit = comm.all_gather(part).reshape(-1, cr.point_width)
                         with tm.phase("verify.krum_wait"):
                             acc_t, node_t = wait()
@@ -995,31 +1046,32 @@ class BiscottiEngine:
                         allm = np.stack([allm[comm.owner(v, self.N), plan.verifiers.index(v)] for v in plan.verifiers])
                     acc_np = np.stack([allm[plan.verifiers.index(v)] for v in vs])
                     acc_row = {v: k for k, v in enumerate(vs)}
-                for v in vs:
-                    accepted_map[v] = [w for w, a_ in zip(inboxes[v], acc_np[acc_row[v]]) if a_]
+                # vectorised over the [verifier, inbox slot] matrix (no per-element Python loop)
+                inbox_arr = np.asarray([inboxes[v] for v in vs], np.int64)
+                acc_b = np.asarray([acc_np[acc_row[v]] for v in vs], bool)
+                for k, v in enumerate(vs):
+                    accepted_map[v] = inbox_arr[k][acc_b[k]].tolist()
                 # the local verifiers sign their accepted commitments on native threads while the GPU
                 # computes shares (main.go:1120-1140); joined where first needed (plain blocks carry
                 # them, --verify-signatures checks them) or at the end of the round
                 # message i = row rows[i] of the commitment table, signed with sks[key_of[i]], nonce id =
                 # the worker; (sl_v, sl_j) = its (verifier, inbox slot) in the signature matrix
-                rows, key_of, ids, sks, bases, sl_v, sl_j = [], [], [], [], [], [], []
-                local_vs = [v for v in vs if v in self.local]
+                lk = [k for k, v in enumerate(vs) if v in self.local]
+                local_vs = [vs[k] for k in lk]
+                sign_job, sl_v, sl_j = None, [], []
                 if local_vs:
                     _materialize_commits()
-                vidx = {v: i for i, v in enumerate(plan.verifiers)}
-                for v in local_vs:
-                    js = np.flatnonzero(acc_np[acc_row[v]]).tolist()
-                    ib, k = inboxes[v], len(sks)
-                    sks.append(self.sk[v])
-                    bases.append(_seed_bytes(cfg.seed, f"nonce-{it}", v))
-                    ws = [ib[j] for j in js]
-                    rows.extend([commit_of.row[w] for w in ws])
-                    key_of.extend([k] * len(ws))
-                    ids.extend(ws)
-                    sl_v.extend([vidx[v]] * len(ws))
-                    sl_j.extend(js)
-                sign_job = R.schnorr_sign_rows_async(commit_of.table, rows, sks, key_of, bases, ids,
-                                                     cfg.host_threads) if rows else None
+                    kk, jj = np.nonzero(acc_b[lk])            # (local verifier, inbox slot) of each signature
+                    if kk.size:
+                        ws = inbox_arr[lk][kk, jj]
+                        rmap = np.full(self.N, -1, np.int64)
+                        rmap[list(commit_of.row)] = list(commit_of.row.values())
+                        vidx = np.asarray([plan.verifiers.index(v) for v in local_vs], np.int64)
+                        sl_v, sl_j = vidx[kk], jj
+                        sks = [self.sk[v] for v in local_vs]
+                        bases = [_seed_bytes(cfg.seed, f"nonce-{it}", v) for v in local_vs]
+                        sign_job = R.schnorr_sign_rows_async(commit_of.table, rmap[ws].tolist(), sks, kk.tolist(),
+                                                             bases, ws.tolist(), max(1, cfg.host_threads - 1))
                 sig_np = np.zeros((nv, ni, 64), np.uint8)
 
                 def _join_signatures(sign_job=sign_job, sl_v=sl_v, sl_j=sl_j, sig_np=sig_np, vs=vs):
@@ -1294,7 +1346,8 @@ class BiscottiEngine:
         # audit queued next on the same stream: the block is built while the audit still runs
         readback = self._d2h_async(status, W_new, *((clock,) if clock is not None else ()))
         audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
-        if self.gpu and single and cfg.pre_step and getattr(self.task, "stateless_step", False):
+        if self.gpu and cfg.pre_step and getattr(self.task, "stateless_step", False):
+            # every rank recovers the same W_new, so each one queues its own local peers' next step
             self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)   # fsm: the round being aggregated
         if kzg_in is not None:
             # each rank audits its own partial aggregate: verifySecret is linear in (C, W, y), so the
@@ -1315,14 +1368,62 @@ class BiscottiEngine:
         return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
                 "clock": clock, "now": now, "readback": readback}
 
+    def _early_vrf_submit(self, block_hash) -> None:
+        """Start the next round's noiser VRF outputs as soon as the block that seeds them is built,
+        before its audit is read and it is committed: for every peer whose output the next head can
+        need (the local peers; every peer when each rank replicates the committee's Krum).  The next
+        head adopts the job when the committed block has this hash (it does unless the audit fails)
+        and the keys match (a churn restart draws new ones)."""
+        cfg = self.cfg
+        if not (self.gpu and cfg.early_vrf and cfg.noising and cfg.num_noisers > 0 and self.sigma > 0):
+            return
+        peers = list(range(self.N)) if self.comm.world > 1 else list(self.local)
+        seeds = [self.vrf_noise_seed[p] for p in peers]
+        job = self.R.vrf_prove_batch_async(seeds, bytes(block_hash), max(1, cfg.host_threads - 1), None,
+                                           self.vrf_dev is not None)
+        self._early_vrf = {"hash": bytes(block_hash), "job": job, "seeds": seeds,
+                           "pos": {p: i for i, p in enumerate(peers)}}
+
+    def _local_commit_rows(self, pending_commits, local_workers: list, qrow: dict) -> torch.Tensor:
+        """Device commitment rows of the local workers in local_workers order.  The commitments are
+        computed per row of qdelta (qrow: one row per local worker, or one per local peer when the
+        pre-step computed them for every local peer)."""
+        rows = self.crypto.commit_rows_tensor(pending_commits).to(self.dev)
+        idx = [qrow[w] for w in local_workers]
+        if idx == list(range(rows.shape[0])):
+            return rows
+        return rows.index_select(0, h2d(idx, torch.long, self.dev))
+
     def _queue_pre_step(self, W: torch.Tensor, it: int) -> dict:
         """The next round's local step for EVERY local peer (its workers are not known before the next
         block's roles) and their commitments (background stream), queued right behind the recovery
         of W -- the GPU runs them while the host reads W back, builds and commits the block; the next
         head adopts them if that block carries W (same device tensor) and discards them otherwise."""
         delta, qdelta = self.task.step(W, it, list(self.local))
-        return {"W": W, "it": it, "delta": delta, "qdelta": qdelta,
-                "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
+        out = {"W": W, "it": it, "delta": delta, "qdelta": qdelta,
+               "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
+        cfg = self.cfg
+        if (cfg.pre_gram and self.comm.world == 1 and self._noise_krum() and self.local):
+            # the noise-aware Krum's d-dimensional phase over EVERY local peer's delta (the workers are
+            # not known yet) and this iteration's noise rows, on its own stream right behind the step:
+            # done long before the noisers are drawn, and the main stream's evaluation does not wait
+            main, gs = S.current(), self.gram_stream
+            S.wait(gs, main)
+            with S.use(gs):
+                g = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
+                g["ev"] = S.record()
+            delta.record_stream(gs)
+            g["xrow"] = {p: p - self.lo for p in self.local}
+            g["row_peers"] = list(self.local)
+            out["gram"] = g
+        return out
+
+    def _noise_krum(self) -> bool:
+        """The noise-aware committee Krum applies: Gram of [deltas; noise table rows] ahead of the VRF."""
+        cfg = self.cfg
+        return bool(self.gpu and cfg.secure_agg and cfg.verification and cfg.defense == "KRUM" and cfg.noising
+                    and self.sigma > 0 and self.noise_tbl is not None and not cfg.noise_independent
+                    and cfg.krum_pregram)
 
     def _d2h(self, *ts: torch.Tensor) -> list:
         """Several device tensors to host numpy arrays with ONE wait (pinned, stream-ordered copies)."""
@@ -1476,6 +1577,7 @@ class BiscottiEngine:
             self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
         with tm.phase("recover.block"):
             block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
+            self._early_vrf_submit(block.hash)
         self._W_next = W_new if st.all() and self.gpu else None
         if audit_ok is not None:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit

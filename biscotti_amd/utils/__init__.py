@@ -134,6 +134,9 @@ class _PinnedRing:
         self.off = 0
 
     def stage(self, arr):
+        return self.buf[self._put(arr):][:arr.nbytes]
+
+    def _put(self, arr) -> int:
         import torch
 
         nb = arr.nbytes
@@ -143,11 +146,29 @@ class _PinnedRing:
         o = self.off
         self.off = (o + nb + 255) & ~255
         self.np[o:o + nb] = arr.reshape(-1).view(np.uint8)
-        return self.buf[o:o + nb]
+        return o
+
+    def upload(self, arr, dtype, device):
+        """Stage `arr` and copy it into a fresh device tensor with ONE bare hipMemcpyAsync on the
+        current stream (a framework-level pinned copy also records a host-allocator event per copy,
+        ~20 us of host time on this stack)."""
+        import torch
+
+        from ..native import hip
+        from . import streams as S
+
+        o = self._put(arr)
+        out = torch.empty(arr.shape, dtype=dtype, device=device)
+        err = hip().bsc_h2d_async(out.data_ptr(), self.buf.data_ptr() + o, arr.nbytes, S.raw())
+        if err != 0:
+            raise RuntimeError(f"hipMemcpyAsync (h2d) failed with hipError {err}")
+        return out
 
 
 _ring = None
 _NP_OF = {}
+# uploads through the bare runtime copy (BISCOTTI_H2D=torch: the framework's pinned .to() instead)
+_DIRECT = os.environ.get("BISCOTTI_H2D", "direct") != "torch"
 
 
 def h2d(data, dtype, device):
@@ -171,4 +192,33 @@ def h2d(data, dtype, device):
         return torch.as_tensor(data, dtype=dtype).pin_memory().to(device, non_blocking=True)
     if _ring is None:
         _ring = _PinnedRing()
+    if _DIRECT:
+        return _ring.upload(arr, dtype, device)
     return _ring.stage(arr).view(dtype).view(arr.shape).to(device, non_blocking=True)
+
+
+def h2d_many(items, device) -> list:
+    """Several small uploads in ONE copy: [(data, dtype), ...] -> device tensors (views of one
+    buffer).  Each hipMemcpyAsync costs ~20-30 us of host time on this stack, so a phase that needs
+    five index tables pays that once."""
+    import torch
+
+    global _ring
+    if torch.device(device).type != "cuda":
+        return [torch.as_tensor(d, dtype=t) for d, t in items]
+    if not _NP_OF:
+        h2d([0], torch.int32, device)   # fills _NP_OF
+    arrs = [np.ascontiguousarray(d, dtype=_NP_OF[t]) for d, t in items]
+    offs, o = [], 0
+    for a in arrs:
+        offs.append(o)
+        o = (o + a.nbytes + 15) & ~15
+    if o == 0 or o > (1 << 20):
+        return [h2d(d, t, device) for d, t in items]
+    raw = np.zeros(o, np.uint8)
+    for a, of in zip(arrs, offs):
+        raw[of:of + a.nbytes] = a.reshape(-1).view(np.uint8)
+    if _ring is None:
+        _ring = _PinnedRing()
+    dev = _ring.upload(raw, torch.uint8, device) if _DIRECT else _ring.stage(raw).to(device, non_blocking=True)
+    return [dev[of:of + a.nbytes].view(t).view(a.shape) for a, of, (_, t) in zip(arrs, offs, items)]

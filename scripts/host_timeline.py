@@ -1,0 +1,64 @@
+"""Host-side timeline of engine rounds: every PhaseTimer phase with its start/end (us from the
+round's first phase), nested phases included, for a few steady-state rounds of the headline config.
+
+    python scripts/host_timeline.py [--rounds 3] [--warm 20] [--set field=value ...]
+"""
+import argparse
+import dataclasses
+import json
+import os
+import sys
+import time
+from contextlib import contextmanager
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from biscotti_amd.parallel.comm import Comm  # noqa: E402
+from biscotti_amd.protocol.config import RunConfig  # noqa: E402
+from biscotti_amd.protocol.engine import BiscottiEngine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--warm", type=int, default=20)
+    ap.add_argument("--set", action="append", default=[])
+    a = ap.parse_args()
+    comm = Comm.init()
+    torch.set_num_threads(min(4, torch.get_num_threads()))
+    kw = dict(num_nodes=100, seed=0, max_iterations=10**9, host_threads=16)
+    types = {f.name: f.type for f in dataclasses.fields(RunConfig)}
+    for item in a.set:
+        k, v = item.split("=", 1)
+        cur = getattr(RunConfig, k)
+        kw[k] = (v.lower() in ("1", "true")) if isinstance(cur, bool) else type(cur)(v)
+    eng = BiscottiEngine(RunConfig(**kw), comm)
+    events = []
+    timer = eng.timer
+    orig = timer.phase
+
+    @contextmanager
+    def phase(name):
+        s = time.perf_counter()
+        with orig(name):
+            yield
+        events.append((name, s, time.perf_counter()))
+    timer.phase = phase
+    for _ in range(a.warm):
+        eng.run_round()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(a.rounds):
+        events.clear()
+        t0 = time.perf_counter()
+        eng.run_round()
+        rows = sorted(events, key=lambda e: e[1])
+        out.append({"wall_us": round(1e6 * (time.perf_counter() - t0), 1),
+                    "phases": [(n, round(1e6 * (s - t0), 1), round(1e6 * (e - s), 1)) for n, s, e in rows]})
+    print(json.dumps(out, indent=0))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

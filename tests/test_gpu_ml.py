@@ -237,6 +237,29 @@ def test_engine_rounds_on_gpu(early, spec_msm, pre_step):
     eng.close()
 
 
+def test_pre_gram_and_early_vrf_keep_the_chain():
+    """The Krum Gram queued with the pre-step (rows = every local peer, on its own stream) and the VRF
+    outputs started at block build give byte-identical chains to the in-round Gram (rows = workers)
+    and the VRF submitted by the head -- with poisoners, so Krum's selection decides the blocks."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    chains, stats = [], []
+    for on in (True, False):
+        cfg = RunConfig(num_nodes=20, dataset="mnist", seed=4, max_iterations=100, deterministic_time=True,
+                        poisoning=0.3, epsilon=1.0, pre_gram=on, early_vrf=on)
+        eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
+        for _ in range(6):
+            eng.run_round()
+        chains.append([bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))])
+        stats.append(dict(eng.stats))
+        eng.close()
+    assert chains[0] == chains[1]
+    assert stats[0].get("early_vrf", 0) >= 4 and "early_vrf" not in stats[1]
+    assert stats[0].get("device_aggregations", 0) >= 4
+
+
 @pytest.mark.parametrize("U,n,V", [(94, 70, 3), (150, 140, 5), (256, 256, 3), (300, 200, 26)])
 def test_krum_committee_matches_reference(U, n, V):
     """Committee Multi-Krum (one Gram over the candidate rows, per-verifier inboxes, vote and leader
