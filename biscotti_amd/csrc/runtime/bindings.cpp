@@ -203,6 +203,7 @@ struct SignJob {
   std::shared_future<void> done = done_p.get_future().share();
   bool started = false;
   std::atomic<bool> exited{false};
+  std::shared_ptr<VrfJob> after_vrf;  // start only once this VRF batch's outputs are known
   ~SignJob() {
     if (started) {  // the task's last act is setting `exited` (nothing touches the job after it)
       done.wait();
@@ -266,6 +267,8 @@ static void start_sign_job(SignJob* jp) {
   jp->started = true;
   dispatcher().submit([jp] {
     try {
+      if (jp->after_vrf) jp->after_vrf->beta_ready.wait();
+      jp->after_vrf.reset();
       run_sign_job(*jp);
     } catch (const std::exception& e) {
       jp->error = e.what();
@@ -609,11 +612,16 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   // same, message i = table[rows[i]] (e.g. the marshalled commitments of the round, uint8 [n, 64])
   m.def("schnorr_sign_rows_async", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> table,
                                       std::vector<int> rows, std::vector<py::bytes> sks, std::vector<int> key_of,
-                                      std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads) {
+                                      std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads,
+                                      std::shared_ptr<VrfJob> after_vrf) {
+    // after_vrf: the signatures yield the host threads to a VRF batch whose outputs gate the next
+    // round (they start once its outputs are known)
     auto job = make_sign_job_rows(table, rows, sks, key_of, nonce_base, nonce_ids, threads);
+    job->after_vrf = std::move(after_vrf);
     start_sign_job(job.get());
     return job;
-  });
+  }, py::arg("table"), py::arg("rows"), py::arg("sks"), py::arg("key_of"), py::arg("nonce_base"),
+     py::arg("nonce_ids"), py::arg("threads"), py::arg("after_vrf") = nullptr);
   m.def("client_key_from_entropy", [](py::bytes e) {
     auto kp = client_key_from_entropy(B(e));
     return py::make_tuple(P(kp.first.to_be()), P(kp.second.marshal()));
@@ -1197,8 +1205,52 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     if (outs.size() != selfs.size()) throw std::runtime_error("outs/selfs length mismatch");
     std::vector<std::vector<i64>> r;
     r.reserve(outs.size());
-    for (size_t k = 0; k < outs.size(); ++k) r.push_back(select_noisers(stake, B(outs[k]), selfs[k], nn, n));
+    const Lottery table(stake, n, Bytes{});
+    for (size_t k = 0; k < outs.size(); ++k) r.push_back(select_noisers(table, B(outs[k]), selfs[k], nn));
     return r;
+  });
+  // every worker's noisers straight from a VRF batch's outputs (no Python bytes in between): waits
+  // for the outputs only; out_index[k] = the job's output of worker selfs[k] (empty: k itself).
+  // Returns int64 [len(selfs), nn].  Same draws as select_noisers (equivalence-tested).
+  m.def("select_noisers_job", [](const std::map<i64, i64>& stake, VrfJob& job, std::vector<i64> out_index,
+                                 std::vector<i64> selfs, i64 nn, i64 n) {
+    {
+      py::gil_scoped_release rel;
+      job.beta_ready.wait();
+    }
+    if (!job.beta_error.empty()) throw std::runtime_error(job.beta_error);
+    const size_t k = selfs.size();
+    if (!out_index.empty() && out_index.size() != k) throw std::runtime_error("select_noisers_job: index length");
+    const Lottery table(stake, n, Bytes{});
+    const i64 holders = i64(table.ids.size());
+    py::array_t<int64_t> res({py::ssize_t(k), py::ssize_t(nn)});
+    int64_t* o = res.mutable_data();
+    Bytes input;
+    input.reserve(64);
+    for (size_t w = 0; w < k; ++w) {
+      const size_t src = out_index.empty() ? w : size_t(out_index[w]);
+      if (src >= job.out.size()) throw std::runtime_error("select_noisers_job: output index out of range");
+      const Bytes& beta = job.out[src].first;
+      const i64 self = selfs[w];
+      const i64 others = holders - (std::binary_search(table.ids.begin(), table.ids.end(), self) ? 1 : 0);
+      if (others < nn) throw std::runtime_error("lottery: not enough peers for noisers");
+      input.assign(beta.begin(), beta.end());
+      size_t i = 0;
+      i64 got = 0;
+      while (got < nn) {   // Lottery::draw over the shared ticket table
+        if (i + 1 >= input.size()) {
+          input = Sha256::digest(input);
+          i = 0;
+        }
+        const i64 idx = i64((size_t(input[i]) * 256 + size_t(input[i + 1])) % size_t(table.total()));
+        ++i;
+        const i64 c = table.ticket(idx);
+        bool dup = c == self;
+        for (i64 q = 0; q < got && !dup; ++q) dup = o[w * nn + q] == c;
+        if (!dup) o[w * nn + got++] = c;
+      }
+    }
+    return res;
   });
   m.def("krum_scores", [](py::array_t<double, py::array::c_style | py::array::forcecast> X, i64 groupsize) {
     if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");

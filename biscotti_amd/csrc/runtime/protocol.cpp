@@ -65,7 +65,13 @@ void select_roles(const std::map<i64, i64>& stake, const Bytes& hash, i64 nv, i6
 }
 
 std::vector<i64> select_noisers(const std::map<i64, i64>& stake, const Bytes& out, i64 self, i64 nn, i64 n) {
-  Lottery l(stake, n, out);
+  return select_noisers(Lottery(stake, n, Bytes{}), out, self, nn);
+}
+
+std::vector<i64> select_noisers(const Lottery& table, const Bytes& out, i64 self, i64 nn) {
+  Lottery l = table;
+  l.input = out;
+  l.i = 0;
   const i64 others = i64(l.ids.size()) - (std::binary_search(l.ids.begin(), l.ids.end(), self) ? 1 : 0);
   if (others < nn) fail("lottery: not enough peers for noisers");
   std::set<i64> seen;

@@ -70,6 +70,9 @@ void select_roles(const std::map<i64, i64>& stake, const Bytes& block_hash, i64 
                   std::vector<i64>* verifiers, std::vector<i64>* miners);
 std::vector<i64> select_noisers(const std::map<i64, i64>& stake, const Bytes& vrf_output, i64 source_id,
                                 i64 nn, i64 n);
+// the same draw from a prebuilt ticket table (`table`'s input is ignored): a batch over every worker
+// builds the stake prefix sums once instead of once per worker
+std::vector<i64> select_noisers(const Lottery& table, const Bytes& vrf_output, i64 source_id, i64 nn);
 
 // Multi-Krum (client_obj.py:114-143) -- host reference; X is row-major [n, d] float64.
 std::vector<double> krum_scores(const double* X, i64 n, i64 d, i64 groupsize);

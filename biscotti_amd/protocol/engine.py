@@ -385,6 +385,8 @@ class BiscottiEngine:
         self._W_next = None          # device copy of the model a block under construction carries
         self._pre = None             # next round's local step + commitments, queued behind the recovery
         self._early_vrf = None       # next round's VRF outputs, started as soon as the block hash exists
+        self._pre_vrf_work: list = []  # host work for the next round's VRF wait (deferred signature prep)
+        self._sign_joins: list = []  # deferred signature joins of the last rounds (secure path)
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
         self._kzg_pending: list = []   # launched audits (device) or checked ones (CPU)
@@ -499,6 +501,13 @@ class BiscottiEngine:
             if self.vrf_dev is not None and getattr(self, "vrf_stream", None) is not None:
                 self.vrf_dev.drain(self.vrf_stream)
                 self.stats["vrf_device_proofs"] = self.vrf_dev.proofs
+        if final:   # the last deferred signature batch (each round joins the previous one's)
+            work, self._pre_vrf_work = self._pre_vrf_work, []
+            for f in work:
+                f(None)
+            joins, self._sign_joins = self._sign_joins, []
+            for join in joins:
+                join()
         futs, self._pending_roles = getattr(self, "_pending_roles", None), None
         for fut in futs or ():
             if fut is not None:
@@ -813,11 +822,12 @@ class BiscottiEngine:
         """Each worker's noisers from its own VRF output (getVRFNoisers, vrf.go:54-100).  Waits for
         the outputs only; the proofs finish on the native threads and are joined at round end.
         index: positions of local_workers in the job's output list (an early job covers more peers)."""
-        betas = fut_noise.betas() if fut_noise is not None else []
-        if index is not None and betas:
-            betas = [betas[i] for i in index]
-        sel = self.R.select_noisers_batch(stake, betas, local_workers, self.cfg.num_noisers, self.N) if betas else []
-        return dict(zip(local_workers, sel))
+        if fut_noise is None or not local_workers:
+            return {}
+        # the lottery reads the job's outputs natively (no 64-byte Python objects in between)
+        sel = self.R.select_noisers_job(stake, fut_noise, list(index) if index is not None else [], local_workers,
+                                        self.cfg.num_noisers, self.N)
+        return dict(zip(local_workers, sel.tolist()))
 
     def _noise_scales(self, noisers: dict, ws: list) -> np.ndarray:
         """float32 [len(ws), nn]: each noiser's vector weight (getNoise's -sigma/sqrt(B)); 0 for
@@ -846,31 +856,45 @@ class BiscottiEngine:
         nz = h2d(ids, torch.int32, self.dev)
         return K.dp_noise(delta, nz, sc, cfg.seed, it, table=self.noise_tbl)
 
-    def _launch_krum(self, X, xrow, plan, live, inboxes, spec, box, pre=None, noisers=None, local_workers=None):
-        """Queue the committee's Multi-Krum (one Gram over the candidate rows X, every live verifier's
-        selection on its own inbox, the >= floor(nv/2) vote and the leader's arrival cap) and, behind
-        it, the device-side follow-up of the selection (_on_accept).  xrow: worker -> row of X.
-        pre: the phase-1 Gram of gram_stacked_async (X is then None: the noised rows are assembled
-        from it with the noisers' ids and scales).  Returns the callable giving (acc, node)."""
-        cfg, fsm = self.cfg, self.fsm
+    def _sign_threads(self) -> int:
+        """Threads of a signature batch: cfg.sign_threads (0: all but one of host_threads).  A narrow
+        batch leaves most of the pool to the VRF outputs that gate the next round."""
+        n = self.cfg.sign_threads
+        return max(1, n if n > 0 else self.cfg.host_threads - 1)
+
+    def _krum_static(self, xrow, U, plan, live, inboxes, spec) -> dict:
+        """The part of a Krum launch that does not depend on the noisers (inbox rows, leader arrival
+        ranks, Krum row -> speculative MSM row), uploaded in ONE copy.  run_round prepares it while
+        the host still waits for the VRF outputs."""
+        fsm = self.fsm
         vs = [v for v in plan.verifiers if v in inboxes]
         n = len(inboxes[vs[0]])
-        U = X.shape[0] if X is not None else pre["U1"]
         inbox_np = np.asarray([[xrow[w] for w in inboxes[v]] for v in vs], np.int32)
         rank = np.full(U, -1, np.int32)
         for r, w in enumerate(fsm.leader_arrivals()):
             if live[w] and w in xrow:
                 rank[xrow[w]] = r
-        cap = fsm.leader_cap_size()
-        need = len(plan.verifiers) // 2
-        clip = fsm.krum_clip(n)
         ups = [(inbox_np, torch.int32), (rank, torch.int32)]
-        amap = None
         if spec is not None:
             amap = np.full(U, -1, np.int32)
-            for i, w in enumerate(spec[0]):
-                amap[xrow[w]] = i
+            amap[[xrow[w] for w in spec[0]]] = np.arange(len(spec[0]), dtype=np.int32)
             ups.append((amap, torch.int32))
+        got = h2d_many(ups, self.dev)
+        return {"U": U, "n": n, "clip": fsm.krum_clip(n), "need": len(plan.verifiers) // 2,
+                "cap": fsm.leader_cap_size(), "inbox": got[0], "rank": got[1],
+                "amap": got[2] if spec is not None else None}
+
+    def _launch_krum(self, X, xrow, plan, live, inboxes, spec, box, pre=None, noisers=None, local_workers=None,
+                     static=None):
+        """Queue the committee's Multi-Krum (one Gram over the candidate rows X, every live verifier's
+        selection on its own inbox, the >= floor(nv/2) vote and the leader's arrival cap) and, behind
+        it, the device-side follow-up of the selection (_on_accept).  xrow: worker -> row of X.
+        pre: the phase-1 Gram of gram_stacked_async (X is then None: the noised rows are assembled
+        from it with the noisers' ids and scales).  Returns the callable giving (acc, node)."""
+        U = X.shape[0] if X is not None else pre["U1"]
+        st = static if static is not None and static["U"] == U else self._krum_static(xrow, U, plan, live, inboxes, spec)
+        n, clip, need, cap = st["n"], st["clip"], st["need"], st["cap"]
+        ups = []
         if pre is not None:
             # one (noisers, scales) row per Gram row; rows of peers that are not workers this round
             # (the pre-step's Gram covers every local peer) are never in an inbox: zero weights
@@ -887,12 +911,10 @@ class BiscottiEngine:
                     nz_np[at] = np.asarray([noisers[w] for w in ws], np.int32)
                     sc_np[at] = self._noise_scales(noisers, ws)
             ups += [(nz_np, torch.int32), (sc_np, torch.float32)]
-        # every index table of the launch in ONE upload
-        got = h2d_many(ups, self.dev)
-        inbox_t, rank_t = got[0], got[1]
-        on_accept = self._on_accept(spec, got[2] if amap is not None else None, plan, live, box)
+        inbox_t, rank_t, amap_t = st["inbox"], st["rank"], st["amap"]
+        on_accept = self._on_accept(spec, amap_t, plan, live, box)
         if pre is not None:
-            nz, sc = got[-2], got[-1]
+            nz, sc = h2d_many(ups, self.dev)   # the noisers' ids and weights: ONE upload
             if "ev" in pre:   # produced on the Gram stream
                 S.current().wait_event(pre["ev"])
             return K.krum_committee_noise_async(pre, nz, sc, inbox_t, n - clip, n - clip, need, rank_t, cap,
@@ -934,6 +956,17 @@ class BiscottiEngine:
             qrow = head["qrow"]
         early = head.get("early")
         krum_pre = head.get("krum_pre")
+        kst = None
+        with tm.phase("pre_vrf"):
+            # host work that does not need the VRF outputs, done while they are computed: the previous
+            # round's signature batch (starts once these outputs are known) and Krum's static tables
+            work, self._pre_vrf_work = self._pre_vrf_work, []
+            for f in work:
+                f(fut_noise)
+            if (self.gpu and krum_pre is not None and not early and cfg.verification and inboxes
+                    and cfg.defense == "KRUM"):
+                kst = self._krum_static(krum_pre["xrow"] if "xrow" in krum_pre else row_of, krum_pre["U1"], plan,
+                                        live, inboxes, spec)
         with tm.phase("vrf_join"):
             noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake,
                                                                            head.get("vrf_workers", local_workers),
@@ -1004,7 +1037,7 @@ class BiscottiEngine:
                     # evaluates the whole committee itself (identical inputs, deterministic kernels)
                     with tm.phase("verify.defense"):
                         wait = early["krum"] if early else self._launch_krum(
-                            X, xrow, plan, live, inboxes, spec, box, pre=krum_pre, noisers=noisers,
+                            X, xrow, plan, live, inboxes, spec, box, pre=krum_pre, noisers=noisers, static=kst,
                             local_workers=krum_pre.get("row_peers", workers) if mr_pre or (
                                 krum_pre is not None and "row_peers" in krum_pre) else local_workers)
                         if mr_pre:
@@ -1056,28 +1089,49 @@ class BiscottiEngine:
                 # them, --verify-signatures checks them) or at the end of the round
                 # message i = row rows[i] of the commitment table, signed with sks[key_of[i]], nonce id =
                 # the worker; (sl_v, sl_j) = its (verifier, inbox slot) in the signature matrix
+                # on the secure path nothing in the round reads the signatures (Q5): their batch yields
+                # the host threads to the next round's VRF outputs and is joined one round later
+                defer_sign = (self.gpu and cfg.early_vrf and cfg.secure_agg and not cfg.verify_signatures
+                              and cfg.noising and self.sigma > 0)
                 lk = [k for k, v in enumerate(vs) if v in self.local]
                 local_vs = [vs[k] for k in lk]
-                sign_job, sl_v, sl_j = None, [], []
+                sig_np = np.zeros((nv, ni, 64), np.uint8)
+                sign = {"prep": None, "job": None, "sl": None}
                 if local_vs:
                     _materialize_commits()
-                    kk, jj = np.nonzero(acc_b[lk])            # (local verifier, inbox slot) of each signature
-                    if kk.size:
-                        ws = inbox_arr[lk][kk, jj]
-                        rmap = np.full(self.N, -1, np.int64)
-                        rmap[list(commit_of.row)] = list(commit_of.row.values())
-                        vidx = np.asarray([plan.verifiers.index(v) for v in local_vs], np.int64)
-                        sl_v, sl_j = vidx[kk], jj
-                        sks = [self.sk[v] for v in local_vs]
-                        bases = [_seed_bytes(cfg.seed, f"nonce-{it}", v) for v in local_vs]
-                        sign_job = R.schnorr_sign_rows_async(commit_of.table, rmap[ws].tolist(), sks, kk.tolist(),
-                                                             bases, ws.tolist(), max(1, cfg.host_threads - 1))
-                sig_np = np.zeros((nv, ni, 64), np.uint8)
+                    table, rowmap = commit_of.table, commit_of.row
+                    acc_l, inb_l = acc_b[lk], inbox_arr[lk]
+                    vidx = np.asarray([plan.verifiers.index(v) for v in local_vs], np.int64)
+                    sks = [self.sk[v] for v in local_vs]
+                    nonce_keys = [(v, it) for v in local_vs]
 
-                def _join_signatures(sign_job=sign_job, sl_v=sl_v, sl_j=sl_j, sig_np=sig_np, vs=vs):
+                    def _prep_sign(after_vrf=None, sign=sign):
+                        # message i = row rows[i] of the commitment table, signed with sks[key_of[i]], nonce
+                        # id = the worker; (sl_v, sl_j) = its (verifier, inbox slot) in the signature matrix
+                        sign["prep"] = None
+                        kk, jj = np.nonzero(acc_l)            # (local verifier, inbox slot) of each signature
+                        if kk.size:
+                            ws = inb_l[kk, jj]
+                            rmap = np.full(self.N, -1, np.int64)
+                            rmap[list(rowmap)] = list(rowmap.values())
+                            bases = [_seed_bytes(cfg.seed, f"nonce-{i}", v) for v, i in nonce_keys]
+                            sign["sl"] = (vidx[kk], jj)
+                            sign["job"] = R.schnorr_sign_rows_async(table, rmap[ws].tolist(), sks, kk.tolist(), bases,
+                                                                    ws.tolist(), self._sign_threads(), after_vrf)
+                    sign["prep"] = _prep_sign
+                    if defer_sign:   # prepared in the next round's VRF wait, started once its outputs are known
+                        self._pre_vrf_work.append(_prep_sign)
+                    else:
+                        _prep_sign()
+
+                def _join_signatures(sign=sign, sig_np=sig_np, vs=vs):
                     with tm.phase("verify.sign_join"):
-                        if sign_job is not None:
-                            sig_np[sl_v, sl_j] = sign_job.result_array()
+                        if sign["prep"] is not None:   # deferred and not prepared yet: start it now
+                            self._pre_vrf_work = [f for f in self._pre_vrf_work if f is not sign["prep"]]
+                            sign["prep"]()
+                        if sign["job"] is not None:
+                            sl_v, sl_j = sign["sl"]
+                            sig_np[sl_v, sl_j] = sign["job"].result_array()
                         self.last_signatures = sig_np   # [nv, ni, 64]: this rank's verifiers' signatures
                         # the signatures travel to the workers (and on to the miners) only where a
                         # consumer reads them: plain blocks carry them, --verify-signatures checks them;
@@ -1109,6 +1163,13 @@ class BiscottiEngine:
         # audit (_finish_secagg); several ranks run it after the block (its signature all_gather
         # must come at the same point on every rank)
         self._idle_work = pending_signatures
+        if pending_signatures is not None and defer_sign:
+            # joined at the next round's drain point instead of under this round's audit
+            # (two rounds later: the batch starts behind the next round's VRF outputs)
+            self._idle_work = None
+            self._sign_joins.append(pending_signatures)
+            while len(self._sign_joins) > 2:
+                self._sign_joins.pop(0)()
         if cfg.secure_agg:
             block = self._secure_aggregation(plan, live, approved, delta, qdelta, local_workers, qrow,
                                              commit_of, signatures, spec, box.get("sa") if cfg.verification else None)

@@ -35,6 +35,18 @@ def main():
         kw[k] = (v.lower() in ("1", "true")) if isinstance(cur, bool) else type(cur)(v)
     eng = BiscottiEngine(RunConfig(**kw), comm)
     events = []
+    jobs = []   # (kind, submit time, job): the native VRF / signature batches of the round
+    R = eng.R
+
+    class Spy:
+        def __getattr__(self, k):
+            return getattr(R, k)
+
+        def vrf_prove_batch_async(self, *a, **kw):
+            j = R.vrf_prove_batch_async(*a, **kw)
+            jobs.append(("vrf%d" % len(a[0]), time.perf_counter(), j))
+            return j
+    eng.R = Spy()
     timer = eng.timer
     orig = timer.phase
 
@@ -51,11 +63,22 @@ def main():
     out = []
     for _ in range(a.rounds):
         events.clear()
+        jobs.clear()
         t0 = time.perf_counter()
         eng.run_round()
         rows = sorted(events, key=lambda e: e[1])
-        out.append({"wall_us": round(1e6 * (time.perf_counter() - t0), 1),
-                    "phases": [(n, round(1e6 * (s - t0), 1), round(1e6 * (e - s), 1)) for n, s, e in rows]})
+        t1 = time.perf_counter()
+        time.sleep(0.01)   # let this round's jobs finish before reading their timings
+        js = []
+        for kind, ts, j in jobs:
+            j.betas()
+            q, run = j.timing_us()
+            js.append((kind, round(1e6 * (ts - t0), 1), round(q, 1), round(run, 1)))
+        out.append({"wall_us": round(1e6 * (t1 - t0), 1),
+                    "phases": [(n, round(1e6 * (s - t0), 1), round(1e6 * (e - s), 1)) for n, s, e in rows],
+                    "jobs (kind, submit_us, queued_us, run_us)": js})
+        for _ in range(3):   # steady state again after the pause
+            eng.run_round()
     print(json.dumps(out, indent=0))
     eng.close()
 

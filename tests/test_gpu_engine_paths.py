@@ -127,3 +127,29 @@ def test_fedsys_on_gpu():
                        Comm(device=torch.device("cuda", 0)))
     errs = [eng.run_round().test_error for _ in range(6)]
     assert min(errs) < errs[0]
+
+
+def test_deferred_signatures_valid_on_gpu():
+    """GPU secure path: the verifiers' signature batch starts behind the next round's VRF outputs and
+    is joined a round later; after drain() every accepted slot verifies against the worker's
+    commitment in the block, and an uninterrupted run keeps its chain valid."""
+    eng = _engine(num_nodes=20, num_verifiers=3)
+    for _ in range(4):
+        r = eng.run_round()
+        eng.drain()
+        sig = eng.last_signatures
+        blk = eng.fsm.chain.latest()
+        commits = {w: bytes(u.commitment) for w, u in zip(r.node_list, blk.data.deltas)} if not r.empty else {}
+        n_ok = 0
+        for vi, v in enumerate(r.verifiers):
+            for j, w in enumerate(r.inboxes.get(v, [])):
+                s_ = sig[vi, j].tobytes()
+                if any(s_) and w in commits:
+                    assert eng.R.schnorr_verify(commits[w], eng.pk[v], s_)
+                    n_ok += 1
+        assert r.empty or n_ok > 0
+    for _ in range(4):   # rounds without drain: each joins the previous round's batch
+        eng.run_round()
+    eng.drain()
+    assert eng.fsm.chain.verify()[0]
+    eng.close()

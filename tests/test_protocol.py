@@ -160,3 +160,22 @@ def test_gob_float_vector_matches_scalar_encoder(rt):
         raw = rev.to_bytes(8, "big").lstrip(b"\x00")
         return bytes([256 - len(raw)]) + raw
     assert all(rt.gob_float(v) == slow(v) for v in vals)
+
+
+def test_select_noisers_job_matches_per_worker_lottery():
+    """The batched noiser draw that reads a VRF batch's outputs natively (one ticket table for every
+    worker, output index remapping) equals select_noisers run per worker on the same outputs."""
+    from biscotti_amd.native import rt
+
+    R = rt()
+    stake = {i: 10 + (i * 7) % 50 for i in range(60) if i % 9}
+    seeds = [bytes([i]) * 32 for i in range(60)]
+    job = R.vrf_prove_batch_async(seeds, b"alpha" * 6 + b"xy", 2, None, True)
+    betas = job.betas()
+    selfs = list(range(5, 55))
+    idx = [s for s in selfs]
+    for nn in (1, 2, 3):
+        got = R.select_noisers_job(stake, job, idx, selfs, nn, 60).tolist()
+        assert got == [R.select_noisers(stake, betas[i], s, nn, 60) for i, s in zip(idx, selfs)]
+    assert R.select_noisers_job(stake, job, [], list(range(60)), 2, 60).tolist() == \
+        R.select_noisers_batch(stake, betas, list(range(60)), 2, 60)
