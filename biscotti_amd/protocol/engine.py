@@ -171,7 +171,9 @@ class _SpecShares:
     def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream, deferred: bool = False, group_rows: int = 0):
         self.eng, self.qdelta, self.rows, self.stream = eng, qdelta, rows, stream
         self.group_rows = 0 if deferred else group_rows
-        self.alive = torch.ones((len(rows),), dtype=torch.int32, device=qdelta.device)
+        # the row list and the all-ones flags in ONE upload (no fill kernel), on the caller's stream
+        self.rows_t, self.alive = h2d_many([(rows, torch.int32), (np.ones(len(rows), np.int32), torch.int32)],
+                                           qdelta.device)
         self.pts = self.ys = self.ev = None
         # deferred: launched once the selection has set the flags -> only the kept rows are computed,
         # packed densely over the grid
@@ -183,12 +185,11 @@ class _SpecShares:
         main = S.current()
         S.wait(self.stream, main)              # qdelta (and any flag updates) come from main
         with S.use(self.stream):
-            rows_t = h2d(self.rows, torch.int32, self.qdelta.device)
-            self.pts, self.ys = self.eng.shares(self.qdelta, rows_t, check_rows=False, alive=self.alive,
+            self.pts, self.ys = self.eng.shares(self.qdelta, self.rows_t, check_rows=False, alive=self.alive,
                                                 compact=self.deferred, group_rows=self.group_rows)
             self.ev = torch.cuda.Event()
             self.ev.record(self.stream)
-        for t in (self.qdelta, self.alive):
+        for t in (self.qdelta, self.alive, self.rows_t):
             t.record_stream(self.stream)
         for t in (self.pts, self.ys):              # allocated on the side stream, used on main
             t.record_stream(main)
@@ -385,6 +386,7 @@ class BiscottiEngine:
         self._W_next = None          # device copy of the model a block under construction carries
         self._pre = None             # next round's local step + commitments, queued behind the recovery
         self._early_vrf = None       # next round's VRF outputs, started as soon as the block hash exists
+        self._pinned: dict = {}      # persistent pinned read-back buffers (_d2h_async)
         self._pre_vrf_work: list = []  # host work for the next round's VRF wait (deferred signature prep)
         self._sign_joins: list = []  # deferred signature joins of the last rounds (secure path)
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
@@ -1092,7 +1094,7 @@ class BiscottiEngine:
                 # on the secure path nothing in the round reads the signatures (Q5): their batch yields
                 # the host threads to the next round's VRF outputs and is joined one round later
                 defer_sign = (self.gpu and cfg.early_vrf and cfg.secure_agg and not cfg.verify_signatures
-                              and cfg.noising and self.sigma > 0)
+                              and fut_noise is not None)
                 lk = [k for k, v in enumerate(vs) if v in self.local]
                 local_vs = [vs[k] for k in lk]
                 sig_np = np.zeros((nv, ni, 64), np.uint8)
@@ -1239,8 +1241,7 @@ class BiscottiEngine:
         S.wait(bg, main)
         with S.use(bg):
             out = fn()
-            ev = torch.cuda.Event()
-            ev.record(bg)
+            ev = S.record(bg) if self.cfg.join_background else None
         for t in inputs:
             if isinstance(t, torch.Tensor):
                 t.record_stream(bg)
@@ -1333,7 +1334,7 @@ class BiscottiEngine:
         main = S.current() if self.gpu else None
         # ---- this rank's partial sums
         single = comm.world == 1
-        ys_part = torch.zeros((nch, T), dtype=torch.int64, device=self.dev)
+        ys_part = None   # this rank's share sums (several ranks / host path); one rank fuses them below
         ys_fused = mask_fused = None   # one rank, GPU: the share sums are fused into the recovery kernel
         cs_part = None
         if pts is not None and (not isinstance(rowsel, list) or rowsel):
@@ -1377,6 +1378,8 @@ class BiscottiEngine:
                 if kzg:
                     kzg_in = (cs_part, self.crypto.sum_rows(flat[rows_l][:, wcols.long()]),
                               ys_part.index_select(1, ycols_t.long()))
+        if ys_part is None and ys_fused is None:   # no local rows: nothing to add
+            ys_part = torch.zeros((nch, T), dtype=torch.int64, device=self.dev)
         if audit and cs_part is None:   # no local rows: the neutral element (point at infinity)
             cs_part = torch.zeros((nch, pw), dtype=pdt, device=self.dev)
         # ---- combine over ranks: ONE all_gather (share sums, commitment sums, clock)
@@ -1436,7 +1439,8 @@ class BiscottiEngine:
         head adopts the job when the committed block has this hash (it does unless the audit fails)
         and the keys match (a churn restart draws new ones)."""
         cfg = self.cfg
-        if not (self.gpu and cfg.early_vrf and cfg.noising and cfg.num_noisers > 0 and self.sigma > 0):
+        # (getRoles draws every peer's noisers whether or not noise is added: main.go:507)
+        if not (self.gpu and cfg.early_vrf and cfg.num_noisers > 0):
             return
         peers = list(range(self.N)) if self.comm.world > 1 else list(self.local)
         seeds = [self.vrf_noise_seed[p] for p in peers]
@@ -1497,8 +1501,13 @@ class BiscottiEngine:
             out = [t.numpy() for t in ts]
             return lambda: out
         hs = []
-        for t in ts:
-            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        for i, t in enumerate(ts):
+            # persistent pinned buffers per (slot, shape, dtype): a round reads its copies before the
+            # next round queues new ones into the same buffer
+            key = (i, tuple(t.shape), t.dtype)
+            h = self._pinned.get(key)
+            if h is None:
+                h = self._pinned[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             h.copy_(t, non_blocking=True)
             hs.append(h)
         ev = S.record()
@@ -1522,10 +1531,12 @@ class BiscottiEngine:
         if self.comm.world == 1:
             S.wait(main, self.side_stream)
         ok = self.crypto.check_aggregate(coeffs, csum)
-        host = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
+        key = ("audit", tuple(ok.shape), ok.dtype)
+        host = self._pinned.get(key)
+        if host is None:
+            host = self._pinned[key] = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
         host.copy_(ok, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(main)
+        ev = S.record(main)
 
         def result():
             ev.synchronize()

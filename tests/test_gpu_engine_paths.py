@@ -129,11 +129,12 @@ def test_fedsys_on_gpu():
     assert min(errs) < errs[0]
 
 
-def test_deferred_signatures_valid_on_gpu():
+@pytest.mark.parametrize("noising", [True, False])
+def test_deferred_signatures_valid_on_gpu(noising):
     """GPU secure path: the verifiers' signature batch starts behind the next round's VRF outputs and
     is joined a round later; after drain() every accepted slot verifies against the worker's
     commitment in the block, and an uninterrupted run keeps its chain valid."""
-    eng = _engine(num_nodes=20, num_verifiers=3)
+    eng = _engine(num_nodes=20, num_verifiers=3, noising=noising)
     for _ in range(4):
         r = eng.run_round()
         eng.drain()
@@ -152,4 +153,5 @@ def test_deferred_signatures_valid_on_gpu():
         eng.run_round()
     eng.drain()
     assert eng.fsm.chain.verify()[0]
+    assert eng.stats.get("early_vrf", 0) >= 6 and eng.stats.get("device_aggregations", 0) >= 6
     eng.close()
