@@ -782,6 +782,20 @@ class BiscottiEngine:
                 Xw = g.index_select(0, h2d([self.flat[w] for w in workers], torch.long, self.dev)).contiguous()
                 krum_pre = K.gram_stacked_async(Xw, self.noise_tbl[:, it % 100, :])
                 krum_pre["xrow"] = {w: i for i, w in enumerate(workers)}
+                # the commitments' all_gather right behind it, from the background stream (it waits for
+                # the commitments only), with an asynchronous read-back of the workers' rows: the
+                # signing and the block read them without a device sync behind Krum's aggregation
+                cr, bg = self.crypto, self.bg_stream
+                with S.use(bg):
+                    part = torch.zeros((self.maxlocal, cr.point_width), dtype=cr.point_dtype, device=self.dev)
+                    if local_workers:
+                        part.index_copy_(0, h2d([w - self.lo for w in local_workers], torch.long, self.dev),
+                                         self._local_commit_rows(pending_commits, local_workers, qrow))
+                    g = self.comm.all_gather(part).reshape(-1, cr.point_width)
+                    rows_w = g.index_select(0, h2d([self.flat[w] for w in workers], torch.long, self.dev))
+                    host = torch.empty(rows_w.shape, dtype=rows_w.dtype, pin_memory=True)
+                    host.copy_(rows_w, non_blocking=True)
+                    head["commit_gather"] = (host, S.record(bg))
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
                     qrow=qrow, spec=spec, spec_cand=cand, krum_pre=krum_pre)
         if self.vrf_dev is not None:
@@ -990,6 +1004,10 @@ class BiscottiEngine:
                 if single:
                     if local_workers:
                         commit_of.fill(pending_commits.result(), qrow)
+                elif head.get("commit_gather") is not None:   # gathered in the head (mr_pre)
+                    host, ev = head["commit_gather"]
+                    ev.synchronize()
+                    commit_of.fill(self.crypto.marshal_rows(host), {w: i for i, w in enumerate(workers)})
                 elif workers:   # every worker's commitment: one batched marshal of the gathered rows
                     sel = h2d([self.flat[w] for w in workers], torch.long, self.dev)
                     commit_of.fill(self.crypto.marshal_rows(g_commit.index_select(0, sel)),
@@ -1042,7 +1060,7 @@ class BiscottiEngine:
                             X, xrow, plan, live, inboxes, spec, box, pre=krum_pre, noisers=noisers, static=kst,
                             local_workers=krum_pre.get("row_peers", workers) if mr_pre or (
                                 krum_pre is not None and "row_peers" in krum_pre) else local_workers)
-                        if mr_pre:
+                        if mr_pre and head.get("commit_gather") is None:
                             # the commitments' all_gather, queued behind Krum and its aggregation
                             cr = self.crypto
                             part = torch.zeros((self.maxlocal, cr.point_width), dtype=cr.point_dtype, device=self.dev)
