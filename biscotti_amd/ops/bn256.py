@@ -41,8 +41,12 @@ def choose_b0(d: int, poly: int, total_shares: int, device, fraction: float = 0.
     env = os.environ.get("BSC_TABLE_B0")
     if env:
         return int(env)
-    free, _ = torch.cuda.mem_get_info(device)
-    budget = fraction * free - _SCRATCH_BYTES
+    free, total = torch.cuda.mem_get_info(device)
+    # processes sharing one GPU (several ranks / per-peer processes per device) split the budget
+    # evenly up front, so they all pick the same B0 instead of each taking 60 % of what is left
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    per_gpu = max(1, -(-local // max(1, torch.cuda.device_count())))
+    budget = min(fraction * free, fraction * total / per_gpu) - _SCRATCH_BYTES
     for b0 in B0_CHOICES:
         if table_bytes_for(d, poly, total_shares, b0) <= budget:
             return b0
