@@ -387,6 +387,7 @@ class BiscottiEngine:
         self._pre = None             # next round's local step + commitments, queued behind the recovery
         self._early_vrf = None       # next round's VRF outputs, started as soon as the block hash exists
         self._pinned: dict = {}      # persistent pinned read-back buffers (_d2h_async)
+        self._evals: list = []       # (result, evaluation read-back) of rounds not resolved yet (lazy_eval)
         self._pre_vrf_work: list = []  # host work for the next round's VRF wait (deferred signature prep)
         self._sign_joins: list = []  # deferred signature joins of the last rounds (secure path)
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
@@ -494,6 +495,14 @@ class BiscottiEngine:
                 keep.append(e)
         self._kzg_pending = keep
 
+    def _resolve_evals(self) -> None:
+        """Read the queued evaluations of earlier rounds (lazy_eval) into their results and log them."""
+        evs, self._evals = self._evals, []
+        for res, f in evs:
+            ev = f()
+            res.test_error, res.attack_rate = ev["test_error"], ev["attack_rate"]
+            self._log_round(res)
+
     def drain(self, final: bool = True) -> None:
         """Join work that belongs to rounds already returned: the last host VRF batch and, when
         final, the outstanding KZG audits and the device VRF proofs still queued or in flight."""
@@ -510,6 +519,8 @@ class BiscottiEngine:
             joins, self._sign_joins = self._sign_joins, []
             for join in joins:
                 join()
+        if final:
+            self._resolve_evals()
         futs, self._pending_roles = getattr(self, "_pending_roles", None), None
         for fut in futs or ():
             if fut is not None:
@@ -979,6 +990,7 @@ class BiscottiEngine:
             work, self._pre_vrf_work = self._pre_vrf_work, []
             for f in work:
                 f(fut_noise)
+            self._resolve_evals()
             if (self.gpu and krum_pre is not None and not early and cfg.verification and inboxes
                     and cfg.defense == "KRUM"):
                 kst = self._krum_static(krum_pre["xrow"] if "xrow" in krum_pre else row_of, krum_pre["U1"], plan,
@@ -1215,8 +1227,11 @@ class BiscottiEngine:
             self._head = self._open_round()   # next round's committee + VRF proofs start now
         if self._idle_work is not None:  # every rank, same point: the collective stays aligned
             self._idle_work()
+        lazy = cfg.lazy_eval and self.gpu
         with tm.phase("eval"):
-            ev = eval_pending()
+            # lazy_eval: the evaluation kernels are queued (above) but their two numbers are read in
+            # the next round's VRF wait (or by drain()); the round's result and log lines get them then
+            ev = {"test_error": float("nan"), "attack_rate": float("nan")} if lazy else eval_pending()
         with tm.phase("vrf_drain"):
             # the noiser proofs (nothing in the round consumes them once the lottery has joined on
             # the VRF outputs) and the discarded roles proofs (Q7) finish on the native threads;
@@ -1232,7 +1247,10 @@ class BiscottiEngine:
                           miners=list(plan.miners), test_error=ev["test_error"], attack_rate=ev["attack_rate"],
                           phases=tm.reset(), wall=time.perf_counter() - t_round, inboxes=dict(inboxes),
                           approved_by_krum=sorted(set().union(*accepted_map.values())) if accepted_map else [])
-        self._log_round(res)
+        if lazy:
+            self._evals.append((res, eval_pending))
+        else:
+            self._log_round(res)
         self.rounds_done += 1
         if it == cfg.fail_at and comm.rank == cfg.fail_rank:
             # fault injection: this rank's process dies abruptly after committing block `it`

@@ -155,3 +155,17 @@ def test_deferred_signatures_valid_on_gpu(noising):
     assert eng.fsm.chain.verify()[0]
     assert eng.stats.get("early_vrf", 0) >= 6 and eng.stats.get("device_aggregations", 0) >= 6
     eng.close()
+
+
+def test_lazy_eval_resolves_the_same_numbers():
+    """lazy_eval (bench.py): a round's test error / attack rate are read back in the next round or by
+    drain(); they equal the eagerly read numbers of the same deterministic run."""
+    out = []
+    for lazy in (False, True):
+        eng = _engine(num_nodes=16, lazy_eval=lazy)
+        rs = [eng.run_round() for _ in range(4)]
+        eng.drain()
+        out.append([(r.iteration, r.test_error, r.attack_rate) for r in rs])
+        eng.close()
+    assert out[0] == out[1]
+    assert all(e == e for _, e, _ in out[1])   # no NaN left after drain()
