@@ -742,3 +742,8 @@ extern "C" int bsc_stream_destroy(void* st) { return (int)hipStreamDestroy((hipS
 extern "C" int bsc_h2d_async(void* dst, const void* src, long long nbytes, void* stream) {
   return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyHostToDevice, (hipStream_t)stream);
 }
+
+// Device -> pinned host read-back on a stream (utils.d2h_into): the bare runtime call.
+extern "C" int bsc_d2h_async(void* dst, const void* src, long long nbytes, void* stream) {
+  return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
+}

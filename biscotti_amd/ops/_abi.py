@@ -26,6 +26,7 @@ SIGNATURES = {
     "bsc_stream_create_cumask": [I, P],
     "bsc_stream_destroy": [P],
     "bsc_h2d_async": [P, P, L, P],
+    "bsc_d2h_async": [P, P, L, P],
     "bsc_marshal": [P, I, P, P],
     "bsc_to_affine": [P, I, P, P],
     "bsc_chunk_check": [P, I, I, P, I, I, P, I, I, P, P],

@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from ..native import hip
+from ..utils import d2h_into, pinned
 from ..utils import streams as S
 
 PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
@@ -405,8 +406,8 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
                                           _p(inbox.contiguous()), V, n, groupsize, n_accept, need,
                                           _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _stream()),
            "krum_committee_noise")
-    host = torch.empty(out.shape, dtype=torch.int32, pin_memory=True)
-    host.copy_(out, non_blocking=True)
+    host = pinned("krum_noise", out.shape, torch.int32)
+    d2h_into(host, out)
     ev = S.record()
     if on_accept is not None:
         on_accept(node)
@@ -433,8 +434,8 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
            "eval_error")
     # download queued right behind the kernel: the read-back waits for the evaluation only, not for
     # whatever the caller queues on the stream afterwards (the next round's head)
-    host = torch.empty((2,), dtype=torch.int32, pin_memory=True)
-    host.copy_(err, non_blocking=True)
+    host = pinned("eval", (2,), torch.int32, depth=4)   # lazy_eval reads it one round later
+    d2h_into(host, err)
     ev = S.record()
 
     def result():

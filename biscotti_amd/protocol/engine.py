@@ -38,7 +38,7 @@ from ..native import rt
 from ..ops import bn256 as B
 from ..ops import ml as K
 from ..parallel.comm import Comm
-from ..utils import JsonlWriter, PhaseTimer, flush_logs, get_logger, h2d, h2d_many
+from ..utils import JsonlWriter, PhaseTimer, d2h_into, flush_logs, get_logger, h2d, h2d_many, pinned
 from ..utils import streams as S
 from .config import RunConfig
 
@@ -224,9 +224,8 @@ class DeviceCrypto:
                 if not hasattr(self, "_pins"):
                     self._pins = {}
                 host = self._pins[key] = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
-            host.copy_(jac, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+            d2h_into(host, jac)
+            ev = S.record(stream)
         qdelta.record_stream(stream)
         if stream is not main:
             jac.record_stream(main)
@@ -759,7 +758,8 @@ class BiscottiEngine:
                 # them in that order, and once the committee's selection lands (set_alive) the rows
                 # outside the leader's block are skipped when reached -- the block's rows are the first
                 # approved arrivals, so by then most of them are done and no candidate is ever missing
-                lo_rank = {w: i for i, w in enumerate(fsm.leader_arrivals())}
+                arrivals = head["arrivals"] = fsm.leader_arrivals()   # once per round (Krum's ranks reuse it)
+                lo_rank = {w: i for i, w in enumerate(arrivals)}
                 spec_workers = sorted((w for w in local_workers if w in cand), key=lambda w: lo_rank.get(w, 1 << 30))
                 if spec_workers:
                     defer = cfg.verification and not cfg.spec_msm
@@ -804,8 +804,8 @@ class BiscottiEngine:
                                          self._local_commit_rows(pending_commits, local_workers, qrow))
                     g = self.comm.all_gather(part).reshape(-1, cr.point_width)
                     rows_w = g.index_select(0, h2d([self.flat[w] for w in workers], torch.long, self.dev))
-                    host = torch.empty(rows_w.shape, dtype=rows_w.dtype, pin_memory=True)
-                    host.copy_(rows_w, non_blocking=True)
+                    host = pinned("commit_gather", rows_w.shape, rows_w.dtype)
+                    d2h_into(host, rows_w.contiguous())
                     head["commit_gather"] = (host, S.record(bg))
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
                     qrow=qrow, spec=spec, spec_cand=cand, krum_pre=krum_pre)
@@ -889,7 +889,7 @@ class BiscottiEngine:
         n = self.cfg.sign_threads
         return max(1, n if n > 0 else self.cfg.host_threads - 1)
 
-    def _krum_static(self, xrow, U, plan, live, inboxes, spec) -> dict:
+    def _krum_static(self, xrow, U, plan, live, inboxes, spec, arrivals=None) -> dict:
         """The part of a Krum launch that does not depend on the noisers (inbox rows, leader arrival
         ranks, Krum row -> speculative MSM row), uploaded in ONE copy.  run_round prepares it while
         the host still waits for the VRF outputs."""
@@ -898,7 +898,7 @@ class BiscottiEngine:
         n = len(inboxes[vs[0]])
         inbox_np = np.asarray([[xrow[w] for w in inboxes[v]] for v in vs], np.int32)
         rank = np.full(U, -1, np.int32)
-        for r, w in enumerate(fsm.leader_arrivals()):
+        for r, w in enumerate(arrivals if arrivals is not None else fsm.leader_arrivals()):
             if live[w] and w in xrow:
                 rank[xrow[w]] = r
         ups = [(inbox_np, torch.int32), (rank, torch.int32)]
@@ -994,7 +994,7 @@ class BiscottiEngine:
             if (self.gpu and krum_pre is not None and not early and cfg.verification and inboxes
                     and cfg.defense == "KRUM"):
                 kst = self._krum_static(krum_pre["xrow"] if "xrow" in krum_pre else row_of, krum_pre["U1"], plan,
-                                        live, inboxes, spec)
+                                        live, inboxes, spec, head.get("arrivals"))
         with tm.phase("vrf_join"):
             noisers = early["noisers"] if early else self._select_noisers(fut_noise, stake,
                                                                            head.get("vrf_workers", local_workers),
@@ -1544,7 +1544,7 @@ class BiscottiEngine:
             h = self._pinned.get(key)
             if h is None:
                 h = self._pinned[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-            h.copy_(t, non_blocking=True)
+            d2h_into(h, t.contiguous())
             hs.append(h)
         ev = S.record()
 
@@ -1571,7 +1571,7 @@ class BiscottiEngine:
         host = self._pinned.get(key)
         if host is None:
             host = self._pinned[key] = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
-        host.copy_(ok, non_blocking=True)
+        d2h_into(host, ok.contiguous())
         ev = S.record(main)
 
         def result():

@@ -14,7 +14,6 @@ import logging
 import os
 import sys
 import time
-from contextlib import contextmanager
 
 import numpy as np
 
@@ -81,6 +80,30 @@ def get_logger(name: str = "peer", path: str | None = None, level=logging.INFO) 
     return lg
 
 
+class _Phase:
+    """One timed phase (a plain context manager: a generator-based one costs a few us per use, and
+    a round enters ~25 phases on its critical host thread)."""
+
+    __slots__ = ("timer", "name", "s")
+
+    def __init__(self, timer, name):
+        self.timer, self.name = timer, name
+
+    def __enter__(self):
+        if self.timer.sync:
+            self.timer.sync()
+        self.s = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        tm = self.timer
+        if tm.sync:
+            tm.sync()
+        t = tm.t
+        t[self.name] = t.get(self.name, 0.0) + time.perf_counter() - self.s
+        return False
+
+
 class PhaseTimer:
     """Accumulates wall time per protocol phase; ``sync`` makes GPU work visible to the clock."""
 
@@ -88,17 +111,8 @@ class PhaseTimer:
         self.t: dict[str, float] = {}
         self.sync = sync
 
-    @contextmanager
-    def phase(self, name: str):
-        if self.sync:
-            self.sync()
-        s = time.perf_counter()
-        try:
-            yield
-        finally:
-            if self.sync:
-                self.sync()
-            self.t[name] = self.t.get(name, 0.0) + time.perf_counter() - s
+    def phase(self, name: str) -> _Phase:
+        return _Phase(self, name)
 
     def reset(self) -> dict[str, float]:
         out, self.t = self.t, {}
@@ -195,6 +209,41 @@ def h2d(data, dtype, device):
     if _DIRECT:
         return _ring.upload(arr, dtype, device)
     return _ring.stage(arr).view(dtype).view(arr.shape).to(device, non_blocking=True)
+
+
+_PINNED: dict = {}
+
+
+def pinned(key, shape, dtype, depth: int = 2):
+    """A persistent pinned host buffer for read-backs, rotating over `depth` buffers per (key, shape,
+    dtype): buffers written by bare copies (d2h_into) must never return to an allocator while a copy
+    may be in flight, and a read-back may still be read while the next one is queued."""
+    import torch
+
+    k = (key, tuple(shape), dtype)
+    ent = _PINNED.get(k)
+    if ent is None:
+        ent = _PINNED[k] = [[torch.empty(tuple(shape), dtype=dtype, pin_memory=True) for _ in range(depth)], 0]
+    bufs, i = ent
+    ent[1] = (i + 1) % len(bufs)
+    return bufs[i]
+
+
+def d2h_into(host, t) -> None:
+    """Stream-ordered read-back of device tensor `t` into the pinned host tensor `host` (same shape
+    and dtype) on the current stream: one bare hipMemcpyAsync (``host.copy_(t, non_blocking=True)``
+    also records a host-allocator event, ~20 us of host time per copy on this stack)."""
+    if not _DIRECT:
+        host.copy_(t, non_blocking=True)
+        return
+    from ..native import hip
+    from . import streams as S
+
+    assert host.is_pinned() and not host.is_cuda and t.is_cuda and t.is_contiguous() and host.is_contiguous()
+    assert host.dtype == t.dtype and host.numel() == t.numel()
+    err = hip().bsc_d2h_async(host.data_ptr(), t.data_ptr(), t.numel() * t.element_size(), S.raw())
+    if err != 0:
+        raise RuntimeError(f"hipMemcpyAsync (d2h) failed with hipError {err}")
 
 
 def h2d_many(items, device) -> list:
