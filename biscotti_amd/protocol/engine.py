@@ -189,10 +189,8 @@ class _SpecShares:
                                                 compact=self.deferred, group_rows=self.group_rows)
             self.ev = torch.cuda.Event()
             self.ev.record(self.stream)
-        for t in (self.qdelta, self.alive, self.rows_t):
-            t.record_stream(self.stream)
-        for t in (self.pts, self.ys):              # allocated on the side stream, used on main
-            t.record_stream(main)
+        # used on the side stream / allocated there and used on main: kept for two rounds (S.hold)
+        S.hold(self.qdelta, self.alive, self.rows_t, self.pts, self.ys)
 
 
 class DeviceCrypto:
@@ -226,9 +224,7 @@ class DeviceCrypto:
                 host = self._pins[key] = torch.empty(jac.shape, dtype=jac.dtype, pin_memory=True)
             d2h_into(host, jac)
             ev = S.record(stream)
-        qdelta.record_stream(stream)
-        if stream is not main:
-            jac.record_stream(main)
+        S.hold(qdelta, jac)
         return _PendingCommitments(host, ev, jac)
 
     def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
@@ -536,6 +532,9 @@ class BiscottiEngine:
                 if head.get(k) is not None:
                     head[k].result()
         head = None  # drop the round's tensors while their streams are all still alive
+        if self.gpu:
+            torch.cuda.synchronize(self.dev)
+            S.clear_holds()
         self._side_work = []
         self._agg_idx.clear()   # resident index tensors were used on the side stream destroyed below
         import gc
@@ -1252,6 +1251,7 @@ class BiscottiEngine:
         else:
             self._log_round(res)
         self.rounds_done += 1
+        S.rotate_holds()   # cross-stream tensors of two rounds ago are free to go
         if it == cfg.fail_at and comm.rank == cfg.fail_rank:
             # fault injection: this rank's process dies abruptly after committing block `it`
             # (the reference's FAIL_PROB crash / failAndRestartLocal.sh kill); the surviving ranks'
@@ -1278,9 +1278,7 @@ class BiscottiEngine:
         with S.use(bg):
             out = fn()
             ev = S.record(bg) if self.cfg.join_background else None
-        for t in inputs:
-            if isinstance(t, torch.Tensor):
-                t.record_stream(bg)
+        S.hold(*[t for t in inputs if isinstance(t, torch.Tensor)])
         self._side_work.append((ev, out))
         return out
 
@@ -1398,8 +1396,7 @@ class BiscottiEngine:
                     with S.use(st):
                         cs_part = B.sum_rows(flat, rows_t, ccols, check=False, row_mask=mask)
                     if st is not main:
-                        for t in (pts, ccols) + ((mask,) if mask is not None else (rows_t,)):
-                            t.record_stream(st)
+                        S.hold(pts, ccols, mask if mask is not None else rows_t)
                 # the miners' witness sums: no consumer on the protocol path (background stream); the
                 # KZG audit, when on, reads them from there
                 ws_part = self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
@@ -1513,7 +1510,7 @@ class BiscottiEngine:
             with S.use(gs):
                 g = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
                 g["ev"] = S.record()
-            delta.record_stream(gs)
+            S.hold(delta)
             g["xrow"] = {p: p - self.lo for p in self.local}
             g["row_peers"] = list(self.local)
             out["gram"] = g

@@ -72,3 +72,27 @@ def record(stream: torch.cuda.Stream | None = None) -> torch.cuda.Event:
     ev = torch.cuda.Event()
     ev.record(stream if stream is not None else current())
     return ev
+
+
+# ---------------------------------------------------------------------------- cross-stream lifetimes
+# A tensor used on a stream other than the one it was allocated on must not be reused before that
+# stream is done with it.  `Tensor.record_stream` does that with an event recorded at every free
+# and queried at later allocations (~14 per round here, and every allocation then pays the
+# queries).  A round's cross-stream work is complete two rounds later (each stream's work of round
+# r is waited on by the host through a read-back of round r or r+1), so the engine instead keeps such
+# tensors referenced for two rounds: hold() during the round, rotate_holds() at its end.
+_holds: list = [[]]
+
+
+def hold(*tensors) -> None:
+    _holds[-1].extend(tensors)
+
+
+def rotate_holds(depth: int = 2) -> None:
+    _holds.append([])
+    while len(_holds) > depth + 1:
+        _holds.pop(0)
+
+
+def clear_holds() -> None:
+    _holds[:] = [[]]
