@@ -384,7 +384,8 @@ class BiscottiEngine:
         self._pinned: dict = {}      # persistent pinned read-back buffers (_d2h_async)
         self._evals: list = []       # (result, evaluation read-back) of rounds not resolved yet (lazy_eval)
         self._pre_vrf_work: list = []  # host work for the next round's VRF wait (deferred signature prep)
-        self._sign_joins: list = []  # deferred signature joins of the last rounds (secure path)
+        self._sign_joins: list = []
+        self._stale_vrf: list = []     # early VRF batches the next head did not adopt (joined by drain)  # deferred signature joins of the last rounds (secure path)
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
         self._kzg_pending: list = []   # launched audits (device) or checked ones (CPU)
@@ -516,6 +517,7 @@ class BiscottiEngine:
                 join()
         if final:
             self._resolve_evals()
+        self._stale_vrf = [j for j in self._stale_vrf if not j.done()] if not final else []
         futs, self._pending_roles = getattr(self, "_pending_roles", None), None
         for fut in futs or ():
             if fut is not None:
@@ -689,16 +691,20 @@ class BiscottiEngine:
             dev = self.vrf_dev is not None
             nthr = max(1, cfg.host_threads - 1) if self.gpu else cfg.host_threads
             vseeds = seeds if vrf_workers is local_workers else [self.vrf_noise_seed[w] for w in vrf_workers]
-            early, self._early_vrf = self._early_vrf, None
+            ej, self._early_vrf = self._early_vrf, None
             fut_noise = None
-            if early is not None and vseeds and early["hash"] == bytes(latest_hash):
+            if ej is not None and vseeds and ej["hash"] == bytes(latest_hash):
                 # the outputs started when the block was built (_early_vrf_submit): adopt them if they
                 # cover these workers with the same keys
-                pos = early["pos"]
-                if all(w in pos and early["seeds"][pos[w]] == self.vrf_noise_seed[w] for w in vrf_workers):
-                    fut_noise = early["job"]
+                pos = ej["pos"]
+                if all(w in pos and ej["seeds"][pos[w]] == self.vrf_noise_seed[w] for w in vrf_workers):
+                    fut_noise = ej["job"]
                     head["vrf_index"] = [pos[w] for w in vrf_workers]
                     self.stats["early_vrf"] = self.stats.get("early_vrf", 0) + 1
+            if ej is not None and fut_noise is not ej["job"]:
+                # not adopted (a failed audit changed the block, or a restart its keys): joined later,
+                # not here -- dropping a running job would wait for it
+                self._stale_vrf.append(ej["job"])
             if fut_noise is None:
                 fut_noise = R.vrf_prove_batch_async(vseeds, latest_hash, nthr, None, dev) if vseeds else None
             fut_roles = None
