@@ -1191,7 +1191,8 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       .def("commit_block", &RoundFSM::commit_block)
       .def("is_poisoner", &RoundFSM::is_poisoner, py::arg("id"), py::arg("fedsys") = false)
       .def("is_colluder", &RoundFSM::is_colluder)
-      .def("round_seed", &RoundFSM::round_seed);
+      .def("round_seed", &RoundFSM::round_seed)
+      .def("successor", &RoundFSM::successor);
   m.def("select_roles", [](const std::map<i64, i64>& stake, py::bytes h, i64 nv, i64 na, i64 n) {
     std::vector<i64> v, mm;
     select_roles(stake, B(h), nv, na, n, &v, &mm);

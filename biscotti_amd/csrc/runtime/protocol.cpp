@@ -370,6 +370,17 @@ Block RoundFSM::make_empty_block() {
   return chain.make_block(d, stake, 0);
 }
 
+RoundFSM RoundFSM::successor(const Block& b) {
+  Blockchain saved = std::move(chain);  // the copy below must not duplicate the whole chain
+  chain = Blockchain();
+  chain.blocks.push_back(b);
+  RoundFSM s = *this;
+  chain = std::move(saved);
+  if (!b.stake.empty()) s.stake = b.stake;
+  s.plan = RoundPlan();
+  return s;
+}
+
 int RoundFSM::commit_block(const Block& b) {
   int r = chain.add_block(b);
   if (r >= 0 && !b.stake.empty()) stake = b.stake;

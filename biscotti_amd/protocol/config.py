@@ -49,6 +49,8 @@ class RunConfig:
     roles_vrf_proof: bool = True    # getVRFRoles computes (and discards) a proof; keep the work
     verify_signatures: bool = False  # miners check verifier signatures (commented out in reference, Q5)
     host_threads: int = 16
+    spec_head: bool = True          # GPU, one rank: the next round's share MSM is launched when the block that
+    #                                 seeds its plan is built (plan from fsm.successor), before the audit
     lazy_eval: bool = False         # GPU: a round's test error / attack rate are read (and logged) in the next
     #                                 round's VRF wait or by drain(), not at its end (bench.py sets it)
     sign_threads: int = 4           # verifier signature batches (Schnorr) run on this many host threads

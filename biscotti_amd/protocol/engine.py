@@ -349,6 +349,8 @@ class BiscottiEngine:
             # the pre-step's Krum Gram (_queue_pre_step): beside the main stream, so the evaluation and
             # the audit queued there do not wait for it
             self.gram_stream = torch.cuda.Stream(device=self.dev, priority=lo)
+            # small uploads that must not queue behind any round work (_spec_head_launch)
+            self.upload_stream = torch.cuda.Stream(device=self.dev, priority=hi)
             torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
             torch.cuda.set_stream(self.main_stream)
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
@@ -385,7 +387,8 @@ class BiscottiEngine:
         self._evals: list = []       # (result, evaluation read-back) of rounds not resolved yet (lazy_eval)
         self._pre_vrf_work: list = []  # host work for the next round's VRF wait (deferred signature prep)
         self._sign_joins: list = []
-        self._stale_vrf: list = []     # early VRF batches the next head did not adopt (joined by drain)  # deferred signature joins of the last rounds (secure path)
+        self._stale_vrf: list = []     # early VRF batches the next head did not adopt (joined by drain)
+        self._spec_next = None        # next round's share MSM launched at block build (_spec_head_launch)  # deferred signature joins of the last rounds (secure path)
         self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0}
         # batched verifySecret audit (K13): G2 side = (g2key[0], g2key[1]) = (G2, s G2)
         self._kzg_pending: list = []   # launched audits (device) or checked ones (CPU)
@@ -722,6 +725,7 @@ class BiscottiEngine:
         with tm.phase("local_step"):
             if use_pre:
                 self.stats["pre_steps"] = self.stats.get("pre_steps", 0) + 1
+                S.current().wait_event(pre["ev"])   # the step ran on the Gram stream
                 qdelta, qrow = pre["qdelta"], {w: w - self.lo for w in local_workers}
                 delta = pre["delta"]
                 # with the pre-step's Krum Gram (rows = every local peer) nothing reads the workers'
@@ -739,7 +743,15 @@ class BiscottiEngine:
             # side stream, launched by the committee's selection (only the kept rows are computed) or,
             # with spec_msm, speculatively over every candidate (rows rejected later are cancelled)
             inboxes = {}
-            if cfg.verification:
+            sn, self._spec_next = self._spec_next, None
+            if sn is not None and not (use_pre and pre is sn["pre"] and sn["hash"] == bytes(latest_hash)
+                                       and sn["it"] == plan.iteration and sn["verifiers"] == list(plan.verifiers)
+                                       and sn["miners"] == list(plan.miners) and sn["workers"] == workers
+                                       and all(live)):
+                sn = None   # the committed block or the plan differs: the speculative MSM is not used
+            if sn is not None:
+                inboxes = sn["inboxes"]
+            elif cfg.verification:
                 for v, ib in zip(plan.verifiers, fsm.verifier_inboxes(workers)):
                     if live[v]:
                         inboxes[v] = list(ib)
@@ -749,7 +761,7 @@ class BiscottiEngine:
             qrow = qrow or row_of                                   # rows of qdelta (MSMs, commitments)
             spec = None
             cand = set()
-            if self.gpu and cfg.secure_agg:
+            if self.gpu and cfg.secure_agg and sn is None:
                 # replicated on every rank: the rows (of all ranks) whose shares are computed up front
                 cand = self._block_candidates(plan, workers, inboxes)
                 cap = fsm.leader_cap_size()
@@ -758,7 +770,11 @@ class BiscottiEngine:
                     # speculative MSM covers a prefix of that order with margin for rejections
                     k = min(len(cand), int(np.ceil(cfg.spec_margin * cap)) + 2)
                     cand = set([w for w in fsm.leader_arrivals() if w in cand][:k])
-            if self.gpu and cfg.secure_agg and local_workers:
+            if sn is not None:
+                # launched at the previous block's build (_spec_head_launch), from this very plan
+                cand, spec, head["arrivals"] = sn["cand"], sn["spec"], sn["arrivals"]
+                self.stats["spec_head"] = self.stats.get("spec_head", 0) + 1
+            elif self.gpu and cfg.secure_agg and local_workers:
                 # speculative rows in leader arrival order: with spec_group_rows the MSM works through
                 # them in that order, and once the committee's selection lands (set_alive) the rows
                 # outside the leader's block are skipped when reached -- the block's rows are the first
@@ -1448,10 +1464,11 @@ class BiscottiEngine:
         # the recovered model (and the clocks) are read back right behind the recovery, AHEAD of the
         # audit queued next on the same stream: the block is built while the audit still runs
         readback = self._d2h_async(status, W_new, *((clock,) if clock is not None else ()))
-        audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
         if self.gpu and cfg.pre_step and getattr(self.task, "stateless_step", False):
-            # every rank recovers the same W_new, so each one queues its own local peers' next step
+            # every rank recovers the same W_new, so each one queues its own local peers' next step (on
+            # the Gram stream, behind the recovery but not behind the audit queued next on main)
             self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)   # fsm: the round being aggregated
+        audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
         if kzg_in is not None:
             # each rank audits its own partial aggregate: verifySecret is linear in (C, W, y), so the
             # partial sums of honest shares satisfy it exactly like the total does
@@ -1470,6 +1487,41 @@ class BiscottiEngine:
                 self._kzg_host(cs_k, ws_k, y_k, xs_list, self.fsm.iteration)
         return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
                 "clock": clock, "now": now, "readback": readback}
+
+    def _spec_head_launch(self, block) -> None:
+        """Launch the next round's speculative share MSM as soon as the block that seeds the next plan is
+        built, before its audit is read and it is committed: the plan, inboxes and leader arrival order
+        come from fsm.successor(block) (the FSM as it will be after the commit).  The MSM reads the
+        pre-step's quantised updates (it waits for the step only, not for the audit).  The next head
+        adopts it when the committed block and its plan match (they do unless the audit fails)."""
+        cfg, pre = self.cfg, self._pre
+        if not (cfg.spec_head and self.gpu and self.comm.world == 1 and cfg.secure_agg and cfg.verification
+                and cfg.spec_msm and cfg.spec_group_rows > 0 and cfg.churn == 0 and cfg.churn_kill_per_min == 0
+                and not self._partitions and pre is not None and pre["W"] is self._W_next and self.local):
+            return
+        shadow = self.fsm.successor(block)
+        live = [1] * self.N
+        plan = shadow.begin_round(live)
+        if plan.done:
+            return
+        workers = list(plan.workers)
+        inboxes = {v: list(ib) for v, ib in zip(plan.verifiers, shadow.verifier_inboxes(workers))}
+        cand = set(workers) if len(plan.verifiers) // 2 == 0 else set().union(*inboxes.values())
+        arrivals = shadow.leader_arrivals()
+        lo_rank = {w: i for i, w in enumerate(arrivals)}
+        spec_workers = sorted((w for w in workers if w in self.local and w in cand),
+                              key=lambda w: lo_rank.get(w, 1 << 30))
+        if not spec_workers:
+            return
+        side = self.side_stream
+        side.wait_event(pre["ev"])   # the step only (it ran on the Gram stream), not the audit on main
+        # the row list goes up on an otherwise idle stream (not behind the audit on main or the Gram)
+        with S.use(self.upload_stream):
+            sp = self.crypto.shares_async(pre["qdelta"], [w - self.lo for w in spec_workers], side,
+                                          group_rows=cfg.spec_group_rows)
+        self._spec_next = {"hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
+                           "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
+                           "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}
 
     def _early_vrf_submit(self, block_hash) -> None:
         """Start the next round's noiser VRF outputs as soon as the block that seeds them is built,
@@ -1503,20 +1555,24 @@ class BiscottiEngine:
         block's roles) and their commitments (background stream), queued right behind the recovery
         of W -- the GPU runs them while the host reads W back, builds and commits the block; the next
         head adopts them if that block carries W (same device tensor) and discards them otherwise."""
-        delta, qdelta = self.task.step(W, it, list(self.local))
-        out = {"W": W, "it": it, "delta": delta, "qdelta": qdelta,
-               "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
+        # on the Gram stream, right behind the recovery: the audit queued on the main stream runs beside
+        # it instead of in front of it; consumers on other streams wait for out["ev"]
         cfg = self.cfg
+        main, gs = S.current(), self.gram_stream
+        S.wait(gs, main)
+        with S.use(gs):
+            delta, qdelta = self.task.step(W, it, list(self.local))
+            ev = S.record()
+            out = {"W": W, "it": it, "delta": delta, "qdelta": qdelta, "ev": ev,
+                   "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
+        S.hold(delta, qdelta)
         if (cfg.pre_gram and self.comm.world == 1 and self._noise_krum() and self.local):
             # the noise-aware Krum's d-dimensional phase over EVERY local peer's delta (the workers are
-            # not known yet) and this iteration's noise rows, on its own stream right behind the step:
+            # not known yet) and this iteration's noise rows, on the same stream right behind the step:
             # done long before the noisers are drawn, and the main stream's evaluation does not wait
-            main, gs = S.current(), self.gram_stream
-            S.wait(gs, main)
             with S.use(gs):
                 g = K.gram_stacked_async(delta, self.noise_tbl[:, it % 100, :])
                 g["ev"] = S.record()
-            S.hold(delta)
             g["xrow"] = {p: p - self.lo for p in self.local}
             g["row_peers"] = list(self.local)
             out["gram"] = g
@@ -1690,6 +1746,8 @@ class BiscottiEngine:
             block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
             self._early_vrf_submit(block.hash)
         self._W_next = W_new if st.all() and self.gpu else None
+        if self._W_next is not None:
+            self._spec_head_launch(block)
         if audit_ok is not None:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()

@@ -238,9 +238,11 @@ def test_engine_rounds_on_gpu(early, spec_msm, pre_step):
 
 
 def test_pre_gram_and_early_vrf_keep_the_chain():
-    """The Krum Gram queued with the pre-step (rows = every local peer, on its own stream) and the VRF
-    outputs started at block build give byte-identical chains to the in-round Gram (rows = workers)
-    and the VRF submitted by the head -- with poisoners, so Krum's selection decides the blocks."""
+    """The Krum Gram queued with the pre-step (rows = every local peer, on its own stream), the VRF
+    outputs started at block build and the next round's share MSM launched from fsm.successor(block)
+    before the audit give byte-identical chains to the in-round Gram (rows = workers), the VRF
+    submitted by the head and the MSM launched by the head -- with poisoners, so Krum's selection
+    decides the blocks."""
     from biscotti_amd.parallel.comm import Comm
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
@@ -248,7 +250,7 @@ def test_pre_gram_and_early_vrf_keep_the_chain():
     chains, stats = [], []
     for on in (True, False):
         cfg = RunConfig(num_nodes=20, dataset="mnist", seed=4, max_iterations=100, deterministic_time=True,
-                        poisoning=0.3, epsilon=1.0, pre_gram=on, early_vrf=on)
+                        poisoning=0.3, epsilon=1.0, pre_gram=on, early_vrf=on, spec_head=on)
         eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
         for _ in range(6):
             eng.run_round()
@@ -257,6 +259,7 @@ def test_pre_gram_and_early_vrf_keep_the_chain():
         eng.close()
     assert chains[0] == chains[1]
     assert stats[0].get("early_vrf", 0) >= 4 and "early_vrf" not in stats[1]
+    assert stats[0].get("spec_head", 0) >= 4 and "spec_head" not in stats[1]
     assert stats[0].get("device_aggregations", 0) >= 4
 
 

@@ -179,3 +179,29 @@ def test_select_noisers_job_matches_per_worker_lottery():
         assert got == [R.select_noisers(stake, betas[i], s, nn, 60) for i, s in zip(idx, selfs)]
     assert R.select_noisers_job(stake, job, [], list(range(60)), 2, 60).tolist() == \
         R.select_noisers_batch(stake, betas, list(range(60)), 2, 60)
+
+
+def test_successor_gives_the_next_plan_before_commit():
+    """fsm.successor(block) (used to launch the next round's share MSM before the block's audit is read)
+    yields the same plan, verifier inboxes and leader arrival order as the FSM after the commit."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    eng = BiscottiEngine(RunConfig(num_nodes=12, dataset="mnist", seed=7, max_iterations=100,
+                                   deterministic_time=True), Comm())
+    for _ in range(3):
+        eng.run_round()
+        fsm = eng.fsm
+        live = [1] * 12
+        shadow = fsm.successor(fsm.chain.latest())
+        p1 = shadow.begin_round(live)
+        got = (list(p1.verifiers), list(p1.miners), list(p1.workers), p1.iteration,
+               [list(x) for x in shadow.verifier_inboxes(list(p1.workers))], list(shadow.leader_arrivals()))
+        saved = fsm.iteration
+        p2 = fsm.begin_round(live)
+        want = (list(p2.verifiers), list(p2.miners), list(p2.workers), p2.iteration,
+                [list(x) for x in fsm.verifier_inboxes(list(p2.workers))], list(fsm.leader_arrivals()))
+        fsm.iteration = saved   # undo the probe's begin_round
+        assert got == want
+    eng.close()
