@@ -1752,6 +1752,16 @@ class BiscottiEngine:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()
                 self._idle_work = None
+            if self.gpu and (self._pre_vrf_work or self._evals):
+                # the next round's VRF batch has just started (_early_vrf_submit): this round's deferred
+                # signature prep (its batch starts behind those outputs) and the earlier rounds'
+                # evaluation read-backs fill the audit wait instead of the next round's VRF wait
+                with tm.phase("recover.idle"):
+                    ej = self._early_vrf["job"] if self._early_vrf is not None else None
+                    work, self._pre_vrf_work = self._pre_vrf_work, []
+                    for f in work:
+                        f(ej)
+                    self._resolve_evals()
             with tm.phase("recover.audit"):
                 ok = audit_ok()
             if not ok.all():
