@@ -373,7 +373,9 @@ Block RoundFSM::make_empty_block() {
 RoundFSM RoundFSM::successor(const Block& b) {
   Blockchain saved = std::move(chain);  // the copy below must not duplicate the whole chain
   chain = Blockchain();
-  chain.blocks.push_back(b);
+  Block head;                            // the plan reads only the latest hash (roles, round seeds)
+  head.hash = b.hash;
+  chain.blocks.push_back(std::move(head));
   RoundFSM s = *this;
   chain = std::move(saved);
   if (!b.stake.empty()) s.stake = b.stake;

@@ -142,7 +142,7 @@ class RoundFSM {
   bool is_poisoner(i64 id, bool fedsys = false) const;
   bool is_colluder(i64 id) const { return cfg.colluders > 0 && id >= cfg.collusion_thresh; }
   u64 round_seed(u64 salt) const;
-  // The FSM as it will be once `b` is committed (its stake adopted), with a chain holding only `b`:
+  // The FSM as it will be once `b` is committed (its stake adopted), with a chain holding only b's hash:
   // begin_round / verifier_inboxes / leader_arrivals on it give the next round's plan before `b`'s
   // commit (the engine launches the next round's share MSM while it still reads the audit).
   RoundFSM successor(const Block& b);
