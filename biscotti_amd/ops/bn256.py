@@ -46,7 +46,7 @@ def choose_b0(d: int, poly: int, total_shares: int, device, fraction: float = 0.
     # evenly up front, so they all pick the same B0 instead of each taking 60 % of what is left
     local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
     per_gpu = max(1, -(-local // max(1, torch.cuda.device_count())))
-    budget = min(fraction * free, fraction * total / per_gpu) - _SCRATCH_BYTES
+    budget = min(fraction * free, (fraction if per_gpu == 1 else 0.66) * total / per_gpu) - _SCRATCH_BYTES
     for b0 in B0_CHOICES:
         if table_bytes_for(d, poly, total_shares, b0) <= budget:
             return b0
