@@ -403,6 +403,26 @@ class BiscottiEngine:
         self.rounds_done = 0
         self._partitions = cfg.partitions()
         self._head = None
+        if self.gpu and cfg.secure_agg and 0 < cfg.num_miners <= 4:
+            # every full-quorum miner layout's aggregation indices and exact recovery weights (~8 ms of
+            # host work each, the parts are a permutation of 0..M-1) at setup, not in the first rounds
+            # that meet them; layouts with offline miners are still built on first use
+            import itertools
+
+            M = cfg.num_miners
+            for perm in itertools.permutations(range(M)):
+                self._agg_index(list(range(M)), {i: perm[i] for i in range(M)})
+        if self.vrf_dev is not None:
+            # every peer's VRF key material (secret scalar, nonce prefix, public key: a fixed-base
+            # multiplication each) derived and cached now -- the host batches and the device prover's
+            # key table share the cache -- instead of inside the first rounds
+            self.vrf_dev._rows(list(self.vrf_noise_seed.values()) + list(self.vrf_roles_seed.values()))
+            # one proof now: the prover kernel's code object is loaded at its first launch (several ms),
+            # which would otherwise land in the round that fills the first 16-round batch
+            with S.use(self.vrf_stream):
+                self.vrf_dev.prove([self.vrf_noise_seed[0]], [bytes(self.vrf_dev.ALPHA_LEN)])
+            torch.cuda.synchronize(self.dev)
+            self.vrf_dev.proofs = 0
         import atexit
         import weakref
         ref = weakref.ref(self)
