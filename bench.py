@@ -103,6 +103,22 @@ def _host_threads() -> int:
     return max(4, min(16, cpus // max(1, local)))
 
 
+def _spawn_ranks(n: int) -> int:
+    """Run this same command under torch.distributed.run with n local ranks (127.0.0.1 rendezvous on a
+    free port) as a child process; the parent only waits (it must not initialise the GPU)."""
+    import os
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4")))
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +136,18 @@ def main() -> int:
     ap.add_argument("--phase-sync", action="store_true",
                     help="synchronise the GPU at every phase boundary (per-phase GPU attribution, slower)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    import os
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launched without torchrun: start the N rank processes ourselves (one per GPU, RCCL over xGMI)
+        # from this parent, which never touches the GPU, and exit with their status
+        return _spawn_ranks(a.gpus)
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank number "
+                         f"as {a.gpus} GPUs")
     if a.fedsys:
         a.config = "fedsys"
     over, ref_s, ref_acc, ref_extra, ref_src = PRESETS[a.config]

@@ -941,6 +941,38 @@ extern "C" __global__ void k_add_rows(const float* delta, int D, const int* rows
 // ---------------------------------------------------------------- C ABI launchers
 static inline int nblk(long long n, int bs) { return (int)((n + bs - 1) / bs); }
 
+// =====================================================================================
+// K11 (several ranks): a rank's partial share-value sums of its kept rows, exact in int64:
+// out[c] = sum over selected rows r of ys[r][c], c < C (C = nchunks * TOTAL_SHARES).  Rows come from an
+// index list, a device-side selection mask (the committee's block mask) or all rows.  One thread per
+// column; consecutive threads read consecutive columns of a row (coalesced), rows in order (exact and
+// order-independent anyway: integer adds).  The sums go straight into the aggregation's all_gather.
+// =====================================================================================
+extern "C" __global__ void __launch_bounds__(256) k_sum_rows_i64(const long long* __restrict__ ys, int R, long long C,
+                                                                const int* __restrict__ rows, int nsel,
+                                                                const int* __restrict__ mask,
+                                                                long long* __restrict__ out) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  long long s = 0;
+  for (int i = 0; i < nsel; ++i) {
+    const int r = rows != nullptr ? rows[i] : i;
+    if (r < 0 || r >= R) continue;
+    if (mask != nullptr && !mask[r]) continue;
+    s += ys[(size_t)r * C + c];
+  }
+  out[c] = s;
+}
+
+extern "C" int bsc_sum_rows_i64(const long long* ys, int R, long long C, const int* rows, int nsel, const int* mask,
+                                long long* out, void* stream) {
+  if (C <= 0) return 0;
+  if (rows == nullptr) nsel = R;
+  hipLaunchKernelGGL(k_sum_rows_i64, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ys, R, C,
+                     rows, nsel, mask, out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int bsc_softmax_step(const float* X, const int* y, const long long* off, const int* ntrain,
                                 const int* pid, const double* W, int D_IN, int D_OUT, int B, int P, unsigned long long seed,
                                 int iteration, float max_norm, double qscale, float* delta, long long* qdelta,

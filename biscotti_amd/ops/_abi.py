@@ -48,6 +48,7 @@ SIGNATURES = {
     "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P, P],
     "bsc_recover": [P, I, I, P, I, I, P, D, P, P, P, P],
     "bsc_add_rows": [P, I, P, I, P, P, P],
+    "bsc_sum_rows_i64": [P, I, L, P, I, P, P, P],
     "bsc_recover_w": [P, I, I, I, P, P, P, I, P, P, I, I, U64, U64, I, P, D, P, P, P, P, P],
 }
 

@@ -42,10 +42,10 @@ def choose_b0(d: int, poly: int, total_shares: int, device, fraction: float = 0.
     if env:
         return int(env)
     free, total = torch.cuda.mem_get_info(device)
-    # processes sharing one GPU (several ranks / per-peer processes per device) split the budget
-    # evenly up front, so they all pick the same B0 instead of each taking 60 % of what is left
-    local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-    per_gpu = max(1, -(-local // max(1, torch.cuda.device_count())))
+    # processes sharing one GPU (several ranks / per-peer processes per device) split the budget evenly
+    # up front, so they all pick the same B0 instead of each taking 60 % of what is left.  The count
+    # comes from Comm.init (ranks with the same host and device UUID); one rank per GPU -> no split
+    per_gpu = max(1, int(os.environ.get("BISCOTTI_RANKS_PER_DEVICE", "1")))
     budget = min(fraction * free, (fraction if per_gpu == 1 else 0.66) * total / per_gpu) - _SCRATCH_BYTES
     for b0 in B0_CHOICES:
         if table_bytes_for(d, poly, total_shares, b0) <= budget:

@@ -220,6 +220,30 @@ def noise_vector(noiser: int, iteration: int, D: int, seed: int) -> np.ndarray:
     return _gauss(r[0], r[1])
 
 
+class NoiseRows:
+    """Every noiser's 100 pre-sampled N(0,1) vectors (client_obj.py:61-63 pre-samples samples[100][D] per
+    peer at init): rows(it) -> fp32 [N, D] whose row j is the vector noiser j contributes at iteration
+    it (mod 100), before scaling.  GPU: ONE resident table [N, 100, D] (noise_table; 314 MB for MNIST x
+    100 peers), rows() a strided view.  CPU: generated per iteration from the same Philox stream
+    (bit-identical to dp_noise's regeneration) and cached for the last iteration."""
+
+    def __init__(self, N: int, D: int, seed: int, device):
+        self.N, self.D, self.seed = N, D, seed
+        self.device = torch.device(device)
+        self.table = noise_table(N, D, seed, device) if self.device.type == "cuda" else None
+        self._m, self._rows = None, None
+
+    def rows(self, it: int) -> torch.Tensor:
+        m = it % 100
+        if self.table is not None:
+            return self.table[:, m, :]
+        if self._m != m:
+            r = philox4x32(np.arange(self.D)[None, :], m, np.arange(self.N)[:, None], 0xA11CE, self.seed & MASK32,
+                           (self.seed >> 32) & MASK32)
+            self._rows, self._m = torch.from_numpy(_gauss(r[0], r[1])), m
+        return self._rows
+
+
 # ---------------------------------------------------------------------------- K5 Multi-Krum
 def krum_async(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
     """Queue Multi-Krum over the rows of X (fp32 [n, d], GPU); returns a callable giving
@@ -271,13 +295,35 @@ def krum(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
     return acc, scores
 
 
-def _committee_host(X, inbox, groupsize, n_accept, need, lead_rank, cap):
-    """fp64 torch reference of the committee Krum (same tie-breaks as the kernels)."""
-    Xd = X.double().cpu()
+def _gram_exact_order(S: torch.Tensor) -> torch.Tensor:
+    """fp64 Gram of the rows of S with every entry reduced in ONE fixed order whatever the number of rows:
+    exact products (fp32 x fp32 fits fp64), then a pairwise tree of element-wise adds over the
+    zero-padded inner dimension.  A candidate pair therefore gets bit-identical distances on one rank
+    and on several (different row sets), which a BLAS GEMM -- blocked by matrix size and threads --
+    does not guarantee."""
+    S = S.double().cpu()
+    U, D = S.shape
+    Dp = 1 << max(0, (max(D, 1) - 1).bit_length())
+    Sp = torch.zeros((U, Dp), dtype=torch.float64)
+    Sp[:, :D] = S
+    G = torch.empty((U, U), dtype=torch.float64)
+    for i in range(U):
+        P = Sp[i][None, :] * Sp
+        while P.shape[1] > 1:
+            h = P.shape[1] // 2
+            P = P[:, :h] + P[:, h:]
+        G[i] = P[:, 0]
+    return G
+
+
+def _committee_host(X, inbox, groupsize, n_accept, need, lead_rank, cap, G=None):
+    """fp64 torch reference of the committee Krum (same tie-breaks as the kernels).  G: the candidates'
+    fp64 Gram when the caller has it (the noise-aware form assembles it), else X X^T."""
     ib = inbox.cpu().long()
     V, n = ib.shape
-    U = Xd.shape[0]
-    G = Xd @ Xd.T
+    if G is None:
+        G = _gram_exact_order(X)
+    U = G.shape[0]
     sq = torch.diagonal(G)
     acc = torch.zeros((V, n), dtype=torch.bool)
     sigs = torch.zeros((U,), dtype=torch.long)
@@ -376,6 +422,8 @@ def gram_stacked_async(X, T_rows, kchunk: int = 512) -> dict:
     assert X.dtype == torch.float32 and T_rows.dtype == torch.float32
     U = U1 + U2
     assert 0 < U <= 1024, "committee Krum size limits"
+    if X.device.type != "cuda":
+        return {"gram_full": _gram_exact_order(torch.cat([X, T_rows])), "U1": U1, "U": U}
     Tt = (U + 15) // 16
     npairs = Tt * (Tt + 1) // 2
     nsplit = (D + kchunk - 1) // kchunk
@@ -398,6 +446,20 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
     assert inbox.dtype == torch.int32 and lead_rank.dtype == torch.int32 and lead_rank.numel() == U1
     assert nz.dtype == torch.int32 and sc.dtype == torch.float32 and tuple(nz.shape) == (U1, nn)
     assert 0 < n <= 256 and 0 < V <= 64 and n <= U1 and 0 < nn <= 16
+    if "gram_full" in pre:   # CPU: the same assembly as k_krum_rows_noise, term by term in its order
+        G, inv = pre["gram_full"], 1.0 / nn
+        z, w = nz.long(), sc.double()
+        Gx = G[:U1, :U1].clone()
+        for t in range(nn):
+            Gx += inv * w[None, :, t] * G[:U1, U1 + z[:, t]]
+            Gx += inv * w[:, None, t] * G[U1 + z[:, t], :U1]
+        for s_ in range(nn):
+            for t in range(nn):
+                Gx += inv * inv * w[:, None, s_] * w[None, :, t] * G[(U1 + z[:, s_])[:, None], (U1 + z[:, t])[None, :]]
+        acc, node = _committee_host(None, inbox, groupsize, n_accept, need, lead_rank, cap, G=Gx)
+        if on_accept is not None:
+            on_accept(node.to(torch.int32))
+        return lambda: (acc, node)
     dev = pre["gram"].device
     scores = torch.empty((V, n), dtype=torch.float64, device=dev)
     out = torch.empty((V * n + U1,), dtype=torch.int32, device=dev)
@@ -559,6 +621,25 @@ def recover_rows(ys, mask, ycols, xs, weights: dict, A_dev, basis_dev, poly: int
                                weights["shift"], weights["inv_lo"], weights["inv_hi"], d, _p(W), float(qscale),
                                _p(W_new), _p(coeffs), _p(status), _p(agg), _stream()), "recover_w")
     return W_new, coeffs, status, agg
+
+
+def sum_rows_i64(ys: torch.Tensor, rows: torch.Tensor | None = None, mask: torch.Tensor | None = None):
+    """out[...] = sum over the selected rows r of ys[r, ...] (int64, exact): a rank's partial share-value
+    sums of its kept workers (aggregateSecret's Y sums, kyber.go:244-287).  rows: int32 row indices, or
+    mask: int32 [R] flags (device-side selection), or neither (every row)."""
+    R = ys.shape[0]
+    C = ys[0].numel() if R else int(np.prod(ys.shape[1:]))
+    out = torch.empty(ys.shape[1:], dtype=torch.int64, device=ys.device)
+    if ys.device.type != "cuda":
+        sel = ys if rows is None and mask is None else ys[rows.long()] if rows is not None else ys[mask.bool()]
+        out.copy_(sel.sum(0))
+        return out
+    assert ys.dtype == torch.int64 and ys.is_contiguous()
+    assert rows is None or (rows.dtype == torch.int32 and rows.is_contiguous())
+    assert mask is None or (mask.dtype == torch.int32 and mask.numel() == R)
+    nsel = rows.numel() if rows is not None else R
+    _check(hip().bsc_sum_rows_i64(_p(ys), R, C, _p(rows), nsel, _p(mask), _p(out), _stream()), "sum_rows_i64")
+    return out
 
 
 def add_rows(delta, rows, W):

@@ -94,7 +94,27 @@ class Comm:
             except TypeError:
                 dist.init_process_group(be, rank=rank, world_size=world)
         be = dist.get_backend() if dist.is_initialized() else "none"
-        return Comm(world, rank, dev, be)
+        c = Comm(world, rank, dev, be)
+        if dev.type == "cuda":
+            # how many ranks share this GPU (1 on a node with one rank per GPU; several in rehearsals on a
+            # 1-GPU box): the HBM table budget is split between them (ops/bn256.choose_b0)
+            os.environ["BISCOTTI_RANKS_PER_DEVICE"] = str(c.ranks_sharing_device())
+        return c
+
+    def ranks_sharing_device(self) -> int:
+        """Ranks whose GPU is this rank's GPU (same host, same device UUID), from one all_gather_object
+        at start-up -- HIP_VISIBLE_DEVICES isolation, shared boxes and multi-node jobs all count right."""
+        if self.world == 1 or self.device.type != "cuda":
+            return 1
+        import socket
+
+        props = torch.cuda.get_device_properties(self.device)
+        me = (socket.gethostname(), str(getattr(props, "uuid", "")) or f"{props.name}:{self.device.index}",
+              os.environ.get("NCCL_HOSTID", ""))
+        everyone = [None] * self.world
+        dist.all_gather_object(everyone, me)
+        # a distinct NCCL_HOSTID per rank (the RCCL-over-sockets rehearsal) still shares the physical GPU
+        return sum(1 for o in everyone if o[:2] == me[:2])
 
     def shutdown(self) -> None:
         if self.world > 1 and dist.is_initialized():

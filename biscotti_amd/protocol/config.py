@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import argparse
 from dataclasses import dataclass, field, fields
+from typing import ClassVar
 
 
 @dataclass
@@ -39,23 +40,19 @@ class RunConfig:
     churn: float = 0.0              # fraction of peers offline per round (fault-tolerance runs)
     churn_kill_per_min: float = 0.0  # process churn (eval/eval_FT): peers killed per minute, restarted after
     #                                  60/rate - 5 s with fresh VRF keys, rejoining through chain sync
-    churn_round_s: float = 25.44    # seconds per reference round (maps churn seconds onto rounds)
     partition: str = ""             # network partition injection (DistSys/blockNode.sh drops one peer's port
     #                                 for 30 s): "peer:first_iteration:rounds[,...]" -- the peer is
     #                                 unreachable (and unreaching) for those rounds
+    fail_at: str = ""               # fault injection "IT[@RANK]": that rank (default 0) dies right after
+    #                                 committing iteration IT (the reference's FAIL_PROB crash, made
+    #                                 deterministic; torchrun restarts the job from chain_file)
     data_dir: str | None = None     # real MNIST .npy shards (reference layout), else synthetic
     commit_key: str | None = None   # commitKey.json (else generated: PK[i] = 2^i G1, s = 2)
     pkey_file: str | None = None    # pKeyG1.json (else derived from seed)
-    roles_vrf_proof: bool = True    # getVRFRoles computes (and discards) a proof; keep the work
     verify_signatures: bool = False  # miners check verifier signatures (commented out in reference, Q5)
-    host_threads: int = 16
-    spec_head: bool = True          # GPU, one rank: the next round's share MSM is launched when the block that
-    #                                 seeds its plan is built (plan from fsm.successor), before the audit
+    host_threads: int = 16          # native crypto pool of this rank (bench.py sizes it from the CPU quota)
     lazy_eval: bool = False         # GPU: a round's test error / attack rate are read (and logged) in the next
     #                                 round's VRF wait or by drain(), not at its end (bench.py sets it)
-    sign_threads: int = 4           # verifier signature batches (Schnorr) run on this many host threads
-    #                                 (0: host_threads - 1); they overlap the VRF outputs that gate a round
-    roles_vrf_threads: int = 8      # the discarded roles proof (Q7) runs in the background on fewer threads
     log_dir: str | None = None
     trace_file: str | None = None
     chain_file: str | None = None   # append-only chain persistence (checkpoint / resume)
@@ -64,51 +61,50 @@ class RunConfig:
     log_every_peer: bool = False    # one Train Error line per local peer (reference style)
     deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
     phase_sync: bool = False        # device sync at phase boundaries (diagnostics: per-phase GPU times)
-    side_stream_skip_every: int = 4  # speculative-MSM stream leaves every Nth CU free (0: no CU mask)
-    main_stream_exclusive: bool = False  # critical-path stream masked to exactly the CUs the MSM leaves free
     audit_aggregate: bool = True    # check the recovered aggregate against the miners' summed chunk
     #                                 commitments (verifyCommitment on the aggregate; not in the reference)
-    noise_table: bool = True        # GPU: every noiser's 100 noise vectors resident in HBM (pre-sampled
-    #                                 like client_obj.py:61-63) instead of regenerated each round
     comm_timeout_s: float = 300.0   # collective timeout: a dead rank fails the job instead of hanging it
-    fail_at: int = -1               # fault injection: rank `fail_rank` dies right after committing this
-    fail_rank: int = 0              #   iteration (the reference's FAIL_PROB crash, made deterministic)
-    spec_msm: bool = True           # share MSM speculatively alongside verification, over the candidates most
-    #                                 likely to end in the block (False: after the committee's selection,
-    #                                 the block's rows only -- least work, started later)
-    spec_group_rows: int = 8        # speculative MSM over EVERY candidate, G rows at a time in leader arrival
-    #                                 order; rows outside the block are skipped once the selection lands
-    spec_margin: float = 1.7        # speculative rows: the first ceil(margin * cap) + 2 candidates in leader
-    #                                 arrival order (the block takes the first `cap` approved of them;
-    #                                 a block row outside this prefix falls back to a top-up MSM)
-    shared_inbox: bool = False      # all verifiers judge one inbox (round-1 model); default: each verifier
-    #                                 collects its own first krum_thresh arrivals (krum.go:284-322)
-    miner_cap: bool = True          # leader's block = first NUM_SAMPLES/2 approved arrivals (main.go:360)
-    noise_independent: bool = False  # ablation: each worker draws private noise instead of its noisers'
-    #                                  shared pre-sampled vectors (client_obj.py:97-98); not the reference
-    krum_pregram: bool = True       # one rank, table noise: Krum's Gram over [deltas; noise vectors] runs
-    #                                 before the VRF outputs arrive; only an O(n^2) assembly waits for them
-    join_background: bool = False   # main stream waits for the background (witness-sum) work each round
     vrf_device: bool = True         # GPU: the VRF proofs nothing reads (roles proof Q7, the noiser proofs)
     #                                 run on the device (kernels/vrf.hip); the host computes only the
     #                                 64-byte outputs the lottery consumes
-    vrf_device_batch_rounds: int = 16  # rounds of proofs per device launch (a launch takes ~5 ms whatever its size)
     kzg_audit: str = "off"          # batched verifySecret (kyber.go:650-673) over every (chunk, share point) of
     #                                 the aggregate: off | consistent (y against PK[poly*k]) | literal (y
     #                                 against G1: the reference's formula, which only chunk 0 satisfies, Q9).
-    #                                 Device RLC sums (kzg.hip) + one host 3-pairing product per round,
-    #                                 joined lazily; failures are counted and logged, never block the chain
-    kzg_batch_rounds: int = 16      # rounds whose audits share one pairing product (sums of independent RLCs)
-    early_krum: bool = False        # one rank: queue noise + Krum + device aggregation with the round head
-    early_vrf: bool = True          # GPU: the next round's noiser VRF outputs start as soon as the block that
-    #                                 seeds them is built (before its audit is read and it is committed)
-    pre_gram: bool = True           # GPU, one rank: the noise-aware Krum Gram over [every local peer's delta;
-    #                                 noise rows] is queued with the pre-step, behind the recovery
-    pre_step: bool = True           # GPU (any world size): the next round's local step (every local peer) and its
-    #                                 commitments are queued right behind this round's recovery, before the
-    #                                 host builds the block; the head adopts them if the block carries that
-    #                                 model (stateless local steps only: Philox minibatches keyed by peer, round)
-    #                                 (shortens the GPU chain; costs host time before the previous round ends)
+    #                                 Device RLC sums (kzg.hip) + one host 3-pairing product per batch of
+    #                                 rounds, joined lazily; failures are counted and logged, never block the chain
+    ablation: str = ""              # comma list of semantic / pipeline ablations (experiments and tests only):
+    #   noise_independent  each worker draws private noise instead of its noisers' shared pre-sampled
+    #                      vectors (client_obj.py:97-98 shares them; docs/ROBUSTNESS.md)
+    #   shared_inbox       all verifiers judge one inbox (round-1 model; the reference: krum.go:284-322)
+    #   no_miner_cap       the leader's block takes every approved update, not its first NUM_SAMPLES/2
+    #   no_roles_proof     skip the discarded getVRFRoles proof (Q7)
+    #   no_pipeline        GPU: no cross-round pipelining (pre-step, pre-Gram, early VRF, next-round MSM
+    #                      at block build): the chain must not change (tests)
+
+    # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
+    # took 25-31 s per round, nsdi-eval/churn/*.log)
+    churn_round_s: ClassVar[float] = 25.44
+    ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline")
+
+    def has(self, ablation: str) -> bool:
+        """True when `ablation` (one of ABLATIONS) is switched on."""
+        assert ablation in self.ABLATIONS, ablation
+        return ablation in {a.strip() for a in self.ablation.split(",")}
+
+    @property
+    def noise_independent(self) -> bool:
+        return self.has("noise_independent")
+
+    @property
+    def roles_vrf_proof(self) -> bool:
+        return not self.has("no_roles_proof")
+
+    def fail_point(self) -> tuple[int, int]:
+        """(iteration, rank) of the injected crash; iteration -1 when none."""
+        if not self.fail_at:
+            return -1, 0
+        it, _, rank = str(self.fail_at).partition("@")
+        return int(it), int(rank or 0)
 
     def validate(self) -> None:
         """Reject configurations the kernels cannot run, up front (instead of a launch error in the
@@ -153,6 +149,13 @@ class RunConfig:
                     err.append(f"partition {peer}:{first}:{rounds}: peer out of range or no rounds")
         except ValueError:
             err.append(f"partition {self.partition!r}: expected peer:first_iteration:rounds[,...]")
+        bad = {a.strip() for a in self.ablation.split(",") if a.strip()} - set(self.ABLATIONS)
+        if bad:
+            err.append(f"unknown ablation(s) {sorted(bad)}: expected {', '.join(self.ABLATIONS)}")
+        try:
+            self.fail_point()
+        except ValueError:
+            err.append(f"fail_at {self.fail_at!r}: expected IT or IT@RANK")
         if self.kzg_audit not in ("off", "consistent", "literal"):
             err.append(f"kzg_audit {self.kzg_audit!r}: expected off | consistent | literal")
         if err:
@@ -187,8 +190,8 @@ class RunConfig:
         pc.default_stake = self.default_stake
         pc.stake_unit = self.stake_unit
         pc.seed = self.seed & (2**64 - 1)
-        pc.shared_inbox = self.shared_inbox
-        pc.miner_cap = self.miner_cap
+        pc.shared_inbox = self.has("shared_inbox")
+        pc.miner_cap = not self.has("no_miner_cap")
         pc.derive()
         return pc
 
@@ -229,7 +232,9 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--data-dir", default=None)
     ap.add_argument("--commit-key", default=None)
     ap.add_argument("--pkey-file", default=None)
-    ap.add_argument("--no-roles-vrf-proof", dest="roles_vrf_proof", action="store_false")
+    ap.add_argument("--no-roles-vrf-proof", dest="no_roles_vrf_proof", action="store_true",
+                    help="skip the discarded getVRFRoles proof (ablation no_roles_proof)")
+    ap.add_argument("--ablation", default="", help="comma list of RunConfig.ABLATIONS (experiments)")
     ap.add_argument("--verify-signatures", action="store_true")
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--log-dir", default=None)
@@ -239,18 +244,30 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--device", default=None)
     ap.add_argument("--log-every-peer", action="store_true")
     ap.add_argument("--deterministic-time", action="store_true")
-    ap.add_argument("--no-phase-sync", dest="phase_sync", action="store_false")
+    ap.add_argument("--phase-sync", action="store_true",
+                    help="synchronise the device at every phase boundary (per-phase GPU times; slower)")
     ap.add_argument("--no-audit-aggregate", dest="audit_aggregate", action="store_false")
-    ap.add_argument("--no-noise-table", dest="noise_table", action="store_false")
     ap.add_argument("--no-vrf-device", dest="vrf_device", action="store_false",
                     help="compute every VRF proof on host threads")
     ap.add_argument("--kzg-audit", default="off", choices=["off", "consistent", "literal"],
                     help="batched verifySecret over each round's aggregate (K13)")
     ap.add_argument("--comm-timeout", dest="comm_timeout_s", type=float, default=300.0)
     ap.add_argument("--fail-at", type=int, default=-1, help="fault injection: die after committing this iteration")
-    ap.add_argument("--fail-rank", type=int, default=0)
+    ap.add_argument("--fail-rank", type=int, default=0, help="the rank --fail-at kills")
 
 
 def config_from_args(ns: argparse.Namespace) -> RunConfig:
+    """RunConfig from parsed reference + framework flags (flags the config has no field for, such as a
+    CLI's own --rounds, are ignored)."""
     names = {f.name for f in fields(RunConfig)}
-    return RunConfig(**{k: v for k, v in vars(ns).items() if k in names})
+    v = vars(ns)
+    kw = {k: x for k, x in v.items() if k in names}
+    abl = [a for a in str(v.get("ablation", "") or "").split(",") if a.strip()]
+    if v.get("no_roles_vrf_proof"):
+        abl.append("no_roles_proof")
+    kw["ablation"] = ",".join(dict.fromkeys(a.strip() for a in abl))
+    if int(v.get("fail_at", -1) if v.get("fail_at") is not None else -1) >= 0:
+        kw["fail_at"] = f"{int(v['fail_at'])}@{int(v.get('fail_rank', 0) or 0)}"
+    else:
+        kw.pop("fail_at", None)
+    return RunConfig(**kw)

@@ -1,0 +1,291 @@
+"""Round head: everything a round needs that depends only on the latest block.
+
+A head is opened as soon as the block that seeds it is committed (DistSys/main.go
+prepareForNextIteration, :1062-1187): the live set and committee plan (stake lottery on the block
+hash, vrf.go:103-182), the workers' noiser VRF outputs (vrf.go:54-100; each rank proves only the
+peers it hosts), the local SGD step (client.py:38-65), the full-vector commitments
+(honest.go:165-200), the speculative share MSM (kyber.go:484-646) and, for the noise-aware
+committee Krum, the Gram of [every peer's delta; the noisers' pre-sampled vectors].
+
+Cross-round pipelining (GPU; off with the ``no_pipeline`` ablation, which must not change the chain):
+  * pre-step    the next round's local step + commitments (+ the Gram, gathered across ranks) are
+                queued right behind the recovery of the model they start from
+  * early VRF   the next round's noiser VRF outputs start when the block is built, before its audit
+  * spec head   the next round's share MSM starts when the block is built, from fsm.successor(block)
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import ml as K
+from ..utils import h2d
+from ..utils import streams as S
+
+SPEC_GROUP_ROWS = 8   # speculative MSM rows per group, in leader arrival order (late cancellation)
+
+
+class RoundHeadMixin:
+    # ------------------------------------------------------------------ the head
+    def _open_round(self) -> dict:
+        """Round head: live set, committee plan, the VRF outputs and the device work of the round that
+        needs nothing but the latest block; consumed by run_round."""
+        cfg, R, fsm = self.cfg, self.R, self.fsm
+        with self.timer.phase("head.plan"):
+            live = self._live_mask()
+            plan = fsm.begin_round(live)
+        head = {"live": live, "plan": plan}
+        if plan.done:
+            return head
+        latest_hash = fsm.chain.latest().hash
+        workers = [w for w in plan.workers if live[w]]
+        local_workers = [w for w in workers if w in self.local]
+        head.update(workers=workers, local_workers=local_workers, stake=dict(fsm.stake))
+        # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  Only the 64-byte
+        # outputs gate the round (noiser lottery -> noise -> Krum -> the selection that cancels speculative
+        # MSM rows); every rank computes them for the peers it hosts only (the reference: each peer proves
+        # its own), on host_threads - 1 native threads; the proofs nothing reads run on the device.
+        with self.timer.phase("head.vrf_submit"):
+            seeds = [self.vrf_noise_seed[w] for w in local_workers]
+            dev = self.vrf_dev is not None
+            nthr = max(1, cfg.host_threads - 1) if self.gpu else cfg.host_threads
+            ej, self._early_vrf = self._early_vrf, None
+            fut_noise = None
+            if ej is not None and seeds and ej["hash"] == bytes(latest_hash):
+                # the outputs started when the block was built (_early_vrf_submit): adopted if they cover
+                # these workers with the same keys
+                pos = ej["pos"]
+                if all(w in pos and ej["seeds"][pos[w]] == self.vrf_noise_seed[w] for w in local_workers):
+                    fut_noise = ej["job"]
+                    head["vrf_index"] = [pos[w] for w in local_workers]
+                    self.stats["early_vrf"] = self.stats.get("early_vrf", 0) + 1
+            if ej is not None and fut_noise is not ej["job"]:
+                # not adopted (a failed audit changed the block, or a restart its keys): joined later, not
+                # here -- dropping a running job would wait for it
+                self._stale_vrf.append(ej["job"])
+            if fut_noise is None:
+                fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, nthr, None, dev) if seeds else None
+                self.stats["vrf_outputs"] += len(seeds)
+            fut_roles = None
+            roles = [self.vrf_roles_seed[p] for p in self.local if live[p]] if cfg.roles_vrf_proof else []
+            if roles and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
+                fut_roles = R.vrf_prove_batch_async(roles, latest_hash, 8, fut_noise)
+        head.update(fut_noise=fut_noise, fut_roles=fut_roles)
+        tm, it = self.timer, plan.iteration
+        # the local step (and the commitments) may already be in flight: queued behind the recovery of the
+        # model this head starts from (_queue_pre_step), for every local peer.  The decision is the same
+        # on every rank (the pre-step is queued at the same point everywhere): the Gram gather depends on it.
+        pre, self._pre = self._pre, None
+        use_pre = pre is not None and pre["it"] == it and pre["W"] is self.W
+        with tm.phase("local_step"):
+            if use_pre:
+                self.stats["pre_steps"] = self.stats.get("pre_steps", 0) + 1
+                S.current().wait_event(pre["ev"])   # the step ran on the Gram stream
+                delta, qdelta = pre["delta"], pre["qdelta"]          # rows: every local peer
+                row_of = {w: w - self.lo for w in local_workers}
+            else:
+                delta, qdelta = self.task.step(self.W, it, local_workers)
+                row_of = {w: i for i, w in enumerate(local_workers)}
+        with tm.phase("commit"):
+            # every live verifier collects its own first krum_thresh arrivals (krum.go:284-322); only updates
+            # that can end in the leader's block secret-share: the MSM runs speculatively on the CU-masked
+            # side stream over every candidate, in leader arrival order, and the committee's selection
+            # cancels the rows it rejects
+            inboxes = {}
+            sn, self._spec_next = self._spec_next, None
+            if sn is not None and not (use_pre and pre is sn["pre"] and sn["hash"] == bytes(latest_hash)
+                                       and sn["it"] == it and sn["verifiers"] == list(plan.verifiers)
+                                       and sn["miners"] == list(plan.miners) and sn["workers"] == workers
+                                       and all(live)):
+                sn = None   # the committed block or the plan differs: the speculative MSM is not used
+            if sn is not None:
+                inboxes = sn["inboxes"]
+            elif cfg.verification:
+                for v, ib in zip(plan.verifiers, fsm.verifier_inboxes(workers)):
+                    if live[v]:
+                        inboxes[v] = list(ib)
+            spec = None
+            cand = set()
+            if sn is not None:
+                # launched at the previous block's build (_spec_head_launch), from this very plan
+                cand, spec, head["arrivals"] = sn["cand"], sn["spec"], sn["arrivals"]
+                self.stats["spec_head"] = self.stats.get("spec_head", 0) + 1
+            elif self.gpu and cfg.secure_agg:
+                # replicated on every rank: the rows (of all ranks) whose shares are computed up front
+                cand = self._block_candidates(plan, workers, inboxes)
+                if local_workers:
+                    arrivals = head["arrivals"] = fsm.leader_arrivals()   # once per round (Krum reuses it)
+                    lo_rank = {w: i for i, w in enumerate(arrivals)}
+                    spec_workers = sorted((w for w in local_workers if w in cand),
+                                          key=lambda w: lo_rank.get(w, 1 << 30))
+                    if spec_workers:
+                        spec = (spec_workers, self.crypto.shares_async(qdelta, [row_of[w] for w in spec_workers],
+                                                                       self.side_stream,
+                                                                       group_rows=SPEC_GROUP_ROWS))
+            # full-vector commitments on the background stream: their first consumer is the signing after
+            # Krum, so noise + Krum on the main stream do not queue behind them
+            pending_commits = pre["commits"] if use_pre else \
+                self.crypto.commitments_async(qdelta, self.bg_stream if self.gpu else None)
+        # noise-aware committee Krum: the d-dimensional part (the Gram of every peer's delta stacked over
+        # the noisers' pre-sampled vectors of this iteration) depends only on this head, so it runs while
+        # the host computes the VRF outputs; after the noisers are known only an O(n^2) assembly remains
+        krum_pre = None
+        if self._noise_krum() and inboxes and workers:   # replicated condition (the Gram gathers)
+            with tm.phase("verify.pregram"):
+                krum_pre = pre.get("gram") if use_pre else None
+                if krum_pre is None:
+                    krum_pre = self._gram_rows(delta, row_of, it)
+        head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
+                    spec=spec, spec_cand=cand, krum_pre=krum_pre)
+        if self.vrf_dev is not None:
+            # the proofs nobody reads -- every noiser proof and the roles proofs -- on the device, on their
+            # own low-priority stream
+            self.vrf_dev.submit(seeds + roles, latest_hash, self.vrf_stream)
+        return head
+
+    def _block_candidates(self, plan, workers, inboxes) -> set:
+        """Workers whose update can end in this round's block: without verification every live worker
+        (capped to the leader's first arrivals); with it, every update some live verifier judges -- or
+        every live worker when floor(nv/2) == 0 signatures suffice (the nv = 1 quirk, main.go:1686:
+        updates no verifier saw are approved too)."""
+        if not self.cfg.verification:
+            return set(self.fsm.leader_cap(workers))
+        if len(plan.verifiers) // 2 == 0:
+            return set(workers)
+        out: set = set()
+        for ib in inboxes.values():
+            out.update(ib)
+        return out
+
+    # ------------------------------------------------------------------ noise-aware Krum, phase 1
+    def _noise_krum(self) -> bool:
+        """The noise-aware committee Krum applies: every worker's noised update is its delta plus the mean
+        of its noisers' pre-sampled vectors (client_obj.py:97-98), so Krum's Gram can be taken over
+        [deltas; noise vectors] before the noisers are known.  Same answer on every rank."""
+        cfg = self.cfg
+        return bool(cfg.secure_agg and cfg.verification and cfg.defense == "KRUM" and cfg.noising
+                    and self.sigma > 0 and cfg.num_noisers >= 1 and self.noise_rows is not None
+                    and not cfg.noise_independent and self.comm.world * self.maxlocal + self.N <= 1024)
+
+    def _gram_rows(self, delta: torch.Tensor, row_of: dict | None, it: int) -> dict:
+        """Phase 1 of the noise-aware committee Krum over the flat peer layout: row r * maxlocal + j is
+        rank r's j-th peer (self.flat), then the N noise rows of this iteration.  delta holds every
+        local peer (row_of None, the pre-step) or the rows row_of names.  Several ranks: ONE all_gather
+        of the [maxlocal, d] delta buffers (called at the same point on every rank)."""
+        ml, d = self.maxlocal, self.d
+        if row_of is None and delta.shape[0] == ml:
+            buf = delta
+        else:
+            buf = torch.zeros((ml, d), dtype=torch.float32, device=self.dev)
+            if row_of is None:
+                buf[: delta.shape[0]] = delta
+            elif row_of:
+                ws = list(row_of)
+                src = delta if [row_of[w] for w in ws] == list(range(delta.shape[0])) else \
+                    delta.index_select(0, h2d([row_of[w] for w in ws], torch.long, self.dev))
+                buf.index_copy_(0, h2d([w - self.lo for w in ws], torch.long, self.dev), src)
+        X = self.comm.all_gather(buf).reshape(-1, d) if self.comm.world > 1 else buf
+        g = K.gram_stacked_async(X.contiguous(), self.noise_rows.rows(it))
+        g["xrow"] = self.flat
+        return g
+
+    # ------------------------------------------------------------------ cross-round pipelining
+    def _pipelined(self) -> bool:
+        return self.gpu and not self.cfg.has("no_pipeline")
+
+    def _queue_pre_step(self, W: torch.Tensor, it: int) -> dict:
+        """The next round's local step for EVERY local peer (its workers are not known before the next
+        block's roles) and their commitments (background stream), queued right behind the recovery of
+        W -- the GPU runs them while the host reads W back, builds and commits the block; the next head
+        adopts them if that block carries W (same device tensor) and discards them otherwise.  Every rank
+        queues it at the same point (the recovery is replicated), so the Gram's gather lines up."""
+        main, gs = S.current(), self.gram_stream
+        S.wait(gs, main)
+        with S.use(gs):
+            delta, qdelta = self.task.step(W, it, list(self.local))
+            ev = S.record()
+            out = {"W": W, "it": it, "delta": delta, "qdelta": qdelta, "ev": ev,
+                   "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
+        S.hold(delta, qdelta)
+        if self._noise_krum():
+            # the noise-aware Krum's d-dimensional phase over EVERY peer's delta (the workers are not known
+            # yet) and this iteration's noise rows, on the same stream right behind the step: done long
+            # before the noisers are drawn, and the main stream's evaluation does not wait for it
+            with S.use(gs):
+                g = self._gram_rows(delta, None, it)
+                g["ev"] = S.record()
+            out["gram"] = g
+        return out
+
+    def _spec_head_launch(self, block) -> None:
+        """Launch the next round's speculative share MSM as soon as the block that seeds the next plan is
+        built, before its audit is read and it is committed: the plan, inboxes and leader arrival order
+        come from fsm.successor(block) (the FSM as it will be after the commit).  The MSM reads the
+        pre-step's quantised updates (it waits for the step only, not for the audit).  The next head
+        adopts it when the committed block and its plan match (they do unless the audit fails).  Local
+        work only (no collective): each rank launches its own peers' rows."""
+        cfg, pre = self.cfg, self._pre
+        if not (self._pipelined() and cfg.secure_agg and cfg.verification and cfg.churn == 0
+                and cfg.churn_kill_per_min == 0 and not self._partitions and pre is not None
+                and pre["W"] is self._W_next and self.local):
+            return
+        shadow = self.fsm.successor(block)
+        live = [1] * self.N
+        plan = shadow.begin_round(live)
+        if plan.done:
+            return
+        workers = list(plan.workers)
+        inboxes = {v: list(ib) for v, ib in zip(plan.verifiers, shadow.verifier_inboxes(workers))}
+        cand = set(workers) if len(plan.verifiers) // 2 == 0 else set().union(*inboxes.values())
+        arrivals = shadow.leader_arrivals()
+        lo_rank = {w: i for i, w in enumerate(arrivals)}
+        spec_workers = sorted((w for w in workers if w in self.local and w in cand),
+                              key=lambda w: lo_rank.get(w, 1 << 30))
+        if not spec_workers:
+            return
+        side = self.side_stream
+        side.wait_event(pre["ev"])   # the step only (it ran on the Gram stream), not the audit on main
+        # the row list goes up on an otherwise idle stream (not behind the audit on main or the Gram)
+        with S.use(self.upload_stream):
+            sp = self.crypto.shares_async(pre["qdelta"], [w - self.lo for w in spec_workers], side,
+                                          group_rows=SPEC_GROUP_ROWS)
+        self._spec_next = {"hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
+                           "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
+                           "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}
+
+    def _early_vrf_submit(self, block_hash) -> None:
+        """Start the next round's noiser VRF outputs as soon as the block that seeds them is built, before
+        its audit is read and it is committed, for every peer this rank hosts (its workers are not known
+        yet).  The next head adopts the job when the committed block has this hash (it does unless the
+        audit fails) and the keys match (a churn restart draws new ones)."""
+        cfg = self.cfg
+        # (getRoles draws every peer's noisers whether or not noise is added: main.go:507)
+        if not (self._pipelined() and cfg.num_noisers > 0 and self.local):
+            return
+        peers = list(self.local)
+        seeds = [self.vrf_noise_seed[p] for p in peers]
+        job = self.R.vrf_prove_batch_async(seeds, bytes(block_hash), max(1, cfg.host_threads - 1), None,
+                                           self.vrf_dev is not None)
+        self.stats["vrf_outputs"] += len(seeds)
+        self._early_vrf = {"hash": bytes(block_hash), "job": job, "seeds": seeds,
+                           "pos": {p: i for i, p in enumerate(peers)}}
+
+    # ------------------------------------------------------------------ commitments
+    def _local_commit_rows(self, pending_commits, local_workers: list, row_of: dict) -> torch.Tensor:
+        """Device commitment rows of the local workers in local_workers order.  The commitments are
+        computed per row of qdelta (row_of: one row per local worker, or one per local peer when the
+        pre-step computed them for every local peer)."""
+        rows = self.crypto.commit_rows_tensor(pending_commits).to(self.dev)
+        idx = [row_of[w] for w in local_workers]
+        if idx == list(range(rows.shape[0])):
+            return rows
+        return rows.index_select(0, h2d(idx, torch.long, self.dev))
+
+    def _local_commit_buf(self, head: dict) -> torch.Tensor:
+        """[maxlocal, point width] buffer whose row (w - lo) holds local worker w's commitment (the
+        flat-layout part of a gather)."""
+        cr, lw = self.crypto, head["local_workers"]
+        part = torch.zeros((self.maxlocal, cr.point_width), dtype=cr.point_dtype, device=self.dev)
+        if lw:
+            part.index_copy_(0, h2d([w - self.lo for w in lw], torch.long, self.dev),
+                             self._local_commit_rows(head["pending_commits"], lw, head["row_of"]))
+        return part

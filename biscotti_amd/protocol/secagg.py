@@ -1,0 +1,396 @@
+"""Secure aggregation and block building: share routing, the miners' sums, exact recovery, the aggregate
+audit and the leader's block.
+
+Reference: RegisterSecret / processShare (main.go:256-367), aggregateSecret (kyber.go:244-287), the
+leader's node-list intersection and share gather (main.go:2046-2189,2237-2324), recoverSecret
+(kyber.go:809-857) and createBlockSecAgg (honest.go:391-440); the plain path is RegisterUpdate +
+createBlock (main.go:375-390, honest.go:346-388).
+
+Share sums are additive, so each rank sums its own workers' share columns for all miners at once and
+ONE all_gather (the reduce-scatter to the miners fused with the leader's gather) hands
+every rank the per-rank partials; every rank then recovers the aggregate itself (exact integer
+recovery on identical inputs), so all ranks build the leader's block bit for bit.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import bn256 as B
+from ..ops import ml as K
+from ..utils import d2h_into, h2d
+from ..utils import streams as S
+
+
+class SecAggMixin:
+    # ------------------------------------------------------------------ off-critical-path work
+    def _background(self, fn, *inputs):
+        """Run `fn` on the background stream behind everything queued so far on the main stream.
+        Nothing on the round's critical path reads the result: its inputs and outputs are
+        stream-ordered on the background stream, so the main stream never waits for it (it overlaps
+        the next round's head).  Without a GPU it runs inline."""
+        if not self.gpu:
+            return fn()
+        main = S.current()
+        bg = self.bg_stream
+        S.wait(bg, main)
+        with S.use(bg):
+            out = fn()
+        S.hold(*[t for t in inputs if isinstance(t, torch.Tensor)])
+        return out
+
+    # ------------------------------------------------------------------ device-side aggregation
+    def _predict_miners(self, plan, live):
+        """(contributing miners, share part of each) exactly as leader_view / route_shares report them
+        whenever at least one update is approved: parts follow the live miners in address order
+        (route_shares), the leader comes first and then plan.miners order (leader_view)."""
+        if not live[plan.leader]:
+            return None
+        addr = self.fsm.addresses
+        part, k = {}, 0
+        for m in sorted(plan.miners, key=lambda m_: addr[m_]):
+            if live[m]:
+                part[m] = k
+                k += 1
+        contributing = [plan.leader] + [m for m in plan.miners if m != plan.leader and live[m]]
+        if self.pc.shares_per_miner * len(contributing) < self.cfg.poly_size:
+            return None   # too few live miners for a quorum (leader_view): the round's block is empty
+        return contributing, part
+
+    def _spec_aggregate(self, spec, pred, node) -> dict:
+        """Queue the secure aggregation of the rows the committee's selection kept -- masked share-value
+        sums, the cross-rank combination, exact recovery (main stream), the audit's commitment sums +
+        check (side stream), the witness sums (background stream) -- right behind the selection
+        kernels, before the host has read the selection.  Every rank queues it at the same point (the
+        selection is replicated), so its collective lines up.  The host later adopts it if the
+        approvals, miners and parts match (_secure_aggregation).  node: device int32 mask over the
+        Krum rows (the leader's block)."""
+        contributing, part = pred
+        sp = spec[1] if spec is not None else None
+        pts = ys = alive = None
+        if sp is not None:
+            sp.launch()
+            pts, ys, alive = sp.pts, sp.ys, sp.alive
+            S.current().wait_event(sp.ev)          # the MSM's shares
+        agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration))
+        agg["contributing"], agg["part"], agg["accepted"], agg["node"] = list(contributing), dict(part), None, node
+        return agg
+
+    def _agg_index(self, contributing, part):
+        """Resident index tensors of one miner layout (a handful recur: the parts are a permutation of
+        0..M-1): chunk-commitment columns, witness columns, the contributing miners' share columns and
+        their x-points, uploaded once."""
+        # the indices depend only on the sequence of parts (which miner holds which share slice), not
+        # on the miners' ids: M! layouts (6 for three miners) cover every round
+        key = tuple(part[m] for m in contributing)
+        hit = self._agg_idx.get(key)
+        if hit is None:
+            spm, T, nch = self.pc.shares_per_miner, self.T, self.nchunks
+            base = np.arange(nch) * (T + 1)
+            ycols = np.concatenate([spm * part[m] + np.arange(spm) for m in contributing])
+            wc = np.concatenate([(base[:, None] + spm * part[m] + np.arange(spm)[None, :]).reshape(-1)
+                                 for m in contributing])
+            assert wc.max() < nch * (T + 1) and ycols.max() < T
+            wts = K.recovery_weights((ycols - 10).tolist(), self.cfg.poly_size)
+            parts = [base + T, wc, ycols, ycols - 10, np.asarray(wts["basis"])]
+            idx = h2d(np.concatenate(parts).astype(np.int32), torch.int32, self.dev)
+            offs = np.cumsum([0] + [len(x) for x in parts])
+            A_dev = h2d(wts["A"].reshape(-1), torch.int64, self.dev)
+            sl = [idx[offs[i]:offs[i + 1]] for i in range(5)]
+            hit = (sl[:4], (ycols - 10).tolist(), (wts, A_dev, sl[4]))
+            if len(self._agg_idx) < 256:
+                self._agg_idx[key] = hit
+        return hit
+
+    def _aggregate(self, pts, ys, rowsel, contributing, part, now) -> dict:
+        """Secure aggregation of this rank's kept rows, combined over ranks, then exact recovery.
+
+        Every miner sums the shares it received (aggregateSecret, kyber.go:244-287) and the leader
+        recovers from the miners' sums (kyber.go:809-857).  Each rank sums its own workers' share
+        columns (one kernel) and ONE all_gather hands every rank all partials; the fused recovery kernel
+        adds them up.  The chunk-commitment sums (identical for every miner: same node list) travel in
+        the same buffer for the audit; the witness sums, which no consumer on the protocol path reads,
+        stay per-rank partials on the background stream (the KZG audit reads them when on).
+
+        pts [R, nch, T+1, pw] / ys [R, nch, T] (None: no local rows); rowsel: device int32 mask [R]
+        or a host list of row indices.  Returns the handles _finish_secagg consumes."""
+        cfg, comm = self.cfg, self.comm
+        T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
+        audit = cfg.audit_aggregate
+        kzg = cfg.kzg_audit != "off"
+        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
+        kzg_in = None   # this rank's (commitment sums, witness sums, share sums) for the KZG audit
+        main = S.current() if self.gpu else None
+        single = comm.world == 1
+        ys_part = None   # this rank's share sums (several ranks / host path); one rank fuses them below
+        ys_fused = mask_fused = None   # one rank, GPU: the share sums are fused into the recovery kernel
+        cs_part = None
+        if pts is not None and (not isinstance(rowsel, list) or rowsel):
+            flat = pts.view(pts.shape[0], nch * (T + 1), pw)
+            if self.gpu:
+                rows_t = None if not isinstance(rowsel, list) else h2d(rowsel, torch.int32, self.dev)
+                mask = rowsel if rows_t is None else None
+                if single:
+                    ys_fused = ys
+                    if mask is not None:
+                        mask_fused = mask
+                    else:
+                        sel = np.zeros(ys.shape[0], np.int32)
+                        sel[np.asarray(rowsel)] = 1
+                        mask_fused = h2d(sel, torch.int32, self.dev)
+                else:
+                    ys_part = K.sum_rows_i64(ys, rows=rows_t, mask=mask)   # [nch, T], one kernel
+                if audit or kzg:
+                    # the commitment sums on the side stream (the MSM's stream, now done with these rows)
+                    st = self.side_stream
+                    S.wait(st, main)
+                    with S.use(st):
+                        cs_part = B.sum_rows(flat, rows_t, ccols, check=False, row_mask=mask)
+                    S.hold(pts, ccols, mask if mask is not None else rows_t)
+                # the miners' witness sums: no consumer on the protocol path (background stream); the KZG
+                # audit, when on, reads them from there
+                ws_part = self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
+                                           flat, wcols, mask if mask is not None else rows_t)
+                if kzg:
+                    kzg_in = (cs_part, ws_part, None if single else ys_part.index_select(1, ycols_t.long()))
+            else:
+                rows_l = list(rowsel)
+                ys_part = ys[rows_l].sum(0)
+                if audit or kzg:
+                    cs_part = self.crypto.sum_rows(flat[rows_l][:, ccols.long()])
+                if kzg:
+                    kzg_in = (cs_part, self.crypto.sum_rows(flat[rows_l][:, wcols.long()]),
+                              ys_part.index_select(1, ycols_t.long()))
+        if ys_part is None and ys_fused is None:   # no local rows: nothing to add
+            ys_part = torch.zeros((nch, T), dtype=torch.int64, device=self.dev)
+        if audit and cs_part is None:   # no local rows: the neutral element (point at infinity)
+            cs_part = torch.zeros((nch, pw), dtype=pdt, device=self.dev)
+        # ---- combine over ranks: ONE all_gather (share sums, commitment sums, clock)
+        clock = None
+        ys_src = None
+        if comm.world > 1:
+            if self.gpu and audit:
+                S.wait(main, self.side_stream)   # the commitment sums travel in the gather
+            parts = [ys_part.reshape(1, -1), torch.full((1, 1), now, dtype=torch.int64, device=self.dev)]
+            if audit:
+                parts.append(cs_part.reshape(1, -1))
+            got = comm.all_gather_packed(parts)
+            ys_src = got[0].view(comm.world, nch, T)      # the recovery kernel sums the ranks' partials
+            clock = got[1].reshape(comm.world)
+            if audit:
+                cs_all = got[2].view(comm.world, nch, pw)
+                cs_tot = B.sum_rows(cs_all.contiguous(), None, None, check=False) if self.gpu else \
+                    self.crypto.sum_rows(cs_all)
+        else:
+            ys_src = ys_part.reshape(1, nch, T) if ys_part is not None else None
+            cs_tot = cs_part
+        if self.gpu:
+            src = ys_fused if ys_fused is not None else ys_src
+            W_new, coeffs, status, agg = K.recover_rows(src.contiguous(), mask_fused if ys_fused is not None else None,
+                                                        ycols_t, xs_t, wts, A_dev, basis_dev, cfg.poly_size, self.d,
+                                                        self.W, 10.0 ** cfg.precision)
+        else:
+            agg = ys_src.sum(0).index_select(1, ycols_t.long()).contiguous()   # [nch, npts]
+            W_new, coeffs, status = K.recover(agg, xs_t.cpu(), cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
+        # the recovered model (and the clocks) are read back right behind the recovery, AHEAD of the
+        # audit queued next on the same stream: the block is built while the audit still runs
+        readback = self._d2h_async(status, W_new, *((clock,) if clock is not None else ()))
+        if self._pipelined() and getattr(self.task, "stateless_step", False):
+            # every rank recovers the same W_new, so each one queues its own local peers' next step (on the
+            # Gram stream, behind the recovery but not behind the audit queued next on main)
+            self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)   # fsm: the round being aggregated
+        audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
+        out = {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
+               "clock": clock, "now": now, "readback": readback}
+        if kzg_in is not None:
+            # each rank audits its own partial aggregate (verifySecret is linear in (C, W, y)); staged only
+            # once the aggregate is adopted (_finish_secagg), behind the work that produced these sums
+            cs_k, ws_k, y_k = kzg_in
+            out["kzg_in"] = (cs_k, ws_k, agg if y_k is None else y_k, xs_t)
+            if self.gpu:
+                out["kzg_events"] = [S.record(main), S.record(self.side_stream), S.record(self.bg_stream)]
+        return out
+
+    # ------------------------------------------------------------------ read-backs and the audit
+    def _d2h_async(self, *ts: torch.Tensor):
+        """Queue the copies now (on the current stream, behind what produced the tensors and ahead of
+        anything queued later); the returned callable waits for them and gives numpy arrays."""
+        if not self.gpu:
+            out = [t.numpy() for t in ts]
+            return lambda: out
+        hs = []
+        for i, t in enumerate(ts):
+            # persistent pinned buffers per (slot, shape, dtype): a round reads its copies before the next
+            # round queues new ones into the same buffer
+            key = (i, tuple(t.shape), t.dtype)
+            h = self._pinned.get(key)
+            if h is None:
+                h = self._pinned[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            d2h_into(h, t.contiguous())
+            hs.append(h)
+        ev = S.record()
+
+        def wait():
+            ev.synchronize()
+            return [h.numpy() for h in hs]
+        return wait
+
+    def _audit(self, coeffs: torch.Tensor, csum: torch.Tensor):
+        """Queue the aggregate audit (recovered chunks vs the miners' summed chunk commitments); returns a
+        callable giving ok int32 [n_miners, nchunks].  On the GPU the check runs on the main stream (high
+        priority, every CU: the MSM is done by now) while the host builds the block (gob + SHA-256)."""
+        if not self.gpu:
+            ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
+            return lambda: ok
+        main = S.current()
+        S.wait(main, self.side_stream)   # the commitment sums
+        ok = self.crypto.check_aggregate(coeffs, csum)
+        key = ("audit", tuple(ok.shape), ok.dtype)
+        host = self._pinned.get(key)
+        if host is None:
+            host = self._pinned[key] = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
+        d2h_into(host, ok.contiguous())
+        ev = S.record(main)
+
+        def result():
+            ev.synchronize()
+            return host.numpy()
+        return result
+
+    # ------------------------------------------------------------------ secure aggregation path
+    def _secure_aggregation(self, plan, live, approved, qdelta, local_workers, row_of, commit_of,
+                            signatures, spec=None, sa=None):
+        cfg, R, fsm, tm = self.cfg, self.R, self.fsm, self.timer
+        self._last_nodes = []
+        if cfg.verify_signatures and cfg.verification:
+            # miners reject shares without >= nv/2 valid verifier signatures (main.go:269-277, Q5)
+            need = len(plan.verifiers) // 2
+            approved = [w for w in approved
+                        if sum(any(R.schnorr_verify(commit_of[w], self.pk[v], sg) for v in plan.verifiers)
+                               for sg in signatures.get(w, [])) >= need]
+        with tm.phase("shares"):
+            routes = fsm.route_shares(approved)
+            lv = fsm.leader_view(routes)
+        if not (lv.leader_online and lv.quorum):
+            return None
+        node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
+        part_of = {m: dict(routes[m])[node_list[0]] for m in contributing}
+        if sa is not None and sa.get("accepted") is not None and contributing == sa["contributing"] \
+                and part_of == sa["part"] and set(node_list) == sa["accepted"]:
+            # the device already aggregated exactly these workers' shares (queued behind the committee's
+            # selection, before the host knew the approvals): recovery and audit are in flight
+            self.stats["device_aggregations"] = self.stats.get("device_aggregations", 0) + 1
+            with tm.phase("recover"):
+                return self._finish_secagg(plan, node_list, commit_of, sa)
+        # host-decided path (no device selection, RONI, or a prediction mismatch): the leader's block
+        # carries lv.node_list only (its first NUM_SAMPLES/2 arrivals), so only those workers' shares are
+        # computed; every rank takes this branch together (replicated decisions)
+        with tm.phase("shares"):
+            local_used = [w for w in node_list if w in self.local]
+            pts = ys = None
+            rowsel: list = []
+            if local_used:
+                spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
+                if spec is not None and all(w in spec_row for w in local_used):
+                    sp = spec[1]
+                    sp.launch()
+                    pts, ys = sp.pts, sp.ys
+                    if self.gpu:
+                        S.current().wait_event(sp.ev)
+                    rowsel = [spec_row[w] for w in local_used]   # rows of the speculative tensors
+                else:
+                    sel = h2d([row_of[w] for w in local_used], torch.long, self.dev)
+                    pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
+                    rowsel = list(range(len(local_used)))
+        with tm.phase("recover"):
+            agg = self._aggregate(pts, ys, rowsel, contributing, part_of, self._now(plan.iteration))
+            return self._finish_secagg(plan, node_list, commit_of, agg)
+
+    def _finish_secagg(self, plan, node_list, commit_of, h):
+        """Read back the recovered model (and the ranks' clocks), fall back to least squares for
+        inconsistent chunks, build the block, then check the aggregate audit (running on the device
+        meanwhile)."""
+        cfg, R, fsm, tm = self.cfg, self.R, self.fsm, self.timer
+        W_new, status, agg, xs, audit_ok = h["W_new"], h["status"], h["agg"], h["xs"], h["audit_ok"]
+        with tm.phase("recover.readback"):
+            got = h["readback"]()
+            st, W_np = got[0], got[1]
+            if h["clock"] is not None:
+                now = int(got[2][self.comm.owner(plan.leader, self.N)])   # the leader's clock stamps the block
+            else:
+                now = h["now"]
+        if not st.all():  # inconsistent shares: the reference's float64 least squares
+            aggn, Wn = agg.cpu().numpy(), self.W.cpu().numpy()
+            for k in np.nonzero(st == 0)[0]:
+                c = R.recover_lstsq(xs, [int(v) for v in aggn[k]], cfg.poly_size - 1)
+                for j, v in enumerate(c):
+                    i = k * cfg.poly_size + j
+                    if i < self.d:
+                        W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
+            self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
+        with tm.phase("recover.block"):
+            block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
+            self._early_vrf_submit(block.hash)
+        self._W_next = W_new if st.all() and self.gpu else None
+        if self._W_next is not None:
+            self._spec_head_launch(block)
+        if audit_ok is not None:
+            if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
+                self._idle_work()
+                self._idle_work = None
+            if self.gpu and (self._pre_vrf_work or self._evals):
+                # the next round's VRF batch has just started (_early_vrf_submit): this round's deferred
+                # signature prep (its batch starts behind those outputs) and the earlier rounds' evaluation
+                # read-backs fill the audit wait instead of the next round's VRF wait
+                with tm.phase("recover.idle"):
+                    ej = self._early_vrf["job"] if self._early_vrf is not None else None
+                    work, self._pre_vrf_work = self._pre_vrf_work, []
+                    for f in work:
+                        f(ej)
+                    self._resolve_evals()
+            with tm.phase("recover.audit"):
+                ok = audit_ok()
+            if not ok.all():
+                # a miner's sums do not commit to the recovered update: refuse it (the round ends like the
+                # reference's missing-quorum path, with an empty block)
+                self.stats["audit_failures"] += 1
+                self.log.info("aggregate audit failed for %d (miner, chunk) pairs in iteration %d: empty block",
+                              int((ok == 0).sum()), plan.iteration)
+                return None
+        self._last_nodes = node_list
+        if cfg.kzg_audit != "off":
+            self._kzg_adopt(h, plan.iteration)   # only aggregates that end in the chain are audited
+            if self._kzg_pending:
+                self._kzg_poll()
+        return block
+
+    # ------------------------------------------------------------------ plain aggregation path
+    def _plain_aggregation(self, plan, live, approved, delta_w, noised, local_workers, commit_of, signatures,
+                           gathered=(None, None, None)):
+        """RegisterUpdate path (-sa=false): the leader miner's block carries every routed update in full.
+        delta_w / noised: the local workers' rows in local_workers order.  With several ranks the deltas,
+        noised deltas and clocks already travelled in the verification all_gather, so every rank builds
+        the leader's block itself (no broadcast)."""
+        fsm, comm, tm = self.fsm, self.comm, self.timer
+        self._last_nodes = []
+        with tm.phase("aggregate"):
+            routes = fsm.route_updates(approved)
+            leader = plan.leader
+            if not live[leader] or not routes.get(leader):
+                return None
+            ups = list(routes[leader])
+            now = self._now(plan.iteration)
+            if comm.world == 1:
+                idx = {w: i for i, w in enumerate(local_workers)}
+                sel = h2d([idx[w] for w in ups], torch.long, self.dev)
+                dsrc, nsrc = delta_w, noised
+            else:
+                dsrc, nsrc, ts = gathered
+                sel = h2d([self.flat[w] for w in ups], torch.long, self.dev)
+                now = int(ts[comm.owner(leader, self.N)])
+            dv = dsrc.index_select(0, sel).double().cpu().numpy()
+            nv = nsrc.index_select(0, sel).double().cpu().numpy()
+            blk = fsm.make_plain_block_arrays(self.W.cpu().numpy(), ups, dv, nv, [commit_of[w] for w in ups],
+                                              [signatures.get(w, []) for w in ups], now)
+            self._last_nodes = ups
+            return blk

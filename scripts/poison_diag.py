@@ -25,14 +25,14 @@ CONFIGS = {
     "mnist100_clean_ep1": dict(num_nodes=100, epsilon=1.0),
     "mnist100_po30_ep1": dict(num_nodes=100, poisoning=0.3, epsilon=1.0),
     "mnist100_po30_ep1_5v": dict(num_nodes=100, poisoning=0.3, epsilon=1.0, num_verifiers=5),
-    "mnist100_po30_ep1_shared": dict(num_nodes=100, poisoning=0.3, epsilon=1.0, shared_inbox=True, miner_cap=False),
+    "mnist100_po30_ep1_shared": dict(num_nodes=100, poisoning=0.3, epsilon=1.0, ablation="shared_inbox,no_miner_cap"),
     "mnist200_po30_ep1": dict(num_nodes=200, poisoning=0.3, epsilon=1.0),
     "mnist50_po30_ep1": dict(num_nodes=50, poisoning=0.3, epsilon=1.0),
     "mnist50_po30_ep1_5v": dict(num_nodes=50, poisoning=0.3, epsilon=1.0, num_verifiers=5),
     "mnist50_po50_ep1_5v": dict(num_nodes=50, poisoning=0.5, epsilon=1.0, num_verifiers=5),
     "mnist100_po30_nonoise": dict(num_nodes=100, poisoning=0.3, noising=False),
-    "mnist100_po30_ep1_indepnoise": dict(num_nodes=100, poisoning=0.3, epsilon=1.0, noise_independent=True),
-    "mnist50_po30_ep1_indepnoise": dict(num_nodes=50, poisoning=0.3, epsilon=1.0, noise_independent=True),
+    "mnist100_po30_ep1_indepnoise": dict(num_nodes=100, poisoning=0.3, epsilon=1.0, ablation="noise_independent"),
+    "mnist50_po30_ep1_indepnoise": dict(num_nodes=50, poisoning=0.3, epsilon=1.0, ablation="noise_independent"),
     # creditcard label flip, 50 peers (nsdi-eval/credit)
     "credit50_clean": dict(num_nodes=50, dataset="creditcard"),
     "credit50_po30_3v": dict(num_nodes=50, dataset="creditcard", poisoning=0.3),

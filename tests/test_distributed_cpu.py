@@ -57,10 +57,15 @@ def _worker(rank, world, port, kw, rounds, q):
         r = eng.run_round()
         per_round.append((len(calls) - n0, len(reads) - r0, r.empty))
     if count:
-        # every non-empty secure round: the verification gather + the aggregation gather, and one
-        # batched read-back of the recovered model (+ clocks); nothing else crosses ranks
-        assert all(c == 2 and rd <= 2 for c, rd, empty in per_round if not empty), per_round
+        # every non-empty secure round after the first (whose head is opened inside it): the noise-aware
+        # Gram's delta gather (the next round's head), the gather of commitments + noiser ids after the
+        # VRF outputs and the aggregation gather -- 2 without the noise-aware Krum -- and one batched
+        # read-back of the recovered model (+ clocks); nothing else crosses ranks
+        want = 3 if eng._noise_krum() else 2
+        assert all(c == want and rd <= 2 for c, rd, empty in per_round[1:] if not empty), (want, per_round)
         assert any(not empty for *_, empty in per_round)
+        # each rank computes the VRF outputs of the peers it hosts only (heads of rounds + 1)
+        assert eng.stats["vrf_outputs"] <= (rounds + 1) * len(eng.local), (eng.stats["vrf_outputs"], len(eng.local))
     q.put((rank, [bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))]))
     comm.barrier()
     comm.shutdown()
@@ -116,15 +121,27 @@ def test_three_ranks_uneven_packing():
     assert multi[0] == single
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_collectives_per_round(world):
-    """A secure-aggregation round with Multi-Krum issues exactly two collectives of any kind on
-    2-4 ranks (the verification all_gather and the aggregation all_gather) and at most two batched
-    read-backs: no accept-mask, share, signature or block traffic (every rank replicates the
-    committee and the recovery)."""
-    kw = dict(KW, num_nodes=9, seed=3)
+@pytest.mark.parametrize("world,noising", [(2, True), (4, True), (8, True), (3, False)])
+def test_collectives_per_round(world, noising):
+    """A secure-aggregation round with Multi-Krum issues a fixed number of collectives of any kind on 2-8
+    ranks (3 with the noise-aware Krum: delta gather, commitments + noiser ids, aggregation; 2 without)
+    and at most two batched read-backs: no accept-mask, share, signature or block traffic (every rank
+    replicates the committee and the recovery).  Every rank proves only its own peers' VRF outputs, and
+    all ranks hold the single-process chain."""
+    kw = dict(KW, num_nodes=9, seed=3, noising=noising)
+    single = _run(1, kw, 3)[0]
     out = _run(world, dict(kw, _count_collectives=True), 3)
-    assert all(out[r] == out[0] for r in range(world))
+    assert all(out[r] == single for r in range(world))
+
+
+def test_mnist_noise_aware_krum_ranks_match_single_process():
+    """MNIST with the noise-aware committee Krum (Gram over [deltas; noise vectors] on the flat peer layout,
+    noiser ids gathered): 1 rank and 3 ranks give the same chain, poisoners included."""
+    kw = dict(num_nodes=8, dataset="mnist", num_verifiers=2, num_miners=2, num_noisers=2, epsilon=1.0,
+              device="cpu", seed=4, deterministic_time=True, poisoning=0.25)
+    single = _run(1, kw, 3)[0]
+    multi = _run(3, kw, 3)
+    assert multi[0] == multi[1] == multi[2] == single
 
 
 def test_peer_processes_localtest_oracle():

@@ -78,7 +78,7 @@ def test_poisoners_on_gpu():
     assert all(set(r.node_list) <= set(r.approved) for r in res)
 
 
-@pytest.mark.parametrize("nv,extra", [(3, {"noise_independent": True}), (5, {"noise_independent": True}),
+@pytest.mark.parametrize("nv,extra", [(3, {"ablation": "noise_independent"}), (5, {"ablation": "noise_independent"}),
                                       (3, {"noising": False})])
 def test_krum_rejects_label_flip_poisoners(nv, extra):
     """30% 1->7 label-flip poisoners, every verifier with its own inbox: after a 10-round burn-in at

@@ -200,9 +200,8 @@ def test_recover_rows_fused_weights(cols):
     assert st2.cpu()[7] == 0 and st2.cpu().sum() == nch - 1
 
 
-@pytest.mark.parametrize("early,spec_msm,pre_step", [(False, True, True), (True, True, True), (False, False, True),
-                                                   (False, True, False)])
-def test_engine_rounds_on_gpu(early, spec_msm, pre_step):
+@pytest.mark.parametrize("ablation", ["", "no_pipeline"])
+def test_engine_rounds_on_gpu(ablation):
     """Whole GPU round pipeline (speculative shares on the CU-masked stream, async commitments,
     pipelined round heads): each block's model is EXACTLY the old model plus the sum of the
     included workers' quantised updates, recomputed independently through the Philox step."""
@@ -210,8 +209,8 @@ def test_engine_rounds_on_gpu(early, spec_msm, pre_step):
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
-    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, early_krum=early, spec_msm=spec_msm,
-                    pre_step=pre_step)
+    cfg = RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, ablation=ablation)
+    pre_step = not ablation
     eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
     res = []
     for _ in range(5):
@@ -250,7 +249,7 @@ def test_pre_gram_and_early_vrf_keep_the_chain():
     chains, stats = [], []
     for on in (True, False):
         cfg = RunConfig(num_nodes=20, dataset="mnist", seed=4, max_iterations=100, deterministic_time=True,
-                        poisoning=0.3, epsilon=1.0, pre_gram=on, early_vrf=on, spec_head=on)
+                        poisoning=0.3, epsilon=1.0, ablation="" if on else "no_pipeline")
         eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
         for _ in range(6):
             eng.run_round()

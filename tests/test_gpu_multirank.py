@@ -80,11 +80,16 @@ def test_gpu_two_ranks_match_single_process(secure_agg):
     assert multi[0] == single
 
 
-def test_gpu_four_ranks_poisoning_and_churn_match_single_process():
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_gpu_four_ranks_poisoning_and_churn_match_single_process(backend):
+    """4 ranks with poisoners and churn, over gloo and over RCCL (socket transport between the ranks
+    sharing cuda:0): every device-side multi-rank path -- the pre-step's delta gather and noise-aware
+    Gram, the commitments + noiser-ids gather, the per-rank share sums and their gather, the replicated
+    recovery -- must give the single-process chain byte for byte."""
     kw = dict(num_nodes=16, dataset="mnist", seed=9, deterministic_time=True, max_iterations=100, poisoning=0.3,
               churn=0.1, num_verifiers=3)
     single = _run(1, kw, 4)[0]
-    multi = _run(4, kw, 4)
+    multi = _run(4, kw, 4, backend=backend)
     assert multi[0] == multi[1] == multi[2] == multi[3]
     assert multi[0] == single
 

@@ -205,3 +205,28 @@ def test_successor_gives_the_next_plan_before_commit():
         fsm.iteration = saved   # undo the probe's begin_round
         assert got == want
     eng.close()
+
+
+def test_cli_defaults_match_runconfig():
+    """The reference + framework flags with an empty argv give RunConfig() exactly (no knob whose CLI
+    default silently differs from the config default, e.g. a store_false flag turning phase sync on);
+    --fail-at/--fail-rank and --no-roles-vrf-proof map onto fail_at / ablation."""
+    import argparse
+
+    from biscotti_amd.protocol.config import RunConfig, add_framework_flags, add_reference_flags, config_from_args
+
+    ap = argparse.ArgumentParser()
+    add_reference_flags(ap)
+    add_framework_flags(ap)
+    assert config_from_args(ap.parse_args([])) == RunConfig()
+    cfg = config_from_args(ap.parse_args(["--fail-at", "2", "--fail-rank", "1", "--no-roles-vrf-proof",
+                                          "--phase-sync"]))
+    assert cfg.fail_point() == (2, 1) and not cfg.roles_vrf_proof and cfg.phase_sync
+    assert RunConfig().fail_point() == (-1, 0)
+    import dataclasses
+
+    assert len(dataclasses.fields(RunConfig)) < 50
+    import pytest
+
+    with pytest.raises(ValueError):
+        RunConfig(ablation="early_krum").validate()
