@@ -448,7 +448,7 @@ extern "C" __global__ void __launch_bounds__(128) k_krum_accept(const double* sc
 //                        reduced) Gram, rank-select of the groupsize-2 nearest neighbours, score
 //   KC3 k_krum_vote      one block: per-verifier selection of the n_accept lowest scores, signature
 //                        count per worker row, approval (>= need), leader cap by arrival rank
-// Limits: U <= 1024 rows, inbox n <= 256, verifiers V <= 64 (checked by the launcher).
+// Limits: U <= 1024 rows, inbox n <= 256 on this path; larger committees take the *_big kernels below.
 // =====================================================================================
 namespace {
 __device__ __forceinline__ int pair_index(int ti, int tj, int T) {
@@ -678,6 +678,209 @@ extern "C" __global__ void __launch_bounds__(1024) k_krum_vote(const double* sco
     }
     node[w] = keep;
   }
+}
+
+// ---- large committees (an inbox of more than 256 updates, or more than 1024 candidate rows): the
+// reference's Krum has no size limit (client_obj.py:114-143).  A row's distances are sorted in LDS
+// (bitonic) and its score is the sum of the sorted values at positions 1 .. groupsize-2 -- the same
+// multiset as k_krum_rows' rank select (ties cannot change it); the vote counts signatures in a global
+// workspace and the leader cap runs one thread per candidate row.  Limits: U <= 8192, n <= 4096.
+namespace {
+__device__ void bitonic_sort_lds(double* a, int npow2) {
+  for (int k = 2; k <= npow2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < npow2; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const double x = a[i], y = a[ixj];
+          if ((x > y) == up) {
+            a[i] = y;
+            a[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+}  // namespace
+
+template <bool NOISE>
+__global__ void __launch_bounds__(1024) k_krum_rows_big(const double* gram, int T, int U1, const int* nz,
+                                                        const float* sc, int nn, const int* inbox, int n, int npow2,
+                                                        int groupsize, double* scores) {
+  extern __shared__ double row[];   // [npow2]
+  __shared__ double xaa;
+  const int i = blockIdx.x, v = blockIdx.y;
+  const int* box = inbox + (size_t)v * n;
+  const int a = box[i];
+  if (threadIdx.x == 0) xaa = NOISE ? xx_dot(gram, T, U1, nz, sc, nn, a, a) : gram_at(gram, T, a, a);
+  __syncthreads();
+  for (int t = threadIdx.x; t < npow2; t += blockDim.x) {
+    double val = __builtin_huge_val();
+    if (t < n) {
+      const int b = box[t];
+      val = NOISE ? xaa + xx_dot(gram, T, U1, nz, sc, nn, b, b) - 2.0 * xx_dot(gram, T, U1, nz, sc, nn, a, b)
+                  : xaa + gram_at(gram, T, b, b) - 2.0 * gram_at(gram, T, a, b);
+    }
+    row[t] = val;
+  }
+  __syncthreads();
+  bitonic_sort_lds(row, npow2);
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    const int hi = min(groupsize - 1, n);
+    for (int j = 1; j < hi; ++j) s += row[j];
+    scores[(size_t)v * n + i] = s;
+  }
+}
+
+// per-verifier selection (one block per verifier): the n_accept lowest scores, index tie-break; the
+// signatures each candidate row collects go to `sigs` (zeroed by the launcher)
+extern "C" __global__ void __launch_bounds__(1024) k_krum_select_big(const double* scores, const int* inbox, int n,
+                                                                    int n_accept, int* acc, int* sigs) {
+  extern __shared__ double sv[];   // [n]
+  const int v = blockIdx.x;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) sv[e] = scores[(size_t)v * n + e];
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double s = sv[i];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += (sv[j] < s) || (sv[j] == s && j < i);
+    const int ok = rank < n_accept ? 1 : 0;
+    acc[(size_t)v * n + i] = ok;
+    if (ok) atomicAdd(&sigs[inbox[(size_t)v * n + i]], 1);
+  }
+}
+
+// approval (>= need signatures, submitted) and the leader's cap: the first `cap` approved rows in
+// leader arrival order (cap <= 0: all); one thread per candidate row
+extern "C" __global__ void __launch_bounds__(256) k_krum_cap_big(const int* sigs, const int* lead_rank, int U,
+                                                                int need, int cap, int* node) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= U) return;
+  const int lr = lead_rank[w];
+  int keep = (lr >= 0 && sigs[w] >= need) ? 1 : 0;
+  if (keep && cap > 0) {
+    int before = 0;
+    for (int x = 0; x < U; ++x) before += (lead_rank[x] >= 0 && sigs[x] >= need && lead_rank[x] < lr) ? 1 : 0;
+    keep = before < cap;
+  }
+  node[w] = keep;
+}
+
+namespace {
+int krum_vote_any(hipStream_t s, const double* scores, const int* inbox, int V, int n, int n_accept, int U, int need,
+                  const int* lead_rank, int cap, int* acc, int* node, int* ws) {
+  if (U <= 1024 && n <= 256) {
+    hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U, need, lead_rank,
+                       cap, acc, node);
+  } else {
+    if (ws == nullptr) return -1;
+    hipMemsetAsync(ws, 0, (size_t)U * sizeof(int), s);
+    hipLaunchKernelGGL(k_krum_select_big, dim3(V), dim3(1024), (size_t)n * sizeof(double), s, scores, inbox, n,
+                       n_accept, acc, ws);
+    hipLaunchKernelGGL(k_krum_cap_big, dim3((U + 255) / 256), dim3(256), 0, s, (const int*)ws, lead_rank, U, need, cap,
+                       node);
+  }
+  return 0;
+}
+int pow2_at_least(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+}  // namespace
+
+// =====================================================================================
+// LSH sieve (ML/code/logistic_aggregator.py:7-29, the third poisoning defence next to Krum and RONI):
+// every update's weight is 1 / #(its near neighbours within squared distance thr among the
+// (centred) updates), so a cluster of sybil updates shares the weight of one.  The reference asks a
+// FALCONN index (random-projection LSH) for the neighbours; here:
+//   LS1 k_lsh_codes    L tables x K sign bits of <x_i - mu, r> per row (one block per row)
+//   LS2 k_lsh_count    neighbour count of each listed row: candidates share a bucket in some table
+//                      (L = 0: every pair, the exact query), confirmed on the f64 Gram (KC1 tiles;
+//                      centring cancels in differences)
+//   LS3 k_weighted_rows  out = sum_i w_i x_i in fp64
+// =====================================================================================
+extern "C" __global__ void __launch_bounds__(256) k_lsh_codes(const float* X, const float* mu, int n, int D,
+                                                             const float* planes, int L, int K,
+                                                             unsigned int* codes) {
+  __shared__ float red[4][64];
+  const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int P = L * K;   // <= 64 planes
+  float acc[64];
+#pragma unroll
+  for (int q = 0; q < 64; ++q) acc[q] = 0.f;
+  for (int k = t; k < D; k += 256) {
+    const float v = X[(size_t)i * D + k] - mu[k];
+#pragma unroll
+    for (int q = 0; q < 64; ++q)
+      if (q < P) acc[q] += v * planes[(size_t)q * D + k];
+  }
+#pragma unroll
+  for (int q = 0; q < 64; ++q) {
+    float v = acc[q];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wid][q] = v;
+  }
+  __syncthreads();
+  if (t < L) {
+    unsigned int c = 0;
+    for (int b = 0; b < K; ++b) {
+      const int q = t * K + b;
+      const float v = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
+      c |= (v > 0.f ? 1u : 0u) << b;
+    }
+    codes[(size_t)i * L + t] = c;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_lsh_count(const double* gram, int T, const unsigned int* codes,
+                                                             int L, const int* rows, int m, double thr, int* counts) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= m) return;
+  const int i = rows[a];
+  const double gii = gram_at(gram, T, i, i);
+  int c = 0;
+  for (int b = 0; b < m; ++b) {
+    const int j = rows[b];
+    bool cand = L == 0 || j == i;
+    for (int tb = 0; tb < L && !cand; ++tb) cand = codes[(size_t)i * L + tb] == codes[(size_t)j * L + tb];
+    if (!cand) continue;
+    const double d2 = gii + gram_at(gram, T, j, j) - 2.0 * gram_at(gram, T, i, j);
+    c += (j == i || d2 < thr) ? 1 : 0;
+  }
+  counts[a] = c;
+}
+
+extern "C" __global__ void k_weighted_rows(const float* X, int n, int D, const double* w, double* out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= D) return;
+  double acc = 0.0;
+  for (int i = 0; i < n; ++i) acc += w[i] * (double)X[(size_t)i * D + k];
+  out[k] = acc;
+}
+
+extern "C" int bsc_lsh_codes(const float* X, const float* mu, int n, int D, const float* planes, int L, int K,
+                             unsigned int* codes, void* stream) {
+  if (n <= 0 || L <= 0) return 0;
+  if (L * K > 64 || K > 32 || K <= 0) return -1;
+  hipLaunchKernelGGL(k_lsh_codes, dim3(n), dim3(256), 0, (hipStream_t)stream, X, mu, n, D, planes, L, K, codes);
+  return (int)hipGetLastError();
+}
+extern "C" int bsc_lsh_count(const double* gram, int U, const unsigned int* codes, int L, const int* rows, int m,
+                             double thr, int* counts, void* stream) {
+  if (m <= 0) return 0;
+  const int T = (U + 15) / 16;
+  hipLaunchKernelGGL(k_lsh_count, dim3((m + 255) / 256), dim3(256), 0, (hipStream_t)stream, gram, T, codes, L, rows, m,
+                     thr, counts);
+  return (int)hipGetLastError();
+}
+extern "C" int bsc_weighted_rows(const float* X, int n, int D, const double* w, double* out, void* stream) {
+  if (D <= 0) return 0;
+  hipLaunchKernelGGL(k_weighted_rows, dim3((D + 255) / 256), dim3(256), 0, (hipStream_t)stream, X, n, D, w, out);
+  return (int)hipGetLastError();
 }
 
 // =====================================================================================
@@ -1021,12 +1224,14 @@ extern "C" int bsc_krum(const float* X, int n, int D, int ksplit, double* part, 
 // Committee Multi-Krum: X [U, D] fp32; inbox [V, n] rows of X; lead_rank [U] (-1: not submitted).
 // part: [nsplit, npairs, 256] f64 scratch (npairs = T(T+1)/2, T = ceil(U/16), nsplit = ceil(D/kchunk));
 // scores [V, n] f64; acc [V, n] int32; node [U] int32.
+// Limits: U <= 8192 candidate rows, inbox n <= 4096, V <= 64 verifiers; ws: int32 [U] workspace
+// (used when n > 256 or U > 1024).
 extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, const int* inbox, int V, int n,
                                   int groupsize, int n_accept, int need, const int* lead_rank, int cap, double* part,
-                                  double* gram, unsigned int* count, double* scores, int* acc, int* node,
+                                  double* gram, unsigned int* count, double* scores, int* acc, int* node, int* ws,
                                   void* stream) {
   if (U <= 0 || V <= 0 || n <= 0) return 0;
-  if (U > 1024 || n > 256 || V > 64 || n > U || kchunk <= 0) return -1;
+  if (U > 8192 || n > 4096 || V > 64 || n > U || kchunk <= 0) return -1;
   const int T = (U + 15) / 16;
   const int npairs = T * (T + 1) / 2;
   const int nsplit = (D + kchunk - 1) / kchunk;
@@ -1034,19 +1239,21 @@ extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, cons
   // count: npairs zeroed counters (re-armed by the kernel itself)
   hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part, gram, count,
                      (const float*)nullptr, U, 0ll);
-  hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, gram, T, inbox, n, groupsize, scores);
-  hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U, need, lead_rank, cap,
-                     acc, node);
+  if (n <= 256) {
+    hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, gram, T, inbox, n, groupsize, scores);
+  } else {
+    const int np2 = pow2_at_least(n);
+    hipLaunchKernelGGL(k_krum_rows_big<false>, dim3(n, V), dim3(1024), (size_t)np2 * sizeof(double), s, gram, T, U,
+                       (const int*)nullptr, (const float*)nullptr, 0, inbox, n, np2, groupsize, scores);
+  }
+  if (krum_vote_any(s, scores, inbox, V, n, n_accept, U, need, lead_rank, cap, acc, node, ws) != 0) return -1;
   return (int)hipGetLastError();
 }
-
-// Noise-aware committee Krum, phase 1 (before the noisers are known): Gram of the stacked rows
-// [X (U1 rows, stride D); X2 (U2 rows, stride stride2)] -> gram [npairs][256].
 extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
                                 double* part, double* gram, unsigned int* count, void* stream) {
   const int U = U1 + U2;
   if (U <= 0) return 0;
-  if (U > 1024 || kchunk <= 0) return -1;
+  if (U > 8192 || kchunk <= 0) return -1;
   const int T = (U + 15) / 16;
   const int npairs = T * (T + 1) / 2;
   const int nsplit = (D + kchunk - 1) / kchunk;
@@ -1054,24 +1261,25 @@ extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2,
                      gram, count, X2, U1, stride2);
   return (int)hipGetLastError();
 }
-
-// phase 2 (once the noisers are known): scores of every verifier's inbox from the expanded Gram,
-// then the vote.  nz/sc: [U1][nn] noiser ids (rows U1 + id of the Gram) and scales.
 extern "C" int bsc_krum_committee_noise(const double* gram, int U1, int U, const int* nz, const float* sc, int nn,
                                         const int* inbox, int V, int n, int groupsize, int n_accept, int need,
-                                        const int* lead_rank, int cap, double* scores, int* acc, int* node,
+                                        const int* lead_rank, int cap, double* scores, int* acc, int* node, int* ws,
                                         void* stream) {
   if (U1 <= 0 || V <= 0 || n <= 0) return 0;
-  if (U > 1024 || U1 > 1024 || n > 256 || V > 64 || n > U1 || nn <= 0 || nn > 16) return -1;
+  if (U > 8192 || U1 > 8192 || n > 4096 || V > 64 || n > U1 || nn <= 0 || nn > 16) return -1;
   const int T = (U + 15) / 16;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_krum_rows_noise, dim3(n, V), dim3(256), 0, s, gram, T, U1, nz, sc, nn, inbox, n, groupsize,
-                     scores);
-  hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U1, need, lead_rank, cap,
-                     acc, node);
+  if (n <= 256) {
+    hipLaunchKernelGGL(k_krum_rows_noise, dim3(n, V), dim3(256), 0, s, gram, T, U1, nz, sc, nn, inbox, n, groupsize,
+                       scores);
+  } else {
+    const int np2 = pow2_at_least(n);
+    hipLaunchKernelGGL(k_krum_rows_big<true>, dim3(n, V), dim3(1024), (size_t)np2 * sizeof(double), s, gram, T, U1,
+                       nz, sc, nn, inbox, n, np2, groupsize, scores);
+  }
+  if (krum_vote_any(s, scores, inbox, V, n, n_accept, U1, need, lead_rank, cap, acc, node, ws) != 0) return -1;
   return (int)hipGetLastError();
 }
-
 extern "C" int bsc_eval_error(const float* X, const int* y, int N, int D_IN, int D_OUT, const double* W,
                               int transform, int split, unsigned int* err, void* stream) {
   if (D_OUT > 16 || D_IN <= 0) return -1;

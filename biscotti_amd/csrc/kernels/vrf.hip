@@ -3,20 +3,24 @@
 // worker's noiser VRF (vrf.go:54-100; the lottery reads only the 64-byte output, which the host
 // computes on the critical path).  The host runtime (runtime/vrf.cpp) is the bit-exact oracle.
 //
-// One thread per proof, everything on the device: SHA-512 (try-and-increment hash to curve, nonce,
-// challenge), GF(2^255 - 19) arithmetic, point decompression, x*H and k*H over ONE signed radix-16
-// table of H (the two variable-base multiplications share it), k*B over a resident fixed-base
-// table (64 windows x 8 multiples, uploaded once), one field inversion for the three point
-// encodings, and the scalar arithmetic mod L.
+// Latency, not throughput, is what matters: a round submits ~200 proofs (a few waves on a 1024-SIMD
+// chip) and the last round's proofs must finish before a timed run ends.  A proof's work is therefore
+// split over the three waves of a workgroup (16 proofs per workgroup), wave-uniform roles, LDS hand-off:
+//   phase 1  hash to curve, try-and-increment: 12 counters per proof tried at once (3 waves x 4 lanes);
+//            the smallest counter that decodes wins (the RFC's choice), so one round almost always ends it
+//   phase 2  wave 0: cofactor, the signed radix-16 table of H (global scratch) -> Gamma = x*H
+//            wave 1: cofactor, encode(H) (one inversion), nonce k = SHA512(prefix || H) mod L  -> V = k*H
+//            wave 2: U = k*B over the resident fixed-base table, 4 lanes per proof x 16 windows each
+//   phase 4  wave 0: the three encodings with one inversion, the challenge hash, s = k + c x mod L
+// The critical path is one variable-base multiplication plus two inversions (~3.2k field products)
+// instead of the serial ~6.6k of a thread-per-proof design.  Hot loops are kept rolled so a wave's loop
+// body fits the instruction cache (the unrolled thread-per-proof kernel streamed ~0.5 MB of code).
 //
 // Field elements: 10 unsigned 32-bit limbs in radix 2^25.5 (26, 25, 26, ... bits).  A product is
 // 100 32x32->64 multiply-adds (v_mad_u64_u32) into 64-bit column sums, then one carry chain; the
 // wrap-around 2^255 = 19 is folded into the multiplicands (19 g_j), and the odd-odd products carry
 // an extra factor 2 (2^26 * 2^25 = 2^51 = 2 * 2^50.5...).  Limbs stay non-negative: subtraction adds
 // 4p first.  Bounds: carried limbs are < 2^26 + 2^9, so a column sum is < 2^62.
-//
-// The batch is a whole round's (or several rounds') proofs: ~200-800 threads, a few waves; the
-// kernel runs on a low-priority stream while the protocol's critical path owns the rest of the GPU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -187,6 +191,7 @@ __device__ fe fe_mul(const fe& f, const fe& g) {
 }
 __device__ __forceinline__ fe fe_sq(const fe& a) { return fe_mul(a, a); }
 __device__ fe fe_sqn(fe a, int n) {
+#pragma unroll 1
   for (int i = 0; i < n; ++i) a = fe_sq(a);
   return a;
 }
@@ -359,16 +364,16 @@ __device__ void signed_digits(int8_t e[64], const uint32_t k[8]) {
   e[63] = (int8_t)(e[63] + carry);
 }
 // k * P with P's table (1P..8P, cached) already in `tbl` (global scratch of this thread)
-__device__ ge ge_mul_tbl(const uint32_t* tbl, const uint32_t k[8]) {
+// not inlined: waves 0 and 1 of a workgroup run this one copy (x H and k H) from the instruction cache
+__device__ __attribute__((noinline)) ge ge_mul_tbl(const uint32_t* tbl, const uint32_t k[8]) {
   int8_t e[64];
   signed_digits(e, k);
   ge r = ge_identity();
+#pragma unroll 1
   for (int w = 63; w >= 0; --w) {
     if (w != 63) {
-      r = ge_dbl(r, false);
-      r = ge_dbl(r, false);
-      r = ge_dbl(r, false);
-      r = ge_dbl(r, true);
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j) r = ge_dbl(r, j == 3);
     }
     const int d = e[w];
     if (d > 0) r = ge_add_cached(r, ld_gc(tbl + (d - 1) * 40));
@@ -475,80 +480,217 @@ __device__ void sc_reduce_words(uint32_t out[8], const uint32_t* in, int nbits) 
 
 constexpr uint8_t SUITE = 0x03;
 
+
+
+// r = (256-bit little-endian value given as 8 words) * 2^32 + w, reduced mod L (r < L on entry).
+// L = 2^252 + delta: q = X >> 252 over-estimates floor(X / L) by at most one, so X - q L lies in
+// (-L, L) and one conditional add of L finishes the step.
+__device__ void sc_step(unsigned long long r[4], uint32_t w) {
+  typedef unsigned __int128 u128;
+  unsigned long long x[5];
+  x[0] = (r[0] << 32) | w;
+  x[1] = (r[1] << 32) | (r[0] >> 32);
+  x[2] = (r[2] << 32) | (r[1] >> 32);
+  x[3] = (r[3] << 32) | (r[2] >> 32);
+  x[4] = r[3] >> 32;
+  const unsigned long long q = (x[4] << 4) | (x[3] >> 60);   // X >> 252 (< 2^37)
+  // X - q L, five limbs, two's complement
+  unsigned long long borrow = 0, carry = 0;
+  for (int i = 0; i < 5; ++i) {
+    const u128 m = (u128)q * (i < 4 ? C_L[i] : 0ull) + carry;
+    carry = (unsigned long long)(m >> 64);
+    const unsigned long long lo = (unsigned long long)m;
+    const unsigned long long d = x[i] - lo - borrow;
+    borrow = (x[i] < lo) || (x[i] - lo < borrow);
+    x[i] = d;
+  }
+  if ((long long)x[4] < 0) {   // negative: add L back
+    unsigned long long c = 0;
+    for (int i = 0; i < 4; ++i) {
+      const u128 sum = (u128)x[i] + C_L[i] + c;
+      x[i] = (unsigned long long)sum;
+      c = (unsigned long long)(sum >> 64);
+    }
+  }
+  for (int i = 0; i < 4; ++i) r[i] = x[i];
+}
+// out = (little-endian words in[0..nw)) mod L, most significant word first
+__device__ void sc_reduce_fast(uint32_t out[8], const uint32_t* in, int nw) {
+  unsigned long long r[4] = {0, 0, 0, 0};
+#pragma unroll 1
+  for (int i = nw - 1; i >= 0; --i) sc_step(r, in[i]);
+  for (int i = 0; i < 4; ++i) {
+    out[2 * i] = (uint32_t)r[i];
+    out[2 * i + 1] = (uint32_t)(r[i] >> 32);
+  }
+}
+
+constexpr int VP = 16;     // proofs per workgroup
+constexpr int VTRY = 12;   // hash-to-curve counters tried at once per proof (3 waves x 4 lanes)
+
+__device__ __forceinline__ void st_ge(uint32_t* p, const ge& a) {
+  st_fe(p, a.X); st_fe(p + 10, a.Y); st_fe(p + 20, a.Z); st_fe(p + 30, a.T);
+}
+__device__ __forceinline__ ge ld_ge(const uint32_t* p) { return ge{ld_fe(p), ld_fe(p + 10), ld_fe(p + 20), ld_fe(p + 30)}; }
+__device__ __forceinline__ uint32_t le_word(const uint8_t* d, int i) {
+  return (uint32_t)d[4 * i] | ((uint32_t)d[4 * i + 1] << 8) | ((uint32_t)d[4 * i + 2] << 16) | ((uint32_t)d[4 * i + 3] << 24);
+}
+
 }  // namespace
 
 // keys: [nkeys][24] words = x (clamped secret, 8 LE words), prefix (8), pk encoding (8);
 // key_idx / alpha_idx: [n]; alphas: [nalpha][alpha_len] bytes; btab: [512][32] words;
-// scratch: [n][320] words (the per-thread table of H); pi: [n][80] bytes; beta: [n][64] or null.
-extern "C" __global__ void __launch_bounds__(64) k_vrf_prove(const uint32_t* __restrict__ keys,
-                                                            const int* __restrict__ key_idx,
-                                                            const uint8_t* __restrict__ alphas,
-                                                            const int* __restrict__ alpha_idx, int alpha_len, int n,
-                                                            const uint32_t* __restrict__ btab, uint32_t* scratch,
-                                                            uint8_t* __restrict__ pi, uint8_t* __restrict__ beta) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const uint32_t* key = keys + (long long)key_idx[t] * 24;
-  const uint8_t* alpha = alphas + (long long)alpha_idx[t] * alpha_len;
-  uint32_t x[8], prefix[8], pk[8];
-  for (int i = 0; i < 8; ++i) {
-    x[i] = key[i];
-    prefix[i] = key[8 + i];
-    pk[i] = key[16 + i];
-  }
+// scratch: [n][320] words (the table of H of each proof); pi: [n][80] bytes; beta: [n][64] or null.
+// Grid: ceil(n / 16) workgroups of 192 threads (3 waves); thread (wave w, lane l) works on proof
+// 16 * blockIdx.x + (l & 15) with sub-lane q = l >> 4.
+extern "C" __global__ void __launch_bounds__(192) k_vrf_prove(const uint32_t* __restrict__ keys,
+                                                             const int* __restrict__ key_idx,
+                                                             const uint8_t* __restrict__ alphas,
+                                                             const int* __restrict__ alpha_idx, int alpha_len, int n,
+                                                             const uint32_t* __restrict__ btab, uint32_t* scratch,
+                                                             uint8_t* __restrict__ pi, uint8_t* __restrict__ beta) {
+  __shared__ int s_ok[VTRY][VP];          // phase 1: counter j of proof p decoded
+  __shared__ int s_win[VP];               // the winning counter slot (-1: none yet)
+  __shared__ uint32_t s_h[VP][20];        // decoded H (affine x, y) of the winner
+  __shared__ uint32_t s_k[VP][8];         // nonce k
+  __shared__ uint32_t s_hstr[VP][8];      // encode(8 H)
+  __shared__ uint32_t s_gamma[VP][40];    // Gamma (wave 0)
+  __shared__ uint32_t s_v[VP][40];        // V (wave 1)
+  __shared__ uint32_t s_u[4][VP][40];     // U partial sums over 16 windows each (wave 2)
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int p = l & 15, q = l >> 4;
+  const int t = blockIdx.x * VP + p;
+  const bool valid = t < n;
+  const int tt = valid ? t : 0;
+  const uint32_t* key = keys + (long long)key_idx[tt] * 24;
+  const uint8_t* alpha = alphas + (long long)alpha_idx[tt] * alpha_len;
+  uint32_t pk[8];
+  for (int i = 0; i < 8; ++i) pk[i] = key[16 + i];
   const fe d = fe_const(C_D), d2 = fe_const(C_D2);
-  // ---- H = encode_to_curve_try_and_increment(pk, alpha)
-  ge H;
-  bool found = false;
-  for (int ctr = 0; ctr < 256 && !found; ++ctr) {
-    Sha512 s;
-    sha_init(s);
-    sha_byte(s, SUITE);
-    sha_byte(s, 0x01);
-    sha_words(s, pk, 8);
-    sha_bytes(s, alpha, alpha_len);
-    sha_byte(s, (uint8_t)ctr);
-    sha_byte(s, 0x00);
-    uint8_t dig[64];
-    sha_final(s, dig);
-    found = ge_frombytes(H, dig, d);
+  // ---------------- phase 1: H = encode_to_curve_try_and_increment(pk, alpha), 12 counters at once
+  const int slot = w * 4 + q;
+  if (threadIdx.x < VP) s_win[threadIdx.x] = -1;
+  for (int base = 0; base < 256; base += VTRY) {
+    const int ctr = base + slot;
+    ge cand;
+    bool ok = false;
+    __syncthreads();
+    if (valid && s_win[p] < 0 && ctr < 256) {
+      Sha512 sh;
+      sha_init(sh);
+      sha_byte(sh, SUITE);
+      sha_byte(sh, 0x01);
+      sha_words(sh, pk, 8);
+      sha_bytes(sh, alpha, alpha_len);
+      sha_byte(sh, (uint8_t)ctr);
+      sha_byte(sh, 0x00);
+      uint8_t dig[64];
+      sha_final(sh, dig);
+      ok = ge_frombytes(cand, dig, d);
+    }
+    s_ok[slot][p] = ok ? 1 : 0;
+    __syncthreads();
+    if (ok && s_win[p] < 0) {
+      int first = slot;
+      for (int j = 0; j < slot; ++j)
+        if (s_ok[j][p]) { first = j; break; }
+      if (first == slot) {   // the smallest decoding counter of this proof: publish H
+        st_fe(&s_h[p][0], cand.X);
+        st_fe(&s_h[p][10], cand.Y);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < VP) {
+      int first = -1;
+      for (int j = 0; j < VTRY && first < 0; ++j)
+        if (s_ok[j][threadIdx.x]) first = j;
+      if (first >= 0 && s_win[threadIdx.x] < 0) s_win[threadIdx.x] = base + first;
+    }
+    __syncthreads();
+    const int pending = (threadIdx.x < VP && blockIdx.x * VP + threadIdx.x < n && s_win[threadIdx.x] < 0) ? 1 : 0;
+    if (!__syncthreads_or(pending)) break;
   }
-  if (!found) return;   // probability 2^-256: the host marks an all-zero proof as failed
-  H = ge_dbl(ge_dbl(ge_dbl(H, false), false), true);   // cofactor 8
-  // ---- one table of H for x*H and k*H
-  uint32_t* tbl = scratch + (long long)t * 320;
-  {
-    const gc c1 = ge_cache(H, d2);
-    st_gc(tbl, c1);
-    ge acc = ge_dbl(H, true);
-    st_gc(tbl + 40, ge_cache(acc, d2));
-    for (int i = 2; i < 8; ++i) {
-      acc = ge_add_cached(acc, c1);
-      st_gc(tbl + 40 * i, ge_cache(acc, d2));
+  const bool have = valid && s_win[p] >= 0;   // probability 2^-256 of no valid counter: the host marks
+  //                                             an all-zero proof as failed
+  ge H;
+  if (have) {
+    const fe hx = ld_fe(&s_h[p][0]), hy = ld_fe(&s_h[p][10]);
+    H = ge{hx, hy, fe_small(1), fe_mul(hx, hy)};
+  }
+  uint32_t* tbl = scratch + (long long)tt * 320;
+  // ---------------- phase 2: the table of 8H (wave 0), the nonce (wave 1)
+  if (have && q == 0 && w <= 1) {
+    H = ge_dbl(ge_dbl(ge_dbl(H, false), false), true);   // cofactor 8
+    if (w == 0) {
+      const gc c1 = ge_cache(H, d2);
+      st_gc(tbl, c1);
+      ge acc = ge_dbl(H, true);
+      st_gc(tbl + 40, ge_cache(acc, d2));
+#pragma unroll 1
+      for (int i = 2; i < 8; ++i) {
+        acc = ge_add_cached(acc, c1);
+        st_gc(tbl + 40 * i, ge_cache(acc, d2));
+      }
+    } else {
+      const fe hzi = fe_invert(H.Z);
+      uint32_t hstr[8];
+      enc_affine(hstr, fe_mul(H.X, hzi), fe_mul(H.Y, hzi));
+      Sha512 sh;
+      sha_init(sh);
+      uint32_t prefix[8];
+      for (int i = 0; i < 8; ++i) prefix[i] = key[8 + i];
+      sha_words(sh, prefix, 8);
+      sha_words(sh, hstr, 8);
+      uint8_t dig[64];
+      sha_final(sh, dig);
+      uint32_t dw[16];
+      for (int i = 0; i < 16; ++i) dw[i] = le_word(dig, i);
+      uint32_t k[8];
+      sc_reduce_fast(k, dw, 16);
+      for (int i = 0; i < 8; ++i) {
+        s_k[p][i] = k[i];
+        s_hstr[p][i] = hstr[i];
+      }
     }
   }
-  const ge Gamma = ge_mul_tbl(tbl, x);
-  // ---- hstr = encode(H); nonce k = SHA512(prefix || hstr) mod L
-  const fe hzi = fe_invert(H.Z);
-  uint32_t hstr[8];
-  enc_affine(hstr, fe_mul(H.X, hzi), fe_mul(H.Y, hzi));
-  uint32_t k[8];
-  {
-    Sha512 s;
-    sha_init(s);
-    sha_words(s, prefix, 8);
-    sha_words(s, hstr, 8);
-    uint8_t dig[64];
-    sha_final(s, dig);
-    uint32_t dw[16];
-    for (int i = 0; i < 16; ++i)
-      dw[i] = (uint32_t)dig[4 * i] | ((uint32_t)dig[4 * i + 1] << 8) | ((uint32_t)dig[4 * i + 2] << 16) |
-              ((uint32_t)dig[4 * i + 3] << 24);
-    sc_reduce_words(k, dw, 512);
+  __syncthreads();   // the table (global, workgroup-visible after the barrier) and k are ready
+  // ---------------- phase 3: Gamma = x H (wave 0) | V = k H (wave 1) | U = k B (wave 2, 4 lanes per proof)
+  if (have && w == 0 && q == 0) {
+    uint32_t x[8];
+    for (int i = 0; i < 8; ++i) x[i] = key[i];
+    st_ge(&s_gamma[p][0], ge_mul_tbl(tbl, x));
+  } else if (have && w == 1 && q == 0) {
+    uint32_t k[8];
+    for (int i = 0; i < 8; ++i) k[i] = s_k[p][i];
+    st_ge(&s_v[p][0], ge_mul_tbl(tbl, k));
+  } else if (have && w == 2) {
+    uint32_t k[8];
+    for (int i = 0; i < 8; ++i) k[i] = s_k[p][i];
+    int8_t e[64];
+    signed_digits(e, k);
+    ge r = ge_identity();
+#pragma unroll 1
+    for (int wi = 16 * q; wi < 16 * q + 16; ++wi) {
+      const int dg = e[wi];
+      if (dg > 0) r = ge_add_cached(r, ld_btab(btab, wi * 8 + dg - 1));
+      else if (dg < 0) r = ge_add_cached(r, gc_neg(ld_btab(btab, wi * 8 - dg - 1)));
+    }
+    st_ge(&s_u[q][p][0], r);
   }
-  const ge U = ge_mul_base(btab, k);
-  const ge V = ge_mul_tbl(tbl, k);
-  // ---- encodings of Gamma, U, V with one inversion
+  __syncthreads();
+  // ---------------- phase 4: encodings, challenge, s (wave 0, one lane per proof)
+  if (!(have && w == 0 && q == 0)) return;
+  const ge Gamma = ld_ge(&s_gamma[p][0]);
+  const ge V = ld_ge(&s_v[p][0]);
+  ge U = ld_ge(&s_u[0][p][0]);
+#pragma unroll 1
+  for (int j = 1; j < 4; ++j) U = ge_add_cached(U, ge_cache(ld_ge(&s_u[j][p][0]), d2));
+  uint32_t k[8], hstr[8], x[8];
+  for (int i = 0; i < 8; ++i) {
+    k[i] = s_k[p][i];
+    hstr[i] = s_hstr[p][i];
+    x[i] = key[i];
+  }
   const fe zgu = fe_mul(Gamma.Z, U.Z);
   const fe inv = fe_invert(fe_mul(zgu, V.Z));
   const fe ziV = fe_mul(inv, zgu);
@@ -559,26 +701,24 @@ extern "C" __global__ void __launch_bounds__(64) k_vrf_prove(const uint32_t* __r
   enc_affine(eg, fe_mul(Gamma.X, ziG), fe_mul(Gamma.Y, ziG));
   enc_affine(eu, fe_mul(U.X, ziU), fe_mul(U.Y, ziU));
   enc_affine(ev, fe_mul(V.X, ziV), fe_mul(V.Y, ziV));
-  // ---- c = SHA512(suite || 0x02 || Y || H || Gamma || U || V || 0x00)[0..16]
+  // c = SHA512(suite || 0x02 || Y || H || Gamma || U || V || 0x00)[0..16]
   uint8_t cdig[64];
   {
-    Sha512 s;
-    sha_init(s);
-    sha_byte(s, SUITE);
-    sha_byte(s, 0x02);
-    sha_words(s, pk, 8);
-    sha_words(s, hstr, 8);
-    sha_words(s, eg, 8);
-    sha_words(s, eu, 8);
-    sha_words(s, ev, 8);
-    sha_byte(s, 0x00);
-    sha_final(s, cdig);
+    Sha512 sh;
+    sha_init(sh);
+    sha_byte(sh, SUITE);
+    sha_byte(sh, 0x02);
+    sha_words(sh, pk, 8);
+    sha_words(sh, hstr, 8);
+    sha_words(sh, eg, 8);
+    sha_words(sh, eu, 8);
+    sha_words(sh, ev, 8);
+    sha_byte(sh, 0x00);
+    sha_final(sh, cdig);
   }
-  // ---- s = (k + c x) mod L: 128 x 256-bit product plus k, reduced bitwise
+  // s = (k + c x) mod L: 128 x 256-bit product plus k
   uint32_t cw[4];
-  for (int i = 0; i < 4; ++i)
-    cw[i] = (uint32_t)cdig[4 * i] | ((uint32_t)cdig[4 * i + 1] << 8) | ((uint32_t)cdig[4 * i + 2] << 16) |
-            ((uint32_t)cdig[4 * i + 3] << 24);
+  for (int i = 0; i < 4; ++i) cw[i] = le_word(cdig, i);
   uint32_t prod[13];
   for (int i = 0; i < 13; ++i) prod[i] = 0;
   for (int i = 0; i < 4; ++i) {
@@ -603,8 +743,8 @@ extern "C" __global__ void __launch_bounds__(64) k_vrf_prove(const uint32_t* __r
     }
   }
   uint32_t sc[8];
-  sc_reduce_words(sc, prod, 13 * 32);
-  // ---- pi = Gamma (32) || c (16) || s (32)
+  sc_reduce_fast(sc, prod, 13);
+  // pi = Gamma (32) || c (16) || s (32)
   uint8_t* o = pi + (long long)t * 80;
   for (int i = 0; i < 8; ++i)
     for (int b = 0; b < 4; ++b) o[4 * i + b] = (uint8_t)(eg[i] >> (8 * b));
@@ -616,13 +756,13 @@ extern "C" __global__ void __launch_bounds__(64) k_vrf_prove(const uint32_t* __r
     const fe zi = fe_invert(G8.Z);
     uint32_t e8[8];
     enc_affine(e8, fe_mul(G8.X, zi), fe_mul(G8.Y, zi));
-    Sha512 s;
-    sha_init(s);
-    sha_byte(s, SUITE);
-    sha_byte(s, 0x03);
-    sha_words(s, e8, 8);
-    sha_byte(s, 0x00);
-    sha_final(s, beta + (long long)t * 64);
+    Sha512 sh;
+    sha_init(sh);
+    sha_byte(sh, SUITE);
+    sha_byte(sh, 0x03);
+    sha_words(sh, e8, 8);
+    sha_byte(sh, 0x00);
+    sha_final(sh, beta + (long long)t * 64);
   }
 }
 
@@ -631,7 +771,7 @@ extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uin
                              void* stream) {
   if (n <= 0) return 0;
   if (alpha_len < 0 || alpha_len > 1024) return -1;
-  hipLaunchKernelGGL(k_vrf_prove, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, keys, key_idx, alphas,
+  hipLaunchKernelGGL(k_vrf_prove, dim3((n + VP - 1) / VP), dim3(192), 0, (hipStream_t)stream, keys, key_idx, alphas,
                      alpha_idx, alpha_len, n, btab, scratch, pi, beta);
   return (int)hipGetLastError();
 }

@@ -40,15 +40,18 @@ SIGNATURES = {
     "bsc_logreg_step": [P, P, P, P, P, P, I, I, I, U64, P, D, D, P, D, P, P, P],
     "bsc_dp_noise": [P, I, I, P, I, P, U64, I, P, P],
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],
-    "bsc_krum_committee": [P, I, I, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, P],
+    "bsc_krum_committee": [P, I, I, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, P, P],
     "bsc_gram_stacked": [P, I, P, I, L, I, I, P, P, P, P],
-    "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P],
+    "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_noise_table": [I, I, U64, P, P],
     "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P, P],
     "bsc_recover": [P, I, I, P, I, I, P, D, P, P, P, P],
     "bsc_add_rows": [P, I, P, I, P, P, P],
     "bsc_sum_rows_i64": [P, I, L, P, I, P, P, P],
+    "bsc_lsh_codes": [P, P, I, I, P, I, I, P, P],
+    "bsc_lsh_count": [P, I, P, I, P, I, D, P, P],
+    "bsc_weighted_rows": [P, I, I, P, P, P],
     "bsc_recover_w": [P, I, I, I, P, P, P, I, P, P, I, I, U64, U64, I, P, D, P, P, P, P, P],
 }
 

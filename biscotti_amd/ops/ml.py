@@ -347,6 +347,9 @@ def _committee_host(X, inbox, groupsize, n_accept, need, lead_rank, cap, G=None)
     return acc, node
 
 
+KRUM_MAX_ROWS = 8192    # committee Krum: candidate rows (Gram operand rows)
+KRUM_MAX_INBOX = 4096   # committee Krum: updates per verifier inbox
+
 _COUNTERS: dict = {}
 
 
@@ -382,7 +385,7 @@ def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lea
             on_accept(node.to(torch.int32))
         return lambda: (acc, node)
     assert X.dtype == torch.float32 and inbox.dtype == torch.int32 and lead_rank.dtype == torch.int32
-    assert 0 < U <= 1024 and 0 < n <= 256 and 0 < V <= 64 and n <= U, "committee Krum size limits"
+    assert 0 < U <= KRUM_MAX_ROWS and 0 < n <= KRUM_MAX_INBOX and 0 < V <= 64 and n <= U, "committee Krum size limits"
     assert lead_rank.numel() == U
     T = (U + 15) // 16
     npairs = T * (T + 1) // 2
@@ -394,9 +397,10 @@ def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lea
     scores = torch.empty((V, n), dtype=torch.float64, device=dev)
     out = torch.empty((V * n + U,), dtype=torch.int32, device=dev)
     acc, node = out[: V * n], out[V * n:]
+    ws = torch.empty((U,), dtype=torch.int32, device=dev) if (U > 1024 or n > 256) else None
     _check(hip().bsc_krum_committee(_p(X.contiguous()), U, D, kchunk, _p(inbox.contiguous()), V, n, groupsize, n_accept,
                                     need, _p(lead_rank.contiguous()), cap, _p(part), _p(gram), _p(count), _p(scores),
-                                    _p(acc), _p(node), _stream()), "krum_committee")
+                                    _p(acc), _p(node), _p(ws), _stream()), "krum_committee")
     host = torch.empty(out.shape, dtype=torch.int32, pin_memory=True)
     host.copy_(out, non_blocking=True)
     ev = S.record()
@@ -421,7 +425,7 @@ def gram_stacked_async(X, T_rows, kchunk: int = 512) -> dict:
     assert X.is_contiguous() and T_rows.stride(1) == 1 and T_rows.shape[1] == D
     assert X.dtype == torch.float32 and T_rows.dtype == torch.float32
     U = U1 + U2
-    assert 0 < U <= 1024, "committee Krum size limits"
+    assert 0 < U <= KRUM_MAX_ROWS, "committee Krum size limits"
     if X.device.type != "cuda":
         return {"gram_full": _gram_exact_order(torch.cat([X, T_rows])), "U1": U1, "U": U}
     Tt = (U + 15) // 16
@@ -445,7 +449,7 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
     nn = nz.shape[1]
     assert inbox.dtype == torch.int32 and lead_rank.dtype == torch.int32 and lead_rank.numel() == U1
     assert nz.dtype == torch.int32 and sc.dtype == torch.float32 and tuple(nz.shape) == (U1, nn)
-    assert 0 < n <= 256 and 0 < V <= 64 and n <= U1 and 0 < nn <= 16
+    assert 0 < n <= KRUM_MAX_INBOX and 0 < V <= 64 and n <= U1 and 0 < nn <= 16
     if "gram_full" in pre:   # CPU: the same assembly as k_krum_rows_noise, term by term in its order
         G, inv = pre["gram_full"], 1.0 / nn
         z, w = nz.long(), sc.double()
@@ -464,10 +468,11 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
     scores = torch.empty((V, n), dtype=torch.float64, device=dev)
     out = torch.empty((V * n + U1,), dtype=torch.int32, device=dev)
     acc, node = out[: V * n], out[V * n:]
+    ws = torch.empty((U1,), dtype=torch.int32, device=dev) if (U1 > 1024 or n > 256) else None
     _check(hip().bsc_krum_committee_noise(_p(pre["gram"]), U1, U, _p(nz.contiguous()), _p(sc.contiguous()), nn,
                                           _p(inbox.contiguous()), V, n, groupsize, n_accept, need,
-                                          _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _stream()),
-           "krum_committee_noise")
+                                          _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _p(ws),
+                                          _stream()), "krum_committee_noise")
     host = pinned("krum_noise", out.shape, torch.int32)
     d2h_into(host, out)
     ev = S.record()

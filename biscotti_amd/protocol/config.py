@@ -28,7 +28,7 @@ class RunConfig:
     perc_samples: int = 70          # -ns
     rand_sample: bool = False       # -rs
     # --- compile-time constants of the reference (main.go:28-58, honest.go:44-57)
-    defense: str = "KRUM"           # POISON_DEFENSE (KRUM | RONI)
+    defense: str = "KRUM"           # POISON_DEFENSE (KRUM | RONI), or LSH (the sieve of ML/code/logistic_aggregator.py)
     max_iterations: int = 100       # MAX_ITERATIONS
     poly_size: int = 10             # POLY_SIZE
     precision: int = 4              # PRECISION
@@ -108,7 +108,7 @@ class RunConfig:
 
     def validate(self) -> None:
         """Reject configurations the kernels cannot run, up front (instead of a launch error in the
-        middle of a round).  Limits: committee Multi-Krum <= 1024 candidate rows, inbox <= 256,
+        middle of a round).  Limits: committee Multi-Krum <= 8192 candidate rows, inbox <= 4096,
         <= 64 verifiers (ml.hip KC1-KC3); exact recovery <= 32 share points per chunk and poly <= 16
         (k_recover_w); local step B <= 16 and <= 16 classes (k_softmax_step); <= 16 noisers."""
         import math
@@ -122,13 +122,13 @@ class RunConfig:
         if self.num_nodes - committee < 1:
             err.append(f"{self.num_nodes} nodes leave no worker beside {committee} committee members")
         workers = max(0, self.num_nodes - min(committee, self.num_nodes))
-        if workers > 1024:
-            err.append(f"{workers} workers per round: committee Krum takes at most 1024 candidates")
+        if workers > 8192:
+            err.append(f"{workers} workers per round: committee Krum takes at most 8192 candidates")
         thresh = min(int(self.num_nodes * self.perc_samples / 100.0), max(workers, 0))
         if self.rand_sample:
             thresh = max(workers, 0)
-        if self.verification and thresh > 256:
-            err.append(f"verifier inbox of {thresh} updates: committee Krum takes at most 256 per verifier")
+        if self.verification and thresh > 4096:
+            err.append(f"verifier inbox of {thresh} updates: committee Krum takes at most 4096 per verifier")
         if self.num_verifiers > 64:
             err.append("at most 64 verifiers")
         if self.num_miners <= 0 or self.num_verifiers < 0 or self.num_noisers < 0:
@@ -156,6 +156,8 @@ class RunConfig:
             self.fail_point()
         except ValueError:
             err.append(f"fail_at {self.fail_at!r}: expected IT or IT@RANK")
+        if self.defense not in ("KRUM", "RONI", "LSH"):
+            err.append(f"defense {self.defense!r}: expected KRUM | RONI | LSH")
         if self.kzg_audit not in ("off", "consistent", "literal"):
             err.append(f"kzg_audit {self.kzg_audit!r}: expected off | consistent | literal")
         if err:
@@ -223,7 +225,7 @@ def add_reference_flags(ap: argparse.ArgumentParser) -> None:
 
 
 def add_framework_flags(ap: argparse.ArgumentParser) -> None:
-    ap.add_argument("--defense", default="KRUM", choices=["KRUM", "RONI"])
+    ap.add_argument("--defense", default="KRUM", choices=["KRUM", "RONI", "LSH"])
     ap.add_argument("--max-iterations", type=int, default=100)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--churn", type=float, default=0.0)

@@ -156,7 +156,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.vrf_dev = None
         if self.gpu and cfg.vrf_device:
             from ..ops.vrf import DeviceVrfProver
-            self.vrf_dev = DeviceVrfProver(self.dev, 16)
+            self.vrf_dev = DeviceVrfProver(self.dev, 1)
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
         self._pre = None             # next round's local step + commitments, queued behind the recovery
@@ -321,6 +321,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             work, self._pre_vrf_work = self._pre_vrf_work, []
             for f in work:
                 f(head["fut_noise"])
+            if head.get("vrf_proofs") is not None:
+                self.vrf_dev.submit(*head["vrf_proofs"], self.vrf_stream)
             self._resolve_evals()
             if krum_pre is not None and cfg.verification and inboxes and cfg.defense == "KRUM":
                 kst = self._krum_static(krum_pre["xrow"], krum_pre["U1"], plan, live, inboxes, head["spec"],

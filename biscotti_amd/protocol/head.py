@@ -133,13 +133,15 @@ class RoundHeadMixin:
             with tm.phase("verify.pregram"):
                 krum_pre = pre.get("gram") if use_pre else None
                 if krum_pre is None:
-                    krum_pre = self._gram_rows(delta, row_of, it)
+                    # the pre-step's delta holds every local peer (no row selection needed)
+                    krum_pre = self._gram_rows(delta, None if use_pre else row_of, it)
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
                     spec=spec, spec_cand=cand, krum_pre=krum_pre)
         if self.vrf_dev is not None:
-            # the proofs nobody reads -- every noiser proof and the roles proofs -- on the device, on their
-            # own low-priority stream
-            self.vrf_dev.submit(seeds + roles, latest_hash, self.vrf_stream)
+            # the proofs nobody reads -- every noiser proof and the roles proofs -- go to the device prover
+            # when the round runs (run_round's VRF wait), one launch per round on their own low-priority
+            # stream: a timed window then contains exactly its rounds' proofs
+            head["vrf_proofs"] = (seeds + roles, bytes(latest_hash))
         return head
 
     def _block_candidates(self, plan, workers, inboxes) -> set:
@@ -164,7 +166,7 @@ class RoundHeadMixin:
         cfg = self.cfg
         return bool(cfg.secure_agg and cfg.verification and cfg.defense == "KRUM" and cfg.noising
                     and self.sigma > 0 and cfg.num_noisers >= 1 and self.noise_rows is not None
-                    and not cfg.noise_independent and self.comm.world * self.maxlocal + self.N <= 1024)
+                    and not cfg.noise_independent and self.comm.world * self.maxlocal + self.N <= K.KRUM_MAX_ROWS)
 
     def _gram_rows(self, delta: torch.Tensor, row_of: dict | None, it: int) -> dict:
         """Phase 1 of the noise-aware committee Krum over the flat peer layout: row r * maxlocal + j is
@@ -206,7 +208,8 @@ class RoundHeadMixin:
             out = {"W": W, "it": it, "delta": delta, "qdelta": qdelta, "ev": ev,
                    "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
         S.hold(delta, qdelta)
-        if self._noise_krum():
+        import os
+        if self._noise_krum() and (self.comm.world == 1 or os.environ.get("BISCOTTI_MR_PREGATHER", "1") == "1"):
             # the noise-aware Krum's d-dimensional phase over EVERY peer's delta (the workers are not known
             # yet) and this iteration's noise rows, on the same stream right behind the step: done long
             # before the noisers are drawn, and the main stream's evaluation does not wait for it
@@ -224,6 +227,9 @@ class RoundHeadMixin:
         adopts it when the committed block and its plan match (they do unless the audit fails).  Local
         work only (no collective): each rank launches its own peers' rows."""
         cfg, pre = self.cfg, self._pre
+        import os
+        if self.comm.world > 1 and os.environ.get("BISCOTTI_MR_SPEC_HEAD", "1") != "1":
+            return
         if not (self._pipelined() and cfg.secure_agg and cfg.verification and cfg.churn == 0
                 and cfg.churn_kill_per_min == 0 and not self._partitions and pre is not None
                 and pre["W"] is self._W_next and self.local):

@@ -272,6 +272,15 @@ class VerifyMixin:
                         kept = None
                         self.stats["spec_misses"] = self.stats.get("spec_misses", 0) + 1
                     box["sa"]["accepted"] = kept
+            elif cfg.defense == "LSH":
+                # LSH sieve (logistic_aggregator.py:7-29): like Krum a pure function of the (gathered)
+                # noised updates, so every rank evaluates every verifier's inbox itself
+                from ..ops.lsh import sieve_accept
+
+                with tm.phase("verify.defense"):
+                    acc_np = sieve_accept(X, [[xrow[w] for w in inboxes[v]] for v in vs], self.d,
+                                          seed=self.fsm.round_seed(13)).astype(np.uint8)
+                acc_row = {v: k for k, v in enumerate(vs)}
             else:
                 # RONI: each verifier judges with its own data, so only its rank can decide; the accept
                 # matrix [nv, ni] travels in one all_gather on several ranks

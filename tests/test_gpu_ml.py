@@ -364,3 +364,48 @@ def test_noise_table_fused_row_gather():
     rows = torch.tensor([4, 0, 5, 2], dtype=torch.int32).cuda()
     got = K.dp_noise(delta, noisers, scales, 7, 4, table=tbl, rows=rows)
     assert torch.equal(got, full[rows.long()])
+
+
+@pytest.mark.parametrize("U,n,V", [(500, 400, 3), (1300, 700, 4)])
+def test_krum_committee_large_inboxes(U, n, V):
+    """Committees past the LDS fast path (inbox > 256 updates, > 1024 candidate rows; the reference's Krum
+    has no size limit, client_obj.py:114-143): rows sorted in LDS + workspace vote, against the fp64
+    reference (BLAS Gram here: the test's rows have no near-ties)."""
+    g = torch.Generator().manual_seed(U + n)
+    X = torch.randn((U, 7850), generator=g) * 0.1
+    bad = torch.randperm(U, generator=g)[: U // 5]
+    X[bad] += 0.5 * torch.randn((1, 7850), generator=g)
+    inbox = torch.stack([torch.sort(torch.randperm(U, generator=g)[:n]).values for _ in range(V)]).int()
+    rank = torch.randperm(U, generator=g).int()
+    rank[torch.randperm(U, generator=g)[:5]] = -1
+    clip = n // 2
+    need, cap = V // 2, n // 3
+    Xd = X.double()
+    acc_ref, node_ref = K._committee_host(None, inbox, n - clip, n - clip, need, rank, cap, G=Xd @ Xd.T)
+    acc, node = K.krum_committee_async(X.cuda(), inbox.cuda(), n - clip, n - clip, need, rank.cuda(), cap)()
+    assert torch.equal(acc, acc_ref)
+    assert torch.equal(node, node_ref)
+    for v in range(V):
+        assert not acc[v][torch.isin(inbox[v].long(), bad)].any()
+
+
+def test_krum_committee_noise_aware_large_inbox():
+    """Noise-aware assembly with an inbox of 400 (sorted-row path) against explicitly noised rows."""
+    g = torch.Generator().manual_seed(77)
+    U1, N, nn, D, it = 600, 300, 2, 7850, 1
+    delta = (torch.randn((U1, D), generator=g) * 0.05).float()
+    delta[-100:] += 0.3 * torch.randn((1, D), generator=g)
+    tbl = torch.randn((N, 2, D), generator=g).float()
+    nz = torch.randint(0, N, (U1, nn), generator=g).int()
+    sc = torch.full((U1, nn), -0.76, dtype=torch.float32)
+    X64 = delta.double() + (sc.double()[:, :, None] * tbl[:, it].double()[nz.long()]).sum(1) / nn
+    n, V = 400, 3
+    inbox = torch.stack([torch.sort(torch.randperm(U1, generator=g)[:n]).values for _ in range(V)]).int()
+    rank = torch.randperm(U1, generator=g).int()
+    clip = n // 2
+    acc_ref, node_ref = K._committee_host(None, inbox, n - clip, n - clip, 1, rank, 60, G=X64 @ X64.T)
+    pre = K.gram_stacked_async(delta.cuda(), tbl.cuda()[:, it, :])
+    acc, node = K.krum_committee_noise_async(pre, nz.cuda(), sc.cuda(), inbox.cuda(), n - clip, n - clip, 1,
+                                             rank.cuda(), 60)()
+    assert torch.equal(acc, acc_ref)
+    assert torch.equal(node, node_ref)
