@@ -4,8 +4,8 @@ The protocol computes two VRF proofs per peer per round that nothing reads (the 
 getVRFRoles, quirk Q7, and the proof half of every worker's noiser VRF, vrf.go:54-100 -- only the
 64-byte output feeds the lottery).  Round 1 spent ~37 ms of host CPU per round on them; here the
 host computes the outputs the lottery needs (VrfJob outputs_only) and the proofs are queued for the
-device, one launch per round (batch_rounds) on a low-priority stream; the kernel splits each proof over
-the three waves of a workgroup, so a launch's latency is about one variable-base scalar multiplication.  Bit-exact with runtime/vrf.cpp
+device, batch_rounds rounds per launch on a low-priority stream; the kernel splits each proof over the
+three waves of a workgroup, so a launch's latency is about one variable-base scalar multiplication.  Bit-exact with runtime/vrf.cpp
 (tests/test_gpu_vrf.py), which is itself pinned to the RFC's example vector.
 """
 from __future__ import annotations

@@ -130,9 +130,10 @@ def test_runconfig_rejects_unsupported_shapes():
 
     from biscotti_amd.protocol.config import RunConfig
 
-    RunConfig(num_nodes=200).validate()               # 200 peers: inbox 140 <= 256
+    RunConfig(num_nodes=200).validate()               # 200 peers: inbox 140
+    RunConfig(num_nodes=400).validate()               # inbox 280 > 256: the sorted-row Krum kernels
     RunConfig(num_nodes=100, dataset="lfw").validate()
-    for bad in (dict(num_nodes=400), dict(num_verifiers=65, num_nodes=200), dict(num_miners=1, poly_size=20),
+    for bad in (dict(num_nodes=6000), dict(num_verifiers=65, num_nodes=200), dict(num_miners=1, poly_size=20),
                 dict(batch_size=32), dict(dataset="cifar"), dict(num_nodes=5, num_verifiers=3, num_miners=2)):
         with _pt.raises(ValueError):
             RunConfig(**bad).validate()
