@@ -1,0 +1,124 @@
+// Native round driver pieces: the secure aggregation a round queues behind the committee's selection,
+// enqueued from C++ in ONE call instead of ~25 Python-level tensor / stream operations (each 5-20 us
+// of the round's host thread, which is the round's critical path).
+//
+// bsc_round_secagg  -- the miners' sums and the leader's recovery (aggregateSecret + recoverSecret,
+//                      DistSys/kyber.go:244-287,809-857) for the rows the selection kept:
+//                        side: chunk-commitment sums of the kept rows (the audit's input)
+//                        bg:   witness sums (no consumer on the protocol path)
+//                        main: fused share sums + exact recovery + W update (k_recover_w), then the
+//                              read-back of (status, W_new) into pinned memory, event `readback`
+// bsc_round_audit   -- verifyCommitment on the aggregate (kyber.go:564-577): main waits for the side
+//                      stream's sums, k_chunk_check, read-back of the verdicts, event `audit`
+// bsc_round_wait    -- host wait for one of the two events
+//
+// The launchers of the individual kernels (msm.hip, ml.hip) are called directly; every buffer is
+// resident (allocated once by the engine), so the call allocates nothing.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
+                             int ncols, const int* row_mask, uint32_t* out, void* stream);
+extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, const int* mask, const int* ycols,
+                             const int* xs, int npts, const long long* A, const int* basis, int poly, int shift,
+                             unsigned long long inv_lo, unsigned long long inv_hi, int d, const double* W,
+                             double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out,
+                             void* stream);
+extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
+                               const uint32_t* csum, int nm, int nch, int* ok, void* stream);
+
+namespace {
+struct RoundCtx {
+  hipStream_t main, side, bg;
+  hipEvent_t ev_main, ev_side, ev_readback, ev_audit;
+  const uint32_t* tbl_pk;
+  int d, poly, T, nch, b0, nw;
+  double qscale;
+};
+#define RC_CHECK(x)                        \
+  do {                                     \
+    const int e_ = (int)(x);               \
+    if (e_ != 0) return e_;                \
+  } while (0)
+}  // namespace
+
+extern "C" void* bsc_round_create(void* main, void* side, void* bg, const uint32_t* tbl_pk, int d, int poly, int T,
+                                  int b0, int nw, double qscale) {
+  RoundCtx* c = new RoundCtx();
+  c->main = (hipStream_t)main;
+  c->side = (hipStream_t)side;
+  c->bg = (hipStream_t)bg;
+  c->tbl_pk = tbl_pk;
+  c->d = d;
+  c->poly = poly;
+  c->T = T;
+  c->nch = (d + poly - 1) / poly;
+  c->b0 = b0;
+  c->nw = nw;
+  c->qscale = qscale;
+  hipEvent_t* evs[4] = {&c->ev_main, &c->ev_side, &c->ev_readback, &c->ev_audit};
+  for (hipEvent_t* e : evs)
+    if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+      delete c;
+      return nullptr;
+    }
+  return c;
+}
+
+extern "C" void bsc_round_destroy(void* ctx) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr) return;
+  hipEventDestroy(c->ev_main);
+  hipEventDestroy(c->ev_side);
+  hipEventDestroy(c->ev_readback);
+  hipEventDestroy(c->ev_audit);
+  delete c;
+}
+
+// pts [R][nch * (T + 1)][24] Jacobian shares + chunk commitments of the speculative rows, ys [R][nch][T]
+// share values, mask [R] the selection's keep flags; ccols [nch] / wcols [nwc] the commitment and witness
+// columns, ycols / xs [npts] the contributing miners' share columns and x-points; A / basis / shift /
+// inv the exact recovery weights of this miner layout; W the current model.  Outputs (resident):
+// W_new [d], coeffs [nch][poly], status [nch], agg [nch][npts], cs [nch][24], ws [nwc][24]; pinned host
+// copies h_status [nch], h_W [d].  audit = 0: no commitment sums.
+extern "C" int bsc_round_secagg(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask,
+                                const int* ccols, const int* wcols, int nwc, const int* ycols, const int* xs, int npts,
+                                const long long* A, const int* basis, int shift, unsigned long long inv_lo,
+                                unsigned long long inv_hi, const double* W, double* W_new, long long* coeffs,
+                                int* status, long long* agg, uint32_t* cs, uint32_t* ws, int* h_status, double* h_W,
+                                int audit) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || R <= 0) return -1;
+  const int ncols_in = c->nch * (c->T + 1);
+  RC_CHECK(hipEventRecord(c->ev_main, c->main));
+  if (audit) {
+    RC_CHECK(hipStreamWaitEvent(c->side, c->ev_main, 0));
+    RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, ccols, c->nch, mask, cs, c->side));
+    RC_CHECK(hipEventRecord(c->ev_side, c->side));
+  }
+  RC_CHECK(hipStreamWaitEvent(c->bg, c->ev_main, 0));
+  RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->bg));
+  RC_CHECK(bsc_recover_w(ys, R, c->nch, c->T, mask, ycols, xs, npts, A, basis, c->poly, shift, inv_lo, inv_hi, c->d, W,
+                         c->qscale, W_new, coeffs, status, agg, c->main));
+  RC_CHECK(hipMemcpyAsync(h_status, status, (size_t)c->nch * sizeof(int), hipMemcpyDeviceToHost, c->main));
+  RC_CHECK(hipMemcpyAsync(h_W, W_new, (size_t)c->d * sizeof(double), hipMemcpyDeviceToHost, c->main));
+  RC_CHECK(hipEventRecord(c->ev_readback, c->main));
+  return 0;
+}
+
+extern "C" int bsc_round_audit(void* ctx, const long long* coeffs, const uint32_t* cs, int* ok, int* h_ok) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr) return -1;
+  RC_CHECK(hipStreamWaitEvent(c->main, c->ev_side, 0));
+  RC_CHECK(bsc_chunk_check(coeffs, c->d, c->poly, c->tbl_pk, c->b0, c->nw, cs, 1, c->nch, ok, c->main));
+  RC_CHECK(hipMemcpyAsync(h_ok, ok, (size_t)c->nch * sizeof(int), hipMemcpyDeviceToHost, c->main));
+  RC_CHECK(hipEventRecord(c->ev_audit, c->main));
+  return 0;
+}
+
+// which: 0 = the recovery read-back, 1 = the audit read-back
+extern "C" int bsc_round_wait(void* ctx, int which) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr) return -1;
+  return (int)hipEventSynchronize(which == 0 ? c->ev_readback : c->ev_audit);
+}

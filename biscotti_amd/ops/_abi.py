@@ -53,10 +53,16 @@ SIGNATURES = {
     "bsc_lsh_count": [P, I, P, I, P, I, D, P, P],
     "bsc_weighted_rows": [P, I, I, P, P, P],
     "bsc_recover_w": [P, I, I, I, P, P, P, I, P, P, I, I, U64, U64, I, P, D, P, P, P, P, P],
+    # round.hip
+    "bsc_round_create": [P, P, P, P, I, I, I, I, I, D],
+    "bsc_round_destroy": [P],
+    "bsc_round_secagg": [P, P, I, P, P, P, P, I, P, P, I, P, P, I, U64, U64, P, P, P, P, P, P, P, P, P, I],
+    "bsc_round_audit": [P, P, P, P, P],
+    "bsc_round_wait": [P, I],
 }
 
 
-RESTYPES = {"bsc_stream_create_cumask": C.c_void_p}
+RESTYPES = {"bsc_stream_create_cumask": C.c_void_p, "bsc_round_create": C.c_void_p, "bsc_round_destroy": None}
 
 
 def declare(lib) -> None:

@@ -320,3 +320,77 @@ def cu_masked_stream(device, skip_every: int = 4):
     if not ptr:
         raise RuntimeError("hipExtStreamCreateWithCUMask failed")
     return torch.cuda.ExternalStream(ptr, device=device), used.value
+
+
+class NativeSecAgg:
+    """The round's secure aggregation enqueued natively (kernels/round.hip): one call queues the miners'
+    commitment / witness sums (side / background streams), the fused share sums + exact recovery + W
+    update and the read-back (main stream); a second queues the aggregate audit.  Every buffer is
+    resident; the recovered model goes to a ring of 4 buffers (the newest is the engine's W, the one
+    before may still feed the next round's pre-step).  Single rank, speculative (masked) rows."""
+
+    W_RING = 4
+
+    def __init__(self, eng: DeviceCommitEngine, main, side, bg, qscale: float):
+        self.eng, dev = eng, eng.device
+        d, nch, poly = eng.d, eng.nchunks, eng.poly
+        self.ctx = hip().bsc_round_create(main.cuda_stream, side.cuda_stream, bg.cuda_stream, _ptr(eng.tbl_pk), d, poly,
+                                          eng.T, eng.b0, eng.nw, float(qscale))
+        if not self.ctx:
+            raise RuntimeError("bsc_round_create failed")
+        self.W_ring = [torch.empty((d,), dtype=torch.float64, device=dev) for _ in range(self.W_RING)]
+        self.k = 0
+        self.coeffs = torch.empty((nch, poly), dtype=torch.int64, device=dev)
+        self.status = torch.empty((nch,), dtype=torch.int32, device=dev)
+        self.cs = torch.empty((nch, 24), dtype=torch.int32, device=dev)
+        self.ok = torch.empty((1, nch), dtype=torch.int32, device=dev)
+        self.h_status = torch.empty((nch,), dtype=torch.int32, pin_memory=True)
+        self.h_W = torch.empty((d,), dtype=torch.float64, pin_memory=True)
+        self.h_ok = torch.empty((1, nch), dtype=torch.int32, pin_memory=True)
+        self._by_shape: dict = {}
+
+    def _buf(self, key, shape, dtype):
+        t = self._by_shape.get(key)
+        if t is None:
+            t = self._by_shape[key] = torch.empty(shape, dtype=dtype, device=self.eng.device)
+        return t
+
+    def secagg(self, pts, ys, mask, ccols, wcols, ycols, xs, wts: dict, A_dev, basis_dev, W, audit: bool):
+        """Queue sums + recovery + read-back; returns (W_new, coeffs, status, agg) device tensors."""
+        R = pts.shape[0]
+        npts, nwc = ycols.numel(), wcols.numel()
+        nch = self.eng.nchunks
+        self.k = (self.k + 1) % self.W_RING
+        W_new = self.W_ring[self.k]
+        agg = self._buf(("agg", npts), (nch, npts), torch.int64)
+        ws = self._buf(("ws", nwc), (nwc, 24), torch.int32)
+        err = hip().bsc_round_secagg(self.ctx, _ptr(pts), R, _ptr(ys), _ptr(mask), _ptr(ccols), _ptr(wcols), nwc,
+                                     _ptr(ycols), _ptr(xs), npts, _ptr(A_dev), _ptr(basis_dev), wts["shift"],
+                                     wts["inv_lo"], wts["inv_hi"], _ptr(W), _ptr(W_new), _ptr(self.coeffs),
+                                     _ptr(self.status), _ptr(agg), _ptr(self.cs), _ptr(ws), self.h_status.data_ptr(),
+                                     self.h_W.data_ptr(), int(audit))
+        if err != 0:
+            raise RuntimeError(f"bsc_round_secagg failed ({err})")
+        return W_new, self.coeffs, self.status, agg
+
+    def readback(self):
+        """Callable: waits for the recovery's read-back -> [status, W_new] numpy views (pinned)."""
+        def wait():
+            _check(hip().bsc_round_wait(self.ctx, 0), "round_wait")
+            return [self.h_status.numpy(), self.h_W.numpy()]
+        return wait
+
+    def audit(self):
+        """Queue the aggregate audit on main; returns the callable giving ok int32 [1, nchunks]."""
+        _check(hip().bsc_round_audit(self.ctx, _ptr(self.coeffs), _ptr(self.cs), _ptr(self.ok), self.h_ok.data_ptr()),
+               "round_audit")
+
+        def result():
+            _check(hip().bsc_round_wait(self.ctx, 1), "round_wait")
+            return self.h_ok.numpy()
+        return result
+
+    def close(self) -> None:
+        if self.ctx:
+            hip().bsc_round_destroy(self.ctx)
+            self.ctx = None

@@ -16,6 +16,12 @@ injects such a crash deterministically.
 
 At exit rank 0 prints the chain with PrintChain's format (blockchain.go:43-54) to stdout, which
 is what localTest.sh compares between peers.
+
+Talking to peers outside the job (reference peers included) uses the reference's own transport, Go
+net/rpc + gob (parallel/netrpc.py): ``--rpc-listen HOST:PORT`` serves the ``Peer`` RPC methods on
+rank 0 over the job's chain (RegisterPeer hands it to joiners, RegisterBlock accepts extensions,
+RequestNoise / VerifyUpdateKRUM / RegisterSecret / GetMinerPart answer with this peer's roles), and
+``--rpc-flood ADDR[,ADDR...]`` sends every committed block to those peers (RegisterBlock, main.go:1403-1444).
 """
 from __future__ import annotations
 
@@ -33,6 +39,8 @@ def main(argv=None) -> int:
     add_framework_flags(ap)
     ap.add_argument("--rounds", type=int, default=None, help="stop after this many rounds")
     ap.add_argument("--print-chain", default="rank0", choices=["rank0", "all", "none"])
+    ap.add_argument("--rpc-listen", default=None, help="HOST:PORT: serve the Peer net/rpc methods (rank 0)")
+    ap.add_argument("--rpc-flood", default="", help="comma list of HOST:PORT peers that receive every block")
     ns = ap.parse_args(argv)
     cfg = config_from_args(ns)
     if cfg.num_nodes <= 0 or not cfg.dataset:
@@ -55,13 +63,30 @@ def main(argv=None) -> int:
 
     comm = Comm.init(device=cfg.device, timeout_s=cfg.comm_timeout_s)
     eng = BiscottiEngine(cfg, comm)
+    srv, flood = None, [a for a in ns.rpc_flood.split(",") if a.strip()] if comm.rank == 0 else []
+    if ns.rpc_listen and comm.rank == 0:
+        from .parallel import netrpc
+
+        host, port = ns.rpc_listen.rsplit(":", 1)
+        me = eng.lo
+        svc = netrpc.PeerService(eng.R, eng.fsm.chain, peer_id=me, sk=eng.sk[me],
+                                 noise=lambda it: eng.task.noise_scale(eng.sigma) * _noise_row(eng, me, it),
+                                 krum_thresh=max(1, eng.pc.krum_thresh))
+        srv = netrpc.RpcServer(svc.handlers(), host, int(port)).start()
+        eng.log.info("serving Peer net/rpc on %s:%d", *srv.addr)
     n = 0
     while ns.rounds is None or n < ns.rounds:
         r = eng.run_round()
         if r is None:
             eng.log.info("Reached the max iterations!")
             break
+        if flood:
+            from .parallel import netrpc
+
+            netrpc.flood_block(flood, eng.fsm.chain.latest())
         n += 1
+    if srv is not None:
+        srv.close()
     if cfg.colluders > 0:
         print(eng.stats["unmasked_updates"], eng.stats["total_updates"], cfg.colluders / 100.0, cfg.num_noisers)
     if ns.print_chain == "all" or (ns.print_chain == "rank0" and comm.rank == 0):
@@ -71,6 +96,13 @@ def main(argv=None) -> int:
     eng.close()
     comm.shutdown()
     return 0
+
+
+def _noise_row(eng, peer: int, it: int):
+    """Peer `peer`'s pre-sampled N(0,1) vector of iteration `it` (RequestNoise payload before scaling)."""
+    from .ops import ml as K
+
+    return K.noise_vector(peer, it, eng.d, eng.cfg.seed)
 
 
 if __name__ == "__main__":

@@ -139,6 +139,12 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
             HostCrypto(key, cfg.poly_size, self.T, cfg.host_threads)
         self.nchunks = self.crypto.nchunks
+        # one rank: the aggregation behind the committee's selection is enqueued natively (round.hip);
+        # BISCOTTI_NATIVE_SECAGG=0 keeps the Python path (A/B measurements)
+        self._native = None
+        if self.gpu and self.comm.world == 1 and os.environ.get("BISCOTTI_NATIVE_SECAGG", "1") == "1":
+            self._native = B.NativeSecAgg(self.crypto.eng, self.main_stream, self.side_stream, self.bg_stream,
+                                          10.0 ** cfg.precision)
         if cfg.pkey_file:
             ks = self.R.read_client_keys(cfg.pkey_file)
             self.sk = {i: ks[i][0] for i in range(self.N)}
@@ -292,6 +298,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             # the HBM-resident tables (up to ~90 GB) go now, not whenever the engine is collected
             if isinstance(self.crypto, DeviceCrypto):
                 self.crypto.eng.release()
+            if self._native is not None:
+                self._native.close()
+                self._native = None
             self.noise_rows = None
             if getattr(self, "side_cus", 0):
                 # every tensor used on the CU-masked stream is gone (round locals, the head above): flush the

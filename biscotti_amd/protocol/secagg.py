@@ -118,6 +118,8 @@ class SecAggMixin:
         T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
         audit = cfg.audit_aggregate
         kzg = cfg.kzg_audit != "off"
+        if self._native is not None and pts is not None and not isinstance(rowsel, list) and not kzg:
+            return self._aggregate_native(pts, ys, rowsel, contributing, part, now)
         (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
         kzg_in = None   # this rank's (commitment sums, witness sums, share sums) for the KZG audit
         main = S.current() if self.gpu else None
@@ -210,6 +212,23 @@ class SecAggMixin:
             if self.gpu:
                 out["kzg_events"] = [S.record(main), S.record(self.side_stream), S.record(self.bg_stream)]
         return out
+
+    def _aggregate_native(self, pts, ys, mask, contributing, part, now) -> dict:
+        """_aggregate's one-rank device path in two native calls (kernels/round.hip): the miners' sums, the
+        recovery and its read-back, then -- after the next round's pre-step is queued on the Gram stream
+        -- the aggregate audit.  Same kernels, same streams, same order as the Python path."""
+        cfg = self.cfg
+        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
+        na = self._native
+        W_new, coeffs, status, agg = na.secagg(pts.contiguous(), ys.contiguous(), mask, ccols, wcols, ycols_t, xs_t,
+                                               wts, A_dev, basis_dev, self.W, cfg.audit_aggregate)
+        S.hold(pts, ys, mask)   # read on the side and background streams
+        readback = na.readback()
+        if self._pipelined() and getattr(self.task, "stateless_step", False):
+            self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)
+        audit_ok = na.audit() if cfg.audit_aggregate else None
+        return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
+                "clock": None, "now": now, "readback": readback}
 
     # ------------------------------------------------------------------ read-backs and the audit
     def _d2h_async(self, *ts: torch.Tensor):

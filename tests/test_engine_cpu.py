@@ -109,7 +109,7 @@ def test_process_churn_rejoin_with_chain_sync():
     from biscotti_amd.protocol.engine import BiscottiEngine
 
     cfg = RunConfig(num_nodes=8, dataset="creditcard", num_verifiers=1, num_miners=2, num_noisers=1,
-                    noising=False, device="cpu", seed=5, churn_kill_per_min=6.0)
+                    noising=False, device="cpu", seed=5, churn_kill_per_min=4.8, deterministic_time=True)
     eng = BiscottiEngine(cfg)
     seeds0 = dict(eng.vrf_noise_seed)
     res = [eng.run_round() for _ in range(10)]
