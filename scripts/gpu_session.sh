@@ -26,6 +26,18 @@ if has long; then
   grep '^{' gpurun_out/bench_long_$TAG.txt | tail -1 > gpurun_out/bench_long_$TAG.json
   python -c "import json; d=json.load(open('gpurun_out/bench_long_$TAG.json')); print('long ms/round', round(d['ms_per_step'],3), 'acc', d['final_test_acc'], 'phases', {k: round(v,3) for k,v in d['phase_ms_per_round'].items()})"
 fi
+if has acc10; then   # headline accuracy over 10 independent 100-round runs (final + last-10 mean, mean +- std)
+  timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 --seeds 10 > gpurun_out/acc10_$TAG.txt 2>&1 || { echo "ACC10 FAILED"; tail -20 gpurun_out/acc10_$TAG.txt; exit 1; }
+  grep '^{' gpurun_out/acc10_$TAG.txt | tail -1 > gpurun_out/acc10_$TAG.json
+  python -c "import json; d=json.load(open('gpurun_out/acc10_$TAG.json')); print('acc10 final', d['final_test_acc_mean_std'], 'last10', d['test_acc_last10_mean_std'], 'ms', round(d['ms_per_step'],3))"
+fi
+for cfgname in poison30 poison30_200; do
+  if has $cfgname; then   # BASELINE config 4 over 5 seeds
+    timeout -k 10 600 python bench.py --gpus 1 --config $cfgname --steps 20 --warmup 5 --seeds 5 > gpurun_out/${cfgname}_$TAG.txt 2>&1 || { echo "$cfgname FAILED"; tail -20 gpurun_out/${cfgname}_$TAG.txt; exit 1; }
+    grep '^{' gpurun_out/${cfgname}_$TAG.txt | tail -1 > gpurun_out/${cfgname}_$TAG.json
+    python -c "import json; d=json.load(open('gpurun_out/${cfgname}_$TAG.json')); print('$cfgname acc', d['final_test_acc_mean_std'], 'last10', d['test_acc_last10_mean_std'], 'att', d['attack_rate_last10_mean_std'], 'ms', round(d['ms_per_step'],3))"
+  fi
+done
 for n in 2 4; do
   if has rccl$n; then
     BISCOTTI_RCCL_SHARED_DEVICE=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \

@@ -169,3 +169,26 @@ def test_lazy_eval_resolves_the_same_numbers():
         eng.close()
     assert out[0] == out[1]
     assert all(e == e for _, e, _ in out[1])   # no NaN left after drain()
+
+
+def test_mnist_label_flip_rejection_floor_default_noise():
+    """BASELINE config 4 (MNIST, 30% 1->7 label-flip poisoners, epsilon 1) under the reference's DEFAULT
+    noise semantics (workers noised with their noisers' shared pre-sampled vectors, client_obj.py:97-98):
+    after a 10-round burn-in at least 75% of the poisoners' updates that reach a verifier stay out of the
+    blocks -- today's measured floor (0.80-0.84 rejection at 100 peers, docs/ROBUSTNESS.md), asserted so a
+    regression shows.  The reference's 0.029 attack rate stays parity-unpinned (synthetic digits)."""
+    eng = _engine(num_nodes=100, poisoning=0.3, epsilon=1.0, seed=7)
+    pois = {p for p in range(100) if eng.fsm.is_poisoner(p)}
+    seen = kept = 0
+    for _ in range(30):
+        r = eng.run_round()
+        if r.iteration < 10:
+            continue
+        judged = set().union(*r.inboxes.values()) if r.inboxes else set()
+        seen += len(judged & pois)
+        kept += len(set(r.node_list) & pois)
+    ok, why = eng.fsm.chain.verify()
+    eng.close()
+    assert ok, why
+    assert seen > 0
+    assert kept <= 0.25 * seen, (kept, seen)
