@@ -203,16 +203,21 @@ def main() -> int:
     last = None
     phases: dict = {}
     results = []
+    walls = []
     for _ in range(a.steps):
+        tr = time.perf_counter()
         last = eng.run_round()
+        walls.append(time.perf_counter() - tr)
         results.append(last)
         for k, v in last.phases.items():
             phases[k] = phases.get(k, 0.0) + v
+    t_drain = time.perf_counter()
     if hasattr(eng, "drain"):
         eng.drain()   # host work of the timed rounds still in flight (and their evaluations) inside the clock
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    drain_s = time.perf_counter() - t_drain
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     host_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)   # every thread of this rank
     stats0 = {k: v for k, v in getattr(eng, "stats", {}).items() if isinstance(v, (int, float))}
@@ -290,6 +295,8 @@ def main() -> int:
             "final_test_acc_mean_std": ms(finals),
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
+            "drain_ms": 1e3 * drain_s,          # inside the timed window: joins of the last rounds' work
+            "round_wall_ms": [round(1e3 * w, 3) for w in walls],
             "host_cpu_ms_per_round": 1e3 * host_cpu / max(a.steps, 1),
             "engine_stats": stats0,
             "table_gb": (eng.crypto.eng.table_bytes() / 1e9) if hasattr(getattr(eng, "crypto", None), "eng") else 0.0,
