@@ -204,6 +204,7 @@ def main() -> int:
     phases: dict = {}
     results = []
     walls = []
+    seg0 = torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) if eng.gpu else 0
     for _ in range(a.steps):
         tr = time.perf_counter()
         last = eng.run_round()
@@ -218,6 +219,8 @@ def main() -> int:
     comm.barrier()
     elapsed = time.perf_counter() - t0
     drain_s = time.perf_counter() - t_drain
+    # device memory segments the caching allocator had to hipMalloc inside the timed window
+    seg_new = (torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) - seg0) if eng.gpu else 0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     host_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)   # every thread of this rank
     stats0 = {k: v for k, v in getattr(eng, "stats", {}).items() if isinstance(v, (int, float))}
@@ -296,6 +299,7 @@ def main() -> int:
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
             "drain_ms": 1e3 * drain_s,          # inside the timed window: joins of the last rounds' work
+            "device_segments_allocated_timed": seg_new,
             "round_wall_ms": [round(1e3 * w, 3) for w in walls],
             "host_cpu_ms_per_round": 1e3 * host_cpu / max(a.steps, 1),
             "engine_stats": stats0,

@@ -213,8 +213,11 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         # audit sums (kernels/kzg.hip) -- gets a stream of its own
         self.vrf_stream = torch.cuda.Stream(device=self.dev, priority=lo)
         # the pre-step and its Krum Gram (_queue_pre_step): beside the main stream, so the evaluation and
-        # the audit queued there do not wait for it
-        self.gram_stream = torch.cuda.Stream(device=self.dev, priority=lo)
+        # the audit queued there do not wait for it.  High priority: the Gram is on the next round's critical
+        # path (Krum waits for it) and is released together with the speculative MSM; at low priority the MSM
+        # took the CUs first and the Gram ran 5x slower (200 -> 1000 us; verify.krum_wait 0.32 -> 0.02 ms,
+        # driver-style round 1.75 -> 1.55 ms, profiles/r3/gram_priority_ab.txt)
+        self.gram_stream = torch.cuda.Stream(device=self.dev, priority=hi)
         # small uploads that must not queue behind any round work (_spec_head_launch)
         self.upload_stream = torch.cuda.Stream(device=self.dev, priority=hi)
         torch.cuda.synchronize(self.dev)   # everything set up so far is visible to the new streams
