@@ -637,16 +637,19 @@ extern "C" int bsc_alive_compact(const int* alive, int n, int* compact, void* st
 
 // alive[map[j]] = accept[j] for every verified update j with a speculative row (map[j] >= 0):
 // agent-scope stores, read by a k_shares_msm still running on another stream.
-extern "C" __global__ void k_set_alive(const int* accept, const int* map, int n, int* alive) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const int r = map[j];
-  if (r >= 0) __hip_atomic_store(alive + r, accept[j] ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// alive[i] = accept[src[i]] for every speculative row i (src[i] < 0: the row is no candidate of the
+// selection -- e.g. a peer the pre-step computed that turned out not to be a worker -- and is dropped).
+// Device-scope stores: a share MSM still running on another stream skips the rows cleared here.
+extern "C" __global__ void k_set_alive(const int* accept, const int* src, int n, int* alive) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int j = src[i];
+  __hip_atomic_store(alive + i, (j >= 0 && accept[j]) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-extern "C" int bsc_set_alive(const int* accept, const int* map, int n, int* alive, void* stream) {
+extern "C" int bsc_set_alive(const int* accept, const int* src, int n, int* alive, void* stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_set_alive, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, accept, map, n, alive);
+  hipLaunchKernelGGL(k_set_alive, dim3(blocks_for(n, 64)), dim3(64), 0, (hipStream_t)stream, accept, src, n, alive);
   return (int)hipGetLastError();
 }
 

@@ -256,13 +256,14 @@ def sum_rows(pts: torch.Tensor, rows: torch.Tensor | None, cols: torch.Tensor | 
     return out
 
 
-def set_alive(accept: torch.Tensor, rows_map: torch.Tensor, alive: torch.Tensor) -> None:
-    """alive[rows_map[j]] = accept[j] for rows_map[j] >= 0 (device-scope stores: a share MSM running
-    on another stream sees them and skips the rejected rows).  accept, rows_map: int32 [n]."""
-    n = accept.numel()
-    assert accept.dtype == torch.int32 and rows_map.dtype == torch.int32 and rows_map.numel() == n
+def set_alive(accept: torch.Tensor, src: torch.Tensor, alive: torch.Tensor) -> None:
+    """alive[i] = accept[src[i]] for every speculative row i, 0 where src[i] < 0 (device-scope stores: a
+    share MSM running on another stream sees them and skips the dropped rows).  accept: int32 over the
+    selection's rows; src, alive: int32 [n speculative rows]."""
+    n = alive.numel()
+    assert accept.dtype == torch.int32 and src.dtype == torch.int32 and src.numel() == n
     assert alive.dtype == torch.int32
-    _check(hip().bsc_set_alive(_ptr(accept), _ptr(rows_map), n, _ptr(alive), _stream()), "set_alive")
+    _check(hip().bsc_set_alive(_ptr(accept), _ptr(src), n, _ptr(alive), _stream()), "set_alive")
 
 
 def marshal_host(pts: torch.Tensor) -> "np.ndarray":

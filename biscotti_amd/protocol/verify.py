@@ -92,7 +92,7 @@ class VerifyMixin:
     # ------------------------------------------------------------------ committee Multi-Krum
     def _krum_static(self, xrow, U, plan, live, inboxes, spec, arrivals=None) -> dict:
         """The part of a Krum launch that does not depend on the noisers (inbox rows, leader arrival
-        ranks, Krum row -> speculative MSM row), uploaded in ONE copy.  run_round prepares it while
+        ranks, speculative MSM row -> Krum row), uploaded in ONE copy.  run_round prepares it while
         the host still waits for the VRF outputs."""
         fsm = self.fsm
         vs = [v for v in plan.verifiers if v in inboxes]
@@ -104,9 +104,11 @@ class VerifyMixin:
                 rank[xrow[w]] = r
         ups = [(inbox_np, torch.int32), (rank, torch.int32)]
         if spec is not None:
-            amap = np.full(U, -1, np.int32)
-            amap[[xrow[w] for w in spec[0]]] = np.arange(len(spec[0]), dtype=np.int32)
-            ups.append((amap, torch.int32))
+            # speculative row -> selection row; -1 for rows that are no live worker (the pre-step's MSM
+            # covers every local peer): their flags are cleared, so neither the MSM nor the sums use them
+            wk = {w for w in plan.workers if live[w]}
+            src = np.asarray([xrow[w] if w in wk and w in xrow else -1 for w in spec[0]], np.int32)
+            ups.append((src, torch.int32))
         got = h2d_many(ups, self.dev)
         return {"U": U, "n": n, "clip": fsm.krum_clip(n), "need": len(plan.verifiers) // 2,
                 "cap": fsm.leader_cap_size(), "inbox": got[0], "rank": got[1],
@@ -134,7 +136,8 @@ class VerifyMixin:
         """Device-side follow-up of the committee's selection: this rank's share rows' flags become the
         leader's block mask (rows outside it are cancelled) and the aggregation of the kept rows is
         queued -- on EVERY rank, with or without local rows, so the aggregation's collective lines up;
-        its handle lands in box['sa'].  amap_t: device int32 [U], Krum row -> speculative MSM row."""
+        its handle lands in box['sa'].  amap_t: device int32 [n speculative rows], speculative row -> Krum
+        row (-1: dropped)."""
         sp = spec[1] if spec is not None else None
         pred = self._predict_miners(plan, live) if self.gpu and self.cfg.secure_agg else None
 

@@ -179,7 +179,7 @@ def test_chunk_check_audits_aggregate(rt, d, b0):
 
 def test_shares_msm_late_cancellation(rt):
     """Rows whose alive flag is cleared are skipped; the others are bit-identical to a full run,
-    and set_alive maps verifier-order accept flags onto speculative rows."""
+    and set_alive gathers the selection's accept flags onto the speculative rows."""
     from biscotti_amd.ops import bn256 as B
     d = 40
     key = rt.CommitKey.generate(d, 3)
@@ -188,10 +188,11 @@ def test_shares_msm_late_cancellation(rt):
     rows = torch.arange(4, dtype=torch.int32, device="cuda")
     full_p, full_y = eng.shares(q, rows)
     alive = torch.ones(4, dtype=torch.int32, device="cuda")
-    # verifier order [2, 0, 3, 1 (not speculative)]: accept, reject, accept, reject
-    B.set_alive(torch.tensor([1, 0, 1, 0], dtype=torch.int32, device="cuda"),
-                torch.tensor([2, 0, 3, -1], dtype=torch.int32, device="cuda"), alive)
-    assert alive.tolist() == [0, 1, 1, 1]
+    # selection rows: accept, reject, accept, accept; speculative rows 0..3 are selection rows 1, none
+    # (not a candidate), 0, 3
+    B.set_alive(torch.tensor([1, 0, 1, 1], dtype=torch.int32, device="cuda"),
+                torch.tensor([1, -1, 0, 3], dtype=torch.int32, device="cuda"), alive)
+    assert alive.tolist() == [0, 0, 1, 1]
     p, y = eng.shares(q, rows, alive=alive)
-    for r in (1, 2, 3):
+    for r in (2, 3):
         assert torch.equal(p[r], full_p[r]) and torch.equal(y[r], full_y[r])
