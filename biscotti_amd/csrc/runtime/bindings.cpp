@@ -838,9 +838,10 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         for (auto& o : j.out) r.append(py::make_tuple(P(o.first), P(o.second)));
         return r;
       })
-      // join without materialising the proofs as Python objects (callers that discard them)
+      // join without materialising the proofs as Python objects (callers that discard them); a finished
+      // job is joined without the GIL round trip
       .def("wait", [](VrfJob& j) {
-        {
+        if (!j.finished.load(std::memory_order_acquire)) {
           py::gil_scoped_release rel;
           j.done.wait();
         }

@@ -108,6 +108,8 @@ class RoundHeadMixin:
             if sn is not None:
                 # launched at the previous block's build (_spec_head_launch), from this very plan
                 cand, spec, head["arrivals"] = sn["cand"], sn["spec"], sn["arrivals"]
+                if sn.get("kst") is not None:
+                    head["kst"] = sn["kst"]   # Krum's static tables, built in the previous round's audit wait
                 self.stats["spec_head"] = self.stats.get("spec_head", 0) + 1
             elif self.gpu and cfg.secure_agg:
                 # replicated on every rank: the rows (of all ranks) whose shares are computed up front
@@ -254,7 +256,7 @@ class RoundHeadMixin:
         with S.use(self.upload_stream):
             sp = self.crypto.shares_async(pre["qdelta"], [w - self.lo for w in spec_workers], side,
                                           group_rows=SPEC_GROUP_ROWS)
-        self._spec_next = {"hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
+        self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
                            "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
                            "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}
 

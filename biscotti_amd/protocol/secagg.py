@@ -357,16 +357,17 @@ class SecAggMixin:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()
                 self._idle_work = None
-            if self.gpu and (self._pre_vrf_work or self._evals):
+            if self.gpu:
                 # the next round's VRF batch has just started (_early_vrf_submit): this round's deferred
-                # signature prep (its batch starts behind those outputs) and the earlier rounds' evaluation
-                # read-backs fill the audit wait instead of the next round's VRF wait
+                # signature prep (its batch starts behind those outputs), the earlier rounds' evaluation
+                # read-backs and the next round's host preparation fill the audit wait
                 with tm.phase("recover.idle"):
                     ej = self._early_vrf["job"] if self._early_vrf is not None else None
                     work, self._pre_vrf_work = self._pre_vrf_work, []
                     for f in work:
                         f(ej)
                     self._resolve_evals()
+                    self._prepare_next_in_wait()
             with tm.phase("recover.audit"):
                 ok = audit_ok()
             if not ok.all():
@@ -382,6 +383,24 @@ class SecAggMixin:
             if self._kzg_pending:
                 self._kzg_poll()
         return block
+
+    def _prepare_next_in_wait(self) -> None:
+        """Host work of the NEXT round that is ready before this round's audit is read: the host marshal of
+        its commitments (the pre-step's commitment MSM has usually landed by now; never waited for here)
+        and Krum's static tables for the successor plan the speculative MSM was launched from.  Both are
+        used only if the next head adopts the pre-step / the speculative plan (the committed block matches)."""
+        pre, sn = self._pre, self._spec_next
+        pc = pre.get("commits") if pre is not None else None
+        if pc is not None and getattr(pc, "value", 1) is None and pc.event.query():
+            pc.result()
+        if sn is None or sn.get("kst") is not None or pre is None or sn.get("pre") is not pre:
+            return
+        g = pre.get("gram")
+        cfg = self.cfg
+        if g is None or not (cfg.verification and cfg.defense == "KRUM" and sn["inboxes"]):
+            return
+        sn["kst"] = self._krum_static(g["xrow"], g["U1"], sn["plan"], [1] * self.N, sn["inboxes"], sn["spec"],
+                                      sn["arrivals"])
 
     # ------------------------------------------------------------------ plain aggregation path
     def _plain_aggregation(self, plan, live, approved, delta_w, noised, local_workers, commit_of, signatures,

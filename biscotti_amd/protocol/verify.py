@@ -37,6 +37,7 @@ class VerifyMixin:
         # the lottery reads the job's outputs natively (no 64-byte Python objects in between)
         sel = self.R.select_noisers_job(stake, fut_noise, list(index) if index is not None else [], local_workers,
                                         self.cfg.num_noisers, self.N)
+        self._noise_arr = (local_workers, sel)   # the same ids as an array, in local_workers order
         return dict(zip(local_workers, sel.tolist()))
 
     def _noise_scales(self, noisers: dict, ws: list) -> np.ndarray:
@@ -55,12 +56,25 @@ class VerifyMixin:
         nz = np.zeros((self.maxlocal, nn_), np.int32)
         sc = np.zeros((self.maxlocal, nn_), np.float32)
         if local_workers and noisers:
-            at = np.asarray([w - self.lo for w in local_workers])
-            ids = np.asarray([noisers[w] for w in local_workers], np.int64)
+            at = np.asarray(local_workers, np.int64) - self.lo
+            arr = getattr(self, "_noise_arr", None)
+            # the lottery's array (same ids, local_workers order) when it is this round's; else from the dict
+            ids = arr[1].astype(np.int64, copy=False).reshape(len(local_workers), -1) \
+                if arr is not None and arr[0] is local_workers else \
+                np.asarray([noisers[w] for w in local_workers], np.int64).reshape(len(local_workers), -1)
             assert ids.min() >= 0 and ids.max() < self.N, "noiser id out of range"
             nz[at] = ids
-            sc[at] = self._noise_scales(noisers, local_workers)
+            w = np.full(ids.shape, self.task.noise_scale(self.sigma), np.float32)
+            if self.colluders:
+                w[np.isin(ids, self._colluder_arr())] = 0.0
+            sc[at] = w
         return nz, sc
+
+    def _colluder_arr(self) -> np.ndarray:
+        arr = getattr(self, "_colluders_np", None)
+        if arr is None:
+            arr = self._colluders_np = np.fromiter(sorted(self.colluders), np.int64)
+        return arr
 
     def _worker_rows(self, t: torch.Tensor, row_of: dict, ws: list) -> torch.Tensor:
         """Rows of t for the workers ws, in that order."""
@@ -97,17 +111,30 @@ class VerifyMixin:
         fsm = self.fsm
         vs = [v for v in plan.verifiers if v in inboxes]
         n = len(inboxes[vs[0]])
-        inbox_np = np.asarray([[xrow[w] for w in inboxes[v]] for v in vs], np.int32)
+        # peer -> row of xrow as an array (-1: no row), built once per xrow mapping: the lookups below are
+        # numpy gathers instead of per-element dict lookups on the round's host thread
+        key = id(xrow)
+        cached = getattr(self, "_xrow_np", None)
+        if cached is None or cached[0] != key or cached[1] is not xrow:
+            xa = np.full(self.N, -1, np.int64)
+            xa[np.fromiter(xrow.keys(), np.int64)] = np.fromiter(xrow.values(), np.int64)
+            cached = self._xrow_np = (key, xrow, xa)
+        xa = cached[2]
+        live_np = np.asarray(live, bool)
+        inbox_np = xa[np.asarray([inboxes[v] for v in vs], np.int64)].astype(np.int32)
         rank = np.full(U, -1, np.int32)
-        for r, w in enumerate(arrivals if arrivals is not None else fsm.leader_arrivals()):
-            if live[w] and w in xrow:
-                rank[xrow[w]] = r
+        arr = np.asarray(arrivals if arrivals is not None else fsm.leader_arrivals(), np.int64)
+        ok = live_np[arr] & (xa[arr] >= 0)
+        rank[xa[arr[ok]]] = np.nonzero(ok)[0].astype(np.int32)
         ups = [(inbox_np, torch.int32), (rank, torch.int32)]
         if spec is not None:
             # speculative row -> selection row; -1 for rows that are no live worker (the pre-step's MSM
             # covers every local peer): their flags are cleared, so neither the MSM nor the sums use them
-            wk = {w for w in plan.workers if live[w]}
-            src = np.asarray([xrow[w] if w in wk and w in xrow else -1 for w in spec[0]], np.int32)
+            wk = np.zeros(self.N, bool)
+            pw = np.asarray(plan.workers, np.int64)
+            wk[pw[live_np[pw]]] = True
+            sw = np.asarray(spec[0], np.int64)
+            src = np.where(wk[sw] & (xa[sw] >= 0), xa[sw], -1).astype(np.int32)
             ups.append((src, torch.int32))
         got = h2d_many(ups, self.dev)
         return {"U": U, "n": n, "clip": fsm.krum_clip(n), "need": len(plan.verifiers) // 2,

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--scale", type=int, default=30000, help="uniform coefficient range (--dist uniform)")
     ap.add_argument("--dist", default="real", choices=["real", "uniform"],
                     help="real: N(0, 1500^2) integers, the measured spread of quantised MNIST updates")
+    ap.add_argument("--density", type=float, default=1.0,
+                    help="fraction of nonzero coefficients (quantised updates after the first rounds: 0.1-0.25)")
     ap.add_argument("--b0", type=int, default=None)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
@@ -39,10 +41,12 @@ def main():
         c = np.rint(rng.normal(0.0, 1500.0, size=(a.workers, a.d))).astype(np.int64)
     else:
         c = rng.integers(-a.scale, a.scale, size=(a.workers, a.d), dtype=np.int64)
+    if a.density < 1.0:
+        c = np.where(rng.random(c.shape) < a.density, c, 0)
     coeffs = torch.from_numpy(c).cuda()
     allrows = torch.arange(a.workers, dtype=torch.int32, device="cuda")
     rows = allrows[: a.rows].contiguous()
-    res = {"d": a.d, "dist": a.dist, "b0": eng.b0, "key_gen_s": t1 - t0, "table_build_s": t2 - t1,
+    res = {"d": a.d, "dist": a.dist, "density": a.density, "b0": eng.b0, "key_gen_s": t1 - t0, "table_build_s": t2 - t1,
            "table_gb": eng.table_bytes() / 1e9}
     for name, fn in [
         ("commit_rows_all_workers", lambda: eng.commit_rows(coeffs, allrows)),

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--warm", type=int, default=20)
     ap.add_argument("--set", action="append", default=[])
+    ap.add_argument("--wrap", default="", help="comma-separated engine methods (or task./crypto. methods) timed as events")
     a = ap.parse_args()
     comm = Comm.init()
     torch.set_num_threads(min(4, torch.get_num_threads()))
@@ -57,6 +58,26 @@ def main():
             yield
         events.append((name, s, time.perf_counter()))
     timer.phase = phase
+
+    def wrap(obj, name, label):
+        f = getattr(obj, name)
+
+        def w(*a, **kw):
+            s = time.perf_counter()
+            try:
+                return f(*a, **kw)
+            finally:
+                events.append(("@" + label, s, time.perf_counter()))
+        setattr(obj, name, w)
+    for m in filter(None, a.wrap.split(",")):
+        if m.startswith("task."):
+            wrap(eng.task, m[5:], m)
+        elif m.startswith("crypto."):
+            wrap(eng.crypto, m[7:], m)
+        elif m.startswith("fsm."):
+            wrap(eng.fsm, m[4:], m)
+        else:
+            wrap(eng, m, m)
     for _ in range(a.warm):
         eng.run_round()
     torch.cuda.synchronize()
