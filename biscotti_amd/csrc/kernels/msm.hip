@@ -468,11 +468,12 @@ extern "C" __global__ void __launch_bounds__(128) k_sum_rows(const uint32_t* pts
 // Two-level version: block = 32 columns x 8 row groups; each thread sums every 8th row of its
 // column, then an LDS tree over the 8 partials.  8x the parallelism of k_sum_rows, and the column
 // list may concatenate several miners' slots (one launch per rank).
-// row_mask (optional, indexed by input row): rows whose flag is 0 are left out -- the device-side
-// selection of the approved workers' shares, decided by the verification kernels on the GPU.
+// row_mask (optional, indexed by input row, or by position r in `rows` when mask_by_pos): rows whose
+// flag is 0 are left out -- the device-side selection of the approved workers' shares, decided by the
+// verification kernels on the GPU.
 extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
                                                              int nrows, const int* cols, int ncols,
-                                                             const int* row_mask, uint32_t* out) {
+                                                             const int* row_mask, int mask_by_pos, uint32_t* out) {
   // 16 columns x 16 row lanes per block: each lane's serial chain is nrows/16 additions, then a
   // 4-level LDS tree (the sums sit on the round's critical path: latency, not throughput, matters)
   __shared__ uint32_t sh[16][16][24];
@@ -488,7 +489,7 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
       const int rn = r + 16 < nrows ? r + 16 : r;
       const int rown = rows ? rows[rn] : rn;
       const jac nxt = ld_jac(pts + 24 * ((size_t)rown * ncols_in + col));
-      if (row_mask == nullptr || row_mask[row] != 0) acc = jac_add(acc, cur);
+      if (row_mask == nullptr || row_mask[mask_by_pos ? r : row] != 0) acc = jac_add(acc, cur);
       cur = nxt;
       row = rown;
     }
@@ -665,7 +666,17 @@ extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
                              int ncols, const int* row_mask, uint32_t* out, void* stream) {
   if (ncols <= 0) return 0;
   hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 16)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
-                     rows, nrows, cols, ncols, row_mask, out);
+                     rows, nrows, cols, ncols, row_mask, 0, out);
+  return (int)hipGetLastError();
+}
+
+// the same with row_mask indexed by the position in `rows` (a mask over a row list, e.g. the speculative
+// MSM's alive flags applied to the pre-step's per-peer chunk commitments)
+extern "C" int bsc_sum_rows2_pos(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
+                                 int ncols, const int* row_mask, uint32_t* out, void* stream) {
+  if (ncols <= 0) return 0;
+  hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 16)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
+                     rows, nrows, cols, ncols, row_mask, 1, out);
   return (int)hipGetLastError();
 }
 

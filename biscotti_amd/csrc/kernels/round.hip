@@ -24,6 +24,8 @@ extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, con
                              unsigned long long inv_lo, unsigned long long inv_hi, int d, const double* W,
                              double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out,
                              void* stream);
+extern "C" int bsc_sum_rows2_pos(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
+                                 int ncols, const int* row_mask, uint32_t* out, void* stream);
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
                                const uint32_t* csum, int nm, int nch, int* ok, void* stream);
 
@@ -91,7 +93,7 @@ extern "C" int bsc_round_secagg(void* ctx, const uint32_t* pts, int R, const lon
   if (c == nullptr || R <= 0) return -1;
   const int ncols_in = c->nch * (c->T + 1);
   RC_CHECK(hipEventRecord(c->ev_main, c->main));
-  if (audit) {
+  if (audit == 1) {   // audit == 2: the commitment sums were queued early (bsc_round_csum_early)
     RC_CHECK(hipStreamWaitEvent(c->side, c->ev_main, 0));
     RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, ccols, c->nch, mask, cs, c->side));
     RC_CHECK(hipEventRecord(c->ev_side, c->side));
@@ -113,6 +115,24 @@ extern "C" int bsc_round_audit(void* ctx, const long long* coeffs, const uint32_
   RC_CHECK(bsc_chunk_check(coeffs, c->d, c->poly, c->tbl_pk, c->b0, c->nw, cs, 1, c->nch, ok, c->main));
   RC_CHECK(hipMemcpyAsync(h_ok, ok, (size_t)c->nch * sizeof(int), hipMemcpyDeviceToHost, c->main));
   RC_CHECK(hipEventRecord(c->ev_audit, c->main));
+  return 0;
+}
+
+// The audit's commitment sums taken early, from the pre-step's per-peer chunk commitments instead of the
+// share MSM's commitment slots: as soon as the committee's selection has set the speculative rows' flags
+// (queued on main before main waits for the MSM), the side stream sums ccom[rows[r]] over the rows r
+// still alive -- the same rows the share sums use -- while the MSM is still running.  ccom: Jacobian
+// [npeer][nch][24], produced on another stream (ev_ccom).  bsc_round_secagg(.., audit = 2) then skips
+// its own commitment sums and bsc_round_audit waits for these.
+extern "C" int bsc_round_csum_early(void* ctx, const uint32_t* ccom, void* ev_ccom, const int* rows, int R,
+                                    const int* mask, uint32_t* cs) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || R <= 0) return -1;
+  RC_CHECK(hipEventRecord(c->ev_main, c->main));
+  RC_CHECK(hipStreamWaitEvent(c->side, c->ev_main, 0));
+  if (ev_ccom != nullptr) RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_ccom, 0));
+  RC_CHECK(bsc_sum_rows2_pos(ccom, c->nch, rows, R, nullptr, c->nch, mask, cs, c->side));
+  RC_CHECK(hipEventRecord(c->ev_side, c->side));
   return 0;
 }
 

@@ -356,7 +356,7 @@ class NativeSecAgg:
             t = self._by_shape[key] = torch.empty(shape, dtype=dtype, device=self.eng.device)
         return t
 
-    def secagg(self, pts, ys, mask, ccols, wcols, ycols, xs, wts: dict, A_dev, basis_dev, W, audit: bool):
+    def secagg(self, pts, ys, mask, ccols, wcols, ycols, xs, wts: dict, A_dev, basis_dev, W, audit: int):
         """Queue sums + recovery + read-back; returns (W_new, coeffs, status, agg) device tensors."""
         R = pts.shape[0]
         npts, nwc = ycols.numel(), wcols.numel()
@@ -373,6 +373,17 @@ class NativeSecAgg:
         if err != 0:
             raise RuntimeError(f"bsc_round_secagg failed ({err})")
         return W_new, self.coeffs, self.status, agg
+
+    def csum_early(self, ccom, ccom_event, rows, mask) -> None:
+        """Queue the audit's commitment sums now (side stream, behind what main has queued so far -- the
+        selection's flags -- and the pre-step's chunk commitments): cs = sum over the rows r with
+        mask[r] != 0 of ccom[rows[r]].  secagg(.., audit=2) then leaves them out."""
+        R = rows.numel()
+        assert ccom.dtype == torch.int32 and ccom.shape[1] == self.eng.nchunks and ccom.shape[-1] == 24
+        assert rows.dtype == torch.int32 and mask.dtype == torch.int32 and mask.numel() == R
+        ev = ccom_event.cuda_event if ccom_event is not None else None
+        _check(hip().bsc_round_csum_early(self.ctx, _ptr(ccom.contiguous()), ev, _ptr(rows), R, _ptr(mask),
+                                          _ptr(self.cs)), "round_csum_early")
 
     def readback(self):
         """Callable: waits for the recovery's read-back -> [status, W_new] numpy views (pinned)."""

@@ -28,6 +28,7 @@ class _PendingCommitments:
     def __init__(self, host: torch.Tensor, event, jac: torch.Tensor | None = None):
         self.host, self.event, self.value = host, event, None
         self.jac = jac   # device Jacobian rows (multi-rank rounds gather these, not host marshals)
+        self.ccom = self.ccom_event = self.src = None   # per-chunk commitments (chunked=True)
 
     def result(self) -> np.ndarray:
         if self.value is None:
@@ -143,19 +144,29 @@ class DeviceCrypto:
         self.eng = B.DeviceCommitEngine(key, poly, T, device)
         self.d, self.poly, self.T, self.nchunks = self.eng.d, poly, T, self.eng.nchunks
 
-    def commitments_async(self, qdelta: torch.Tensor, stream=None):
+    def commitments_async(self, qdelta: torch.Tensor, stream=None, chunked: bool = False):
         """Fixed-base MSM on device, queued download into pinned memory; result() waits for it and
         marshals on host with one batch inversion -> uint8 [n, 64].  The noise and Krum kernels
-        queue behind the copy instead of waiting for the host to finish with the commitments."""
+        queue behind the copy instead of waiting for the host to finish with the commitments.
+        chunked: the per-chunk commitments C_k (the commitment lanes of the share MSM) are computed
+        first and kept (pending.ccom [n, nch, 1, 24], ready at pending.ccom_event): the full
+        commitment is their sum, and the aggregate audit sums them over the kept rows long before the
+        share MSM ends (NativeSecAgg.csum_early)."""
         n = qdelta.shape[0]
         if n == 0:
             return _Ready(np.zeros((0, 64), np.uint8))
         main = S.current()
         stream = stream or main
         S.wait(stream, main)
+        ccom = ccom_ev = None
         with S.use(stream):
             rows = self._arange(n, qdelta.device)
-            jac = self.eng.commit_rows(qdelta.contiguous(), rows, check_rows=False)
+            if chunked:
+                ccom, _ = self.eng.shares(qdelta.contiguous(), rows, commit_only=True, check_rows=False)
+                ccom_ev = S.record(stream)
+                jac = self.eng.commitments(ccom)
+            else:
+                jac = self.eng.commit_rows(qdelta.contiguous(), rows, check_rows=False)
             # pinned landing buffers are reused round to round (two in flight: the round head is
             # opened while the previous round's marshals may still be read)
             self._pin_i = (getattr(self, "_pin_i", 0) + 1) % 2
@@ -168,7 +179,11 @@ class DeviceCrypto:
             d2h_into(host, jac)
             ev = S.record(stream)
         S.hold(qdelta, jac)
-        return _PendingCommitments(host, ev, jac)
+        out = _PendingCommitments(host, ev, jac)
+        if ccom is not None:
+            S.hold(ccom)
+            out.ccom, out.ccom_event, out.src = ccom, ccom_ev, qdelta
+        return out
 
     def commitments(self, qdelta: torch.Tensor) -> np.ndarray:
         return self.commitments_async(qdelta).result()

@@ -208,7 +208,8 @@ class RoundHeadMixin:
             delta, qdelta = self.task.step(W, it, list(self.local))
             ev = S.record()
             out = {"W": W, "it": it, "delta": delta, "qdelta": qdelta, "ev": ev,
-                   "commits": self.crypto.commitments_async(qdelta, self.bg_stream)}
+                   "commits": self.crypto.commitments_async(
+                       qdelta, self.bg_stream, chunked=self._native is not None and self.cfg.audit_aggregate)}
         S.hold(delta, qdelta)
         if self._noise_krum():
             # the noise-aware Krum's d-dimensional phase over EVERY peer's delta (the workers are not known

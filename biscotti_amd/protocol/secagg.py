@@ -68,11 +68,20 @@ class SecAggMixin:
         contributing, part = pred
         sp = spec[1] if spec is not None else None
         pts = ys = alive = None
+        early_cs = False
         if sp is not None:
             sp.launch()
             pts, ys, alive = sp.pts, sp.ys, sp.alive
+            cfg = self.cfg
+            pc = getattr(self, "_cur_commits", None)
+            if self._native is not None and cfg.audit_aggregate and cfg.kzg_audit == "off" and pc is not None \
+                    and getattr(pc, "ccom", None) is not None and pc.src is sp.qdelta:
+                # the audit's commitment sums from the pre-step's chunk commitments, queued before main waits
+                # for the MSM: they run while the MSM is still busy, not after it
+                self._native.csum_early(pc.ccom, pc.ccom_event, sp.rows_t, alive)
+                early_cs = True
             S.current().wait_event(sp.ev)          # the MSM's shares
-        agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration))
+        agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration), early_cs=early_cs)
         agg["contributing"], agg["part"], agg["accepted"], agg["node"] = list(contributing), dict(part), None, node
         return agg
 
@@ -102,7 +111,7 @@ class SecAggMixin:
                 self._agg_idx[key] = hit
         return hit
 
-    def _aggregate(self, pts, ys, rowsel, contributing, part, now) -> dict:
+    def _aggregate(self, pts, ys, rowsel, contributing, part, now, early_cs: bool = False) -> dict:
         """Secure aggregation of this rank's kept rows, combined over ranks, then exact recovery.
 
         Every miner sums the shares it received (aggregateSecret, kyber.go:244-287) and the leader
@@ -119,7 +128,7 @@ class SecAggMixin:
         audit = cfg.audit_aggregate
         kzg = cfg.kzg_audit != "off"
         if self._native is not None and pts is not None and not isinstance(rowsel, list) and not kzg:
-            return self._aggregate_native(pts, ys, rowsel, contributing, part, now)
+            return self._aggregate_native(pts, ys, rowsel, contributing, part, now, early_cs)
         (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
         kzg_in = None   # this rank's (commitment sums, witness sums, share sums) for the KZG audit
         main = S.current() if self.gpu else None
@@ -213,7 +222,7 @@ class SecAggMixin:
                 out["kzg_events"] = [S.record(main), S.record(self.side_stream), S.record(self.bg_stream)]
         return out
 
-    def _aggregate_native(self, pts, ys, mask, contributing, part, now) -> dict:
+    def _aggregate_native(self, pts, ys, mask, contributing, part, now, early_cs: bool = False) -> dict:
         """_aggregate's one-rank device path in two native calls (kernels/round.hip): the miners' sums, the
         recovery and its read-back, then -- after the next round's pre-step is queued on the Gram stream
         -- the aggregate audit.  Same kernels, same streams, same order as the Python path."""
@@ -221,7 +230,8 @@ class SecAggMixin:
         (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
         na = self._native
         W_new, coeffs, status, agg = na.secagg(pts.contiguous(), ys.contiguous(), mask, ccols, wcols, ycols_t, xs_t,
-                                               wts, A_dev, basis_dev, self.W, cfg.audit_aggregate)
+                                               wts, A_dev, basis_dev, self.W,
+                                               (2 if early_cs else 1) if cfg.audit_aggregate else 0)
         S.hold(pts, ys, mask)   # read on the side and background streams
         readback = na.readback()
         if self._pipelined() and getattr(self.task, "stateless_step", False):

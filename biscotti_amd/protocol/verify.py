@@ -221,6 +221,7 @@ class VerifyMixin:
         workers, local_workers, inboxes = head["workers"], head["local_workers"], head["inboxes"]
         row_of, spec, krum_pre = head["row_of"], head["spec"], head.get("krum_pre")
         pending_commits, fut_noise = head["pending_commits"], head["fut_noise"]
+        self._cur_commits = pending_commits   # the early audit sums read its per-chunk commitments
         single = comm.world == 1
         commit_of = _CommitTable()
         g_commit = g_noised = g_delta = g_ts = None
