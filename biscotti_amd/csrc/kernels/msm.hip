@@ -184,17 +184,21 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
 // coeffs: int64 [*, d] (row stride d); rows: worker rows to process.
 // tbl_pk: [d][PB][16]; tbl_wb: [nchunks][J][PB][T][16]; PB = E0 + (NW-1)*128 entries per base.
 // out_pts: Jacobian [nrows][nchunks][S][24] with S = T+1 (slots 0..T-1 witnesses, slot T the chunk
-// commitment) or S = 1 (commit_only: chunk commitments only).  out_y: int64 [nrows][nchunks][T].
+// commitment) or S = 1 (commit_only == 1: chunk commitments only).  commit_only == 2: witnesses and
+// share values only -- slot T is left untouched (the caller has the chunk commitments already), so a
+// group is T lanes instead of T+1 and no wave runs the commitment lane's extra c_0 addition.
+// out_y: int64 [nrows][nchunks][T].
 extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
     int poly, int T, int B0, int NW, int commit_only, const int* alive, const int* compact, int group_rows,
     uint32_t* out_pts, long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
-  const int S = commit_only ? 1 : T + 1;
+  const int S = commit_only == 1 ? 1 : T + 1;   // output slots per (row, chunk)
+  const int SL = commit_only == 2 ? T : S;      // lanes per (row, chunk)
   // compact (optional): [count, row...] -- only the listed rows are computed, packed densely over the
   // grid (a rejected row costs no SIMD lanes); the grid is sized for nrows, the surplus exits at once
   const int neff = compact != nullptr ? compact[0] : nrows;
-  const long long total = (long long)neff * nchunks * S;
+  const long long total = (long long)neff * nchunks * SL;
   // group_rows G > 0: rows are taken G at a time in list order (the speculative rows arrive sorted
   // by their arrival at the leader), chunk-major inside a group, and the XCD remap is applied per
   // 64-block super-block -- so work proceeds through the row list in dispatch order (rows the
@@ -212,13 +216,13 @@ extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
   const long long g = (long long)lb * blockDim.x + threadIdx.x;
   if (g >= total) return;
   const int G = group_rows > 0 ? min(group_rows, neff) : neff;
-  const long long per_group = (long long)G * nchunks * S;
+  const long long per_group = (long long)G * nchunks * SL;
   const int gq = (int)(g / per_group);
   const int r0 = gq * G, gr = min(G, neff - r0);
   const long long gg = g - (long long)gq * per_group;
-  // chunk-major inside the group: consecutive groups of S lanes share a chunk (and its table lines)
-  const int slot = (int)(gg % S);
-  const long long grp = gg / S;
+  // chunk-major inside the group: consecutive groups of SL lanes share a chunk (and its table lines)
+  const int slot = (int)(gg % SL);
+  const long long grp = gg / SL;
   const int pos = r0 + (int)(grp % gr);
   const int r = compact != nullptr ? compact[1 + pos] : pos;
   const int k = (int)(grp / gr);
@@ -229,7 +233,7 @@ extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
   const int row = rows[r];
   const int prev = k * poly;
   const int L = min(poly, d - prev);
-  const bool is_commit = commit_only || slot == T;
+  const bool is_commit = commit_only == 1 || slot == T;
   const int J = poly - 1;
   const long long* c = coeffs + (size_t)row * d + prev;
 
@@ -597,9 +601,10 @@ extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, i
                               const int* alive, const int* compact, int group_rows, uint32_t* out_pts,
                               long long* out_y, void* stream) {
   if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;  // every int64 scalar must be covered
+  if (commit_only < 0 || commit_only > 2) return -1;
   const int nchunks = (d + poly - 1) / poly;
-  const int S = commit_only ? 1 : T + 1;
-  const long long n = (long long)nrows * nchunks * S;
+  const int SL = commit_only == 1 ? 1 : commit_only == 2 ? T : T + 1;
+  const long long n = (long long)nrows * nchunks * SL;
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_shares_msm, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows,
                      nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, compact, group_rows, out_pts,

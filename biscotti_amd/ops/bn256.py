@@ -140,9 +140,11 @@ class DeviceCommitEngine:
         n = rows.numel()
         if n and check_rows:  # .item() synchronises the stream: callers passing arange skip it
             assert int(rows.min()) >= 0 and int(rows.max()) < coeffs.shape[0], "row index out of range"
-        S = 1 if commit_only else self.T + 1
+        commit_only = int(commit_only)   # 2: witnesses + share values only (slot T left unwritten)
+        S = 1 if commit_only == 1 else self.T + 1
         pts = torch.empty((n, self.nchunks, S, 24), dtype=torch.int32, device=self.device)
-        ys = None if commit_only else torch.empty((n, self.nchunks, self.T), dtype=torch.int64, device=self.device)
+        ys = None if commit_only == 1 else torch.empty((n, self.nchunks, self.T), dtype=torch.int64,
+                                                       device=self.device)
         cidx = None
         if alive is not None:
             assert alive.dtype == torch.int32 and alive.numel() == n
@@ -150,7 +152,7 @@ class DeviceCommitEngine:
                 cidx = torch.empty((n + 1,), dtype=torch.int32, device=self.device)
                 _check(hip().bsc_alive_compact(_ptr(alive), n, _ptr(cidx), _stream()), "alive_compact")
         _check(hip().bsc_shares_msm(_ptr(coeffs), self.d, _ptr(rows), n, _ptr(self.tbl_pk), _ptr(self.tbl_wb),
-                                    self.poly, self.T, self.b0, self.nw, int(commit_only), _ptr(alive), _ptr(cidx),
+                                    self.poly, self.T, self.b0, self.nw, commit_only, _ptr(alive), _ptr(cidx),
                                     int(group_rows), _ptr(pts), _ptr(ys), _stream()),
                "shares_msm")
         return pts, ys

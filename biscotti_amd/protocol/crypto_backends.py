@@ -112,8 +112,12 @@ class _SpecShares:
     flag per row) is cleared for rows the verifiers reject; the MSM skips flagged rows, whether the
     flags were cleared before it started or while it runs.  Consumers wait on `ev`."""
 
-    def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream, deferred: bool = False, group_rows: int = 0):
+    def __init__(self, eng, qdelta: torch.Tensor, rows: list, stream, deferred: bool = False, group_rows: int = 0,
+                 no_commit: bool = False):
         self.eng, self.qdelta, self.rows, self.stream = eng, qdelta, rows, stream
+        # no_commit: the chunk-commitment slots are not computed (the pre-step's chunk commitments feed the
+        # audit); a consumer that needs them must not use these tensors
+        self.no_commit = no_commit
         self.group_rows = 0 if deferred else group_rows
         # the row list and the all-ones flags in ONE upload (no fill kernel), on the caller's stream
         self.rows_t, self.alive = h2d_many([(rows, torch.int32), (np.ones(len(rows), np.int32), torch.int32)],
@@ -129,8 +133,9 @@ class _SpecShares:
         main = S.current()
         S.wait(self.stream, main)              # qdelta (and any flag updates) come from main
         with S.use(self.stream):
-            self.pts, self.ys = self.eng.shares(self.qdelta, self.rows_t, check_rows=False, alive=self.alive,
-                                                compact=self.deferred, group_rows=self.group_rows)
+            self.pts, self.ys = self.eng.shares(self.qdelta, self.rows_t, commit_only=2 if self.no_commit else 0,
+                                                check_rows=False, alive=self.alive, compact=self.deferred,
+                                                group_rows=self.group_rows)
             self.ev = torch.cuda.Event()
             self.ev.record(self.stream)
         # used on the side stream / allocated there and used on main: kept for two rounds (S.hold)
@@ -198,12 +203,13 @@ class DeviceCrypto:
         return self.eng.shares(qdelta, rows)
 
     def shares_async(self, qdelta: torch.Tensor, rows: list, stream, launch: bool = True,
-                     group_rows: int = 0) -> "_SpecShares":
+                     group_rows: int = 0, no_commit: bool = False) -> "_SpecShares":
         """Shares + witnesses of qdelta[rows] on `stream` (the caller's work keeps flowing on its own
         stream).  launch=False prepares the per-row flags only; launch() then starts the MSM after
         everything queued so far on the caller's stream (e.g. Krum's selection), so rows already
         rejected cost nothing."""
-        sp = _SpecShares(self.eng, qdelta, rows, stream, deferred=not launch, group_rows=group_rows)
+        sp = _SpecShares(self.eng, qdelta, rows, stream, deferred=not launch, group_rows=group_rows,
+                         no_commit=no_commit)
         if launch:
             sp.launch()
         return sp

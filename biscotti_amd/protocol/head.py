@@ -254,9 +254,12 @@ class RoundHeadMixin:
         side = self.side_stream
         side.wait_event(pre["ev"])   # the step only (it ran on the Gram stream), not the audit on main
         # the row list goes up on an otherwise idle stream (not behind the audit on main or the Gram)
+        # the audit's commitment sums come from the pre-step's chunk commitments (NativeSecAgg.csum_early):
+        # the MSM then computes the witness lanes only
+        no_commit = getattr(pre["commits"], "ccom", None) is not None and cfg.kzg_audit == "off"
         with S.use(self.upload_stream):
             sp = self.crypto.shares_async(pre["qdelta"], [w - self.lo for w in spec_workers], side,
-                                          group_rows=SPEC_GROUP_ROWS)
+                                          group_rows=SPEC_GROUP_ROWS, no_commit=no_commit)
         self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
                            "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
                            "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}

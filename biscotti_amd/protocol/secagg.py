@@ -80,6 +80,8 @@ class SecAggMixin:
                 # for the MSM: they run while the MSM is still busy, not after it
                 self._native.csum_early(pc.ccom, pc.ccom_event, sp.rows_t, alive)
                 early_cs = True
+            elif sp.no_commit and cfg.audit_aggregate:
+                raise RuntimeError("speculative MSM without commitment slots but no chunk commitments to audit with")
             S.current().wait_event(sp.ev)          # the MSM's shares
         agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration), early_cs=early_cs)
         agg["contributing"], agg["part"], agg["accepted"], agg["node"] = list(contributing), dict(part), None, node
@@ -320,7 +322,8 @@ class SecAggMixin:
             rowsel: list = []
             if local_used:
                 spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
-                if spec is not None and all(w in spec_row for w in local_used):
+                # (an MSM run without its commitment slots cannot feed this path's audit sums: recompute)
+                if spec is not None and all(w in spec_row for w in local_used) and not spec[1].no_commit:
                     sp = spec[1]
                     sp.launch()
                     pts, ys = sp.pts, sp.ys

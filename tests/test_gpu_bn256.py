@@ -106,6 +106,33 @@ def test_shares_msm_matches_host(rt, d, secret, scale, b0):
     np.testing.assert_array_equal(B.marshal(pts_c).cpu().numpy().reshape(3, eng.nchunks, 64), allb[:, :, 21])
     # compacted full-vector commitment kernel == sum of chunk commitments
     np.testing.assert_array_equal(B.marshal_host(eng.commit_rows(ct, rows)), comm)
+    # witness-lanes-only mode (commit_only=2): the same witnesses and share values, slot T not written
+    pts_w, ys_w = eng.shares(ct, rows, commit_only=2)
+    w_only = B.marshal(pts_w[:, :, :21].contiguous()).cpu().numpy().reshape(3, eng.nchunks, 21, 64)
+    np.testing.assert_array_equal(w_only, allb[:, :, :21])
+    np.testing.assert_array_equal(ys_w.cpu().numpy(), ys)
+
+
+def test_sum_rows2_pos_mask_and_early_commitment_sums(rt):
+    """bsc_sum_rows2_pos (mask indexed by the position in the row list): the audit's early commitment sums
+    over the pre-step's per-peer chunk commitments equal the sums over the share MSM's commitment slots."""
+    from biscotti_amd.native import hip
+    from biscotti_amd.ops import bn256 as B
+    d = 75
+    key = rt.CommitKey.generate(d, 3)
+    eng = B.DeviceCommitEngine(key, 10, 21)
+    rng = np.random.default_rng(5)
+    coeffs = torch.from_numpy(rng.integers(-10**4, 10**4, size=(6, d), dtype=np.int64)).cuda()
+    ccom, _ = eng.shares(coeffs, torch.arange(6, dtype=torch.int32, device="cuda"), commit_only=True)
+    rows = torch.tensor([4, 1, 5, 0], dtype=torch.int32, device="cuda")          # speculative row -> peer row
+    mask = torch.tensor([1, 0, 1, 1], dtype=torch.int32, device="cuda")          # alive flags by position
+    out = torch.empty((eng.nchunks, 24), dtype=torch.int32, device="cuda")
+    assert hip().bsc_sum_rows2_pos(ccom.data_ptr(), eng.nchunks, rows.data_ptr(), 4, None, eng.nchunks,
+                                   mask.data_ptr(), out.data_ptr(), None) == 0
+    pts, _ = eng.shares(coeffs, rows)                                            # commitment slots = column T
+    ref = B.sum_rows(pts.reshape(4, -1, 24), None, torch.arange(eng.nchunks, dtype=torch.int32, device="cuda") * 22 + 21,
+                     row_mask=mask)
+    np.testing.assert_array_equal(B.marshal(out).cpu().numpy(), B.marshal(ref).cpu().numpy())
 
 
 @pytest.mark.parametrize("scale,b0", [(3000, 14), (2**40, 14), (2**40, 8), (8193, 14)])
