@@ -1290,6 +1290,16 @@ extern "C" int bsc_eval_error(const float* X, const int* y, int N, int D_IN, int
   return (int)hipGetLastError();
 }
 
+// the evaluation with its accumulator reset and its read-back into pinned memory in one call (the engine
+// queues it every round; three Python-level stream operations cost more host time than the kernel)
+extern "C" int bsc_eval_error_rb(const float* X, const int* y, int N, int D_IN, int D_OUT, const double* W,
+                                 int transform, int split, unsigned int* err, unsigned int* err_host, void* stream) {
+  if (hipMemsetAsync(err, 0, 2 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) return -1;
+  const int rc = bsc_eval_error(X, y, N, D_IN, D_OUT, W, transform, split, err, stream);
+  if (rc != 0) return rc;
+  return (int)hipMemcpyAsync(err_host, err, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, (hipStream_t)stream);
+}
+
 extern "C" int bsc_noise_table(int nnoisers, int D, unsigned long long seed, float* tbl, void* stream) {
   const long long n = (long long)nnoisers * 100 * D;
   if (n <= 0) return 0;

@@ -415,6 +415,62 @@ static G1 g1_from_jac_u32(const uint32_t* p) {
   return g;
 }
 
+// One VRF batch on the native dispatcher: pass 1 computes every output (H, Gamma = x*H, beta), pass 2
+// the proofs unless outputs_only (the device prover makes them, kernels/vrf.hip).
+static std::shared_ptr<VrfJob> vrf_submit(const std::vector<Bytes>& seeds, const Bytes& alpha, int threads,
+                                          std::shared_ptr<VrfJob> after, bool outputs_only) {
+  auto job = std::make_shared<VrfJob>();
+  job->outputs_only = outputs_only;
+  job->after = std::move(after);
+  job->seeds = seeds;
+  job->alpha = alpha;
+  job->out.resize(job->seeds.size());
+  job->stages.resize(job->seeds.size());
+  VrfJob* jp = job.get();
+  job->t_submit = std::chrono::steady_clock::now();
+  job->started = true;
+  dispatcher().submit([jp, threads] {
+    if (jp->after) jp->after->done.wait();
+    jp->t_start = std::chrono::steady_clock::now();
+    bool beta_set = false;
+    try {
+      // pass 1: every output (H, Gamma = x*H, beta); pass 2: the proofs (k*B, k*H, c, s) unless
+      // they are produced elsewhere (outputs_only: the device prover, kernels/vrf.hip)
+      if (jp->outputs_only) {
+        parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+          jp->out[i].first = vrf_beta(VrfKey::cached(jp->seeds[i]), jp->alpha);
+        });
+      } else {
+        parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+          jp->out[i].first = vrf_output(VrfKey::cached(jp->seeds[i]), jp->alpha, &jp->stages[i]);
+        });
+      }
+      jp->beta_p.set_value();
+      beta_set = true;
+      if (!jp->outputs_only) parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+        jp->out[i].second = vrf_finish(VrfKey::cached(jp->seeds[i]), jp->stages[i]);
+        jp->stages[i].st.reset();
+      });
+    } catch (const std::exception& e) {
+      jp->error = e.what();
+      if (!beta_set) jp->beta_error = jp->error;
+    }
+    if (!beta_set) jp->beta_p.set_value();
+    jp->t_end = std::chrono::steady_clock::now();
+    jp->finished.store(true);
+    jp->after.reset();
+    jp->done_p.set_value();
+    jp->exited.store(true, std::memory_order_release);
+  });
+  return job;
+}
+
+// a fixed list of VRF seeds held natively (a rank's peers): a batch over it copies no Python objects
+// (a 100-seed list cost ~20 us of conversion per submission on the round's host thread)
+struct VrfSeedSet {
+  std::vector<Bytes> seeds;
+};
+
 PYBIND11_MODULE(_biscotti_rt, m) {
   m.doc() = "biscotti_amd native host runtime (crypto, ledger, protocol FSM)";
 
@@ -868,52 +924,23 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   });
   m.def("vrf_base_table", [] { return P(vrf_base_table_bytes()); });
   m.def("vrf_beta", [](py::bytes seed, py::bytes alpha) { return P(vrf_beta(VrfKey::cached(B(seed)), B(alpha))); });
+  py::class_<VrfSeedSet, std::shared_ptr<VrfSeedSet>>(m, "VrfSeedSet")
+      .def(py::init([](std::vector<py::bytes> seeds) {
+        auto st = std::make_shared<VrfSeedSet>();
+        for (auto& x : seeds) st->seeds.push_back(B(x));
+        return st;
+      }))
+      .def("__len__", [](const VrfSeedSet& st) { return st.seeds.size(); });
+  m.def("vrf_prove_set_async", [](std::shared_ptr<VrfSeedSet> set, py::bytes alpha, int threads,
+                                  std::shared_ptr<VrfJob> after, bool outputs_only) {
+    return vrf_submit(set->seeds, B(alpha), threads, std::move(after), outputs_only);
+  }, py::arg("seeds"), py::arg("alpha"), py::arg("threads"), py::arg("after") = nullptr,
+     py::arg("outputs_only") = false);
   m.def("vrf_prove_batch_async", [](std::vector<py::bytes> seeds, py::bytes alpha, int threads,
                                     std::shared_ptr<VrfJob> after, bool outputs_only) {
-    auto job = std::make_shared<VrfJob>();
-    job->outputs_only = outputs_only;
-    job->after = std::move(after);
-    for (auto& s : seeds) job->seeds.push_back(B(s));
-    job->alpha = B(alpha);
-    job->out.resize(job->seeds.size());
-    job->stages.resize(job->seeds.size());
-    VrfJob* jp = job.get();
-    job->t_submit = std::chrono::steady_clock::now();
-    job->started = true;
-    dispatcher().submit([jp, threads] {
-      if (jp->after) jp->after->done.wait();
-      jp->t_start = std::chrono::steady_clock::now();
-      bool beta_set = false;
-      try {
-        // pass 1: every output (H, Gamma = x*H, beta); pass 2: the proofs (k*B, k*H, c, s) unless
-        // they are produced elsewhere (outputs_only: the device prover, kernels/vrf.hip)
-        if (jp->outputs_only) {
-          parallel_for(jp->seeds.size(), threads, [&](size_t i) {
-            jp->out[i].first = vrf_beta(VrfKey::cached(jp->seeds[i]), jp->alpha);
-          });
-        } else {
-          parallel_for(jp->seeds.size(), threads, [&](size_t i) {
-            jp->out[i].first = vrf_output(VrfKey::cached(jp->seeds[i]), jp->alpha, &jp->stages[i]);
-          });
-        }
-        jp->beta_p.set_value();
-        beta_set = true;
-        if (!jp->outputs_only) parallel_for(jp->seeds.size(), threads, [&](size_t i) {
-          jp->out[i].second = vrf_finish(VrfKey::cached(jp->seeds[i]), jp->stages[i]);
-          jp->stages[i].st.reset();
-        });
-      } catch (const std::exception& e) {
-        jp->error = e.what();
-        if (!beta_set) jp->beta_error = jp->error;
-      }
-      if (!beta_set) jp->beta_p.set_value();
-      jp->t_end = std::chrono::steady_clock::now();
-      jp->finished.store(true);
-      jp->after.reset();
-      jp->done_p.set_value();
-      jp->exited.store(true, std::memory_order_release);
-    });
-    return job;
+    std::vector<Bytes> ss;
+    for (auto& x : seeds) ss.push_back(B(x));
+    return vrf_submit(ss, B(alpha), threads, std::move(after), outputs_only);
   }, py::arg("seeds"), py::arg("alpha"), py::arg("threads"), py::arg("after") = nullptr,
      py::arg("outputs_only") = false);
 
@@ -1193,7 +1220,37 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       .def("is_poisoner", &RoundFSM::is_poisoner, py::arg("id"), py::arg("fedsys") = false)
       .def("is_colluder", &RoundFSM::is_colluder)
       .def("round_seed", &RoundFSM::round_seed)
-      .def("successor", &RoundFSM::successor);
+      .def("successor", &RoundFSM::successor)
+      // The next round's speculative share plan in ONE call (head.py _spec_head_launch): the FSM as it will
+      // be after committing `b`, every peer live -> (plan, every verifier's inbox, the leader's arrival
+      // order, this rank's candidate workers [lo, hi) sorted by arrival, every candidate sorted), or None
+      // when the run is over.  Candidates: every update some verifier judges, or every worker when
+      // floor(nv/2) == 0 signatures suffice (main.go:1686).
+      .def("spec_plan", [](RoundFSM& f, const Block& b, i64 lo, i64 hi) -> py::object {
+        RoundFSM s = f.successor(b);
+        const i64 n = s.cfg.num_nodes;
+        std::vector<u8> live(size_t(n), 1);
+        const RoundPlan plan = s.begin_round(live);
+        if (plan.done) return py::none();
+        auto inboxes = s.verifier_inboxes(plan.workers);
+        std::vector<u8> cand(size_t(n), 0);
+        if (plan.verifiers.size() / 2 == 0) {
+          for (i64 w : plan.workers) cand.at(size_t(w)) = 1;
+        } else {
+          for (auto& ib : inboxes)
+            for (i64 w : ib) cand.at(size_t(w)) = 1;
+        }
+        auto arrivals = s.leader_arrivals();
+        std::vector<i64> rank(size_t(n), i64(1) << 30);
+        for (size_t i = 0; i < arrivals.size(); ++i) rank.at(size_t(arrivals[i])) = i64(i);
+        std::vector<i64> spec, cands;
+        for (i64 w : plan.workers)
+          if (cand.at(size_t(w)) && w >= lo && w < hi) spec.push_back(w);
+        std::stable_sort(spec.begin(), spec.end(), [&](i64 a, i64 c) { return rank[size_t(a)] < rank[size_t(c)]; });
+        for (i64 w = 0; w < n; ++w)
+          if (cand[size_t(w)]) cands.push_back(w);
+        return py::make_tuple(plan, inboxes, arrivals, spec, cands);
+      }, py::arg("block"), py::arg("lo"), py::arg("hi"));
   m.def("select_roles", [](const std::map<i64, i64>& stake, py::bytes h, i64 nv, i64 na, i64 n) {
     std::vector<i64> v, mm;
     select_roles(stake, B(h), nv, na, n, &v, &mm);

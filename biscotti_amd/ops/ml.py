@@ -487,6 +487,9 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
 
 
 # ---------------------------------------------------------------------------- K2 evaluation
+_EVAL_DEV: dict = {}   # pinned read-back buffer -> its device accumulator (persistent pairs)
+
+
 def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
     """Error rates of W on rows [0, split) and [split, N) of X from ONE kernel launch and one
     read-back (test error + 1->7 attack rate).  Returns a callable giving (err_a, err_b)."""
@@ -496,13 +499,16 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
         a = eval_error(X[:split], y[:split], W, d_in, d_out, transform) if na else 0.0
         b = eval_error(X[split:], y[split:], W, d_in, d_out, transform) if nb else 0.0
         return lambda: (a, b)
-    err = torch.zeros((2,), dtype=torch.int32, device=X.device)
-    _check(hip().bsc_eval_error(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), int(split), _p(err), _stream()),
-           "eval_error")
-    # download queued right behind the kernel: the read-back waits for the evaluation only, not for
-    # whatever the caller queues on the stream afterwards (the next round's head)
-    host = pinned("eval", (2,), torch.int32, depth=4)   # lazy_eval reads it one round later
-    d2h_into(host, err)
+    # accumulator reset, kernel and read-back in one native call; the download is queued right behind the
+    # kernel: the read-back waits for the evaluation only, not for whatever the caller queues on the stream
+    # afterwards (the next round's head).  Device and host buffers rotate together (lazy_eval reads the
+    # host copy up to a few rounds later).
+    host = pinned("eval", (2,), torch.int32, depth=4)
+    err = _EVAL_DEV.get(host.data_ptr())
+    if err is None:
+        err = _EVAL_DEV[host.data_ptr()] = torch.empty((2,), dtype=torch.int32, device=X.device)
+    _check(hip().bsc_eval_error_rb(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), int(split), _p(err),
+                                   host.data_ptr(), _stream()), "eval_error")
     ev = S.record()
 
     def result():

@@ -81,9 +81,11 @@ class DeviceVrfProver:
 
     # ---- round-batched queue: the engine submits each round's proofs, one launch per batch_rounds
     def submit(self, seeds, alpha: bytes, stream) -> None:
-        if seeds:
-            # key rows resolved now (a few dict lookups per round), so a flush only concatenates
-            self._queue.append((np.asarray(self._rows(seeds), np.int32), bytes(alpha)))
+        """seeds: the proving keys' seeds, or already their key rows (int32 array, _rows)."""
+        if len(seeds):
+            # key rows resolved now, so a flush only concatenates
+            rows = seeds if isinstance(seeds, np.ndarray) else np.asarray(self._rows(seeds), np.int32)
+            self._queue.append((rows, bytes(alpha)))
         if len(self._queue) >= self.batch_rounds:
             self.flush(stream)
 

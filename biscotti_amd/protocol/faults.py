@@ -70,6 +70,7 @@ class FaultsMixin:
                 st["rejoins"] += 1
                 e = st["epoch"][p]
                 self.vrf_noise_seed[p] = _seed_bytes(cfg.seed, f"vrf-noise-e{e}", p)
+                self._seed_version = getattr(self, "_seed_version", 0) + 1   # native seed sets are rebuilt
                 self.vrf_roles_seed[p] = _seed_bytes(cfg.seed, f"vrf-roles-e{e}", p)
                 if p in self.local:
                     ok, why = fsm.chain.verify_range(max(0, view - 1), height)

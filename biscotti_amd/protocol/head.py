@@ -24,6 +24,17 @@ from ..utils import streams as S
 SPEC_GROUP_ROWS = 8   # speculative MSM rows per group, in leader arrival order (late cancellation)
 
 
+class PlanView:
+    """A native RoundPlan with its fields converted to Python once: every attribute read of the native
+    object builds a new list (~1-3 us), and a round reads the plan's lists ~25 times."""
+
+    __slots__ = ("iteration", "verifiers", "miners", "workers", "leader", "live", "done")
+
+    def __init__(self, p):
+        self.iteration, self.verifiers, self.miners, self.workers = p.iteration, p.verifiers, p.miners, p.workers
+        self.leader, self.live, self.done = p.leader, p.live, p.done
+
+
 class RoundHeadMixin:
     # ------------------------------------------------------------------ the head
     def _open_round(self) -> dict:
@@ -32,7 +43,7 @@ class RoundHeadMixin:
         cfg, R, fsm = self.cfg, self.R, self.fsm
         with self.timer.phase("head.plan"):
             live = self._live_mask()
-            plan = fsm.begin_round(live)
+            plan = PlanView(fsm.begin_round(live))
         head = {"live": live, "plan": plan}
         if plan.done:
             return head
@@ -45,30 +56,31 @@ class RoundHeadMixin:
         # MSM rows); every rank computes them for the peers it hosts only (the reference: each peer proves
         # its own), on host_threads - 1 native threads; the proofs nothing reads run on the device.
         with self.timer.phase("head.vrf_submit"):
-            seeds = [self.vrf_noise_seed[w] for w in local_workers]
             dev = self.vrf_dev is not None
             nthr = max(1, cfg.host_threads - 1) if self.gpu else cfg.host_threads
             ej, self._early_vrf = self._early_vrf, None
             fut_noise = None
-            if ej is not None and seeds and ej["hash"] == bytes(latest_hash):
-                # the outputs started when the block was built (_early_vrf_submit): adopted if they cover
-                # these workers with the same keys
-                pos = ej["pos"]
-                if all(w in pos and ej["seeds"][pos[w]] == self.vrf_noise_seed[w] for w in local_workers):
-                    fut_noise = ej["job"]
-                    head["vrf_index"] = [pos[w] for w in local_workers]
-                    self.stats["early_vrf"] = self.stats.get("early_vrf", 0) + 1
+            if ej is not None and local_workers and ej["hash"] == bytes(latest_hash) \
+                    and ej["ver"] == getattr(self, "_seed_version", 0):
+                # the outputs started when the block was built (_early_vrf_submit) over every local peer with
+                # the current keys: adopted
+                fut_noise = ej["job"]
+                lo = self.lo
+                head["vrf_index"] = [w - lo for w in local_workers]
+                self.stats["early_vrf"] = self.stats.get("early_vrf", 0) + 1
             if ej is not None and fut_noise is not ej["job"]:
                 # not adopted (a failed audit changed the block, or a restart its keys): joined later, not
                 # here -- dropping a running job would wait for it
                 self._stale_vrf.append(ej["job"])
-            if fut_noise is None:
-                fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, nthr, None, dev) if seeds else None
+            if fut_noise is None and local_workers:
+                seeds = [self.vrf_noise_seed[w] for w in local_workers]
+                fut_noise = R.vrf_prove_batch_async(seeds, latest_hash, nthr, None, dev)
                 self.stats["vrf_outputs"] += len(seeds)
             fut_roles = None
-            roles = [self.vrf_roles_seed[p] for p in self.local if live[p]] if cfg.roles_vrf_proof else []
-            if roles and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
-                fut_roles = R.vrf_prove_batch_async(roles, latest_hash, 8, fut_noise)
+            if cfg.roles_vrf_proof and not dev:  # getVRFRoles proves with the roles key too (result unused, Q7)
+                roles = [self.vrf_roles_seed[p] for p in self.local if live[p]]
+                if roles:
+                    fut_roles = R.vrf_prove_batch_async(roles, latest_hash, 8, fut_noise)
         head.update(fut_noise=fut_noise, fut_roles=fut_roles)
         tm, it = self.timer, plan.iteration
         # the local step (and the commitments) may already be in flight: queued behind the recovery of the
@@ -143,8 +155,28 @@ class RoundHeadMixin:
             # the proofs nobody reads -- every noiser proof and the roles proofs -- go to the device prover
             # when the round runs (run_round's VRF wait), one launch per round on their own low-priority
             # stream: a timed window then contains exactly its rounds' proofs
-            head["vrf_proofs"] = (seeds + roles, bytes(latest_hash))
+            head["vrf_proofs"] = (self._vrf_key_rows(local_workers, live), bytes(latest_hash))
         return head
+
+    def _vrf_key_rows(self, local_workers: list, live) -> "np.ndarray":
+        """The device prover's key rows of this round's proofs: every local worker's noiser proof, then every
+        live local peer's roles proof (getVRFRoles, Q7) -- from per-peer row tables built once per key
+        version (a churn restart draws new keys) instead of per-seed lookups every round."""
+        import numpy as np
+
+        ver = getattr(self, "_seed_version", 0)
+        tab = getattr(self, "_vrf_rows_tab", None)
+        if tab is None or tab[0] != ver:
+            peers = list(self.local)
+            tab = self._vrf_rows_tab = (ver, np.asarray(self.vrf_dev._rows([self.vrf_noise_seed[p] for p in peers]),
+                                                        np.int32),
+                                        np.asarray(self.vrf_dev._rows([self.vrf_roles_seed[p] for p in peers]), np.int32))
+        lo = self.lo
+        parts = [tab[1][np.asarray(local_workers, np.int64) - lo]] if local_workers else []
+        if self.cfg.roles_vrf_proof:
+            lv = np.asarray(live, bool)[lo:lo + len(self.local)]
+            parts.append(tab[2][lv])
+        return np.concatenate(parts) if parts else np.zeros(0, np.int32)
 
     def _block_candidates(self, plan, workers, inboxes) -> set:
         """Workers whose update can end in this round's block: without verification every live worker
@@ -237,18 +269,16 @@ class RoundHeadMixin:
                 and cfg.churn_kill_per_min == 0 and not self._partitions and pre is not None
                 and pre["W"] is self._W_next and self.local):
             return
-        shadow = self.fsm.successor(block)
-        live = [1] * self.N
-        plan = shadow.begin_round(live)
-        if plan.done:
+        # successor FSM, its plan, inboxes, leader arrivals and this rank's candidates in arrival order: one
+        # native call (RoundFSM.spec_plan)
+        got = self.fsm.spec_plan(block, self.local.start, self.local.stop)
+        if got is None:
             return
-        workers = list(plan.workers)
-        inboxes = {v: list(ib) for v, ib in zip(plan.verifiers, shadow.verifier_inboxes(workers))}
-        cand = set(workers) if len(plan.verifiers) // 2 == 0 else set().union(*inboxes.values())
-        arrivals = shadow.leader_arrivals()
-        lo_rank = {w: i for i, w in enumerate(arrivals)}
-        spec_workers = sorted((w for w in workers if w in self.local and w in cand),
-                              key=lambda w: lo_rank.get(w, 1 << 30))
+        plan, ibs, arrivals, spec_workers, cands = got
+        plan = PlanView(plan)
+        workers = plan.workers
+        inboxes = dict(zip(plan.verifiers, ibs))
+        cand = set(cands)
         if not spec_workers:
             return
         side = self.side_stream
@@ -273,13 +303,16 @@ class RoundHeadMixin:
         # (getRoles draws every peer's noisers whether or not noise is added: main.go:507)
         if not (self._pipelined() and cfg.num_noisers > 0 and self.local):
             return
-        peers = list(self.local)
-        seeds = [self.vrf_noise_seed[p] for p in peers]
-        job = self.R.vrf_prove_batch_async(seeds, bytes(block_hash), max(1, cfg.host_threads - 1), None,
-                                           self.vrf_dev is not None)
-        self.stats["vrf_outputs"] += len(seeds)
-        self._early_vrf = {"hash": bytes(block_hash), "job": job, "seeds": seeds,
-                           "pos": {p: i for i, p in enumerate(peers)}}
+        ver = getattr(self, "_seed_version", 0)
+        ss = getattr(self, "_seedset", None)
+        if ss is None or ss[0] != ver:
+            # every local peer's noise VRF seed, held natively (rebuilt when a churn restart draws new keys)
+            ss = self._seedset = (ver, self.R.VrfSeedSet([self.vrf_noise_seed[p] for p in self.local]))
+        job = self.R.vrf_prove_set_async(ss[1], bytes(block_hash), max(1, cfg.host_threads - 1), None,
+                                         self.vrf_dev is not None)
+        self.stats["vrf_outputs"] += len(self.local)
+        # covers every local peer in order: peer p's output is entry p - lo
+        self._early_vrf = {"hash": bytes(block_hash), "job": job, "ver": ver}
 
     # ------------------------------------------------------------------ commitments
     def _local_commit_rows(self, pending_commits, local_workers: list, row_of: dict) -> torch.Tensor:

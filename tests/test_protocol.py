@@ -1,4 +1,5 @@
 """Protocol rules of the native runtime vs literal Python restatements of the reference logic."""
+import pytest
 import hashlib
 import random
 
@@ -205,6 +206,36 @@ def test_successor_gives_the_next_plan_before_commit():
                 [list(x) for x in fsm.verifier_inboxes(list(p2.workers))], list(fsm.leader_arrivals()))
         fsm.iteration = saved   # undo the probe's begin_round
         assert got == want
+    eng.close()
+
+
+@pytest.mark.parametrize("nv,lo,hi", [(3, 0, 12), (3, 4, 9), (1, 0, 12), (1, 2, 7)])
+def test_spec_plan_matches_python_composition(nv, lo, hi):
+    """RoundFSM.spec_plan (the next round's speculative plan in one native call) == the composition of
+    successor / begin_round / verifier_inboxes / leader_arrivals it replaces, candidates included (the
+    floor(nv/2) == 0 case takes every worker)."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    eng = BiscottiEngine(RunConfig(num_nodes=12, dataset="mnist", seed=3, max_iterations=100, num_verifiers=nv,
+                                   deterministic_time=True), Comm())
+    for _ in range(3):
+        eng.run_round()
+        blk = eng.fsm.chain.latest()
+        shadow = eng.fsm.successor(blk)
+        p = shadow.begin_round([1] * 12)
+        workers = list(p.workers)
+        ibs = [list(x) for x in shadow.verifier_inboxes(workers)]
+        cand = set(workers) if len(p.verifiers) // 2 == 0 else set().union(*ibs)
+        arr = list(shadow.leader_arrivals())
+        rank = {w: i for i, w in enumerate(arr)}
+        spec = sorted((w for w in workers if lo <= w < hi and w in cand), key=lambda w: rank.get(w, 1 << 30))
+        plan, ibs2, arr2, spec2, cands2 = eng.fsm.spec_plan(blk, lo, hi)
+        assert (list(plan.verifiers), list(plan.miners), list(plan.workers), plan.iteration) == \
+            (list(p.verifiers), list(p.miners), workers, p.iteration)
+        assert [list(x) for x in ibs2] == ibs and list(arr2) == arr and list(spec2) == spec
+        assert list(cands2) == sorted(cand)
     eng.close()
 
 
