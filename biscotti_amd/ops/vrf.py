@@ -27,10 +27,14 @@ def _i32(b: bytes) -> np.ndarray:
 class DeviceVrfProver:
     ALPHA_LEN = 32
 
-    def __init__(self, device, batch_rounds: int = 1):
+    def __init__(self, device, batch_rounds: int = 1, streams=None):
         self.device = torch.device(device)
         self.btab = torch.from_numpy(_i32(rt().vrf_base_table()).copy()).to(self.device)   # [512 * 32]
         self.batch_rounds = max(1, int(batch_rounds))
+        # streams: launches go round-robin over these (one round's proofs per launch then overlap the
+        # previous rounds' instead of queueing behind them: a launch's latency, ~2 ms, exceeds a round)
+        self.streams = list(streams) if streams else None
+        self._rr = 0
         self._row: dict[bytes, int] = {}
         self._keys: list[np.ndarray] = []
         self._keys_dev = None
@@ -93,6 +97,33 @@ class DeviceVrfProver:
         if not self._queue:
             return
         q, self._queue = self._queue, []
+        if self.streams:
+            stream = self.streams[self._rr % len(self.streams)]
+            self._rr += 1
+        if len(q) == 1:
+            # one round (one message): rows, zero message indices and the 32-byte message in ONE upload
+            rows, alpha = q[0]
+            n = int(rows.size)
+            buf = np.zeros(2 * n + len(alpha) // 4, np.int32)
+            buf[:n] = rows
+            buf[2 * n:] = np.frombuffer(alpha, np.int32)
+            with S.use(stream):
+                if self._keys_dev is None:
+                    self._keys_dev = self._upload(np.concatenate(self._keys))
+                up = self._upload(buf)
+                scratch = torch.empty((n, 320), dtype=torch.int32, device=self.device)
+                pi = torch.empty((n, 80), dtype=torch.uint8, device=self.device)
+                err = hip().bsc_vrf_prove(self._keys_dev.data_ptr(), up.data_ptr(), up[2 * n:].data_ptr(),
+                                          up[n:].data_ptr(), self.ALPHA_LEN, n, self.btab.data_ptr(),
+                                          scratch.data_ptr(), pi.data_ptr(), None, S.raw())
+                if err != 0:
+                    raise RuntimeError(f"HIP launch of vrf_prove failed with hipError {err}")
+                self.proofs += n
+                ev = S.record(stream)
+            self._inflight.append((ev, (pi, scratch, up)))
+            self._inflight = [x for x in self._inflight if not x[0].query()] if len(self._inflight) > 4 \
+                else self._inflight
+            return
         rows = np.concatenate([r for r, _ in q])
         alpha_idx = np.repeat(np.arange(len(q), dtype=np.int32), [r.size for r, _ in q])
         with S.use(stream):   # uploads, scratch and the launch all on the prover's stream

@@ -168,7 +168,11 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             from ..ops.vrf import DeviceVrfProver
             # 16 rounds per launch: a launch (~2.5 ms) keeps ~13 CUs busy and slows the critical path's
             # kernels that share them, so launches are batched (per-round launches measured 2.01 vs 1.85 ms/round)
-            self.vrf_dev = DeviceVrfProver(self.dev, int(os.environ.get("BISCOTTI_VRF_BATCH", "16")))
+            nb = int(os.environ.get("BISCOTTI_VRF_BATCH", "16"))
+            ns = int(os.environ.get("BISCOTTI_VRF_STREAMS", "1"))
+            extra = [torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[0])
+                     for _ in range(ns - 1)] if ns > 1 else []
+            self.vrf_dev = DeviceVrfProver(self.dev, nb, [self.vrf_stream] + extra if extra else None)
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
         self._pre = None             # next round's local step + commitments, queued behind the recovery
