@@ -26,6 +26,10 @@ extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, con
                              void* stream);
 extern "C" int bsc_sum_rows2_pos(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
                                  int ncols, const int* row_mask, uint32_t* out, void* stream);
+extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
+                              const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
+                              const int* alive, const int* compact, int group_rows, uint32_t* out_pts,
+                              long long* out_y, void* stream);
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
                                const uint32_t* csum, int nm, int nch, int* ok, void* stream);
 
@@ -133,6 +137,23 @@ extern "C" int bsc_round_csum_early(void* ctx, const uint32_t* ccom, void* ev_cc
   if (ev_ccom != nullptr) RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_ccom, 0));
   RC_CHECK(bsc_sum_rows2_pos(ccom, c->nch, rows, R, nullptr, c->nch, mask, cs, c->side));
   RC_CHECK(hipEventRecord(c->ev_side, c->side));
+  return 0;
+}
+
+// The next round's speculative share MSM (head.py _spec_head_launch) in one call: the side stream waits for
+// the pre-step (ev_wait: its quantised updates), uploads the row list and the all-ones alive flags from
+// pinned staging (host [2n] int32: rows, then ones) into rows_dev [2n], and runs the MSM over them into
+// resident pts / ys.  The caller rotates staging / device buffers over enough slots that a slot is
+// rewritten only after its MSM and every consumer of its outputs are done.
+extern "C" int bsc_round_spec_msm(void* ctx, void* ev_wait, const long long* coeffs, const int* rows_host,
+                                  int* rows_dev, int n, const uint32_t* tbl_wb, int commit_only, int group_rows,
+                                  uint32_t* pts, long long* ys) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || n <= 0) return -1;
+  if (ev_wait != nullptr) RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_wait, 0));
+  RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, c->side));
+  RC_CHECK(bsc_shares_msm(coeffs, c->d, rows_dev, n, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, commit_only,
+                          rows_dev + n, nullptr, group_rows, pts, ys, c->side));
   return 0;
 }
 

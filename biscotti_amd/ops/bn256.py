@@ -325,6 +325,25 @@ def cu_masked_stream(device, skip_every: int = 4):
     return torch.cuda.ExternalStream(ptr, device=device), used.value
 
 
+class NativeSpec:
+    """Handle of a speculative share MSM launched by NativeSecAgg.spec_msm (same surface as the engine's
+    _SpecShares: the MSM is already running; `ev` marks its end on the side stream)."""
+
+    def __init__(self, qdelta, rows, rows_t, alive, pts, ys, no_commit):
+        from ..utils import streams as S
+
+        self.qdelta, self.rows, self.rows_t, self.alive, self.pts, self.ys = qdelta, rows, rows_t, alive, pts, ys
+        self.no_commit, self.deferred = no_commit, False
+        self.ev = None
+        self._S = S
+
+    def record(self, side) -> None:
+        self.ev = self._S.record(side)
+
+    def launch(self) -> None:   # already running
+        return None
+
+
 class NativeSecAgg:
     """The round's secure aggregation enqueued natively (kernels/round.hip): one call queues the miners'
     commitment / witness sums (side / background streams), the fused share sums + exact recovery + W
@@ -386,6 +405,34 @@ class NativeSecAgg:
         ev = ccom_event.cuda_event if ccom_event is not None else None
         _check(hip().bsc_round_csum_early(self.ctx, _ptr(ccom.contiguous()), ev, _ptr(rows), R, _ptr(mask),
                                           _ptr(self.cs)), "round_csum_early")
+
+    SPEC_SLOTS = 3
+
+    def spec_msm(self, qdelta, rows: list, ev_wait, no_commit: bool, group_rows: int) -> "NativeSpec":
+        """The speculative share MSM of qdelta[rows] on the side stream, behind ev_wait (a torch event: the
+        pre-step), in one native call with resident outputs (a ring of SPEC_SLOTS: a slot is reused three
+        rounds later, long after its round read it).  Returns the handle the engine's aggregation uses
+        (pts, ys, alive, rows_t, ev)."""
+        eng, n = self.eng, len(rows)
+        ring = self.__dict__.get("_spec_ring")
+        if ring is None or ring["cap"] < n:
+            cap, dev = max(n, qdelta.shape[0]), eng.device
+            ring = self._spec_ring = {"cap": cap, "k": 0, "slots": [
+                {"pts": torch.empty((cap, eng.nchunks, eng.T + 1, 24), dtype=torch.int32, device=dev),
+                 "ys": torch.empty((cap, eng.nchunks, eng.T), dtype=torch.int64, device=dev),
+                 "rows": torch.empty((2 * cap,), dtype=torch.int32, device=dev),
+                 "host": torch.empty((2 * cap,), dtype=torch.int32, pin_memory=True)}
+                for _ in range(self.SPEC_SLOTS)]}
+        ring["k"] = (ring["k"] + 1) % self.SPEC_SLOTS
+        sl = ring["slots"][ring["k"]]
+        h = sl["host"].numpy()
+        h[:n] = rows
+        h[n:2 * n] = 1
+        pts, ys = sl["pts"][:n], sl["ys"][:n]
+        _check(hip().bsc_round_spec_msm(self.ctx, ev_wait.cuda_event if ev_wait is not None else None,
+                                        _ptr(qdelta), sl["host"].data_ptr(), _ptr(sl["rows"]), n, _ptr(eng.tbl_wb),
+                                        2 if no_commit else 0, int(group_rows), _ptr(pts), _ptr(ys)), "round_spec_msm")
+        return NativeSpec(qdelta, rows, sl["rows"][:n], sl["rows"][n:2 * n], pts, ys, no_commit)
 
     def readback(self):
         """Callable: waits for the recovery's read-back -> [status, W_new] numpy views (pinned)."""

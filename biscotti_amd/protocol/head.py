@@ -282,14 +282,20 @@ class RoundHeadMixin:
         if not spec_workers:
             return
         side = self.side_stream
-        side.wait_event(pre["ev"])   # the step only (it ran on the Gram stream), not the audit on main
-        # the row list goes up on an otherwise idle stream (not behind the audit on main or the Gram)
         # the audit's commitment sums come from the pre-step's chunk commitments (NativeSecAgg.csum_early):
         # the MSM then computes the witness lanes only
         no_commit = getattr(pre["commits"], "ccom", None) is not None and cfg.kzg_audit == "off"
-        with S.use(self.upload_stream):
-            sp = self.crypto.shares_async(pre["qdelta"], [w - self.lo for w in spec_workers], side,
-                                          group_rows=SPEC_GROUP_ROWS, no_commit=no_commit)
+        rows = [w - self.lo for w in spec_workers]
+        if self._native is not None:
+            # one native call: wait for the step, upload rows + flags, launch (resident output ring)
+            sp = self._native.spec_msm(pre["qdelta"], rows, pre["ev"], no_commit, SPEC_GROUP_ROWS)
+            sp.record(side)
+        else:
+            side.wait_event(pre["ev"])   # the step only (it ran on the Gram stream), not the audit on main
+            # the row list goes up on an otherwise idle stream (not behind the audit on main or the Gram)
+            with S.use(self.upload_stream):
+                sp = self.crypto.shares_async(pre["qdelta"], rows, side, group_rows=SPEC_GROUP_ROWS,
+                                              no_commit=no_commit)
         self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
                            "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
                            "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}

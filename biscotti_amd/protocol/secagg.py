@@ -363,11 +363,11 @@ class SecAggMixin:
         with tm.phase("recover.block"):
             block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
         self._W_next = W_new if st.all() and self.gpu else None
-        # the next round's share MSM first (in MSM-bound rounds it is the device's critical path), then its
-        # VRF outputs (needed only at the next round's noiser lottery)
+        # the next round's VRF outputs first (a native seed set: ~10 us to submit; started later they are not
+        # ready at the next round's noiser lottery), then its share MSM
+        self._early_vrf_submit(block.hash)
         if self._W_next is not None:
             self._spec_head_launch(block)
-        self._early_vrf_submit(block.hash)
         if audit_ok is not None:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()
