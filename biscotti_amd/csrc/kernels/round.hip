@@ -30,13 +30,21 @@ extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, i
                               const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
                               const int* alive, const int* compact, int group_rows, uint32_t* out_pts,
                               long long* out_y, void* stream);
+extern "C" int bsc_softmax_step(const float* X, const int* y, const long long* off, const int* ntrain,
+                                const int* pid, const double* W, int D_IN, int D_OUT, int B, int P, unsigned long long seed,
+                                int iteration, float max_norm, double qscale, float* delta, long long* qdelta,
+                                float* loss, int lo, void* stream);
+extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
+                                double* part, double* gram, unsigned int* count, void* stream);
+extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
+                               void* stream);
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
                                const uint32_t* csum, int nm, int nch, int* ok, void* stream);
 
 namespace {
 struct RoundCtx {
   hipStream_t main, side, bg;
-  hipEvent_t ev_main, ev_side, ev_readback, ev_audit;
+  hipEvent_t ev_main, ev_side, ev_readback, ev_audit, ev_pre;
   const uint32_t* tbl_pk;
   int d, poly, T, nch, b0, nw;
   double qscale;
@@ -62,7 +70,7 @@ extern "C" void* bsc_round_create(void* main, void* side, void* bg, const uint32
   c->b0 = b0;
   c->nw = nw;
   c->qscale = qscale;
-  hipEvent_t* evs[4] = {&c->ev_main, &c->ev_side, &c->ev_readback, &c->ev_audit};
+  hipEvent_t* evs[5] = {&c->ev_main, &c->ev_side, &c->ev_readback, &c->ev_audit, &c->ev_pre};
   for (hipEvent_t* e : evs)
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
       delete c;
@@ -78,6 +86,7 @@ extern "C" void bsc_round_destroy(void* ctx) {
   hipEventDestroy(c->ev_side);
   hipEventDestroy(c->ev_readback);
   hipEventDestroy(c->ev_audit);
+  hipEventDestroy(c->ev_pre);
   delete c;
 }
 
@@ -154,6 +163,44 @@ extern "C" int bsc_round_spec_msm(void* ctx, void* ev_wait, const long long* coe
   RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, c->side));
   RC_CHECK(bsc_shares_msm(coeffs, c->d, rows_dev, n, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, commit_only,
                           rows_dev + n, nullptr, group_rows, pts, ys, c->side));
+  return 0;
+}
+
+// The next round's pre-step (head.py _queue_pre_step) in one call, queued behind everything on main so far
+// (the recovery of W):
+//   gram stream: local SGD step of every local peer (delta, qdelta, loss), event ev_step; then, when
+//                do_gram, the noise-aware Krum's phase-1 Gram of [delta; this iteration's noise rows],
+//                event ev_gram
+//   background:  behind the step, the per-chunk commitments of every row (ccom, event ev_ccom), their
+//                per-row sums = the full commitments (jac), read back into pinned jac_host, event ev_commit
+// Outputs are resident (the caller rotates them over slots); events are caller-owned and re-recorded.
+extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, const int* y, const long long* off,
+                                 const int* ntrain, const int* pid, const double* W, int d_in, int d_out, int B, int P,
+                                 unsigned long long seed, int iteration, float max_norm, double qscale, int lo,
+                                 float* delta, long long* qdelta, float* loss, const uint32_t* tbl_wb,
+                                 const int* rows_arange, uint32_t* ccom, uint32_t* jac, uint32_t* jac_host,
+                                 int do_gram, const float* T_rows, int U2, long long stride2, int kchunk, double* part,
+                                 double* gram, unsigned int* counters, void* ev_step, void* ev_ccom, void* ev_commit,
+                                 void* ev_gram) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || P <= 0 || d_in * d_out + d_out != c->d) return -1;
+  hipStream_t gs = (hipStream_t)gram_stream;
+  RC_CHECK(hipEventRecord(c->ev_pre, c->main));
+  RC_CHECK(hipStreamWaitEvent(gs, c->ev_pre, 0));
+  RC_CHECK(bsc_softmax_step(X, y, off, ntrain, pid, W, d_in, d_out, B, P, seed, iteration, max_norm, qscale, delta,
+                            qdelta, loss, lo, gs));
+  RC_CHECK(hipEventRecord((hipEvent_t)ev_step, gs));
+  RC_CHECK(hipStreamWaitEvent(c->bg, (hipEvent_t)ev_step, 0));
+  RC_CHECK(bsc_shares_msm(qdelta, c->d, rows_arange, P, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, 1, nullptr,
+                          nullptr, 0, ccom, nullptr, c->bg));
+  RC_CHECK(hipEventRecord((hipEvent_t)ev_ccom, c->bg));
+  RC_CHECK(bsc_segment_sum(ccom, P, c->nch, 1, 0, jac, c->bg));
+  RC_CHECK(hipMemcpyAsync(jac_host, jac, (size_t)P * 24 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->bg));
+  RC_CHECK(hipEventRecord((hipEvent_t)ev_commit, c->bg));
+  if (do_gram) {
+    RC_CHECK(bsc_gram_stacked(delta, P, T_rows, U2, stride2, c->d, kchunk, part, gram, counters, gs));
+    RC_CHECK(hipEventRecord((hipEvent_t)ev_gram, gs));
+  }
   return 0;
 }
 

@@ -406,6 +406,64 @@ class NativeSecAgg:
         _check(hip().bsc_round_csum_early(self.ctx, _ptr(ccom.contiguous()), ev, _ptr(rows), R, _ptr(mask),
                                           _ptr(self.cs)), "round_csum_early")
 
+    PRE_SLOTS = 3
+
+    def prestep(self, task, W, it: int, gram_stream, noise_rows, gram_counters, kchunk: int = 512) -> dict:
+        """The next round's pre-step of a SoftmaxTask in ONE native call (bsc_round_prestep): the local step of
+        every local peer on the Gram stream, the per-chunk + full commitments (read back) on the background
+        stream and, with noise_rows (the noise table's rows of this iteration), the noise-aware Krum's Gram.
+        Outputs and events rotate over PRE_SLOTS resident slots (a slot is rewritten three rounds later, after
+        every consumer of its round).  Returns the engine's pre-step dict."""
+        from ..ops import ml as K
+        from ..protocol.crypto_backends import _PendingCommitments
+
+        eng, dev = self.eng, self.eng.device
+        P, d = len(task.peers), eng.d
+        U2 = noise_rows.shape[0] if noise_rows is not None else 0
+        U = P + U2
+        Tt = (U + 15) // 16
+        npairs, nsplit = Tt * (Tt + 1) // 2, (d + kchunk - 1) // kchunk
+        ring = self.__dict__.get("_pre_ring")
+        if ring is None:
+            def ev():
+                e = torch.cuda.Event()
+                e.record(gram_stream)   # materialise the handle (re-recorded natively)
+                return e
+
+            ring = self._pre_ring = {"k": 0, "pid": torch.tensor(task.peers, dtype=torch.int32, device=dev),
+                                     "rows": torch.arange(P, dtype=torch.int32, device=dev), "slots": [
+                {"delta": torch.empty((P, d), dtype=torch.float32, device=dev),
+                 "qdelta": torch.empty((P, d), dtype=torch.int64, device=dev),
+                 "loss": torch.empty((P,), dtype=torch.float32, device=dev),
+                 "ccom": torch.empty((P, eng.nchunks, 1, 24), dtype=torch.int32, device=dev),
+                 "jac": torch.empty((P, 24), dtype=torch.int32, device=dev),
+                 "host": torch.empty((P, 24), dtype=torch.int32, pin_memory=True),
+                 "part": torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev),
+                 "gram": torch.empty((npairs, 256), dtype=torch.float64, device=dev),
+                 "ev": [ev() for _ in range(4)]} for _ in range(self.PRE_SLOTS)]}
+            torch.cuda.synchronize(dev)
+        ring["k"] = (ring["k"] + 1) % self.PRE_SLOTS
+        sl = ring["slots"][ring["k"]]
+        e_step, e_ccom, e_commit, e_gram = sl["ev"]
+        assert sl["part"].shape == (nsplit, npairs, 256), "Gram shape changed between rounds"
+        _check(hip().bsc_round_prestep(
+            self.ctx, gram_stream.cuda_stream, _ptr(task.X), _ptr(task.y), _ptr(task.off), _ptr(task.ntrain),
+            _ptr(ring["pid"]), _ptr(W), task.d_in, task.d_out, task.batch, P, task.seed & (2 ** 64 - 1), int(it),
+            100.0, 1e4, task.peers[0], _ptr(sl["delta"]), _ptr(sl["qdelta"]), _ptr(sl["loss"]), _ptr(eng.tbl_wb),
+            _ptr(ring["rows"]), _ptr(sl["ccom"]), _ptr(sl["jac"]), sl["host"].data_ptr(), int(noise_rows is not None),
+            noise_rows.data_ptr() if noise_rows is not None else None, U2,
+            noise_rows.stride(0) if noise_rows is not None else 0, kchunk, _ptr(sl["part"]), _ptr(sl["gram"]),
+            _ptr(gram_counters), e_step.cuda_event, e_ccom.cuda_event, e_commit.cuda_event, e_gram.cuda_event),
+            "round_prestep")
+        pc = _PendingCommitments(sl["host"], e_commit, sl["jac"])
+        pc.ccom, pc.ccom_event, pc.src = sl["ccom"], e_ccom, sl["qdelta"]
+        out = {"W": W, "it": it, "delta": sl["delta"], "qdelta": sl["qdelta"], "ev": e_step, "commits": pc}
+        task.last_loss = sl["loss"]
+        if noise_rows is not None:
+            out["gram"] = {"gram": sl["gram"], "U1": P, "U": U, "keep": (sl["delta"], noise_rows, sl["part"]),
+                           "ev": e_gram}
+        return out
+
     SPEC_SLOTS = 3
 
     def spec_msm(self, qdelta, rows: list, ev_wait, no_commit: bool, group_rows: int) -> "NativeSpec":

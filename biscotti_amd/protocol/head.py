@@ -235,6 +235,16 @@ class RoundHeadMixin:
         adopts them if that block carries W (same device tensor) and discards them otherwise.  Every rank
         queues it at the same point (the recovery is replicated), so the Gram's gather lines up."""
         main, gs = S.current(), self.gram_stream
+        if self._native is not None and type(self.task).__name__ == "SoftmaxTask" and self.cfg.audit_aggregate \
+                and self.comm.world == 1:
+            # step + commitments + Krum Gram in one native call (resident output ring)
+            nk = self._noise_krum()
+            with S.use(gs):
+                cnt = K._tile_counters(self.dev, 1024)
+            out = self._native.prestep(self.task, W, it, gs, self.noise_rows.rows(it) if nk else None, cnt)
+            if nk:
+                out["gram"]["xrow"] = self.flat
+            return out
         S.wait(gs, main)
         with S.use(gs):
             delta, qdelta = self.task.step(W, it, list(self.local))

@@ -25,6 +25,16 @@ def _run_exact(eng, rounds=4):
         seen.update({(it, p): q[i].clone() for i, p in enumerate(peers)})
         return d, q
     eng.task.step = spy
+    if eng._native is not None:
+        # the one-rank pre-step runs natively (NativeSecAgg.prestep): record its quantised updates too
+        pre_fn = eng._native.prestep
+
+        def pre_spy(task, W, it, *a, **kw):
+            out = pre_fn(task, W, it, *a, **kw)
+            torch.cuda.current_stream().wait_event(out["ev"])   # the step runs on the Gram stream
+            seen.update({(it, p): out["qdelta"][i].clone() for i, p in enumerate(task.peers)})
+            return out
+        eng._native.prestep = pre_spy
     res = []
     for _ in range(rounds):
         W0 = eng.W.clone()
