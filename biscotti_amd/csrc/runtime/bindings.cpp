@@ -471,6 +471,49 @@ struct VrfSeedSet {
   std::vector<Bytes> seeds;
 };
 
+// the noiser lottery over a VRF batch's outputs (select_noisers_job / RoundFSM.select_noisers_job)
+static py::array_t<int64_t> select_noisers_impl(const std::map<i64, i64>& stake, VrfJob& job,
+                                                std::vector<i64> out_index, std::vector<i64> selfs, i64 nn,
+                                                i64 n) {
+  if (job.beta_ready.wait_for(std::chrono::seconds(0)) != std::future_status::ready) {
+    py::gil_scoped_release rel;
+    job.beta_ready.wait();
+  }
+  if (!job.beta_error.empty()) throw std::runtime_error(job.beta_error);
+  const size_t k = selfs.size();
+  if (!out_index.empty() && out_index.size() != k) throw std::runtime_error("select_noisers_job: index length");
+  const Lottery table(stake, n, Bytes{});
+  const i64 holders = i64(table.ids.size());
+  py::array_t<int64_t> res({py::ssize_t(k), py::ssize_t(nn)});
+  int64_t* o = res.mutable_data();
+  Bytes input;
+  input.reserve(64);
+  for (size_t w = 0; w < k; ++w) {
+    const size_t src = out_index.empty() ? w : size_t(out_index[w]);
+    if (src >= job.out.size()) throw std::runtime_error("select_noisers_job: output index out of range");
+    const Bytes& beta = job.out[src].first;
+    const i64 self = selfs[w];
+    const i64 others = holders - (std::binary_search(table.ids.begin(), table.ids.end(), self) ? 1 : 0);
+    if (others < nn) throw std::runtime_error("lottery: not enough peers for noisers");
+    input.assign(beta.begin(), beta.end());
+    size_t i = 0;
+    i64 got = 0;
+    while (got < nn) {   // Lottery::draw over the shared ticket table
+      if (i + 1 >= input.size()) {
+        input = Sha256::digest(input);
+        i = 0;
+      }
+      const i64 idx = i64((size_t(input[i]) * 256 + size_t(input[i + 1])) % size_t(table.total()));
+      ++i;
+      const i64 c = table.ticket(idx);
+      bool dup = c == self;
+      for (i64 q = 0; q < got && !dup; ++q) dup = o[w * nn + q] == c;
+      if (!dup) o[w * nn + got++] = c;
+    }
+  }
+  return res;
+}
+
 PYBIND11_MODULE(_biscotti_rt, m) {
   m.doc() = "biscotti_amd native host runtime (crypto, ledger, protocol FSM)";
 
@@ -1161,6 +1204,29 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         return py::make_tuple(a, online);
       })
       .def("route_shares", &RoundFSM::route_shares)
+      // the noiser lottery with this FSM's stake (no stake map round trip through a Python dict)
+      .def("select_noisers_job", [](const RoundFSM& f, VrfJob& job, std::vector<i64> out_index,
+                                    std::vector<i64> selfs, i64 nn, i64 n) {
+        return select_noisers_impl(f.stake, job, std::move(out_index), std::move(selfs), nn, n);
+      })
+      // route_shares + leader_view without the routes crossing into Python: (leader_online, quorum,
+      // node_list, contributing miners, {miner: share part of the node list's first worker})
+      .def("route_view", [](const RoundFSM& f, const std::vector<i64>& approved) {
+        auto routes = f.route_shares(approved);
+        auto lv = f.leader_view(routes);
+        py::dict part;
+        if (!lv.node_list.empty())
+          for (i64 m : lv.contributing_miners) {
+            auto it = routes.find(m);
+            if (it == routes.end()) continue;
+            for (auto& wp : it->second)
+              if (wp.first == lv.node_list[0]) {
+                part[py::int_(m)] = py::int_(wp.second);
+                break;
+              }
+          }
+        return py::make_tuple(lv.leader_online, lv.quorum, lv.node_list, lv.contributing_miners, part);
+      })
       .def("leader_view", &RoundFSM::leader_view)
       .def("route_updates", &RoundFSM::route_updates)
       .def("make_secagg_block", [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w,
@@ -1273,43 +1339,7 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   // Returns int64 [len(selfs), nn].  Same draws as select_noisers (equivalence-tested).
   m.def("select_noisers_job", [](const std::map<i64, i64>& stake, VrfJob& job, std::vector<i64> out_index,
                                  std::vector<i64> selfs, i64 nn, i64 n) {
-    {
-      py::gil_scoped_release rel;
-      job.beta_ready.wait();
-    }
-    if (!job.beta_error.empty()) throw std::runtime_error(job.beta_error);
-    const size_t k = selfs.size();
-    if (!out_index.empty() && out_index.size() != k) throw std::runtime_error("select_noisers_job: index length");
-    const Lottery table(stake, n, Bytes{});
-    const i64 holders = i64(table.ids.size());
-    py::array_t<int64_t> res({py::ssize_t(k), py::ssize_t(nn)});
-    int64_t* o = res.mutable_data();
-    Bytes input;
-    input.reserve(64);
-    for (size_t w = 0; w < k; ++w) {
-      const size_t src = out_index.empty() ? w : size_t(out_index[w]);
-      if (src >= job.out.size()) throw std::runtime_error("select_noisers_job: output index out of range");
-      const Bytes& beta = job.out[src].first;
-      const i64 self = selfs[w];
-      const i64 others = holders - (std::binary_search(table.ids.begin(), table.ids.end(), self) ? 1 : 0);
-      if (others < nn) throw std::runtime_error("lottery: not enough peers for noisers");
-      input.assign(beta.begin(), beta.end());
-      size_t i = 0;
-      i64 got = 0;
-      while (got < nn) {   // Lottery::draw over the shared ticket table
-        if (i + 1 >= input.size()) {
-          input = Sha256::digest(input);
-          i = 0;
-        }
-        const i64 idx = i64((size_t(input[i]) * 256 + size_t(input[i + 1])) % size_t(table.total()));
-        ++i;
-        const i64 c = table.ticket(idx);
-        bool dup = c == self;
-        for (i64 q = 0; q < got && !dup; ++q) dup = o[w * nn + q] == c;
-        if (!dup) o[w * nn + got++] = c;
-      }
-    }
-    return res;
+    return select_noisers_impl(stake, job, std::move(out_index), std::move(selfs), nn, n);
   });
   m.def("krum_scores", [](py::array_t<double, py::array::c_style | py::array::forcecast> X, i64 groupsize) {
     if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");

@@ -50,7 +50,8 @@ class RoundHeadMixin:
         latest_hash = fsm.chain.latest().hash
         workers = [w for w in plan.workers if live[w]]
         local_workers = [w for w in workers if w in self.local]
-        head.update(workers=workers, local_workers=local_workers, stake=dict(fsm.stake))
+        # stake None: the noiser lottery reads the FSM's stake natively (unchanged until the block commits)
+        head.update(workers=workers, local_workers=local_workers, stake=None)
         # noisers: each worker's own ECVRF over the latest block hash (vrf.go:54-100).  Only the 64-byte
         # outputs gate the round (noiser lottery -> noise -> Krum -> the selection that cancels speculative
         # MSM rows); every rank computes them for the peers it hosts only (the reference: each peer proves

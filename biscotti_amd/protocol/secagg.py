@@ -300,12 +300,10 @@ class SecAggMixin:
                         if sum(any(R.schnorr_verify(commit_of[w], self.pk[v], sg) for v in plan.verifiers)
                                for sg in signatures.get(w, [])) >= need]
         with tm.phase("shares"):
-            routes = fsm.route_shares(approved)
-            lv = fsm.leader_view(routes)
-        if not (lv.leader_online and lv.quorum):
+            # share routing + the leader's view natively (the routes never cross into Python)
+            online, quorum, node_list, contributing, part_of = fsm.route_view(approved)
+        if not (online and quorum):
             return None
-        node_list, contributing = list(lv.node_list), list(lv.contributing_miners)
-        part_of = {m: dict(routes[m])[node_list[0]] for m in contributing}
         if sa is not None and sa.get("accepted") is not None and contributing == sa["contributing"] \
                 and part_of == sa["part"] and set(node_list) == sa["accepted"]:
             # the device already aggregated exactly these workers' shares (queued behind the committee's

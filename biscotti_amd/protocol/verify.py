@@ -35,8 +35,10 @@ class VerifyMixin:
         if fut_noise is None or not local_workers:
             return {}
         # the lottery reads the job's outputs natively (no 64-byte Python objects in between)
-        sel = self.R.select_noisers_job(stake, fut_noise, list(index) if index is not None else [], local_workers,
-                                        self.cfg.num_noisers, self.N)
+        idx = list(index) if index is not None else []
+        sel = self.fsm.select_noisers_job(fut_noise, idx, local_workers, self.cfg.num_noisers, self.N) \
+            if stake is None else self.R.select_noisers_job(stake, fut_noise, idx, local_workers, self.cfg.num_noisers,
+                                                             self.N)
         self._noise_arr = (local_workers, sel)   # the same ids as an array, in local_workers order
         return dict(zip(local_workers, sel.tolist()))
 
@@ -296,7 +298,12 @@ class VerifyMixin:
                 acc_row = {v: k for k, v in enumerate(vs)}
                 if box.get("sa") is not None:   # the rows the device aggregation kept
                     node_np = node_t.numpy()
-                    kept = {w for w in workers if node_np[xrow[w]]}
+                    xc = getattr(self, "_xrow_np", None)
+                    if xc is not None and xc[1] is xrow:   # numpy gather (the _krum_static table)
+                        wk = np.asarray(workers, np.int64)
+                        kept = set(wk[node_np[xc[2][wk]].astype(bool)].tolist())
+                    else:
+                        kept = {w for w in workers if node_np[xrow[w]]}
                     # a block row outside the (replicated) speculative candidates was never computed: the
                     # device aggregate is then incomplete and the host path tops it up
                     if not kept <= head["spec_cand"]:

@@ -262,3 +262,33 @@ def test_cli_defaults_match_runconfig():
 
     with pytest.raises(ValueError):
         RunConfig(ablation="early_krum").validate()
+
+
+def test_route_view_matches_route_shares_and_leader_view():
+    """RoundFSM.route_view (share routing + the leader's view in one native call) == route_shares followed
+    by leader_view and the first node's share part per contributing miner, with all miners live and with
+    one miner offline."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    eng = BiscottiEngine(RunConfig(num_nodes=14, dataset="mnist", seed=4, max_iterations=100,
+                                   deterministic_time=True), Comm())
+    eng.run_round()
+    fsm = eng.fsm
+    for kill in (None, 0):
+        live = [1] * 14
+        plan = fsm.begin_round(live)
+        if kill is not None:
+            live[list(plan.miners)[kill]] = 0
+            plan = fsm.begin_round(live)
+        approved = list(plan.workers)[: 7]
+        routes = fsm.route_shares(approved)
+        lv = fsm.leader_view(routes)
+        online, quorum, nodes, contrib, part = fsm.route_view(approved)
+        assert (online, quorum, list(nodes), list(contrib)) == \
+            (lv.leader_online, lv.quorum, list(lv.node_list), list(lv.contributing_miners))
+        if nodes:
+            assert part == {m: dict(routes[m])[nodes[0]] for m in contrib}
+        fsm.iteration -= 1   # undo the probe's begin_round
+    eng.close()
