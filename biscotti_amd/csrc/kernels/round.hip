@@ -154,13 +154,21 @@ extern "C" int bsc_round_csum_early(void* ctx, const uint32_t* ccom, void* ev_cc
 // pinned staging (host [2n] int32: rows, then ones) into rows_dev [2n], and runs the MSM over them into
 // resident pts / ys.  The caller rotates staging / device buffers over enough slots that a slot is
 // rewritten only after its MSM and every consumer of its outputs are done.
+// The upload goes through `up` (a high-priority stream on every CU, event ev_up): on the CU-masked, low-
+// priority side stream the copy kernel waited ~150 us for a free slot behind the pre-step's MSM.
 extern "C" int bsc_round_spec_msm(void* ctx, void* ev_wait, const long long* coeffs, const int* rows_host,
                                   int* rows_dev, int n, const uint32_t* tbl_wb, int commit_only, int group_rows,
-                                  uint32_t* pts, long long* ys) {
+                                  uint32_t* pts, long long* ys, void* up, void* ev_up) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || n <= 0) return -1;
   if (ev_wait != nullptr) RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_wait, 0));
-  RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, c->side));
+  if (up != nullptr && ev_up != nullptr) {
+    RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, (hipStream_t)up));
+    RC_CHECK(hipEventRecord((hipEvent_t)ev_up, (hipStream_t)up));
+    RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_up, 0));
+  } else {
+    RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, c->side));
+  }
   RC_CHECK(bsc_shares_msm(coeffs, c->d, rows_dev, n, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, commit_only,
                           rows_dev + n, nullptr, group_rows, pts, ys, c->side));
   return 0;

@@ -466,7 +466,7 @@ class NativeSecAgg:
 
     SPEC_SLOTS = 3
 
-    def spec_msm(self, qdelta, rows: list, ev_wait, no_commit: bool, group_rows: int) -> "NativeSpec":
+    def spec_msm(self, qdelta, rows: list, ev_wait, no_commit: bool, group_rows: int, up=None) -> "NativeSpec":
         """The speculative share MSM of qdelta[rows] on the side stream, behind ev_wait (a torch event: the
         pre-step), in one native call with resident outputs (a ring of SPEC_SLOTS: a slot is reused three
         rounds later, long after its round read it).  Returns the handle the engine's aggregation uses
@@ -483,13 +483,21 @@ class NativeSecAgg:
                 for _ in range(self.SPEC_SLOTS)]}
         ring["k"] = (ring["k"] + 1) % self.SPEC_SLOTS
         sl = ring["slots"][ring["k"]]
+        ev_up = None
+        if up is not None:
+            ev_up = sl.get("ev_up")
+            if ev_up is None:
+                ev_up = sl["ev_up"] = torch.cuda.Event()
+                ev_up.record(up)   # materialise the handle (re-recorded natively)
         h = sl["host"].numpy()
         h[:n] = rows
         h[n:2 * n] = 1
         pts, ys = sl["pts"][:n], sl["ys"][:n]
         _check(hip().bsc_round_spec_msm(self.ctx, ev_wait.cuda_event if ev_wait is not None else None,
                                         _ptr(qdelta), sl["host"].data_ptr(), _ptr(sl["rows"]), n, _ptr(eng.tbl_wb),
-                                        2 if no_commit else 0, int(group_rows), _ptr(pts), _ptr(ys)), "round_spec_msm")
+                                        2 if no_commit else 0, int(group_rows), _ptr(pts), _ptr(ys),
+                                        up.cuda_stream if up is not None else None,
+                                        ev_up.cuda_event if ev_up is not None else None), "round_spec_msm")
         return NativeSpec(qdelta, rows, sl["rows"][:n], sl["rows"][n:2 * n], pts, ys, no_commit)
 
     def readback(self):

@@ -299,7 +299,7 @@ class RoundHeadMixin:
         rows = [w - self.lo for w in spec_workers]
         if self._native is not None:
             # one native call: wait for the step, upload rows + flags, launch (resident output ring)
-            sp = self._native.spec_msm(pre["qdelta"], rows, pre["ev"], no_commit, SPEC_GROUP_ROWS)
+            sp = self._native.spec_msm(pre["qdelta"], rows, pre["ev"], no_commit, SPEC_GROUP_ROWS, self.upload_stream)
             sp.record(side)
         else:
             side.wait_event(pre["ev"])   # the step only (it ran on the Gram stream), not the audit on main
