@@ -192,6 +192,14 @@ def main() -> int:
     sync = (lambda: torch.cuda.synchronize()) if eng.gpu else (lambda: None)
     sync()
     setup_s = time.perf_counter() - t_setup   # engine + HBM-resident tables (keygen/bootstrap analogue)
+    # the round's host thread on a core of its own next to the GPU, the native workers beside it
+    # (utils/affinity.py, opt-in with BISCOTTI_PIN=1); undone after the timed rounds
+    placement, cpus0 = None, (os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None)
+    if eng.gpu:
+        from biscotti_amd.native import rt
+        from biscotti_amd.utils.affinity import pin_round_threads
+
+        placement = pin_round_threads(comm.device.index, cfg.host_threads, rt())
     for _ in range(a.warmup):
         eng.run_round()
     comm.barrier()
@@ -222,6 +230,8 @@ def main() -> int:
     # device memory segments the caching allocator had to hipMalloc inside the timed window
     seg_new = (torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) - seg0) if eng.gpu else 0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    if placement is not None:
+        os.sched_setaffinity(0, cpus0)
     host_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)   # every thread of this rank
     stats0 = {k: v for k, v in getattr(eng, "stats", {}).items() if isinstance(v, (int, float))}
     t = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
@@ -298,6 +308,7 @@ def main() -> int:
             "final_test_acc_mean_std": ms(finals),
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
+            "host_placement": placement,
             "drain_ms": 1e3 * drain_s,          # inside the timed window: joins of the last rounds' work
             "device_segments_allocated_timed": seg_new,
             "round_wall_ms": [round(1e3 * w, 3) for w in walls],

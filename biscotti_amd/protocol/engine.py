@@ -211,7 +211,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         VRF outputs / Krum, and the critical path keeps the rest)."""
         lo, hi = torch.cuda.Stream.priority_range()
         self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
-        self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, SIDE_STREAM_SKIP_EVERY)
+        import os
+        skip = int(os.environ.get("BISCOTTI_SIDE_SKIP", str(SIDE_STREAM_SKIP_EVERY)))   # A/B of the CU mask
+        self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, skip)
         # work no consumer in the round waits for (the miners' witness sums, the commitments)
         self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
         # long device work nothing in a round waits for -- the VRF proofs (kernels/vrf.hip) and the KZG
