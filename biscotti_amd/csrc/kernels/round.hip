@@ -38,6 +38,8 @@ extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2,
                                 double* part, double* gram, unsigned int* count, void* stream);
 extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
                                void* stream);
+extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
+                               int B0, int NW, uint32_t* partial, uint32_t* out, void* stream);
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
                                const uint32_t* csum, int nm, int nch, int* ok, void* stream);
 
@@ -189,7 +191,7 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
                                  const int* rows_arange, uint32_t* ccom, uint32_t* jac, uint32_t* jac_host,
                                  int do_gram, const float* T_rows, int U2, long long stride2, int kchunk, double* part,
                                  double* gram, unsigned int* counters, void* ev_step, void* ev_ccom, void* ev_commit,
-                                 void* ev_gram) {
+                                 void* ev_gram, int chunked) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || P <= 0 || d_in * d_out + d_out != c->d) return -1;
   hipStream_t gs = (hipStream_t)gram_stream;
@@ -199,10 +201,14 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
                             qdelta, loss, lo, gs));
   RC_CHECK(hipEventRecord((hipEvent_t)ev_step, gs));
   RC_CHECK(hipStreamWaitEvent(c->bg, (hipEvent_t)ev_step, 0));
-  RC_CHECK(bsc_shares_msm(qdelta, c->d, rows_arange, P, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, 1, nullptr,
-                          nullptr, 0, ccom, nullptr, c->bg));
-  RC_CHECK(hipEventRecord((hipEvent_t)ev_ccom, c->bg));
-  RC_CHECK(bsc_segment_sum(ccom, P, c->nch, 1, 0, jac, c->bg));
+  if (chunked) {
+    RC_CHECK(bsc_shares_msm(qdelta, c->d, rows_arange, P, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, 1, nullptr,
+                            nullptr, 0, ccom, nullptr, c->bg));
+    RC_CHECK(hipEventRecord((hipEvent_t)ev_ccom, c->bg));
+    RC_CHECK(bsc_segment_sum(ccom, P, c->nch, 1, 0, jac, c->bg));
+  } else {   // full commitments only (1024-coefficient slabs; ccom is the slab-partials scratch)
+    RC_CHECK(bsc_commit_rows(qdelta, c->d, rows_arange, P, c->tbl_pk, c->b0, c->nw, ccom, jac, c->bg));
+  }
   RC_CHECK(hipMemcpyAsync(jac_host, jac, (size_t)P * 24 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->bg));
   RC_CHECK(hipEventRecord((hipEvent_t)ev_commit, c->bg));
   if (do_gram) {

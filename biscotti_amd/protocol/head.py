@@ -242,7 +242,10 @@ class RoundHeadMixin:
             nk = self._noise_krum()
             with S.use(gs):
                 cnt = K._tile_counters(self.dev, 1024)
-            out = self._native.prestep(self.task, W, it, gs, self.noise_rows.rows(it) if nk else None, cnt)
+            import os
+            chunked = os.environ.get("BISCOTTI_EARLY_CS", "1") == "1"   # A/B: 0 = full commitments only
+            out = self._native.prestep(self.task, W, it, gs, self.noise_rows.rows(it) if nk else None, cnt,
+                                       chunked=chunked)
             if nk:
                 out["gram"]["xrow"] = self.flat
             return out
