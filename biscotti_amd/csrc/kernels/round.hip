@@ -139,15 +139,18 @@ extern "C" int bsc_round_audit(void* ctx, const long long* coeffs, const uint32_
 // still alive -- the same rows the share sums use -- while the MSM is still running.  ccom: Jacobian
 // [npeer][nch][24], produced on another stream (ev_ccom).  bsc_round_secagg(.., audit = 2) then skips
 // its own commitment sums and bsc_round_audit waits for these.
+// `stream`: where the sums run -- NOT the side stream, which is still busy with the share MSM (they would
+// queue behind it); nullptr = the side stream.
 extern "C" int bsc_round_csum_early(void* ctx, const uint32_t* ccom, void* ev_ccom, const int* rows, int R,
-                                    const int* mask, uint32_t* cs) {
+                                    const int* mask, uint32_t* cs, void* stream) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || R <= 0) return -1;
+  hipStream_t st = stream != nullptr ? (hipStream_t)stream : c->side;
   RC_CHECK(hipEventRecord(c->ev_main, c->main));
-  RC_CHECK(hipStreamWaitEvent(c->side, c->ev_main, 0));
-  if (ev_ccom != nullptr) RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_ccom, 0));
-  RC_CHECK(bsc_sum_rows2_pos(ccom, c->nch, rows, R, nullptr, c->nch, mask, cs, c->side));
-  RC_CHECK(hipEventRecord(c->ev_side, c->side));
+  RC_CHECK(hipStreamWaitEvent(st, c->ev_main, 0));
+  if (ev_ccom != nullptr) RC_CHECK(hipStreamWaitEvent(st, (hipEvent_t)ev_ccom, 0));
+  RC_CHECK(bsc_sum_rows2_pos(ccom, c->nch, rows, R, nullptr, c->nch, mask, cs, st));
+  RC_CHECK(hipEventRecord(c->ev_side, st));
   return 0;
 }
 

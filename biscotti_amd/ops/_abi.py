@@ -23,7 +23,7 @@ SIGNATURES = {
     "bsc_segment_sum": [P, I, I, I, I, P, P],
     "bsc_sum_rows2": [P, I, P, I, P, I, P, P, P],
     "bsc_sum_rows2_pos": [P, I, P, I, P, I, P, P, P],
-    "bsc_round_csum_early": [P, P, P, P, I, P, P],
+    "bsc_round_csum_early": [P, P, P, P, I, P, P, P],
     "bsc_round_spec_msm": [P, P, P, P, P, I, P, I, I, P, P, P, P],
     "bsc_round_prestep": [P, P, P, P, P, P, P, P, I, I, I, I, U64, I, F, D, I, P, P, P, P, P, P, P, P,
                           I, P, I, L, I, P, P, P, P, P, P, P, I],

@@ -395,7 +395,7 @@ class NativeSecAgg:
             raise RuntimeError(f"bsc_round_secagg failed ({err})")
         return W_new, self.coeffs, self.status, agg
 
-    def csum_early(self, ccom, ccom_event, rows, mask) -> None:
+    def csum_early(self, ccom, ccom_event, rows, mask, stream=None) -> None:
         """Queue the audit's commitment sums now (side stream, behind what main has queued so far -- the
         selection's flags -- and the pre-step's chunk commitments): cs = sum over the rows r with
         mask[r] != 0 of ccom[rows[r]].  secagg(.., audit=2) then leaves them out."""
@@ -404,7 +404,8 @@ class NativeSecAgg:
         assert rows.dtype == torch.int32 and mask.dtype == torch.int32 and mask.numel() == R
         ev = ccom_event.cuda_event if ccom_event is not None else None
         _check(hip().bsc_round_csum_early(self.ctx, _ptr(ccom.contiguous()), ev, _ptr(rows), R, _ptr(mask),
-                                          _ptr(self.cs)), "round_csum_early")
+                                          _ptr(self.cs), stream.cuda_stream if stream is not None else None),
+               "round_csum_early")
 
     PRE_SLOTS = 3
 

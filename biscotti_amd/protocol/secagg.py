@@ -78,7 +78,8 @@ class SecAggMixin:
                     and getattr(pc, "ccom", None) is not None and pc.src is sp.qdelta:
                 # the audit's commitment sums from the pre-step's chunk commitments, queued before main waits
                 # for the MSM: they run while the MSM is still busy, not after it
-                self._native.csum_early(pc.ccom, pc.ccom_event, sp.rows_t, alive)
+                # on the (high-priority, otherwise idle) upload stream: the side stream still runs the MSM
+                self._native.csum_early(pc.ccom, pc.ccom_event, sp.rows_t, alive, self.upload_stream)
                 early_cs = True
             elif sp.no_commit and cfg.audit_aggregate:
                 raise RuntimeError("speculative MSM without commitment slots but no chunk commitments to audit with")
