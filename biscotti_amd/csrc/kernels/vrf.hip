@@ -768,6 +768,26 @@ extern "C" __global__ void __launch_bounds__(192) k_vrf_prove(const uint32_t* __
 
 extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
                              int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
+                             void* stream);
+
+// One round's proofs in one call (per-round launches, ops/vrf.py): the staging words [key rows (n) | zeros
+// (n) | the 32-byte message (8 words)] go up from pinned memory, the prover runs, `ev` is recorded -- a
+// resident slot per call, no allocation, ~10 us of the caller's time instead of a Python launch path.
+extern "C" int bsc_vrf_prove_round(const uint32_t* keys, const int* staging_host, int* staging_dev, int n,
+                                   const uint32_t* btab, uint32_t* scratch, uint8_t* pi, void* stream, void* ev) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpyAsync(staging_dev, staging_host, (2 * (size_t)n + 8) * sizeof(int), hipMemcpyHostToDevice, st) !=
+      hipSuccess)
+    return -1;
+  const int rc = bsc_vrf_prove(keys, staging_dev, (const uint8_t*)(staging_dev + 2 * n), staging_dev + n, 32, n, btab,
+                               scratch, pi, nullptr, stream);
+  if (rc != 0) return rc;
+  return ev != nullptr ? (int)hipEventRecord((hipEvent_t)ev, st) : 0;
+}
+
+extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
+                             int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
                              void* stream) {
   if (n <= 0) return 0;
   if (alpha_len < 0 || alpha_len > 1024) return -1;

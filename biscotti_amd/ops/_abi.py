@@ -37,6 +37,7 @@ SIGNATURES = {
     "bsc_chunk_check": [P, I, I, P, I, I, P, I, I, P, P],
     # vrf.hip
     "bsc_vrf_prove": [P, P, P, P, I, I, P, P, P, P, P],
+    "bsc_vrf_prove_round": [P, P, P, I, P, P, P, P, P],
     # kzg.hip
     "bsc_kzg_blocks": [I, I],
     "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, I, U64, P, P, P],
