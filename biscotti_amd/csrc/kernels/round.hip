@@ -194,26 +194,28 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
                                  const int* rows_arange, uint32_t* ccom, uint32_t* jac, uint32_t* jac_host,
                                  int do_gram, const float* T_rows, int U2, long long stride2, int kchunk, double* part,
                                  double* gram, unsigned int* counters, void* ev_step, void* ev_ccom, void* ev_commit,
-                                 void* ev_gram, int chunked) {
+                                 void* ev_gram, int chunked, void* commit_stream) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || P <= 0 || d_in * d_out + d_out != c->d) return -1;
   hipStream_t gs = (hipStream_t)gram_stream;
+  // the commitments' stream (default: background; an A/B passes one masked to the CUs the MSM leaves)
+  hipStream_t cst = commit_stream != nullptr ? (hipStream_t)commit_stream : c->bg;
   RC_CHECK(hipEventRecord(c->ev_pre, c->main));
   RC_CHECK(hipStreamWaitEvent(gs, c->ev_pre, 0));
   RC_CHECK(bsc_softmax_step(X, y, off, ntrain, pid, W, d_in, d_out, B, P, seed, iteration, max_norm, qscale, delta,
                             qdelta, loss, lo, gs));
   RC_CHECK(hipEventRecord((hipEvent_t)ev_step, gs));
-  RC_CHECK(hipStreamWaitEvent(c->bg, (hipEvent_t)ev_step, 0));
+  RC_CHECK(hipStreamWaitEvent(cst, (hipEvent_t)ev_step, 0));
   if (chunked) {
     RC_CHECK(bsc_shares_msm(qdelta, c->d, rows_arange, P, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, 1, nullptr,
-                            nullptr, 0, ccom, nullptr, c->bg));
-    RC_CHECK(hipEventRecord((hipEvent_t)ev_ccom, c->bg));
-    RC_CHECK(bsc_segment_sum(ccom, P, c->nch, 1, 0, jac, c->bg));
+                            nullptr, 0, ccom, nullptr, cst));
+    RC_CHECK(hipEventRecord((hipEvent_t)ev_ccom, cst));
+    RC_CHECK(bsc_segment_sum(ccom, P, c->nch, 1, 0, jac, cst));
   } else {   // full commitments only (1024-coefficient slabs; ccom is the slab-partials scratch)
-    RC_CHECK(bsc_commit_rows(qdelta, c->d, rows_arange, P, c->tbl_pk, c->b0, c->nw, ccom, jac, c->bg));
+    RC_CHECK(bsc_commit_rows(qdelta, c->d, rows_arange, P, c->tbl_pk, c->b0, c->nw, ccom, jac, cst));
   }
-  RC_CHECK(hipMemcpyAsync(jac_host, jac, (size_t)P * 24 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->bg));
-  RC_CHECK(hipEventRecord((hipEvent_t)ev_commit, c->bg));
+  RC_CHECK(hipMemcpyAsync(jac_host, jac, (size_t)P * 24 * sizeof(uint32_t), hipMemcpyDeviceToHost, cst));
+  RC_CHECK(hipEventRecord((hipEvent_t)ev_commit, cst));
   if (do_gram) {
     RC_CHECK(bsc_gram_stacked(delta, P, T_rows, U2, stride2, c->d, kchunk, part, gram, counters, gs));
     RC_CHECK(hipEventRecord((hipEvent_t)ev_gram, gs));

@@ -26,7 +26,7 @@ SIGNATURES = {
     "bsc_round_csum_early": [P, P, P, P, I, P, P, P],
     "bsc_round_spec_msm": [P, P, P, P, P, I, P, I, I, P, P, P, P],
     "bsc_round_prestep": [P, P, P, P, P, P, P, P, I, I, I, I, U64, I, F, D, I, P, P, P, P, P, P, P, P,
-                          I, P, I, L, I, P, P, P, P, P, P, P, I],
+                          I, P, I, L, I, P, P, P, P, P, P, P, I, P],
     "bsc_commit_rows": [P, I, P, I, P, I, I, P, P, P],
     "bsc_stream_create_cumask": [I, P],
     "bsc_stream_destroy": [P],

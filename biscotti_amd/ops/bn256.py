@@ -410,7 +410,7 @@ class NativeSecAgg:
     PRE_SLOTS = 3
 
     def prestep(self, task, W, it: int, gram_stream, noise_rows, gram_counters, kchunk: int = 512,
-                chunked: bool = True) -> dict:
+                chunked: bool = True, commit_stream=None) -> dict:
         """The next round's pre-step of a SoftmaxTask in ONE native call (bsc_round_prestep): the local step of
         every local peer on the Gram stream, the per-chunk + full commitments (read back) on the background
         stream and, with noise_rows (the noise table's rows of this iteration), the noise-aware Krum's Gram.
@@ -456,7 +456,7 @@ class NativeSecAgg:
             noise_rows.data_ptr() if noise_rows is not None else None, U2,
             noise_rows.stride(0) if noise_rows is not None else 0, kchunk, _ptr(sl["part"]), _ptr(sl["gram"]),
             _ptr(gram_counters), e_step.cuda_event, e_ccom.cuda_event, e_commit.cuda_event, e_gram.cuda_event,
-            int(chunked)), "round_prestep")
+            int(chunked), commit_stream.cuda_stream if commit_stream is not None else None), "round_prestep")
         pc = _PendingCommitments(sl["host"], e_commit, sl["jac"])
         if chunked:   # per-chunk commitments for the early audit sums
             pc.ccom, pc.ccom_event, pc.src = sl["ccom"], e_ccom, sl["qdelta"]

@@ -166,8 +166,10 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.vrf_dev = None
         if self.gpu and cfg.vrf_device:
             from ..ops.vrf import DeviceVrfProver
-            # 16 rounds per launch: a launch (~2.5 ms) keeps ~13 CUs busy and slows the critical path's
-            # kernels that share them, so launches are batched (per-round launches measured 2.01 vs 1.85 ms/round)
+            # 16 rounds per launch: a launch (~2.2 ms) occupies its SIMDs' register files (352 registers per
+            # wave) and slows the MSM waves that share them.  Per-round launches round-robin over several
+            # streams (BISCOTTI_VRF_BATCH=1, BISCOTTI_VRF_STREAMS=3) cut the end-of-run drain from 2.8 to
+            # ~0.9 ms but cost ~0.07 ms in every round (1.45 vs 1.38 ms/round, docs/PERF.md round 3)
             nb = int(os.environ.get("BISCOTTI_VRF_BATCH", "16"))
             ns = int(os.environ.get("BISCOTTI_VRF_STREAMS", "1"))
             extra = [torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[0])
