@@ -961,6 +961,76 @@ extern "C" __global__ void __launch_bounds__(256) k_eval_error(const float* X, c
   }
 }
 
+// The same on a cached, pre-transformed test set: Xt[tile][g][64] holds (x - 0.5) / 0.5 of row
+// tile*16 + (l & 15), feature 4g + (l >> 4) for lane l -- exactly the A operand of one
+// v_mfma_f32_16x16x4f32 step -- built once per task (the test rows never change).  Each MFMA step is one
+// coalesced 256-byte load: the row-strided gathers and the per-element transform of k_eval_error are gone.
+extern "C" __global__ void __launch_bounds__(256) k_eval_error_t(const float* Xt, const int* y, int N, int KG, int D_IN,
+                                                                int D_OUT, const double* W, int split,
+                                                                unsigned int* err) {
+  // 4 waves per tile split the K loop (latency: the evaluation is read one round later and must be done by
+  // then under the share MSM's load), then reduce the logits through LDS
+  __shared__ float red[4][4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, tile = blockIdx.x;
+  const int i = lane & 15, kk = lane >> 4;
+  const bool cval = i < D_OUT;
+  const double* wr = W + (size_t)(cval ? i : 0) * D_IN;
+  const float* xp = Xt + (size_t)tile * KG * 64 + lane;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int gq = (KG + 3) / 4;
+  int g = wid * gq;
+  const int gend = min(KG, g + gq);
+  for (; g + 8 <= gend; g += 8) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = xp[(size_t)(g + u) * 64];
+      const int k = 4 * (g + u) + kk;
+      b[u] = (cval && k < D_IN) ? (float)wr[k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], b[u + 1], acc1, 0, 0, 0);
+    }
+  }
+  for (; g < gend; ++g) {
+    const int k = 4 * g + kk;
+    const float b = (cval && k < D_IN) ? (float)wr[k] : 0.f;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xp[(size_t)g * 64], b, acc0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][r][lane] = acc0[r] + acc1[r];
+  __syncthreads();
+  if (wid != 0) return;
+  const float bias = cval ? (float)W[(size_t)D_OUT * D_IN + i] : 0.f;
+  unsigned int cnt0 = 0, cnt1 = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float logit = (red[0][r][lane] + red[1][r][lane]) + (red[2][r][lane] + red[3][r][lane]);
+    float bv = cval ? logit + bias : -__builtin_huge_valf();
+    int bc = i;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 16);
+      const int oc = __shfl_xor(bc, o, 16);
+      if (ov > bv || (ov == bv && oc < bc)) {
+        bv = ov;
+        bc = oc;
+      }
+    }
+    const int row = tile * 16 + kk * 4 + r;
+    if (i == 0 && row < N && bc != y[row]) {
+      if (row < split) ++cnt0;
+      else ++cnt1;
+    }
+  }
+  if (i == 0) {
+    if (cnt0) atomicAdd(err, cnt0);
+    if (cnt1) atomicAdd(err + 1, cnt1);
+  }
+}
+
 // =====================================================================================
 // K12: exact recovery of the aggregated chunk polynomials from miner shares.
 // ys: int64 [nchunks][npts], xs: int [npts] distinct; deg+1 <= npts.  Newton divided differences
@@ -1297,6 +1367,19 @@ extern "C" int bsc_eval_error_rb(const float* X, const int* y, int N, int D_IN, 
   if (hipMemsetAsync(err, 0, 2 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) return -1;
   const int rc = bsc_eval_error(X, y, N, D_IN, D_OUT, W, transform, split, err, stream);
   if (rc != 0) return rc;
+  return (int)hipMemcpyAsync(err_host, err, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, (hipStream_t)stream);
+}
+
+extern "C" int bsc_eval_error_t_rb(const float* Xt, const int* y, int N, int KG, int D_IN, int D_OUT, const double* W,
+                                   int split, unsigned int* err, unsigned int* err_host, void* stream) {
+  if (D_OUT > 16 || D_IN <= 0 || KG * 4 < D_IN) return -1;
+  if (hipMemsetAsync(err, 0, 2 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) return -1;
+  if (N > 0) {
+    hipLaunchKernelGGL(k_eval_error_t, dim3((N + 15) / 16), dim3(256), 0, (hipStream_t)stream, Xt, y, N, KG, D_IN, D_OUT,
+                       W, split, err);
+    const int rc = (int)hipGetLastError();
+    if (rc != 0) return rc;
+  }
   return (int)hipMemcpyAsync(err_host, err, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, (hipStream_t)stream);
 }
 

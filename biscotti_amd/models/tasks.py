@@ -89,8 +89,10 @@ class SoftmaxTask:
 
     def evaluate_async(self, W: torch.Tensor):
         """Queue the test / attack evaluations now; the returned callable reads them back."""
+        if self.device.type == "cuda" and getattr(self, "_eval_Xt", None) is None:
+            self._eval_Xt = K.eval_tiles(self.eval_X, transform=True)   # the test rows never change
         both = K.eval_errors_async(self.eval_X, self.eval_y, self.eval_split, W, self.d_in, self.d_out,
-                                   transform=True)
+                                   transform=True, Xt=getattr(self, "_eval_Xt", None))
 
         def result():
             err, att = both()

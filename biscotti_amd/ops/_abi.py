@@ -51,6 +51,7 @@ SIGNATURES = {
     "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_eval_error_rb": [P, P, I, I, I, P, I, I, P, P, P],
+    "bsc_eval_error_t_rb": [P, P, I, I, I, I, P, I, P, P, P],
     "bsc_noise_table": [I, I, U64, P, P],
     "bsc_dp_noise_tbl": [P, I, I, P, I, P, P, I, P, P, P],
     "bsc_recover": [P, I, I, P, I, I, P, D, P, P, P, P],

@@ -490,7 +490,17 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
 _EVAL_DEV: dict = {}   # pinned read-back buffer -> its device accumulator (persistent pairs)
 
 
-def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
+def eval_tiles(X: torch.Tensor, transform: bool = True) -> torch.Tensor:
+    """The test set in k_eval_error_t's layout: [ceil(N/16), ceil(d_in/4), 64] fp32, entry [t, g, l] =
+    transform(X[16 t + (l & 15), 4 g + (l >> 4)]) with zero padding (built once per task)."""
+    N, D = X.shape
+    T, KG = (N + 15) // 16, (D + 3) // 4
+    Xp = torch.zeros((T * 16, KG * 4), dtype=torch.float32, device=X.device)
+    Xp[:N, :D] = (X.float() - 0.5) / 0.5 if transform else X.float()
+    return Xp.view(T, 16, KG, 4).permute(0, 2, 3, 1).reshape(T, KG, 64).contiguous()
+
+
+def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True, Xt=None):
     """Error rates of W on rows [0, split) and [split, N) of X from ONE kernel launch and one
     read-back (test error + 1->7 attack rate).  Returns a callable giving (err_a, err_b)."""
     N = X.shape[0]
@@ -507,8 +517,13 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True):
     err = _EVAL_DEV.get(host.data_ptr())
     if err is None:
         err = _EVAL_DEV[host.data_ptr()] = torch.empty((2,), dtype=torch.int32, device=X.device)
-    _check(hip().bsc_eval_error_rb(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), int(split), _p(err),
-                                   host.data_ptr(), _stream()), "eval_error")
+    if Xt is not None:   # cached pre-transformed tiles (k_eval_error_t)
+        assert Xt.shape[0] == (N + 15) // 16 and Xt.shape[1] * 4 >= d_in and Xt.shape[2] == 64
+        _check(hip().bsc_eval_error_t_rb(_p(Xt), _p(y), N, Xt.shape[1], d_in, d_out, _p(W), int(split), _p(err),
+                                         host.data_ptr(), _stream()), "eval_error_t")
+    else:
+        _check(hip().bsc_eval_error_rb(_p(X), _p(y), N, d_in, d_out, _p(W), int(transform), int(split), _p(err),
+                                       host.data_ptr(), _stream()), "eval_error")
     ev = S.record()
 
     def result():

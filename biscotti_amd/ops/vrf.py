@@ -35,6 +35,7 @@ class DeviceVrfProver:
         # previous rounds' instead of queueing behind them: a launch's latency, ~2 ms, exceeds a round)
         self.streams = list(streams) if streams else None
         self._rr = 0
+        self._bufs: dict = {}
         self._row: dict[bytes, int] = {}
         self._keys: list[np.ndarray] = []
         self._keys_dev = None
@@ -61,14 +62,24 @@ class DeviceVrfProver:
         return self._launch(np.asarray(self._rows(seeds), np.int32), list(uniq),
                             np.asarray([uniq[a] for a in alphas], np.int32), beta)
 
-    def _launch(self, rows: np.ndarray, alphas: list, alpha_idx: np.ndarray, beta: bool = False):
+    def _launch(self, rows: np.ndarray, alphas: list, alpha_idx: np.ndarray, beta: bool = False, reuse: bool = False):
         n = int(rows.size)
         if self._keys_dev is None:
             self._keys_dev = self._upload(np.concatenate(self._keys))
         al = self._upload(np.frombuffer(b"".join(alphas), np.uint8))
         idx = self._upload(np.concatenate([rows, alpha_idx]))
-        scratch = torch.empty((max(n, 1), 320), dtype=torch.int32, device=self.device)
-        pi = torch.empty((n, 80), dtype=torch.uint8, device=self.device)
+        # scratch and the (discarded) proofs reuse one buffer per stream: launches on a stream run in order,
+        # and a fresh multi-MB allocation inside a timed round could cost a hipMalloc
+        key = S.raw()
+        buf = self._bufs.get(key) if reuse else None
+        if not reuse:
+            buf = (torch.empty((max(n, 1), 320), dtype=torch.int32, device=self.device),
+                   torch.empty((max(n, 1), 80), dtype=torch.uint8, device=self.device))
+        elif buf is None or buf[0].shape[0] < max(n, 1):
+            cap = max(n, 1, self.batch_rounds * 256)
+            buf = self._bufs[key] = (torch.empty((cap, 320), dtype=torch.int32, device=self.device),
+                                     torch.empty((cap, 80), dtype=torch.uint8, device=self.device))
+        scratch, pi = buf[0][: max(n, 1)], buf[1][:n]
         bt = torch.empty((n, 64), dtype=torch.uint8, device=self.device) if beta else None
         err = hip().bsc_vrf_prove(self._keys_dev.data_ptr(), idx.data_ptr(), al.data_ptr(), idx[n:].data_ptr(),
                                   self.ALPHA_LEN, n, self.btab.data_ptr(), scratch.data_ptr(), pi.data_ptr(),
@@ -77,6 +88,17 @@ class DeviceVrfProver:
             raise RuntimeError(f"HIP launch of vrf_prove failed with hipError {err}")
         self.proofs += n
         return pi, bt
+
+    def reserve(self, stream, n: int) -> None:
+        """Allocate the batched launches' scratch / proof buffers for n proofs now (engine warm-up), not at
+        the first flush inside the timed rounds."""
+        with S.use(stream):
+            key = S.raw()
+            cap = max(n, 1, self.batch_rounds * 256)
+            buf = self._bufs.get(key)
+            if buf is None or buf[0].shape[0] < cap:
+                self._bufs[key] = (torch.empty((cap, 320), dtype=torch.int32, device=self.device),
+                                   torch.empty((cap, 80), dtype=torch.uint8, device=self.device))
 
     def _upload(self, a: np.ndarray) -> torch.Tensor:
         # through the pinned staging ring (utils.h2d), stream-ordered: a pageable .to(device) blocks
@@ -130,7 +152,7 @@ class DeviceVrfProver:
         rows = np.concatenate([r for r, _ in q])
         alpha_idx = np.repeat(np.arange(len(q), dtype=np.int32), [r.size for r, _ in q])
         with S.use(stream):   # uploads, scratch and the launch all on the prover's stream
-            pi, _ = self._launch(rows, [a for _, a in q], alpha_idx)
+            pi, _ = self._launch(rows, [a for _, a in q], alpha_idx, reuse=True)
             ev = S.record(stream)
         self._inflight.append((ev, pi))
         # keep the last few batches alive until their kernels finished (the proofs are discarded)

@@ -251,6 +251,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             # one proof now: the prover kernel's code object is loaded at its first launch (several ms)
             with S.use(self.vrf_stream):
                 self.vrf_dev.prove([self.vrf_noise_seed[self.lo]], [bytes(self.vrf_dev.ALPHA_LEN)])
+            # the batched launches' buffers: noiser + roles proofs of every local peer per round
+            self.vrf_dev.reserve(self.vrf_stream, self.vrf_dev.batch_rounds * 2 * len(self.local))
             torch.cuda.synchronize(self.dev)
             self.vrf_dev.proofs = 0
 

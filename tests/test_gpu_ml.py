@@ -409,3 +409,19 @@ def test_krum_committee_noise_aware_large_inbox():
                                              rank.cuda(), 60)()
     assert torch.equal(acc, acc_ref)
     assert torch.equal(node, node_ref)
+
+
+def test_eval_errors_cached_tiles_match_reference():
+    """k_eval_error_t on the cached pre-transformed tiles (the engine's evaluation): the same error counts
+    as the fp32 torch reference, for a row count that is not a multiple of the 16-row tile."""
+    X, y, off, nt, pid, W = _fed(P=1, n=2347)
+    split = 2000
+    ref_a = K.eval_error(X[:split], y[:split], W, 784, 10)
+    ref_b = K.eval_error(X[split:], y[split:], W, 784, 10)
+    Xc = X.cuda()
+    Xt = K.eval_tiles(Xc, transform=True)
+    assert tuple(Xt.shape) == ((2347 + 15) // 16, 196, 64)
+    a, b = K.eval_errors_async(Xc, y.cuda(), split, W.cuda(), 784, 10, Xt=Xt)()
+    assert abs(a - ref_a) <= 1.0 / split and abs(b - ref_b) <= 1.0 / (2347 - split)
+    a0, b0 = K.eval_errors_async(Xc, y.cuda(), split, W.cuda(), 784, 10)()   # the gather kernel
+    assert abs(a - a0) <= 1.0 / split and abs(b - b0) <= 1.0 / (2347 - split)
