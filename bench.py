@@ -309,7 +309,6 @@ def main() -> int:
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
             "host_placement": placement,
-            "gc_stats": getattr(eng, "_gc_stats", None),
             "drain_ms": 1e3 * drain_s,          # inside the timed window: joins of the last rounds' work
             "device_segments_allocated_timed": seg_new,
             "round_wall_ms": [round(1e3 * w, 3) for w in walls],

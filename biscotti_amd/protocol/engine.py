@@ -206,27 +206,6 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         import gc
         gc.collect()
         gc.freeze()
-        # A round allocates a few thousand short-lived container objects that reference counting frees; the
-        # cyclic collector's generation-0 threshold (700 allocations) then runs several collections per round
-        # and a full one every few rounds (milliseconds once the run's results accumulate).  A larger
-        # threshold keeps the collector but moves it off the rounds' critical path (BISCOTTI_GC0 for A/B).
-        g0 = int(os.environ.get("BISCOTTI_GC0", "0"))
-        if g0 > 0 and self.gpu:
-            t = gc.get_threshold()
-            gc.set_threshold(g0, t[1], t[2])
-        if os.environ.get("BISCOTTI_GC_STATS") == "1":
-            self._gc_stats = {"n": 0, "s": 0.0, "max": 0.0}
-            st = {}
-
-            def cb(phase, info, st=st, acc=self._gc_stats):
-                if phase == "start":
-                    st["t"] = time.perf_counter()
-                elif "t" in st:
-                    dt = time.perf_counter() - st.pop("t")
-                    acc["n"] += 1
-                    acc["s"] += dt
-                    acc["max"] = max(acc["max"], dt)
-            gc.callbacks.append(cb)
 
     def _make_streams(self) -> None:
         """The round's HIP streams: the protocol critical path on a high-priority stream; speculative share
