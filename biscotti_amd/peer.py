@@ -76,7 +76,8 @@ def main(argv=None) -> int:
         eng.log.info("serving Peer net/rpc on %s:%d", *srv.addr)
     n = 0
     while ns.rounds is None or n < ns.rounds:
-        r = eng.run_round()
+        r = eng.run_round(last=ns.rounds is not None and n == ns.rounds - 1) if hasattr(eng, "drain") \
+            else eng.run_round()
         if r is None:
             eng.log.info("Reached the max iterations!")
             break

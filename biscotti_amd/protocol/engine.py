@@ -330,7 +330,10 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         return iteration + 1 if self.cfg.deterministic_time else int(time.time())
 
     # ------------------------------------------------------------------ the round
-    def run_round(self) -> RoundResult | None:
+    def run_round(self, last: bool = False) -> RoundResult | None:
+        """One protocol round.  last: the caller ends its run after this round (its final iteration), so the
+        device VRF proofs still batched are launched with this round's instead of at drain() -- the same
+        proofs, one prover latency earlier.  The protocol's own last iteration (max_iterations) counts too."""
         cfg, R, fsm, comm = self.cfg, self.R, self.fsm, self.comm
         t_round = time.perf_counter()
         tm = self.timer
@@ -351,6 +354,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 f(head["fut_noise"])
             if head.get("vrf_proofs") is not None:
                 self.vrf_dev.submit(*head["vrf_proofs"], self.vrf_stream)
+                if last or it == cfg.max_iterations - 1:
+                    self.vrf_dev.flush(self.vrf_stream)
             self._resolve_evals()
             if krum_pre is not None and cfg.verification and inboxes and cfg.defense == "KRUM":
                 kst = head.get("kst") or self._krum_static(krum_pre["xrow"], krum_pre["U1"], plan, live, inboxes, head["spec"],
