@@ -1324,7 +1324,7 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       // order, this rank's candidate workers [lo, hi) sorted by arrival, every candidate sorted), or None
       // when the run is over.  Candidates: every update some verifier judges, or every worker when
       // floor(nv/2) == 0 signatures suffice (main.go:1686).
-      .def("spec_plan", [](RoundFSM& f, const Block& b, i64 lo, i64 hi) -> py::object {
+      .def("spec_plan", [](RoundFSM& f, const Block& b, i64 lo, i64 hi, std::vector<i64> xrow, i64 U) -> py::object {
         RoundFSM s = f.successor(b);
         const i64 n = s.cfg.num_nodes;
         std::vector<u8> live(size_t(n), 1);
@@ -1347,8 +1347,29 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         std::stable_sort(spec.begin(), spec.end(), [&](i64 a, i64 c) { return rank[size_t(a)] < rank[size_t(c)]; });
         for (i64 w = 0; w < n; ++w)
           if (cand[size_t(w)]) cands.push_back(w);
-        return py::make_tuple(plan, inboxes, arrivals, spec, cands);
-      }, py::arg("block"), py::arg("lo"), py::arg("hi"));
+        if (xrow.empty()) return py::make_tuple(plan, inboxes, arrivals, spec, cands);
+        // Krum's static tables for this plan (verify.py _krum_static): every verifier's inbox as rows of the
+        // selection input (xrow: peer -> row, -1 none), each row's leader-arrival rank, speculative row -> row
+        if (xrow.size() != size_t(n)) throw std::runtime_error("spec_plan: xrow must map every peer");
+        const size_t ni = inboxes.empty() ? 0 : inboxes[0].size();
+        py::array_t<int32_t> inbox({py::ssize_t(inboxes.size()), py::ssize_t(ni)});
+        int32_t* ib = inbox.mutable_data();
+        for (size_t v = 0; v < inboxes.size(); ++v) {
+          if (inboxes[v].size() != ni) throw std::runtime_error("spec_plan: ragged inboxes");
+          for (size_t j = 0; j < ni; ++j) ib[v * ni + j] = int32_t(xrow.at(size_t(inboxes[v][j])));
+        }
+        py::array_t<int32_t> rk(U > 0 ? U : 0);
+        int32_t* r = rk.mutable_data();
+        for (i64 u = 0; u < U; ++u) r[u] = -1;
+        for (size_t i = 0; i < arrivals.size(); ++i) {
+          const i64 x = xrow.at(size_t(arrivals[i]));
+          if (x >= 0 && x < U) r[x] = int32_t(i);
+        }
+        py::array_t<int32_t> src(py::ssize_t(spec.size()));
+        int32_t* sr = src.mutable_data();
+        for (size_t i = 0; i < spec.size(); ++i) sr[i] = int32_t(xrow.at(size_t(spec[i])));
+        return py::make_tuple(plan, inboxes, arrivals, spec, cands, inbox, rk, src);
+      }, py::arg("block"), py::arg("lo"), py::arg("hi"), py::arg("xrow") = std::vector<i64>{}, py::arg("U") = 0);
   m.def("select_roles", [](const std::map<i64, i64>& stake, py::bytes h, i64 nv, i64 na, i64 n) {
     std::vector<i64> v, mm;
     select_roles(stake, B(h), nv, na, n, &v, &mm);

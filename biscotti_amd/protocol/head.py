@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 
 from ..ops import ml as K
-from ..utils import h2d
+from ..utils import h2d, h2d_many
 from ..utils import streams as S
 
 SPEC_GROUP_ROWS = 8   # speculative MSM rows per group, in leader arrival order (late cancellation)
@@ -285,10 +285,15 @@ class RoundHeadMixin:
             return
         # successor FSM, its plan, inboxes, leader arrivals and this rank's candidates in arrival order: one
         # native call (RoundFSM.spec_plan)
-        got = self.fsm.spec_plan(block, self.local.start, self.local.stop)
+        g = pre.get("gram")
+        krum = g is not None and cfg.defense == "KRUM"
+        # with the noise-aware Krum input, the same call also returns Krum's static tables (verify.py
+        # _krum_static) for the successor plan: they go up in one copy below, off the next round's path
+        got = self.fsm.spec_plan(block, self.local.start, self.local.stop, *((self._xrow_list(g["xrow"]), g["U1"])
+                                                                             if krum else ()))
         if got is None:
             return
-        plan, ibs, arrivals, spec_workers, cands = got
+        plan, ibs, arrivals, spec_workers, cands = got[:5]
         plan = PlanView(plan)
         workers = plan.workers
         inboxes = dict(zip(plan.verifiers, ibs))
@@ -313,6 +318,12 @@ class RoundHeadMixin:
         self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
                            "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
                            "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}
+        if krum and ibs:
+            n = len(ibs[0])
+            up = h2d_many([(got[5], torch.int32), (got[6], torch.int32), (got[7], torch.int32)], self.dev)
+            self._spec_next["kst"] = {"U": g["U1"], "n": n, "clip": self.fsm.krum_clip(n),
+                                      "need": len(plan.verifiers) // 2, "cap": self.fsm.leader_cap_size(),
+                                      "inbox": up[0], "rank": up[1], "amap": up[2]}
 
     def _early_vrf_submit(self, block_hash) -> None:
         """Start the next round's noiser VRF outputs as soon as the block that seeds them is built, before

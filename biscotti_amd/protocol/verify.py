@@ -106,6 +106,16 @@ class VerifyMixin:
         return K.dp_noise(delta, nz, sc, cfg.seed, it, table=tbl)
 
     # ------------------------------------------------------------------ committee Multi-Krum
+    def _xrow_list(self, xrow) -> list:
+        """peer -> row of the mapping xrow as a list (-1: no row), built once per mapping (RoundFSM.spec_plan)."""
+        c = getattr(self, "_xrow_l", None)
+        if c is None or c[0] is not xrow:
+            xl = [-1] * self.N
+            for p, r in xrow.items():
+                xl[p] = r
+            c = self._xrow_l = (xrow, xl)
+        return c[1]
+
     def _krum_static(self, xrow, U, plan, live, inboxes, spec, arrivals=None) -> dict:
         """The part of a Krum launch that does not depend on the noisers (inbox rows, leader arrival
         ranks, speculative MSM row -> Krum row), uploaded in ONE copy.  run_round prepares it while

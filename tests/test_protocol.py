@@ -3,6 +3,8 @@ import pytest
 import hashlib
 import random
 
+import numpy as np
+
 
 def _ref_noisers(stake, n, inp, self_, nn):
     """DistSys/vrf.go:54-100 with the explicit ticket list."""
@@ -236,6 +238,17 @@ def test_spec_plan_matches_python_composition(nv, lo, hi):
             (list(p.verifiers), list(p.miners), workers, p.iteration)
         assert [list(x) for x in ibs2] == ibs and list(arr2) == arr and list(spec2) == spec
         assert list(cands2) == sorted(cand)
+        # Krum's static tables (verify.py _krum_static) for a non-identity peer -> row mapping
+        xrow = {q: (11 - q) for q in range(12) if q % 5}
+        xl = [xrow.get(q, -1) for q in range(12)]
+        got = eng.fsm.spec_plan(blk, lo, hi, xl, 12)
+        np.testing.assert_array_equal(got[5], np.array([[xl[w] for w in ib] for ib in ibs], np.int32).reshape(len(ibs), -1))
+        want_rank = np.full(12, -1, np.int32)
+        for i, w in enumerate(arr):
+            if xl[w] >= 0:
+                want_rank[xl[w]] = i
+        np.testing.assert_array_equal(got[6], want_rank)
+        np.testing.assert_array_equal(got[7], np.array([xl[w] for w in spec], np.int32))
     eng.close()
 
 
