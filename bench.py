@@ -192,21 +192,16 @@ def main() -> int:
     sync = (lambda: torch.cuda.synchronize()) if eng.gpu else (lambda: None)
     sync()
     setup_s = time.perf_counter() - t_setup   # engine + HBM-resident tables (keygen/bootstrap analogue)
-    # the round's host thread on a core of its own next to the GPU, the native workers beside it
-    # (utils/affinity.py, opt-in with BISCOTTI_PIN=1); undone after the timed rounds
-    placement, cpus0 = None, (os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None)
-    if eng.gpu:
-        from biscotti_amd.native import rt
-        from biscotti_amd.utils.affinity import pin_round_threads
-
-        placement = pin_round_threads(comm.device.index, cfg.host_threads, rt())
     for _ in range(a.warmup):
         eng.run_round()
     comm.barrier()
     sync()
     import resource
 
+    from biscotti_amd.utils import threadcpu
+
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    th0 = threadcpu.snapshot()
     t0 = time.perf_counter()
     last = None
     phases: dict = {}
@@ -232,10 +227,23 @@ def main() -> int:
     # device memory segments the caching allocator had to hipMalloc inside the timed window
     seg_new = (torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) - seg0) if eng.gpu else 0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
-    if placement is not None:
-        os.sched_setaffinity(0, cpus0)
+    th1 = threadcpu.snapshot()
     host_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)   # every thread of this rank
     stats0 = {k: v for k, v in getattr(eng, "stats", {}).items() if isinstance(v, (int, float))}
+    per_step = 1e3 / max(a.steps, 1)
+    # this rank's host cost: CPU per thread group (the round's Python thread, the native crypto pool, RCCL /
+    # gloo / HIP runtime threads), the round's phases and the engine's fast-path counters
+    mine = {"rank": comm.rank, "host_cpu_ms_per_round": host_cpu * per_step,
+            "thread_cpu_ms_per_round": {k: round(v * per_step, 3)
+                                        for k, v in list(threadcpu.delta_by_group(th0, th1).items())[:10]},
+            "phase_ms_per_round": {k: round(v * per_step, 4) for k, v in sorted(phases.items())},
+            "engine_stats": stats0, "elapsed_s": elapsed}
+    per_rank = [mine]
+    if comm.world > 1:
+        import torch.distributed as dist
+
+        per_rank = [None] * comm.world
+        dist.all_gather_object(per_rank, mine)
     t = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
     if comm.world > 1:
         import torch.distributed as dist
@@ -295,7 +303,8 @@ def main() -> int:
                        f"sec/round + final test acc, {a.config}"),
             "value": s_per_round,
             "unit": "s/round",
-            "n_gpus": comm.world if eng.gpu else 0,
+            "n_gpus": comm.world,
+            "device": comm.device.type,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": 1e3 * s_per_round,
@@ -310,11 +319,11 @@ def main() -> int:
             "final_test_acc_mean_std": ms(finals),
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
-            "host_placement": placement,
             "drain_ms": 1e3 * drain_s,          # inside the timed window: joins of the last rounds' work
             "device_segments_allocated_timed": seg_new,
             "round_wall_ms": [round(1e3 * w, 3) for w in walls],
             "host_cpu_ms_per_round": 1e3 * host_cpu / max(a.steps, 1),
+            "thread_cpu_ms_per_round": mine["thread_cpu_ms_per_round"],
             "engine_stats": stats0,
             "table_gb": (eng.crypto.eng.table_bytes() / 1e9) if hasattr(getattr(eng, "crypto", None), "eng") else 0.0,
             "b0": getattr(getattr(getattr(eng, "crypto", None), "eng", None), "b0", None),
@@ -345,6 +354,8 @@ def main() -> int:
             out["attack_rate_last10_mean_std"] = ms(att10)
         for k, v in ref_extra.items():
             out[f"baseline_{k}"] = v
+        if comm.world > 1:
+            out["per_rank"] = per_rank
         print(json.dumps(out), flush=True)
     comm.barrier()
     if not fedsys:

@@ -24,7 +24,7 @@ CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build"
 RT_NAME = "_biscotti_rt" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
 HIP_LIB = "libbiscotti_hip.so"
-ARCH = os.environ.get("BISCOTTI_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"   # MI355X (CDNA4) only
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

@@ -471,10 +471,12 @@ __device__ __forceinline__ double gram_at(const double* gram, int T, int a, int 
 // pre-sampled vectors of this iteration (a strided view of the resident noise table)
 extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, int U, int D, int kchunk, int T,
                                                               double* part, double* gram, unsigned int* count,
-                                                              const float* X2, int U1, long long stride2) {
+                                                              const float* X2, int U1, long long stride2, int pair0) {
   __shared__ double red[4][256];
   __shared__ unsigned int last;
-  const int pair = blockIdx.x, sp = blockIdx.y;
+  // this launch covers the tile pairs [pair0, pair0 + gridDim.x) (several ranks split one Gram); part and
+  // the arrival counters are indexed by the launch-local pair index, gram by the global one
+  const int lp = blockIdx.x, pair = pair0 + lp, sp = blockIdx.y;
   const int npairs = gridDim.x;
   // decode the pair index (T <= 64: a short scan)
   int ti = 0, rem = pair;
@@ -527,20 +529,20 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
   for (int r = 0; r < 4; ++r) red[wid][((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
   __syncthreads();
   const int e = threadIdx.x;  // 256 threads = the 16x16 tile
-  part[((size_t)sp * npairs + pair) * 256 + e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+  part[((size_t)sp * npairs + lp) * 256 + e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
   // split-K reduction in-kernel: the last split block of this tile pair to finish sums the partials
   // in split order (bit-reproducible) and writes the reduced tile; it also re-arms the counter
   __threadfence();
   __syncthreads();
-  if (e == 0) last = atomicAdd(count + pair, 1u) == (unsigned)(gridDim.y - 1) ? 1u : 0u;
+  if (e == 0) last = atomicAdd(count + lp, 1u) == (unsigned)(gridDim.y - 1) ? 1u : 0u;
   __syncthreads();
   if (!last) return;
   __threadfence();
   double g = 0.0;
   for (int q = 0; q < (int)gridDim.y; ++q)
-    g += __hip_atomic_load(part + ((size_t)q * npairs + pair) * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g += __hip_atomic_load(part + ((size_t)q * npairs + lp) * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   gram[(size_t)pair * 256 + e] = g;
-  if (e == 0) count[pair] = 0u;
+  if (e == 0) count[lp] = 0u;
 }
 
 extern "C" __global__ void __launch_bounds__(256) k_krum_rows(const double* gram, int T, const int* inbox, int n,
@@ -1138,7 +1140,7 @@ constexpr int RW_MAXC = 16;   // coefficients per chunk
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(256) k_recover_w(
-    const long long* ys, int nrows, int nch, int T, const int* mask, const int* ycols, const int* xs, int npts,
+    const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask, const int* ycols, const int* xs, int npts,
     const long long* A, const int* basis, int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi,
     int d, const double* W, double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out) {
   __shared__ long long agg[RW_CPB][RW_MAXP];
@@ -1154,7 +1156,7 @@ extern "C" __global__ void __launch_bounds__(256) k_recover_w(
     long long s = 0;
     const int col = ycols[p];
     for (int r = 0; r < nrows; ++r)
-      if (mask == nullptr || mask[r]) s += ys[((size_t)r * nch + k) * T + col];
+      if (mask == nullptr || mask[r]) s += ys[(size_t)r * rstride + (size_t)k * T + col];
     agg[c][p] = s;
     agg_out[(size_t)k * npts + p] = s;
   }
@@ -1308,7 +1310,7 @@ extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, cons
   hipStream_t s = (hipStream_t)stream;
   // count: npairs zeroed counters (re-armed by the kernel itself)
   hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part, gram, count,
-                     (const float*)nullptr, U, 0ll);
+                     (const float*)nullptr, U, 0ll, 0);
   if (n <= 256) {
     hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, gram, T, inbox, n, groupsize, scores);
   } else {
@@ -1319,17 +1321,27 @@ extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, cons
   if (krum_vote_any(s, scores, inbox, V, n, n_accept, U, need, lead_rank, cap, acc, node, ws) != 0) return -1;
   return (int)hipGetLastError();
 }
-extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
-                                double* part, double* gram, unsigned int* count, void* stream) {
+// Tile pairs [p0, p1) of the stacked Gram only (p1 <= 0: all of them): several ranks split one Gram's tiles
+// and exchange the reduced tiles (engine: the verification all_gather).  part: [nsplit, p1 - p0, 256].
+extern "C" int bsc_gram_stacked_range(const float* X, int U1, const float* X2, int U2, long long stride2, int D,
+                                      int kchunk, int p0, int p1, double* part, double* gram, unsigned int* count,
+                                      void* stream) {
   const int U = U1 + U2;
   if (U <= 0) return 0;
   if (U > 8192 || kchunk <= 0) return -1;
   const int T = (U + 15) / 16;
   const int npairs = T * (T + 1) / 2;
+  if (p1 <= 0 || p1 > npairs) p1 = npairs;
+  if (p0 < 0 || p0 > p1) return -1;
+  if (p0 == p1) return 0;
   const int nsplit = (D + kchunk - 1) / kchunk;
-  hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, (hipStream_t)stream, X, U, D, kchunk, T, part,
-                     gram, count, X2, U1, stride2);
+  hipLaunchKernelGGL(k_gram_pairs, dim3(p1 - p0, nsplit), dim3(256), 0, (hipStream_t)stream, X, U, D, kchunk, T, part,
+                     gram, count, X2, U1, stride2, p0);
   return (int)hipGetLastError();
+}
+extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
+                                double* part, double* gram, unsigned int* count, void* stream) {
+  return bsc_gram_stacked_range(X, U1, X2, U2, stride2, D, kchunk, 0, 0, part, gram, count, stream);
 }
 extern "C" int bsc_krum_committee_noise(const double* gram, int U1, int U, const int* nz, const float* sc, int nn,
                                         const int* inbox, int V, int n, int groupsize, int n_accept, int need,
@@ -1409,16 +1421,28 @@ extern "C" int bsc_recover(const long long* ys, int nchunks, int npts, const int
   return (int)hipGetLastError();
 }
 
+// rstride: int64 elements between consecutive rows of ys (nch * T for a dense [nrows][nch][T] tensor; the
+// packed row length when ys are the ranks' partials inside an all_gather buffer, round.hip)
+extern "C" int bsc_recover_w_strided(const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask,
+                                     const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
+                                     int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
+                                     const double* W, double qscale, double* W_new, long long* coeffs, int* status,
+                                     long long* agg_out, void* stream) {
+  if (nch <= 0) return 0;
+  if (npts > RW_MAXP || poly > RW_MAXC || poly > npts || shift < 0 || shift > 100 || nrows <= 0) return -1;
+  if (rstride < (long long)nch * T) return -1;
+  hipLaunchKernelGGL(k_recover_w, dim3(nblk(nch, RW_CPB)), dim3(256), 0, (hipStream_t)stream, ys, nrows, rstride, nch,
+                     T, mask, ycols, xs, npts, A, basis, poly, shift, inv_lo, inv_hi, d, W, qscale, W_new, coeffs,
+                     status, agg_out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, const int* mask, const int* ycols,
                              const int* xs, int npts, const long long* A, const int* basis, int poly, int shift,
                              unsigned long long inv_lo, unsigned long long inv_hi, int d, const double* W, double qscale,
                              double* W_new, long long* coeffs, int* status, long long* agg_out, void* stream) {
-  if (nch <= 0) return 0;
-  if (npts > RW_MAXP || poly > RW_MAXC || poly > npts || shift < 0 || shift > 100 || nrows <= 0) return -1;
-  hipLaunchKernelGGL(k_recover_w, dim3(nblk(nch, RW_CPB)), dim3(256), 0, (hipStream_t)stream, ys, nrows, nch, T, mask,
-                     ycols, xs, npts, A, basis, poly, shift, inv_lo, inv_hi, d, W, qscale, W_new, coeffs, status,
-                     agg_out);
-  return (int)hipGetLastError();
+  return bsc_recover_w_strided(ys, nrows, (long long)nch * T, nch, T, mask, ycols, xs, npts, A, basis, poly, shift,
+                               inv_lo, inv_hi, d, W, qscale, W_new, coeffs, status, agg_out, stream);
 }
 
 extern "C" int bsc_add_rows(const float* delta, int D, const int* rows, int nrows, const double* W, double* W_new,

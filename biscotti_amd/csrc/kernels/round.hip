@@ -11,6 +11,8 @@
 // bsc_round_audit   -- verifyCommitment on the aggregate (kyber.go:564-577): main waits for the side
 //                      stream's sums, k_chunk_check, read-back of the verdicts, event `audit`
 // bsc_round_wait    -- host wait for one of the two events
+// bsc_round_partials / bsc_round_combine -- the same aggregation on several ranks, split around the one
+//                      all_gather the caller issues between them (below)
 //
 // The launchers of the individual kernels (msm.hip, ml.hip) are called directly; every buffer is
 // resident (allocated once by the engine), so the call allocates nothing.
@@ -24,6 +26,13 @@ extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, con
                              unsigned long long inv_lo, unsigned long long inv_hi, int d, const double* W,
                              double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out,
                              void* stream);
+extern "C" int bsc_recover_w_strided(const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask,
+                                     const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
+                                     int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
+                                     const double* W, double qscale, double* W_new, long long* coeffs, int* status,
+                                     long long* agg_out, void* stream);
+extern "C" int bsc_sum_rows_i64(const long long* ys, int R, long long C, const int* rows, int nsel, const int* mask,
+                                long long* out, void* stream);
 extern "C" int bsc_sum_rows2_pos(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
                                  int ncols, const int* row_mask, uint32_t* out, void* stream);
 extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
@@ -220,6 +229,84 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
     RC_CHECK(bsc_gram_stacked(delta, P, T_rows, U2, stride2, c->d, kchunk, part, gram, counters, gs));
     RC_CHECK(hipEventRecord((hipEvent_t)ev_gram, gs));
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Several ranks (one per GPU).  The aggregation's ONE all_gather moves a packed row per rank,
+//     [ cs: nch x 24 u32 | ys: nch x T int64 | clock: int64 | pad ]      (row_bytes: a multiple of 96)
+// so the gathered buffer is at once a [world][row_bytes / 96][24] point array whose first nch columns are the
+// ranks' chunk-commitment partial sums (bsc_sum_rows2 sums them) and a strided [world][nch][T] share-sum
+// array (k_recover_w with a row stride sums and recovers).  No repacking on either side of the collective.
+//
+// bsc_round_partials: this rank's partials of its kept rows, written straight into its send row -- the
+//   miners' share-value sums (main), the chunk-commitment sums (side, or already queued on another stream by
+//   bsc_round_csum_early into the same slot: audit = 2), the witness sums (background; per-rank, no
+//   consumer on the protocol path), the rank's clock; main then waits for the commitment sums, so the
+//   collective the caller issues next on main sees a complete row.  R = 0: no local rows (zero partials,
+//   the point at infinity for the commitment sums).
+// bsc_round_combine: on main, behind the collective: the commitment totals over the ranks (the audit's
+//   input), the fused share totals + exact recovery + W update, and the read-back of (status, W_new, every
+//   rank's clock) -- event `readback`.
+extern "C" int bsc_round_row_bytes(int nch, int T) {
+  const long long raw = 96ll * nch + 8ll * nch * T + 8;
+  return (int)((raw + 95) / 96 * 96);
+}
+
+extern "C" int bsc_round_partials(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask,
+                                  const int* ccols, const int* wcols, int nwc, uint32_t* ws, unsigned char* send,
+                                  long long clock, int audit) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || R < 0) return -1;
+  const int nch = c->nch, T = c->T;
+  uint32_t* cs_slot = (uint32_t*)send;
+  long long* ys_slot = (long long*)(send + 96ll * nch);
+  unsigned char* clk = send + 96ll * nch + 8ll * nch * T;
+  RC_CHECK(hipEventRecord(c->ev_main, c->main));
+  if (R > 0) {
+    const int ncols_in = nch * (T + 1);
+    if (audit == 1) {
+      RC_CHECK(hipStreamWaitEvent(c->side, c->ev_main, 0));
+      RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, ccols, nch, mask, cs_slot, c->side));
+      RC_CHECK(hipEventRecord(c->ev_side, c->side));
+    }
+    if (nwc > 0 && ws != nullptr) {
+      RC_CHECK(hipStreamWaitEvent(c->bg, c->ev_main, 0));
+      RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->bg));
+    }
+    RC_CHECK(bsc_sum_rows_i64(ys, R, (long long)nch * T, nullptr, R, mask, ys_slot, c->main));
+  } else {
+    RC_CHECK(hipMemsetAsync(ys_slot, 0, 8ull * nch * T, c->main));
+    if (audit != 0) RC_CHECK(hipMemsetAsync(cs_slot, 0, 96ull * nch, c->main));
+  }
+  const unsigned long long u = (unsigned long long)clock;
+  RC_CHECK(hipMemsetD32Async((hipDeviceptr_t)clk, (int)(u & 0xffffffffull), 1, c->main));
+  RC_CHECK(hipMemsetD32Async((hipDeviceptr_t)(clk + 4), (int)(u >> 32), 1, c->main));
+  if (R > 0 && audit != 0) RC_CHECK(hipStreamWaitEvent(c->main, c->ev_side, 0));
+  return 0;
+}
+
+extern "C" int bsc_round_combine(void* ctx, const unsigned char* recv, int world, long long row_bytes,
+                                 const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
+                                 int shift, unsigned long long inv_lo, unsigned long long inv_hi, const double* W,
+                                 double* W_new, long long* coeffs, int* status, long long* agg, uint32_t* cs,
+                                 int* h_status, double* h_W, long long* h_clock, int audit) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || world <= 0 || row_bytes % 96 != 0 || row_bytes < bsc_round_row_bytes(c->nch, c->T)) return -1;
+  const int nch = c->nch, T = c->T;
+  if (audit != 0) {
+    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv, (int)(row_bytes / 96), nullptr, world, nullptr, nch, nullptr, cs,
+                           c->main));
+    RC_CHECK(hipEventRecord(c->ev_side, c->main));   // bsc_round_audit waits for the sums through ev_side
+  }
+  RC_CHECK(bsc_recover_w_strided((const long long*)(recv + 96ll * nch), world, row_bytes / 8, nch, T, nullptr, ycols,
+                                 xs, npts, A, basis, c->poly, shift, inv_lo, inv_hi, c->d, W, c->qscale, W_new, coeffs,
+                                 status, agg, c->main));
+  RC_CHECK(hipMemcpyAsync(h_status, status, (size_t)nch * sizeof(int), hipMemcpyDeviceToHost, c->main));
+  RC_CHECK(hipMemcpyAsync(h_W, W_new, (size_t)c->d * sizeof(double), hipMemcpyDeviceToHost, c->main));
+  RC_CHECK(hipMemcpy2DAsync(h_clock, sizeof(long long), recv + 96ll * nch + 8ll * nch * T, (size_t)row_bytes,
+                            sizeof(long long), (size_t)world, hipMemcpyDeviceToHost, c->main));
+  RC_CHECK(hipEventRecord(c->ev_readback, c->main));
   return 0;
 }
 

@@ -770,6 +770,10 @@ extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uin
                              int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
                              void* stream);
 
+extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
+                             int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
+                             void* stream);
+
 // One round's proofs in one call (per-round launches, ops/vrf.py): the staging words [key rows (n) | zeros
 // (n) | the 32-byte message (8 words)] go up from pinned memory, the prover runs, `ev` is recorded -- a
 // resident slot per call, no allocation, ~10 us of the caller's time instead of a Python launch path.

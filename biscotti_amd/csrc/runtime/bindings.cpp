@@ -50,26 +50,8 @@ static py::int_ pyint_from_u256(const U256& v) {
 #include <functional>
 #include <mutex>
 
-#include <sched.h>
+#include <pthread.h>
 
-// CPUs the native worker threads (pool + dispatcher) run on: set by set_worker_cpus; every worker
-// re-applies it at its next job when the generation changed (threads created before the call included),
-// so the round's critical host thread can keep a core of its own (bench.py pins it next to the GPU).
-static std::mutex g_aff_m;
-static std::vector<int> g_aff_cpus;
-static std::atomic<int> g_aff_gen{0};
-static void apply_worker_affinity(int& seen) {
-  const int g = g_aff_gen.load(std::memory_order_acquire);
-  if (g == seen) return;
-  seen = g;
-  std::lock_guard<std::mutex> lk(g_aff_m);
-  if (g_aff_cpus.empty()) return;
-  cpu_set_t set;
-  CPU_ZERO(&set);
-  for (int c : g_aff_cpus)
-    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
-  sched_setaffinity(0, sizeof(set), &set);   // 0: the calling thread
-}
 class Pool {
   // Several jobs may run at once (background VRF proofs, round-wide Schnorr batches, the main
   // thread's calls): every run() registers its job, works on it itself, and the persistent
@@ -122,7 +104,7 @@ class Pool {
     return nullptr;
   }
   void loop() {
-    int aff = 0;
+    pthread_setname_np(pthread_self(), "bsc-pool");   // per-thread CPU attribution (utils/threadcpu.py)
     std::unique_lock<std::mutex> lk(m_);
     for (;;) {
       Job* j = nullptr;
@@ -130,7 +112,6 @@ class Pool {
       if (stop_) return;
       ++j->active;
       lk.unlock();
-      apply_worker_affinity(aff);
       for (size_t i; (i = j->next.fetch_add(1)) < j->n;) (*j->f)(i);
       lk.lock();
       if (--j->active == 0) done_cv_.notify_all();
@@ -164,7 +145,7 @@ class Dispatcher {
 
  private:
   void loop() {
-    int aff = 0;
+    pthread_setname_np(pthread_self(), "bsc-job");
     std::unique_lock<std::mutex> lk(m_);
     for (;;) {
       ++idle_;
@@ -173,7 +154,6 @@ class Dispatcher {
       std::function<void()> f = std::move(q_.front());
       q_.pop_front();
       lk.unlock();
-      apply_worker_affinity(aff);
       f();
       lk.lock();
     }
@@ -543,13 +523,6 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   m.doc() = "biscotti_amd native host runtime (crypto, ledger, protocol FSM)";
 
   // ---------------------------------------------------------------- hashing
-  m.def("set_worker_cpus", [](std::vector<int> cpus) {
-    {
-      std::lock_guard<std::mutex> lk(g_aff_m);
-      g_aff_cpus = std::move(cpus);
-    }
-    g_aff_gen.fetch_add(1, std::memory_order_release);
-  });
   m.def("sha256", [](py::bytes d) { return P(Sha256::digest(B(d))); });
   m.def("sha512", [](py::bytes d) { return P(Sha512::digest(B(d))); });
   m.def("blake2b", [](py::bytes d, int outlen, py::bytes key) {

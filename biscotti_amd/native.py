@@ -37,9 +37,7 @@ def rt():
 
 
 def hip_library_path() -> Path:
-    # BISCOTTI_HIP_LIB: an alternative build of the same kernels (A/B experiments)
-    alt = os.environ.get("BISCOTTI_HIP_LIB")
-    return Path(alt) if alt else _PKG / "libbiscotti_hip.so"
+    return _PKG / "libbiscotti_hip.so"
 
 
 def hip():

@@ -37,7 +37,6 @@ SIGNATURES = {
     "bsc_chunk_check": [P, I, I, P, I, I, P, I, I, P, P],
     # vrf.hip
     "bsc_vrf_prove": [P, P, P, P, I, I, P, P, P, P, P],
-    "bsc_vrf_prove_round": [P, P, P, I, P, P, P, P, P],
     # kzg.hip
     "bsc_kzg_blocks": [I, I],
     "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, I, U64, P, P, P],
@@ -48,6 +47,7 @@ SIGNATURES = {
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],
     "bsc_krum_committee": [P, I, I, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, P, P],
     "bsc_gram_stacked": [P, I, P, I, L, I, I, P, P, P, P],
+    "bsc_gram_stacked_range": [P, I, P, I, L, I, I, I, I, P, P, P, P],
     "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_eval_error_rb": [P, P, I, I, I, P, I, I, P, P, P],
@@ -61,12 +61,16 @@ SIGNATURES = {
     "bsc_lsh_count": [P, I, P, I, P, I, D, P, P],
     "bsc_weighted_rows": [P, I, I, P, P, P],
     "bsc_recover_w": [P, I, I, I, P, P, P, I, P, P, I, I, U64, U64, I, P, D, P, P, P, P, P],
+    "bsc_recover_w_strided": [P, I, L, I, I, P, P, P, I, P, P, I, I, U64, U64, I, P, D, P, P, P, P, P],
     # round.hip
     "bsc_round_create": [P, P, P, P, I, I, I, I, I, D],
     "bsc_round_destroy": [P],
     "bsc_round_secagg": [P, P, I, P, P, P, P, I, P, P, I, P, P, I, U64, U64, P, P, P, P, P, P, P, P, P, I],
     "bsc_round_audit": [P, P, P, P, P],
     "bsc_round_wait": [P, I],
+    "bsc_round_row_bytes": [I, I],
+    "bsc_round_partials": [P, P, I, P, P, P, P, I, P, P, L, I],
+    "bsc_round_combine": [P, P, I, L, P, P, I, P, P, I, U64, U64, P, P, P, P, P, P, P, P, P, I],
 }
 
 

@@ -45,7 +45,9 @@ def choose_b0(d: int, poly: int, total_shares: int, device, fraction: float = 0.
     # processes sharing one GPU (several ranks / per-peer processes per device) split the budget evenly
     # up front, so they all pick the same B0 instead of each taking 60 % of what is left.  The count
     # comes from Comm.init (ranks with the same host and device UUID); one rank per GPU -> no split
-    per_gpu = max(1, int(os.environ.get("BISCOTTI_RANKS_PER_DEVICE", "1")))
+    from ..parallel.comm import ranks_per_device
+
+    per_gpu = max(1, ranks_per_device())
     budget = min(fraction * free, (fraction if per_gpu == 1 else 0.66) * total / per_gpu) - _SCRATCH_BYTES
     for b0 in B0_CHOICES:
         if table_bytes_for(d, poly, total_shares, b0) <= budget:
@@ -348,8 +350,14 @@ class NativeSecAgg:
     """The round's secure aggregation enqueued natively (kernels/round.hip): one call queues the miners'
     commitment / witness sums (side / background streams), the fused share sums + exact recovery + W
     update and the read-back (main stream); a second queues the aggregate audit.  Every buffer is
-    resident; the recovered model goes to a ring of 4 buffers (the newest is the engine's W, the one
-    before may still feed the next round's pre-step).  Single rank, speculative (masked) rows."""
+    resident; the recovered model goes to a ring of W_RING buffers.  A new model never lands in the
+    buffer it is computed from (the engine's W) nor in the last two results (one of them may still feed a
+    queued pre-step): aggregates that are computed and then dropped (a speculative miss, a failed audit,
+    an empty block) can therefore never overwrite the live model.
+
+    One rank: secagg() does sums + recovery in one call.  Several ranks (one per GPU): partials() writes
+    this rank's partial sums into a packed send row, the caller all_gathers the rows (main stream), and
+    combine() sums the ranks' partials, recovers and reads back (kernels/round.hip)."""
 
     W_RING = 4
 
@@ -370,6 +378,25 @@ class NativeSecAgg:
         self.h_W = torch.empty((d,), dtype=torch.float64, pin_memory=True)
         self.h_ok = torch.empty((1, nch), dtype=torch.int32, pin_memory=True)
         self._by_shape: dict = {}
+        self._recent: list = []   # data pointers of the last two recovered models
+        self.world = 0            # several ranks: set by gather_buffers()
+        self.h_clock = None
+
+    def _next_W(self, W) -> torch.Tensor:
+        """The ring slot for the next recovered model: not W (the input) and not one of the last two
+        results (see the class docstring)."""
+        avoid = set(self._recent) | {W.data_ptr()}
+        for step in range(1, self.W_RING + 1):
+            k = (self.k + step) % self.W_RING
+            if self.W_ring[k].data_ptr() not in avoid:
+                self.k = k
+                break
+        else:   # unreachable with W_RING >= 4
+            raise RuntimeError("NativeSecAgg: no free model buffer")
+        W_new = self.W_ring[self.k]
+        assert W_new.data_ptr() != W.data_ptr(), "recovered model would alias its input"
+        self._recent = (self._recent + [W_new.data_ptr()])[-2:]
+        return W_new
 
     def _buf(self, key, shape, dtype):
         t = self._by_shape.get(key)
@@ -382,8 +409,7 @@ class NativeSecAgg:
         R = pts.shape[0]
         npts, nwc = ycols.numel(), wcols.numel()
         nch = self.eng.nchunks
-        self.k = (self.k + 1) % self.W_RING
-        W_new = self.W_ring[self.k]
+        W_new = self._next_W(W)
         agg = self._buf(("agg", npts), (nch, npts), torch.int64)
         ws = self._buf(("ws", nwc), (nwc, 24), torch.int32)
         err = hip().bsc_round_secagg(self.ctx, _ptr(pts), R, _ptr(ys), _ptr(mask), _ptr(ccols), _ptr(wcols), nwc,
@@ -398,14 +424,53 @@ class NativeSecAgg:
     def csum_early(self, ccom, ccom_event, rows, mask, stream=None) -> None:
         """Queue the audit's commitment sums now (side stream, behind what main has queued so far -- the
         selection's flags -- and the pre-step's chunk commitments): cs = sum over the rows r with
-        mask[r] != 0 of ccom[rows[r]].  secagg(.., audit=2) then leaves them out."""
+        mask[r] != 0 of ccom[rows[r]].  secagg(.., audit=2) / partials(.., audit=2) then leave them out.
+        Several ranks: the sums are this rank's partial and go straight into its send row."""
         R = rows.numel()
         assert ccom.dtype == torch.int32 and ccom.shape[1] == self.eng.nchunks and ccom.shape[-1] == 24
         assert rows.dtype == torch.int32 and mask.dtype == torch.int32 and mask.numel() == R
         ev = ccom_event.cuda_event if ccom_event is not None else None
+        out = self.send.data_ptr() if self.world > 1 else _ptr(self.cs)
         _check(hip().bsc_round_csum_early(self.ctx, _ptr(ccom.contiguous()), ev, _ptr(rows), R, _ptr(mask),
-                                          _ptr(self.cs), stream.cuda_stream if stream is not None else None),
+                                          out, stream.cuda_stream if stream is not None else None),
                "round_csum_early")
+
+    # ---------------------------------------------------------------- several ranks
+    def gather_buffers(self, world: int):
+        """Resident (send [row_bytes], recv [world, row_bytes]) uint8 buffers of the aggregation's packed
+        all_gather (layout: kernels/round.hip, bsc_round_row_bytes)."""
+        if self.world != world:
+            eng = self.eng
+            self.row_bytes = int(hip().bsc_round_row_bytes(eng.nchunks, eng.T))
+            self.send = torch.zeros((self.row_bytes,), dtype=torch.uint8, device=eng.device)
+            self.recv = torch.zeros((world, self.row_bytes), dtype=torch.uint8, device=eng.device)
+            self.h_clock = torch.empty((world,), dtype=torch.int64, pin_memory=True)
+            self.world = world
+        return self.send, self.recv
+
+    def partials(self, pts, ys, mask, ccols, wcols, clock: int, audit: int) -> None:
+        """Queue this rank's partial sums of its kept rows into the send row (pts / ys / mask None: no
+        local rows).  audit: 0 none, 1 commitment sums here, 2 already queued by csum_early."""
+        assert self.world > 0, "gather_buffers() first"
+        R = 0 if pts is None else pts.shape[0]
+        nwc = wcols.numel() if R else 0
+        ws = self._buf(("ws", nwc), (nwc, 24), torch.int32) if nwc else None
+        _check(hip().bsc_round_partials(self.ctx, _ptr(pts) if R else None, R, _ptr(ys) if R else None,
+                                        _ptr(mask) if R else None, _ptr(ccols), _ptr(wcols) if R else None, nwc,
+                                        _ptr(ws), self.send.data_ptr(), int(clock), int(audit)), "round_partials")
+
+    def combine(self, ycols, xs, wts: dict, A_dev, basis_dev, W, audit: int):
+        """Behind the all_gather into recv (main stream): ranks' totals, exact recovery, read-back of
+        (status, W_new, clocks).  Returns (W_new, coeffs, status, agg) device tensors."""
+        npts, nch = ycols.numel(), self.eng.nchunks
+        W_new = self._next_W(W)
+        agg = self._buf(("agg", npts), (nch, npts), torch.int64)
+        _check(hip().bsc_round_combine(self.ctx, self.recv.data_ptr(), self.world, self.row_bytes, _ptr(ycols),
+                                       _ptr(xs), npts, _ptr(A_dev), _ptr(basis_dev), wts["shift"], wts["inv_lo"],
+                                       wts["inv_hi"], _ptr(W), _ptr(W_new), _ptr(self.coeffs), _ptr(self.status),
+                                       _ptr(agg), _ptr(self.cs), self.h_status.data_ptr(), self.h_W.data_ptr(),
+                                       self.h_clock.data_ptr(), int(audit)), "round_combine")
+        return W_new, self.coeffs, self.status, agg
 
     PRE_SLOTS = 3
 
@@ -503,11 +568,15 @@ class NativeSecAgg:
                                         ev_up.cuda_event if ev_up is not None else None), "round_spec_msm")
         return NativeSpec(qdelta, rows, sl["rows"][:n], sl["rows"][n:2 * n], pts, ys, no_commit)
 
-    def readback(self):
-        """Callable: waits for the recovery's read-back -> [status, W_new] numpy views (pinned)."""
+    def readback(self, clocks: bool = False):
+        """Callable: waits for the recovery's read-back -> [status, W_new(, every rank's clock)] numpy views
+        (pinned)."""
         def wait():
             _check(hip().bsc_round_wait(self.ctx, 0), "round_wait")
-            return [self.h_status.numpy(), self.h_W.numpy()]
+            out = [self.h_status.numpy(), self.h_W.numpy()]
+            if clocks:
+                out.append(self.h_clock.numpy())
+            return out
         return wait
 
     def audit(self):

@@ -414,29 +414,107 @@ def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lea
     return result
 
 
-def gram_stacked_async(X, T_rows, kchunk: int = 512) -> dict:
-    """Noise-aware committee Krum, phase 1: f64 Gram of the stacked rows [X; T_rows] (GPU).
+def _pair_tiles(T: int) -> list[tuple[int, int]]:
+    """(ti, tj) of every tile pair ti <= tj of a T x T tile grid, in k_gram_pairs' enumeration order."""
+    return [(ti, tj) for ti in range(T) for tj in range(ti, T)]
+
+
+def _gram_tiles_exact(S: torch.Tensor, p0: int, p1: int, T: int) -> torch.Tensor:
+    """CPU: tiles [p0, p1) of the tiled upper-triangular Gram ([p1 - p0, 256] fp64, entry [p, 16 a + b] =
+    G[16 ti + a, 16 tj + b]) with every entry reduced exactly as _gram_exact_order reduces it."""
+    S = S.double().cpu()
+    U, D = S.shape
+    Dp = 1 << max(0, (max(D, 1) - 1).bit_length())
+    Sp = torch.zeros((T * 16, Dp), dtype=torch.float64)
+    Sp[:U, :D] = S
+    out = torch.zeros((p1 - p0, 256), dtype=torch.float64)
+    for k, (ti, tj) in enumerate(_pair_tiles(T)[p0:p1]):
+        B_ = Sp[tj * 16:(tj + 1) * 16]
+        for a in range(16):
+            P = Sp[ti * 16 + a][None, :] * B_
+            while P.shape[1] > 1:
+                h = P.shape[1] // 2
+                P = P[:, :h] + P[:, h:]
+            out[k, a * 16:(a + 1) * 16] = P[:, 0]
+    return out
+
+
+def gram_full_from_tiles(tiles: torch.Tensor, U: int) -> torch.Tensor:
+    """The symmetric [U, U] Gram out of its tiled upper triangle ([npairs, 256], k_gram_pairs' layout)."""
+    T = (U + 15) // 16
+    G = torch.zeros((T * 16, T * 16), dtype=torch.float64)
+    for k, (ti, tj) in enumerate(_pair_tiles(T)):
+        t = tiles[k].double().cpu().view(16, 16)
+        G[ti * 16:(ti + 1) * 16, tj * 16:(tj + 1) * 16] = t
+        G[tj * 16:(tj + 1) * 16, ti * 16:(ti + 1) * 16] = t.T
+    return G[:U, :U].contiguous()
+
+
+def gram_split(U: int, rank: int, world: int) -> tuple[int, int, int, int]:
+    """(p0, p1, chunk, npairs): the tile pairs [p0, p1) of a U-row Gram that `rank` of `world` computes.
+    Rank r owns [r * chunk, (r + 1) * chunk) clipped to npairs, so the ranks' [chunk, 256] slots
+    all_gathered in rank order start with the whole tiled Gram."""
+    T = (U + 15) // 16
+    npairs = T * (T + 1) // 2
+    chunk = -(-npairs // world)
+    p0 = min(npairs, rank * chunk)
+    return p0, min(npairs, p0 + chunk), chunk, npairs
+
+
+def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | None = None) -> dict:
+    """Noise-aware committee Krum, phase 1: f64 Gram of the stacked rows [X; T_rows].
 
     X fp32 [U1, d] (the workers' deltas, contiguous); T_rows fp32 [U2, d] with contiguous rows (a
     strided view of the resident noise table at this iteration).  Runs before the noisers are known.
-    Returns the handle krum_committee_noise_async consumes."""
+    split = (rank, world): this rank computes only its share of the tile pairs (gram_split) into rows
+    [rank * chunk, ...) of a [world * chunk, 256] buffer; the caller all_gathers the ranks' slots
+    (gram_slot) and calls gram_adopt.  Returns the handle krum_committee_noise_async consumes."""
     U1, D = X.shape
     U2 = T_rows.shape[0]
     assert X.is_contiguous() and T_rows.stride(1) == 1 and T_rows.shape[1] == D
     assert X.dtype == torch.float32 and T_rows.dtype == torch.float32
     U = U1 + U2
     assert 0 < U <= KRUM_MAX_ROWS, "committee Krum size limits"
-    if X.device.type != "cuda":
-        return {"gram_full": _gram_exact_order(torch.cat([X, T_rows])), "U1": U1, "U": U}
     Tt = (U + 15) // 16
     npairs = Tt * (Tt + 1) // 2
+    if split is not None:
+        rank, world = split
+        p0, p1, chunk, _ = gram_split(U, rank, world)
+    else:
+        rank, p0, p1, chunk = 0, 0, npairs, npairs
+    if X.device.type != "cuda":
+        if split is None:
+            return {"gram_full": _gram_exact_order(torch.cat([X, T_rows])), "U1": U1, "U": U}
+        slots = torch.zeros((chunk * split[1], 256), dtype=torch.float64)
+        slots[rank * chunk:rank * chunk + (p1 - p0)] = _gram_tiles_exact(torch.cat([X, T_rows]), p0, p1, Tt)
+        return {"gram": slots, "U1": U1, "U": U, "split": (rank, chunk, npairs)}
     nsplit = (D + kchunk - 1) // kchunk
     dev = X.device
-    part = torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev)
-    gram = torch.empty((npairs, 256), dtype=torch.float64, device=dev)
-    _check(hip().bsc_gram_stacked(_p(X), U1, T_rows.data_ptr(), U2, T_rows.stride(0), D, kchunk, _p(part), _p(gram),
-                                  _p(_tile_counters(dev, npairs)), _stream()), "gram_stacked")
-    return {"gram": gram, "U1": U1, "U": U, "keep": (X, T_rows, part)}
+    part = torch.empty((nsplit, max(1, p1 - p0), 256), dtype=torch.float64, device=dev)
+    gram = torch.empty((chunk * (split[1] if split else 1), 256), dtype=torch.float64, device=dev)
+    _check(hip().bsc_gram_stacked_range(_p(X), U1, T_rows.data_ptr(), U2, T_rows.stride(0), D, kchunk, p0, p1,
+                                        _p(part), _p(gram), _p(_tile_counters(dev, max(1, p1 - p0))), _stream()),
+           "gram_stacked")
+    out = {"gram": gram, "U1": U1, "U": U, "keep": (X, T_rows, part)}
+    if split is not None:
+        out["split"] = (rank, chunk, npairs)
+    return out
+
+
+def gram_slot(pre: dict) -> torch.Tensor:
+    """This rank's [chunk, 256] slot of a split Gram (the part it sends)."""
+    rank, chunk, _ = pre["split"]
+    return pre["gram"][rank * chunk:(rank + 1) * chunk]
+
+
+def gram_adopt(pre: dict, gathered: torch.Tensor) -> None:
+    """Install the all_gathered slots [world, chunk, 256] of a split Gram as the whole Gram."""
+    _, chunk, npairs = pre["split"]
+    full = gathered.reshape(-1, 256)[:npairs]
+    if full.device.type != "cuda":
+        pre["gram_full"] = gram_full_from_tiles(full, pre["U"])
+    pre["gram"] = full
+    del pre["split"]
 
 
 def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accept: int, need: int, lead_rank,

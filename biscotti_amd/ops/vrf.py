@@ -27,14 +27,10 @@ def _i32(b: bytes) -> np.ndarray:
 class DeviceVrfProver:
     ALPHA_LEN = 32
 
-    def __init__(self, device, batch_rounds: int = 1, streams=None):
+    def __init__(self, device, batch_rounds: int = 1):
         self.device = torch.device(device)
         self.btab = torch.from_numpy(_i32(rt().vrf_base_table()).copy()).to(self.device)   # [512 * 32]
         self.batch_rounds = max(1, int(batch_rounds))
-        # streams: launches go round-robin over these (one round's proofs per launch then overlap the
-        # previous rounds' instead of queueing behind them: a launch's latency, ~2 ms, exceeds a round)
-        self.streams = list(streams) if streams else None
-        self._rr = 0
         self._bufs: dict = {}
         self._row: dict[bytes, int] = {}
         self._keys: list[np.ndarray] = []
@@ -119,12 +115,6 @@ class DeviceVrfProver:
         if not self._queue:
             return
         q, self._queue = self._queue, []
-        if self.streams:
-            stream = self.streams[self._rr % len(self.streams)]
-            self._rr += 1
-        if len(q) == 1 and self.streams:
-            self._launch_round_native(q[0][0], q[0][1], stream)
-            return
         if len(q) == 1:
             # one round (one message): rows, zero message indices and the 32-byte message in ONE upload
             rows, alpha = q[0]
@@ -158,50 +148,8 @@ class DeviceVrfProver:
         # keep the last few batches alive until their kernels finished (the proofs are discarded)
         self._inflight = [x for x in self._inflight if not x[0].query()] if len(self._inflight) > 2 else self._inflight
 
-    SLOTS = 6
-
-    def _launch_round_native(self, rows: np.ndarray, alpha: bytes, stream) -> None:
-        """One round's proofs through a resident slot (pinned staging, device staging, scratch, proofs, event):
-        one native call, no allocation (bsc_vrf_prove_round)."""
-        n = int(rows.size)
-        ring = self.__dict__.get("_ring")
-        if ring is None or ring["cap"] < n:
-            cap = max(n, 256)
-
-            def slot():
-                ev = torch.cuda.Event()
-                ev.record(stream)   # materialise the handle (re-recorded natively)
-                return {"host": torch.zeros((2 * cap + 8,), dtype=torch.int32, pin_memory=True),
-                        "dev": torch.empty((2 * cap + 8,), dtype=torch.int32, device=self.device),
-                        "scratch": torch.empty((cap, 320), dtype=torch.int32, device=self.device),
-                        "pi": torch.empty((cap, 80), dtype=torch.uint8, device=self.device), "ev": ev, "used": False}
-            ring = self._ring = {"cap": cap, "k": 0, "slots": [slot() for _ in range(self.SLOTS)]}
-            torch.cuda.synchronize(self.device)
-        ring["k"] = (ring["k"] + 1) % self.SLOTS
-        sl = ring["slots"][ring["k"]]
-        if sl["used"] and not sl["ev"].query():
-            sl["ev"].synchronize()   # the slot's previous launch must be done before its buffers are reused
-        if self._keys_dev is None:
-            with S.use(stream):
-                self._keys_dev = self._upload(np.concatenate(self._keys))
-        h = sl["host"].numpy()
-        h[:n] = rows
-        h[n:2 * n] = 0
-        h[2 * n:2 * n + 8] = np.frombuffer(alpha, np.int32)
-        err = hip().bsc_vrf_prove_round(self._keys_dev.data_ptr(), sl["host"].data_ptr(), sl["dev"].data_ptr(), n,
-                                        self.btab.data_ptr(), sl["scratch"].data_ptr(), sl["pi"].data_ptr(),
-                                        stream.cuda_stream, sl["ev"].cuda_event)
-        if err != 0:
-            raise RuntimeError(f"HIP launch of vrf_prove failed with hipError {err}")
-        sl["used"] = True
-        self.proofs += n
-
     def drain(self, stream) -> None:
         self.flush(stream)
         for ev, _ in self._inflight:
             ev.synchronize()
         self._inflight = []
-        ring = self.__dict__.get("_ring")
-        for sl in (ring["slots"] if ring else ()):
-            if sl["used"]:
-                sl["ev"].synchronize()

@@ -27,6 +27,14 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+_RANKS_PER_DEVICE = 1   # ranks sharing this process's GPU (Comm.init); 1 with one rank per GPU
+
+
+def ranks_per_device() -> int:
+    """How many ranks share this process's GPU: the HBM table budget is split between them
+    (ops/bn256.choose_b0) and the speculative head stays off by default (head.py)."""
+    return _RANKS_PER_DEVICE
+
 
 @dataclass
 class Comm:
@@ -62,7 +70,6 @@ class Comm:
                 os.environ.setdefault("NCCL_IB_DISABLE", "1")
             be = backend or ("nccl" if dev.type == "cuda" else "gloo")
             local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-            be = os.environ.get("BISCOTTI_BACKEND", be)
             if be == "nccl" and torch.cuda.device_count() < local_world and not os.environ.get("NCCL_HOSTID"):
                 # (with a distinct NCCL_HOSTID per rank RCCL treats the ranks as separate hosts and
                 # connects them over its socket transport: the RCCL path rehearsed on one GPU)
@@ -98,7 +105,8 @@ class Comm:
         if dev.type == "cuda":
             # how many ranks share this GPU (1 on a node with one rank per GPU; several in rehearsals on a
             # 1-GPU box): the HBM table budget is split between them (ops/bn256.choose_b0)
-            os.environ["BISCOTTI_RANKS_PER_DEVICE"] = str(c.ranks_sharing_device())
+            global _RANKS_PER_DEVICE
+            _RANKS_PER_DEVICE = c.ranks_sharing_device()
         return c
 
     def ranks_sharing_device(self) -> int:
@@ -152,19 +160,28 @@ class Comm:
         dist.all_gather_into_tensor(out, flat)
         return out.view(self.world, *t.shape)
 
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+        """all_gather of `t` into the caller's (resident) buffer out [world, *t.shape], on the current
+        stream: no allocation, and the receiving buffer's address is stable across rounds."""
+        if self.world == 1:
+            out[0].copy_(t)
+            return out
+        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1))
+        return out
+
     def all_gather_packed(self, parts: list[torch.Tensor]) -> list[torch.Tensor]:
-        """ONE all_gather for several tensors of any dtypes (a round's small messages share a
-        launch instead of paying one xGMI latency each).  parts[i] has shape [L, ...] with the
-        same L everywhere; returns [world, L, ...] per part, bytes reinterpreted back to its dtype."""
-        L = parts[0].shape[0]
-        raw = [p.contiguous().reshape(L, -1).view(torch.uint8) for p in parts]
+        """ONE all_gather for several tensors of any shapes and dtypes (a round's small messages share a
+        launch instead of paying one xGMI latency each): every part's bytes are concatenated into one
+        row per rank.  Each rank passes the same shapes; returns [world, *shape] per part, bytes
+        reinterpreted back to its dtype."""
         if self.world == 1:
             return [p.unsqueeze(0) for p in parts]
-        g = self.all_gather(torch.cat(raw, dim=1))            # [world, L, total bytes]
+        raw = [p.contiguous().reshape(-1).view(torch.uint8) for p in parts]
+        g = self.all_gather(torch.cat(raw))            # [world, total bytes]
         out, o = [], 0
         for p, r in zip(parts, raw):
-            nb = r.shape[1]
-            out.append(g[:, :, o:o + nb].contiguous().view(p.dtype).view(self.world, *p.shape))
+            nb = r.numel()
+            out.append(g[:, o:o + nb].contiguous().view(p.dtype).view(self.world, *p.shape))
             o += nb
         return out
 

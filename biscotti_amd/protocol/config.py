@@ -80,11 +80,14 @@ class RunConfig:
     #   no_roles_proof     skip the discarded getVRFRoles proof (Q7)
     #   no_pipeline        GPU: no cross-round pipelining (pre-step, pre-Gram, early VRF, next-round MSM
     #                      at block build): the chain must not change (tests)
+    #   spec_head_shared   GPU: the next round's share MSM at block build also when several ranks share one
+    #                      GPU (off there by default: rehearsals of the one-rank-per-GPU path force it)
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
     churn_round_s: ClassVar[float] = 25.44
-    ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline")
+    ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
+                                  "spec_head_shared")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

@@ -93,14 +93,28 @@ class HostCrypto:
 
 class _CommitTable(dict):
     """worker -> marshalled commitment (64 bytes), read from the round's uint8 [n, 64] table on first
-    use: the signing reads the table rows natively, only the block's rows become bytes objects."""
+    use: the signing reads the table rows natively, only the block's rows become bytes objects.  The
+    table itself may be bound lazily (fill_lazy): its read-back is then waited for by its first reader
+    (the block build or the signing), never in the middle of the verification phase."""
 
     def __init__(self):
         super().__init__()
-        self.table, self.row = None, {}
+        self._table, self.row, self._load = None, {}, None
+
+    @property
+    def table(self):
+        if self._table is None and self._load is not None:
+            self._table, self._load = self._load(), None
+        return self._table
+
+    def bound(self) -> bool:
+        return self._table is not None or self._load is not None
 
     def fill(self, table: np.ndarray, row: dict) -> None:
-        self.table, self.row = table, row
+        self._table, self.row = table, row
+
+    def fill_lazy(self, load, row: dict) -> None:
+        self._load, self.row = load, row
 
     def __missing__(self, w):
         v = self[w] = self.table[self.row[w]].tobytes()

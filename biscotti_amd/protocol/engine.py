@@ -49,6 +49,7 @@ from .secagg import SecAggMixin
 from .verify import VerifyMixin
 
 SIDE_STREAM_SKIP_EVERY = 4   # the speculative-MSM stream leaves every 4th CU to the critical path
+VRF_BATCH_ROUNDS = 16        # device VRF proofs: rounds per prover launch
 _LOG_WHERE = "engine.py:428"   # file:line the per-round Train Error / Attack Rate lines name
 
 
@@ -81,9 +82,10 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.R = rt()
         self.dev = self.comm.device if cfg.device != "cpu" else torch.device("cpu")
         self.gpu = self.dev.type == "cuda"
-        import os
+        from ..parallel.comm import ranks_per_device
+
         # several ranks share this GPU (rehearsals on a 1-GPU box; Comm.init counts them)
-        self._shared_device = self.gpu and int(os.environ.get("BISCOTTI_RANKS_PER_DEVICE", "1")) > 1
+        self._shared_device = self.gpu and ranks_per_device() > 1
         self.N = cfg.num_nodes
         if self.comm.world > self.N:
             raise ValueError(f"{self.comm.world} ranks for {self.N} peers: every rank must host at least one peer")
@@ -140,12 +142,14 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.crypto = DeviceCrypto(key, cfg.poly_size, self.T, self.dev) if self.gpu else \
             HostCrypto(key, cfg.poly_size, self.T, cfg.host_threads)
         self.nchunks = self.crypto.nchunks
-        # one rank: the aggregation behind the committee's selection is enqueued natively (round.hip);
-        # BISCOTTI_NATIVE_SECAGG=0 keeps the Python path (A/B measurements)
+        # the aggregation behind the committee's selection and the pre-step are enqueued natively (round.hip),
+        # on any number of ranks
         self._native = None
-        if self.gpu and self.comm.world == 1 and os.environ.get("BISCOTTI_NATIVE_SECAGG", "1") == "1":
+        if self.gpu:
             self._native = B.NativeSecAgg(self.crypto.eng, self.main_stream, self.side_stream, self.bg_stream,
                                           10.0 ** cfg.precision)
+            if self.comm.world > 1:
+                self._native.gather_buffers(self.comm.world)
         if cfg.pkey_file:
             ks = self.R.read_client_keys(cfg.pkey_file)
             self.sk = {i: ks[i][0] for i in range(self.N)}
@@ -166,15 +170,10 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.vrf_dev = None
         if self.gpu and cfg.vrf_device:
             from ..ops.vrf import DeviceVrfProver
-            # 16 rounds per launch: a launch (~2.2 ms) occupies its SIMDs' register files (352 registers per
-            # wave) and slows the MSM waves that share them.  Per-round launches round-robin over several
-            # streams (BISCOTTI_VRF_BATCH=1, BISCOTTI_VRF_STREAMS=3) cut the end-of-run drain from 2.8 to
-            # ~0.9 ms but cost ~0.07 ms in every round (1.45 vs 1.38 ms/round, docs/PERF.md round 3)
-            nb = int(os.environ.get("BISCOTTI_VRF_BATCH", "16"))
-            ns = int(os.environ.get("BISCOTTI_VRF_STREAMS", "1"))
-            extra = [torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[0])
-                     for _ in range(ns - 1)] if ns > 1 else []
-            self.vrf_dev = DeviceVrfProver(self.dev, nb, [self.vrf_stream] + extra if extra else None)
+            # VRF_BATCH_ROUNDS rounds per launch: a launch (~2.2 ms) occupies its SIMDs' register files (352
+            # registers per wave) and slows the MSM waves that share them; per-round launches round-robin over
+            # several streams cut the end-of-run drain but cost ~0.07 ms in every round (docs/PERF.md round 3)
+            self.vrf_dev = DeviceVrfProver(self.dev, VRF_BATCH_ROUNDS)
         self._agg_idx: dict = {}      # (contributing, parts) -> resident aggregation index tensors
         self._W_next = None          # device copy of the model a block under construction carries
         self._pre = None             # next round's local step + commitments, queued behind the recovery
@@ -213,9 +212,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         VRF outputs / Krum, and the critical path keeps the rest)."""
         lo, hi = torch.cuda.Stream.priority_range()
         self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
-        import os
-        skip = int(os.environ.get("BISCOTTI_SIDE_SKIP", str(SIDE_STREAM_SKIP_EVERY)))   # A/B of the CU mask
-        self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, skip)
+        self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, SIDE_STREAM_SKIP_EVERY)
         # work no consumer in the round waits for (the miners' witness sums, the commitments)
         self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
         # long device work nothing in a round waits for -- the VRF proofs (kernels/vrf.hip) and the KZG

@@ -220,8 +220,12 @@ class RoundHeadMixin:
                 src = delta if [row_of[w] for w in ws] == list(range(delta.shape[0])) else \
                     delta.index_select(0, h2d([row_of[w] for w in ws], torch.long, self.dev))
                 buf.index_copy_(0, h2d([w - self.lo for w in ws], torch.long, self.dev), src)
-        X = self.comm.all_gather(buf).reshape(-1, d) if self.comm.world > 1 else buf
-        g = K.gram_stacked_async(X.contiguous(), self.noise_rows.rows(it))
+        comm = self.comm
+        X = comm.all_gather(buf).reshape(-1, d) if comm.world > 1 else buf
+        # several ranks: each computes 1/world of the Gram's tile pairs; the tiles travel with the
+        # commitments + noiser ids in the verification all_gather (_gather_verify_inputs)
+        g = K.gram_stacked_async(X.contiguous(), self.noise_rows.rows(it),
+                                 split=(comm.rank, comm.world) if comm.world > 1 else None)
         g["xrow"] = self.flat
         return g
 
@@ -236,18 +240,22 @@ class RoundHeadMixin:
         adopts them if that block carries W (same device tensor) and discards them otherwise.  Every rank
         queues it at the same point (the recovery is replicated), so the Gram's gather lines up."""
         main, gs = S.current(), self.gram_stream
-        if self._native is not None and type(self.task).__name__ == "SoftmaxTask" and self.cfg.audit_aggregate \
-                and self.comm.world == 1:
-            # step + commitments + Krum Gram in one native call (resident output ring)
+        if self._native is not None and type(self.task).__name__ == "SoftmaxTask" and self.cfg.audit_aggregate:
+            # step + chunk commitments (+ one rank: the Krum Gram) in one native call (resident output ring)
             nk = self._noise_krum()
+            single = self.comm.world == 1
             with S.use(gs):
                 cnt = K._tile_counters(self.dev, 1024)
-            import os
-            chunked = os.environ.get("BISCOTTI_EARLY_CS", "1") == "1"   # A/B: 0 = full commitments only
-            out = self._native.prestep(self.task, W, it, gs, self.noise_rows.rows(it) if nk else None, cnt,
-                                       chunked=chunked)
-            if nk:
+            out = self._native.prestep(self.task, W, it, gs, self.noise_rows.rows(it) if nk and single else None, cnt)
+            if nk and single:
                 out["gram"]["xrow"] = self.flat
+            elif nk:
+                # several ranks: the deltas' all_gather and this rank's share of the Gram's tiles, on the Gram
+                # stream behind the step (every rank queues this at the same point)
+                with S.use(gs):
+                    g = self._gram_rows(out["delta"], None, it)
+                    g["ev"] = S.record()
+                out["gram"] = g
             return out
         S.wait(gs, main)
         with S.use(gs):
@@ -275,9 +283,10 @@ class RoundHeadMixin:
         adopts it when the committed block and its plan match (they do unless the audit fails).  Local
         work only (no collective): each rank launches its own peers' rows."""
         cfg, pre = self.cfg, self._pre
-        if self._shared_device:
+        if self._shared_device and not cfg.has("spec_head_shared"):
             # several ranks on one GPU (rehearsals): speculative work only pays when the GPU would idle, and
-            # here the other ranks' critical paths fill it (2-rank RCCL rehearsal: 14.6 vs 3.6 ms/round)
+            # here the other ranks' critical paths fill it (2-rank RCCL rehearsal: 14.6 vs 3.6 ms/round);
+            # the spec_head_shared ablation forces it (the multi-rank GPU tests run the one-rank-per-GPU path)
             return
         if not (self._pipelined() and cfg.secure_agg and cfg.verification and cfg.churn == 0
                 and cfg.churn_kill_per_min == 0 and not self._partitions and pre is not None

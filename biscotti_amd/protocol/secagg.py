@@ -130,8 +130,13 @@ class SecAggMixin:
         T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
         audit = cfg.audit_aggregate
         kzg = cfg.kzg_audit != "off"
-        if self._native is not None and pts is not None and not isinstance(rowsel, list) and not kzg:
-            return self._aggregate_native(pts, ys, rowsel, contributing, part, now, early_cs)
+        if self._native is not None and not isinstance(rowsel, list) and not kzg:
+            # the device-selection path (replicated on every rank, so every rank takes this branch together:
+            # the collective below lines up); a rank without local rows adds zero partials
+            if comm.world > 1:
+                return self._aggregate_native_multi(pts, ys, rowsel, contributing, part, now, early_cs)
+            if pts is not None:
+                return self._aggregate_native(pts, ys, rowsel, contributing, part, now, early_cs)
         (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
         kzg_in = None   # this rank's (commitment sums, witness sums, share sums) for the KZG audit
         main = S.current() if self.gpu else None
@@ -242,6 +247,29 @@ class SecAggMixin:
         audit_ok = na.audit() if cfg.audit_aggregate else None
         return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
                 "clock": None, "now": now, "readback": readback}
+
+    def _aggregate_native_multi(self, pts, ys, mask, contributing, part, now, early_cs: bool = False) -> dict:
+        """_aggregate on several ranks (one per GPU) in two native calls around ONE all_gather of packed
+        rows (kernels/round.hip): this rank's partial share / commitment sums of its kept rows and its
+        clock straight into its send row, the collective on the main stream, then the ranks' totals, the
+        exact recovery and its read-back; the audit as on one rank."""
+        cfg, comm = self.cfg, self.comm
+        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
+        na = self._native
+        send, recv = na.gather_buffers(comm.world)
+        audit = (2 if early_cs else 1) if cfg.audit_aggregate else 0
+        if pts is not None:
+            pts, ys = pts.contiguous(), ys.contiguous()
+            S.hold(pts, ys, mask)   # read on the side and background streams
+        na.partials(pts, ys, mask, ccols, wcols, now, audit)
+        comm.all_gather_into(recv, send)
+        W_new, coeffs, status, agg = na.combine(ycols_t, xs_t, wts, A_dev, basis_dev, self.W, audit)
+        readback = na.readback(clocks=True)
+        if self._pipelined() and getattr(self.task, "stateless_step", False):
+            self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)
+        audit_ok = na.audit() if cfg.audit_aggregate else None
+        return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
+                "clock": True, "now": now, "readback": readback}
 
     # ------------------------------------------------------------------ read-backs and the audit
     def _d2h_async(self, *ts: torch.Tensor):

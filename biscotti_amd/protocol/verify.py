@@ -212,7 +212,17 @@ class VerifyMixin:
         commitments' read-back queued right behind it.  Returns (nz, sc) [U1, nn] on the device."""
         nz_np, sc_np = self._noise_ids_np(noisers, head["local_workers"])
         nz_l, sc_l = h2d_many([(nz_np, torch.int32), (sc_np, torch.float32)], self.dev)
-        got = self.comm.all_gather_packed([self._local_commit_buf(head), nz_l, sc_l])
+        parts = [self._local_commit_buf(head), nz_l, sc_l]
+        pre = head.get("krum_pre")
+        split = pre is not None and "split" in pre
+        if split:
+            # this rank's share of the Gram's tiles rides along (computed on the Gram stream)
+            if self.gpu and "ev" in pre:
+                S.current().wait_event(pre["ev"])
+            parts.append(K.gram_slot(pre))
+        got = self.comm.all_gather_packed(parts)
+        if split:
+            K.gram_adopt(pre, got[3])
         pw, nn_ = self.crypto.point_width, self.cfg.num_noisers
         g_commit = got[0].reshape(-1, pw)
         rows = g_commit.index_select(0, h2d([self.flat[w] for w in head["workers"]], torch.long, self.dev))
@@ -240,17 +250,20 @@ class VerifyMixin:
         need_X = cfg.verification and bool(inboxes)
         noise_aware = krum_pre is not None
 
-        def _materialize_commits():  # first use comes after the Krum kernels are queued
-            if commit_of.table is not None:
+        def _materialize_commits():  # bound lazily: the first reader (signing or block) waits for the copy
+            if commit_of.bound():
                 return
             if single:
                 if local_workers:
-                    commit_of.fill(pending_commits.result(), row_of)
+                    commit_of.fill_lazy(pending_commits.result, row_of)
             elif head.get("commit_gather") is not None:   # gathered with the noisers (noise-aware path)
                 host, ev = head["commit_gather"]
-                if ev is not None:
-                    ev.synchronize()
-                commit_of.fill(self.crypto.marshal_rows(host), {w: i for i, w in enumerate(workers)})
+
+                def load(host=host, ev=ev):
+                    if ev is not None:
+                        ev.synchronize()
+                    return self.crypto.marshal_rows(host)
+                commit_of.fill_lazy(load, {w: i for i, w in enumerate(workers)})
             elif workers:   # every worker's commitment: one batched marshal of the gathered rows
                 sel = h2d([self.flat[w] for w in workers], torch.long, self.dev)
                 commit_of.fill(self.crypto.marshal_rows(g_commit.index_select(0, sel)),
@@ -364,7 +377,7 @@ class VerifyMixin:
             sign = {"prep": None, "job": None, "sl": None}
             if local_vs:
                 _materialize_commits()
-                table, rowmap = commit_of.table, commit_of.row
+                rowmap = commit_of.row
                 acc_l, inb_l = acc_b[lk], inbox_arr[lk]
                 vidx = np.asarray([plan.verifiers.index(v) for v in local_vs], np.int64)
                 sks = [self.sk[v] for v in local_vs]
@@ -383,7 +396,8 @@ class VerifyMixin:
                         rmap[list(rowmap)] = list(rowmap.values())
                         bases = [_seed_bytes(cfg.seed, f"nonce-{i}", v) for v, i in nonce_keys]
                         sign["sl"] = (vidx[kk], jj)
-                        sign["job"] = R.schnorr_sign_rows_async(table, rmap[ws].tolist(), sks, kk.tolist(), bases,
+                        sign["job"] = R.schnorr_sign_rows_async(commit_of.table, rmap[ws].tolist(), sks, kk.tolist(),
+                                                                bases,
                                                                 ws.tolist(), SIGN_THREADS, after_vrf)
                 sign["prep"] = _prep_sign
                 if defer_sign:   # prepared in the next round's VRF wait, started once its outputs are known

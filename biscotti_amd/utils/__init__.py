@@ -166,9 +166,6 @@ class _PinnedRing:
         self.np = self.buf.numpy()
         self.off = 0
 
-    def stage(self, arr):
-        return self.buf[self._put(arr):][:arr.nbytes]
-
     def _put(self, arr) -> int:
         import torch
 
@@ -200,8 +197,6 @@ class _PinnedRing:
 
 _ring = None
 _NP_OF = {}
-# uploads through the bare runtime copy (BISCOTTI_H2D=torch: the framework's pinned .to() instead)
-_DIRECT = os.environ.get("BISCOTTI_H2D", "direct") != "torch"
 
 
 def h2d(data, dtype, device):
@@ -225,9 +220,7 @@ def h2d(data, dtype, device):
         return torch.as_tensor(data, dtype=dtype).pin_memory().to(device, non_blocking=True)
     if _ring is None:
         _ring = _PinnedRing()
-    if _DIRECT:
-        return _ring.upload(arr, dtype, device)
-    return _ring.stage(arr).view(dtype).view(arr.shape).to(device, non_blocking=True)
+    return _ring.upload(arr, dtype, device)
 
 
 _PINNED: dict = {}
@@ -252,9 +245,6 @@ def d2h_into(host, t) -> None:
     """Stream-ordered read-back of device tensor `t` into the pinned host tensor `host` (same shape
     and dtype) on the current stream: one bare hipMemcpyAsync (``host.copy_(t, non_blocking=True)``
     also records a host-allocator event, ~20 us of host time per copy on this stack)."""
-    if not _DIRECT:
-        host.copy_(t, non_blocking=True)
-        return
     from ..native import hip
     from . import streams as S
 
@@ -288,5 +278,5 @@ def h2d_many(items, device) -> list:
         raw[of:of + a.nbytes] = a.reshape(-1).view(np.uint8)
     if _ring is None:
         _ring = _PinnedRing()
-    dev = _ring.upload(raw, torch.uint8, device) if _DIRECT else _ring.stage(raw).to(device, non_blocking=True)
+    dev = _ring.upload(raw, torch.uint8, device)
     return [dev[of:of + a.nbytes].view(t).view(a.shape) for a, of, (_, t) in zip(arrs, offs, items)]

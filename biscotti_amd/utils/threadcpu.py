@@ -1,0 +1,48 @@
+"""Per-thread CPU attribution of this process (Linux /proc): which threads burn the host CPU of a rank --
+the round's Python thread, the native crypto pool (``bsc-pool``) and job threads (``bsc-job``), the HIP
+runtime, RCCL / gloo progress threads, OpenMP workers.  bench.py reports the CPU per thread group over
+the timed rounds, per rank, so a multi-GPU run's host cost can be attributed (docs/PERF.md)."""
+from __future__ import annotations
+
+import os
+
+_TICK = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+
+
+def snapshot() -> dict:
+    """tid -> (thread name, CPU seconds) of every live thread of this process."""
+    out = {}
+    base = "/proc/self/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"{base}/{tid}/stat") as f:
+                st = f.read()
+            with open(f"{base}/{tid}/comm") as f:
+                name = f.read().strip()
+        except OSError:
+            continue
+        # fields after the ")" that closes the (possibly space-containing) name: utime, stime are 14, 15
+        rest = st[st.rindex(")") + 2:].split()
+        out[tid] = (name, (int(rest[11]) + int(rest[12])) / _TICK)
+    return out
+
+
+def _group(name: str) -> str:
+    """Thread groups: names are truncated to 15 characters and often numbered (``bsc-pool``,
+    ``python``/``pt_main_thread``, ``HIP ...``, ``NCCL``/``rccl`` threads, ``gloo`` ...)."""
+    n = name.rstrip("0123456789:-_ ")
+    return n or name
+
+
+def delta_by_group(a: dict, b: dict) -> dict:
+    """CPU seconds per thread group between two snapshots (threads born in between count from 0)."""
+    acc: dict = {}
+    for tid, (name, t1) in b.items():
+        t0 = a.get(tid, (name, 0.0))[1]
+        g = _group(name)
+        acc[g] = acc.get(g, 0.0) + max(0.0, t1 - t0)
+    return dict(sorted(acc.items(), key=lambda kv: -kv[1]))

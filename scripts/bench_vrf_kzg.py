@@ -53,7 +53,6 @@ def main():
     t = time.perf_counter()
     out["kzg_ok"] = R.kzg_check_device_async(res, g2, R.g2_mul(g2, 2)).result()
     out["pairing_ms"] = (time.perf_counter() - t) * 1e3
-    out["lib"] = os.environ.get("BISCOTTI_HIP_LIB", "default")
     print(json.dumps(out))
 
 

@@ -38,13 +38,19 @@ def _worker(rank, world, port, kw, rounds, q, backend="gloo"):
     eng = BiscottiEngine(RunConfig(**kw), comm)
     for _ in range(rounds):
         eng.run_round()
-    q.put((rank, [bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))]))
+    stats = {k: v for k, v in eng.stats.items() if isinstance(v, (int, float))}
+    q.put((rank, ([bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))], stats)))
     comm.barrier()
     eng.close()
     comm.shutdown()
 
 
 def _run(world, kw, rounds, backend="gloo"):
+    """rank -> chain hashes (every rank must agree)."""
+    return {r: h for r, (h, _) in _run_stats(world, kw, rounds, backend).items()}
+
+
+def _run_stats(world, kw, rounds, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -102,3 +108,24 @@ def test_gpu_two_ranks_over_rccl_match_single_process():
     multi = _run(2, kw, 3, backend="nccl")
     assert multi[0] == multi[1]
     assert multi[0] == single
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gpu_one_rank_per_gpu_fast_path_over_rccl(world):
+    """The configuration an 8-GPU node runs (one rank per GPU): the speculative next-round head forced on
+    (ablation spec_head_shared; it is off by default only because these ranks share cuda:0), the native pre-step
+    (local step + chunk commitments), the Gram's tiles split across ranks, the native multi-rank
+    aggregation (partial sums -> one packed all_gather -> recovery).  Every rank must use every fast path
+    in every round after the first, and the chain must equal one process's byte for byte."""
+    rounds = 6
+    kw = dict(num_nodes=20, dataset="mnist", seed=13, deterministic_time=True, max_iterations=100,
+              ablation="spec_head_shared")
+    single, s1 = _run_stats(1, kw, rounds)[0]
+    out = _run_stats(world, kw, rounds, backend="nccl")
+    for r in range(world):
+        hashes, st = out[r]
+        assert hashes == single, f"rank {r} chain differs"
+        for k in ("pre_steps", "spec_head", "device_aggregations", "early_vrf"):
+            assert st.get(k, 0) >= rounds - 1, (r, k, st)
+        assert st.get("spec_misses", 0) == 0 and st.get("audit_failures", 0) == 0, st
+    assert s1.get("spec_head", 0) >= rounds - 1, s1
