@@ -472,7 +472,10 @@ class NativeSecAgg:
                                        self.h_clock.data_ptr(), int(audit)), "round_combine")
         return W_new, self.coeffs, self.status, agg
 
-    PRE_SLOTS = 3
+    # a slot is rewritten PRE_SLOTS pre-steps later; a round can queue two (a speculative aggregate that is
+    # dropped, then the host path's), and its commitment table may be read lazily in the next round's VRF
+    # wait (deferred signing): four slots keep every reader clear of the rewrite
+    PRE_SLOTS = 4
 
     def prestep(self, task, W, it: int, gram_stream, noise_rows, gram_counters, kchunk: int = 512,
                 chunked: bool = True, commit_stream=None) -> dict:

@@ -120,7 +120,17 @@ class _Reader:
         if c < 128:
             return c
         n = 256 - c
+        if n > 8:   # Go's decoder: a uint has at most 8 bytes
+            raise ValueError("gob: uint with more than 8 bytes")
         return int.from_bytes(self.take(n), "big")
+
+    def count(self) -> int:
+        """An element count: every element takes at least one byte, so a count beyond the bytes left in
+        the message is malformed (never allocate or loop on what a peer merely declares)."""
+        n = self.uint()
+        if n > len(self.b) - self.i:
+            raise ValueError("gob: element count exceeds the message")
+        return n
 
     def int(self) -> int:
         u = self.uint()
@@ -131,7 +141,7 @@ class _Reader:
         return struct.unpack("<d", struct.pack("<Q", int.from_bytes(u.to_bytes(8, "big"), "little")))[0]
 
     def bytes_(self) -> bytes:
-        return bytes(self.take(self.uint()))
+        return bytes(self.take(self.count()))
 
 
 # ---------------------------------------------------------------------------- encoder
@@ -375,7 +385,7 @@ class Decoder:
                     if sub == 0:
                         w.name, _ = self._common(r)
                     elif sub == 1:
-                        for _ in range(r.uint()):
+                        for _ in range(r.count()):
                             fname, fid, ff = "", 0, -1
                             while True:
                                 d3 = r.uint()
@@ -421,12 +431,12 @@ class Decoder:
             return r.bytes_().decode()
         w = self.types[tid]
         if w.kind == "slice":
-            n = r.uint()
+            n = r.count()
             if w.elem == 4:   # []float64 fast path
                 return [r.float() for _ in range(n)]
             return [self._value(r, w.elem) for _ in range(n)]
         if w.kind == "map":
-            n = r.uint()
+            n = r.count()
             out = {}
             for _ in range(n):
                 k = self._value(r, w.key)
@@ -443,8 +453,12 @@ class Decoder:
             out[name] = self._value(r, ftid)
 
 
-def read_message(stream) -> bytes:
-    """One message payload from a binary stream (socket file), or EOFError."""
+MAX_MESSAGE = 1 << 30   # Go's decoder refuses messages over 1 GB (tooBig)
+
+
+def read_message(stream, limit: int = MAX_MESSAGE) -> bytes:
+    """One message payload from a binary stream (socket file), or EOFError; messages longer than `limit`
+    bytes (or with a length field over 8 bytes) are refused before anything is allocated."""
     first = stream.read(1)
     if not first:
         raise EOFError
@@ -453,7 +467,11 @@ def read_message(stream) -> bytes:
         n = c
     else:
         k = 256 - c
+        if k > 8:
+            raise ValueError("gob: message length with more than 8 bytes")
         n = int.from_bytes(_read_exact(stream, k), "big")
+    if n > limit:
+        raise ValueError(f"gob: message of {n} bytes exceeds the {limit}-byte limit")
     return _read_exact(stream, n)
 
 

@@ -6,7 +6,8 @@ layer for talking to peers outside the job -- reference peers included -- with t
 understand:
 
   Peer.RegisterPeer      net.TCPAddr -> Blockchain       a joiner adopts the longest chain (main.go:420-436)
-  Peer.RegisterBlock     Block -> bool                   block flooding (main.go:398-409, processBlock)
+  Peer.RegisterBlock     Block -> Block                  block flooding: the block is echoed, processed
+                                                         asynchronously (main.go:398-409, processBlock)
   Peer.RequestNoise      int -> []float64                a noiser's pre-sampled vector (main.go:239-248)
   Peer.VerifyUpdateKRUM  Update -> []byte                a verifier collects its inbox, runs Multi-Krum,
                                                          signs accepted commitments (krum.go:227-365)
@@ -57,10 +58,15 @@ class _ValueReader:
 class RpcServer:
     """net/rpc server: handlers maps "Peer.Method" -> (arg schema, reply schema, fn(args) -> reply).  One
     thread per connection, calls on a connection served in order (Go serves them concurrently; the
-    reference's clients issue one call per connection)."""
+    reference's clients issue one call per connection).  At most `max_conns` connections are served at
+    once (further ones are closed on accept) and a connection idle for `idle_s` is dropped, so a peer
+    cannot exhaust the server's threads; gob messages are size-bounded (gob.read_message)."""
 
-    def __init__(self, handlers: dict, host: str = "127.0.0.1", port: int = 0):
+    def __init__(self, handlers: dict, host: str = "127.0.0.1", port: int = 0, max_conns: int = 64,
+                 idle_s: float = 120.0):
         self.handlers = handlers
+        self._slots = threading.BoundedSemaphore(max_conns)
+        self.idle_s = idle_s
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self.sock.bind((host, port))
@@ -86,6 +92,10 @@ class RpcServer:
                 conn, _ = self.sock.accept()
             except OSError:
                 return
+            if not self._slots.acquire(blocking=False):
+                conn.close()   # too many open connections
+                continue
+            conn.settimeout(self.idle_s)
             threading.Thread(target=self._serve, args=(conn,), daemon=True).start()
 
     def _serve(self, conn) -> None:
@@ -95,8 +105,8 @@ class RpcServer:
             while True:
                 try:
                     hdr = rd.next()
-                except (EOFError, OSError):
-                    return
+                except (EOFError, OSError, ValueError, KeyError, IndexError):
+                    return   # closed, idle, or a malformed stream: drop the connection
                 args = rd.next()   # the body is always read (also for an unknown method)
                 name, seq = hdr.get("ServiceMethod") or "", hdr.get("Seq") or 0
                 h = self.handlers.get(name)
@@ -112,9 +122,12 @@ class RpcServer:
                 out = enc.encode(G.Response, {"ServiceMethod": name, "Seq": seq, "Error": err})
                 out += enc.encode(G.InvalidRequest, {}) if err else enc.encode(rs, reply)
                 _send(conn, out)
+        except (EOFError, OSError, ValueError, KeyError, IndexError):
+            return
         finally:
             f.close()
             conn.close()
+            self._slots.release()
 
 
 class RpcError(RuntimeError):
@@ -183,12 +196,25 @@ class PeerService:
 
     chain: a native Blockchain (the engine's, or a follower's); peer_id, sk: this peer's id and Schnorr
     key; noise(it) -> its scaled noise vector; krum_thresh: KRUM_UPDATETHRESH; krum_timeout_s: the
-    verifier's deadline (startKRUMDeadlineTimer)."""
+    verifier's deadline (startKRUMDeadlineTimer); dim: the model size (updates of another length are
+    refused before they reach an inbox).
+
+    live=True: `chain` belongs to a running engine, whose FSM alone commits blocks.  RegisterBlock then
+    never touches the chain from the RPC thread: verified blocks are queued and the engine's loop takes
+    them between rounds (take_blocks) -- the reference's asynchronous processBlock, without a second
+    writer racing the round's commit.  live=False (a follower / the `serve` CLI): the service owns the
+    chain and appends extensions itself.  Per-iteration state (inboxes, decisions, shares, updates) is
+    kept for the last KEEP_ITERATIONS iterations only."""
+
+    KEEP_ITERATIONS = 4
+    MAX_QUEUED_BLOCKS = 64
 
     def __init__(self, rt, chain, peer_id: int = 0, sk: bytes | None = None, noise=None, krum_thresh: int = 1,
-                 krum_timeout_s: float = 10.0, lock: threading.Lock | None = None):
+                 krum_timeout_s: float = 10.0, lock: threading.Lock | None = None, live: bool = False,
+                 dim: int | None = None):
         self.rt, self.chain, self.id, self.sk, self.noise = rt, chain, peer_id, sk, noise
         self.lock = lock or threading.Lock()
+        self.live, self.dim = live, dim
         self.peers: list = []           # addresses announced through RegisterPeer
         self.krum_thresh, self.krum_timeout_s = krum_thresh, krum_timeout_s
         self._inbox: dict = {}          # iteration -> [Update values]
@@ -196,11 +222,29 @@ class PeerService:
         self._cv = threading.Condition(self.lock)
         self._secrets: dict = {}        # iteration -> {NodeID: MinerPartRPC value}
         self._updates: dict = {}        # iteration -> [Update values]
+        self._blocks: list = []         # live: verified blocks waiting for the engine (take_blocks)
+        self.block_log: list = []       # (iteration, outcome) of every RegisterBlock, newest last (bounded)
+        self._newest = -1
+
+    def _note(self, it: int, what: str) -> None:
+        self.block_log.append((it, what))
+        del self.block_log[:-256]
+
+    def _prune(self, it: int) -> None:
+        """Forget per-iteration state older than the newest iteration seen minus KEEP_ITERATIONS (caller holds
+        the lock)."""
+        if it <= self._newest:
+            return
+        self._newest = it
+        lo = it - self.KEEP_ITERATIONS
+        for d in (self._inbox, self._decided, self._secrets, self._updates):
+            for k in [k for k in d if k < lo]:
+                del d[k]
 
     def handlers(self) -> dict:
         return {
             "Peer.RegisterPeer": (G.TCPAddr, G.Blockchain, self.register_peer),
-            "Peer.RegisterBlock": (G.Block, G.BOOL, self.register_block),
+            "Peer.RegisterBlock": (G.Block, G.Block, self.register_block),
             "Peer.RequestNoise": (G.INT, G.Slice(G.FLOAT), self.request_noise),
             "Peer.VerifyUpdateKRUM": (G.Update, G.BYTES, self.verify_update_krum),
             "Peer.RegisterSecret": (G.MinerPartRPC, G.BOOL, self.register_secret),
@@ -217,23 +261,50 @@ class PeerService:
             self.peers.append(f"{host}:{int(addr.get('Port') or 0)}")
             return {"Blocks": [block_to_gob(self.chain.block(i)) for i in range(len(self.chain))]}
 
-    def register_block(self, v: dict) -> bool:
-        """Append the block if it extends the chain and its hash verifies; a block already held is
-        acknowledged (flooding duplicates), anything else is refused."""
+    def register_block(self, v: dict) -> dict:
+        """RegisterBlock(block, *returnBlock) (main.go:398-409): echo the block and process it
+        asynchronously -- the caller never gets an error (stale, duplicate and conflicting blocks are
+        logged, as processBlock does).  live: queued for the engine; otherwise appended here when its
+        hash verifies and it extends the chain."""
         b = gob_to_block(v, self.rt)
+        it = int(b.data.iteration)
+        ok_hash = bytes(b.compute_hash()) == bytes(b.hash)
         with self.lock:
-            it = b.data.iteration
+            if not ok_hash:
+                self._note(it, "bad-hash")
+            elif self.live:
+                if len(self._blocks) < self.MAX_QUEUED_BLOCKS:
+                    self._blocks.append(b)
+                    self._note(it, "queued")
+                else:
+                    self._note(it, "queue-full")
+            else:
+                self._note(it, self._append(b))
+        return v
+
+    def _append(self, b) -> str:
+        """Follower: append b if it extends the chain (caller holds the lock)."""
+        have = self.chain.get(int(b.data.iteration))
+        if have is not None:
+            return "duplicate" if bytes(have.hash) == bytes(b.hash) else "conflict"
+        if bytes(b.prev_hash) != bytes(self.chain.latest().hash):
+            return "not-extending"
+        self.chain.append(b)
+        return "appended"
+
+    def take_blocks(self) -> list:
+        """live: the blocks received since the last call, each classified against the engine's chain as
+        duplicate (the engine committed the same block), conflict (another block for an iteration the
+        engine has), ahead (an iteration the engine has not reached) -- call between rounds."""
+        with self.lock:
+            got, self._blocks = self._blocks, []
+        out = []
+        for b in got:
+            it = int(b.data.iteration)
             have = self.chain.get(it)
-            if have is not None:
-                if bytes(have.hash) == bytes(b.hash):
-                    return True
-                raise ValueError(f"conflicting block for iteration {it}")
-            if bytes(b.compute_hash()) != bytes(b.hash):
-                raise ValueError("block hash does not verify")
-            if bytes(b.prev_hash) != bytes(self.chain.latest().hash):
-                raise ValueError("block does not extend the chain")
-            self.chain.append(b)
-            return True
+            kind = "ahead" if have is None else ("duplicate" if bytes(have.hash) == bytes(b.hash) else "conflict")
+            out.append((it, kind, b))
+        return out
 
     def get_update_list(self, it: int) -> list:
         with self.lock:
@@ -259,7 +330,13 @@ class PeerService:
         import torch
 
         it = int(u.get("Iteration") or 0)
+        row = u.get("NoisedDelta") or u.get("Delta") or []
+        if self.dim is not None and len(row) != self.dim:
+            raise ValueError(f"update of length {len(row)}: the model has {self.dim} parameters")
         with self._cv:
+            self._prune(it)
+            if it < self._newest - self.KEEP_ITERATIONS:
+                raise ValueError(f"stale update for iteration {it}")
             box = self._inbox.setdefault(it, [])
             box.append(u)
             if len(box) >= self.krum_thresh:
@@ -279,24 +356,33 @@ class PeerService:
         return bytes(self.rt.schnorr_sign(bytes(u.get("Commitment") or b""), self.sk, nonce))
 
     def _decide(self, it, K, torch) -> None:
+        """Krum over the inbox of `it`; a failure is recorded as every update rejected (later callers for
+        the iteration then get that decision instead of re-running a failing Krum)."""
         box = self._inbox[it]
         box.sort(key=lambda x: int(x.get("SourceID") or 0))
-        X = torch.tensor([list(x.get("NoisedDelta") or x.get("Delta") or []) for x in box], dtype=torch.float32)
-        n = len(box)
-        clip = n // 2
-        acc, _ = K.krum(X, n - clip, n - clip) if n > 1 else (torch.ones(n, dtype=torch.bool), None)
-        self._decided[it] = {int(x.get("SourceID") or 0): bool(a) for x, a in zip(box, acc.tolist())}
+        try:
+            X = torch.tensor([list(x.get("NoisedDelta") or x.get("Delta") or []) for x in box], dtype=torch.float32)
+            n = len(box)
+            clip = n // 2
+            acc, _ = K.krum(X, n - clip, n - clip) if n > 1 else (torch.ones(n, dtype=torch.bool), None)
+            self._decided[it] = {int(x.get("SourceID") or 0): bool(a) for x, a in zip(box, acc.tolist())}
+        except Exception:
+            self._decided[it] = {}
         self._cv.notify_all()
 
     # ---- miner
     def register_secret(self, part: dict) -> bool:
         with self.lock:
-            self._secrets.setdefault(int(part.get("Iteration") or 0), {})[int(part.get("NodeID") or 0)] = part
+            it = int(part.get("Iteration") or 0)
+            self._prune(it)
+            self._secrets.setdefault(it, {})[int(part.get("NodeID") or 0)] = part
             return True
 
     def register_update(self, u: dict) -> bool:
         with self.lock:
-            self._updates.setdefault(int(u.get("Iteration") or 0), []).append(u)
+            it = int(u.get("Iteration") or 0)
+            self._prune(it)
+            self._updates.setdefault(it, []).append(u)
             return True
 
     def get_miner_part(self, node_list: list) -> dict:
@@ -340,7 +426,8 @@ def flood_block(peers: list, block, timeout: float = 10.0) -> int:
     ok = 0
     for p in peers:
         try:
-            ok += bool(call(p, "Peer.RegisterBlock", G.Block, v, timeout))
+            call(p, "Peer.RegisterBlock", G.Block, v, timeout)   # the reply echoes the block
+            ok += 1
         except (OSError, RpcError):
             pass
     return ok

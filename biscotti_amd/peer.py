@@ -69,9 +69,10 @@ def main(argv=None) -> int:
 
         host, port = ns.rpc_listen.rsplit(":", 1)
         me = eng.lo
+        # live: the RPC thread never writes the engine's chain; received blocks are taken between rounds
         svc = netrpc.PeerService(eng.R, eng.fsm.chain, peer_id=me, sk=eng.sk[me],
                                  noise=lambda it: eng.task.noise_scale(eng.sigma) * _noise_row(eng, me, it),
-                                 krum_thresh=max(1, eng.pc.krum_thresh))
+                                 krum_thresh=max(1, eng.pc.krum_thresh), live=True, dim=eng.d)
         srv = netrpc.RpcServer(svc.handlers(), host, int(port)).start()
         eng.log.info("serving Peer net/rpc on %s:%d", *srv.addr)
     n = 0
@@ -85,6 +86,13 @@ def main(argv=None) -> int:
             from .parallel import netrpc
 
             netrpc.flood_block(flood, eng.fsm.chain.latest())
+        if srv is not None:
+            # blocks flooded to us by outside peers, handled between rounds (processBlock): this job's own
+            # FSM is the only writer of its chain, so they are counted and logged, never spliced in
+            for it_b, kind, _ in svc.take_blocks():
+                eng.stats[f"rpc_blocks_{kind}"] = eng.stats.get(f"rpc_blocks_{kind}", 0) + 1
+                if kind != "duplicate":
+                    eng.log.info("net/rpc block for iteration %d: %s", it_b, kind)
         n += 1
     if srv is not None:
         srv.close()

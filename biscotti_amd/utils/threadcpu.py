@@ -17,6 +17,7 @@ def snapshot() -> dict:
         tids = os.listdir(base)
     except OSError:
         return out
+    main = str(os.getpid())
     for tid in tids:
         try:
             with open(f"{base}/{tid}/stat") as f:
@@ -27,7 +28,9 @@ def snapshot() -> dict:
             continue
         # fields after the ")" that closes the (possibly space-containing) name: utime, stime are 14, 15
         rest = st[st.rindex(")") + 2:].split()
-        out[tid] = (name, (int(rest[11]) + int(rest[12])) / _TICK)
+        # the process's main thread (the round's host thread) apart from helper threads that inherited its
+        # name (HIP runtime, RCCL proxy / socket threads, OpenMP workers)
+        out[tid] = ("main" if tid == main else name, (int(rest[11]) + int(rest[12])) / _TICK)
     return out
 
 

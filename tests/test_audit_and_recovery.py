@@ -111,3 +111,28 @@ def test_rank_failure_restarts_from_chain_file(tmp_path):
     assert c.verify()[0]
     its = [c.block(i).data.iteration for i in range(len(c))]
     assert its == list(range(-1, len(c) - 1)) and its[-1] >= 5
+
+
+def test_native_secagg_model_ring_never_aliases_the_live_model():
+    """NativeSecAgg's recovered-model ring: aggregates computed and then dropped (speculative misses,
+    failed audits, empty blocks) keep the engine's W unchanged for several rounds; the next model must never
+    land in W's buffer nor in one of the last two results (a queued pre-step may still read it)."""
+    import torch
+
+    from biscotti_amd.ops.bn256 import NativeSecAgg
+
+    na = object.__new__(NativeSecAgg)
+    na.W_ring = [torch.zeros(4, dtype=torch.float64) for _ in range(NativeSecAgg.W_RING)]
+    na.k, na._recent = 0, []
+    W = na.W_ring[1]                # the live model sits in a ring slot (adopted earlier)
+    last = []
+    for _ in range(12):             # twelve dropped aggregates in a row
+        out = na._next_W(W)
+        assert out.data_ptr() != W.data_ptr()
+        assert out.data_ptr() not in last[-2:]
+        last.append(out.data_ptr())
+    W = na._next_W(W)               # adopted: becomes the live model
+    for _ in range(6):
+        out = na._next_W(W)
+        assert out.data_ptr() != W.data_ptr()
+        W = out

@@ -58,11 +58,15 @@ def test_register_peer_and_block_flooding_sync_a_follower(rt):
         assert N.flood_block([fol], eng.fsm.chain.latest()) == 1
         assert bytes(follower_chain.latest().hash) == bytes(eng.fsm.chain.latest().hash)
         assert follower_chain.verify()[0]
-        # a tampered block is refused with the Go-style error string
+        # RegisterBlock(block, *returnBlock): the reply decodes as a Block echoing the one sent
+        echo = N.call(fol, "Peer.RegisterBlock", G.Block, N.block_to_gob(eng.fsm.chain.latest()))
+        assert bytes(echo["Hash"]) == bytes(eng.fsm.chain.latest().hash)
+        # a tampered block is echoed too (processBlock runs asynchronously and only logs) but not appended
         bad = N.block_to_gob(eng.fsm.chain.latest())
         bad["Data"]["Iteration"] += 1
-        with pytest.raises(N.RpcError):
-            N.call(fol, "Peer.RegisterBlock", G.Block, bad)
+        n0 = len(follower_chain)
+        N.call(fol, "Peer.RegisterBlock", G.Block, bad)
+        assert len(follower_chain) == n0
         with pytest.raises(N.RpcError):
             N.call(fol, "Peer.NoSuchMethod", G.INT, 1)
     finally:
@@ -120,6 +124,71 @@ def test_noiser_verifier_and_miner_services(rt):
         assert mp["PolyMap"][0]["Witnesses"] == [two, two]
     finally:
         srv.close()
+
+
+def test_live_service_never_writes_the_engine_chain(rt):
+    """--rpc-listen serves the running engine's chain: a block for the iteration the engine is about to
+    commit arrives over net/rpc first (a reference peer flooding its own block) -- the RPC thread only
+    queues it, the engine commits its own block, and the queued one is classified between rounds."""
+    eng = _chain(rt, 3)
+    other = _chain_seed(rt, 4, seed=3)     # a different chain: its iteration-3 block conflicts with ours
+    svc = N.PeerService(rt, eng.fsm.chain, live=True, dim=eng.d)
+    srv = N.RpcServer(svc.handlers()).start()
+    try:
+        addr = f"127.0.0.1:{srv.addr[1]}"
+        theirs = other.fsm.chain.block(4)
+        assert theirs.data.iteration == eng.fsm.iteration
+        N.call(addr, "Peer.RegisterBlock", G.Block, N.block_to_gob(theirs))
+        assert len(eng.fsm.chain) == 4                # not spliced in by the RPC thread
+        assert eng.run_round() is not None           # the engine's own commit is not refused
+        got = svc.take_blocks()
+        assert [(it, kind) for it, kind, _ in got] == [(3, "conflict")]
+        assert eng.fsm.chain.verify()[0] and len(eng.fsm.chain) == 5
+        # an update of the wrong length never reaches a verifier inbox
+        with pytest.raises(N.RpcError):
+            N.call(addr, "Peer.VerifyUpdateKRUM", G.Update, {"SourceID": 1, "Iteration": 4, "NoisedDelta": [0.0] * 3})
+    finally:
+        srv.close()
+        eng.close()
+        other.close()
+
+
+def _chain_seed(rt, n, seed):
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    eng = BiscottiEngine(RunConfig(num_nodes=6, dataset="creditcard", num_verifiers=2, num_miners=2, num_noisers=1,
+                                   device="cpu", seed=seed, deterministic_time=True))
+    for _ in range(n):
+        eng.run_round()
+    return eng
+
+
+def test_gob_decoder_bounds():
+    """Go's decoder limits: uints of at most 8 bytes, messages of at most 1 GB, and element counts no
+    larger than the bytes left (a declared count is never trusted for an allocation or a loop)."""
+    import io
+
+    with pytest.raises(ValueError):
+        G._Reader(bytes([256 - 9]) + bytes(9)).uint()
+    with pytest.raises(ValueError):
+        G.read_message(io.BytesIO(bytes([256 - 4]) + (1 << 31).to_bytes(4, "big")))
+    with pytest.raises(ValueError):
+        G.read_message(io.BytesIO(bytes([256 - 2]) + (1000).to_bytes(2, "big") + bytes(1000)), limit=999)
+    # a []float64 claiming 2^40 elements in a 10-byte message
+    enc = G.Encoder()
+    msgs = G.split_messages(enc.encode(G.Slice(G.FLOAT), [1.0, 2.0]))
+    dec = G.Decoder()
+    for m in msgs[:-1]:
+        dec.feed_message(m)
+    tid = G._Reader(msgs[-1]).int()
+    forged = bytearray()
+    G.enc_int(forged, tid)
+    G.enc_uint(forged, 0)            # singleton field
+    G.enc_uint(forged, 1 << 40)      # the declared element count
+    G.enc_float(forged, 1.0)
+    with pytest.raises(ValueError):
+        dec.feed_message(bytes(forged))
 
 
 def test_peer_cli_serves_and_floods(tmp_path):
