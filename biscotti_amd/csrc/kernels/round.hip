@@ -19,6 +19,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <chrono>
+#include <thread>
+
 extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
                              int ncols, const int* row_mask, uint32_t* out, void* stream);
 extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, const int* mask, const int* ycols,
@@ -310,9 +313,24 @@ extern "C" int bsc_round_combine(void* ctx, const unsigned char* recv, int world
   return 0;
 }
 
+// Host wait for an event: spin for SPIN_NS (the round's waits are tens to a few hundred us, and a sleeping
+// thread wakes late), then poll with short sleeps -- a long wait (ranks sharing a GPU, a collective behind a
+// slow rank) does not burn a core the way hipEventSynchronize's busy wait does (docs/PERF.md, multi-rank CPU).
+static int host_wait(hipEvent_t ev) {
+  constexpr long long SPIN_NS = 200000;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return (int)e;
+    const long long ns =
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (ns > SPIN_NS) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 // which: 0 = the recovery read-back, 1 = the audit read-back
 extern "C" int bsc_round_wait(void* ctx, int which) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return -1;
-  return (int)hipEventSynchronize(which == 0 ? c->ev_readback : c->ev_audit);
+  return host_wait(which == 0 ? c->ev_readback : c->ev_audit);
 }

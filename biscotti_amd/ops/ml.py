@@ -269,7 +269,7 @@ def krum_async(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=No
         on_accept(acc)
 
     def result():
-        ev.synchronize()
+        S.host_wait(ev)
         return host.bool(), scores
     return result
 
@@ -408,7 +408,7 @@ def krum_committee_async(X, inbox, groupsize: int, n_accept: int, need: int, lea
         on_accept(node)
 
     def result():
-        ev.synchronize()
+        S.host_wait(ev)
         h = host.bool()
         return h[: V * n].view(V, n), h[V * n:]
     return result
@@ -558,7 +558,7 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
         on_accept(node)
 
     def result():
-        ev.synchronize()
+        S.host_wait(ev)
         h = host.bool()
         return h[: V * n].view(V, n), h[V * n:]
     return result
@@ -605,7 +605,7 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True, Xt=None)
     ev = S.record()
 
     def result():
-        ev.synchronize()
+        S.host_wait(ev)
         e = host.tolist()
         return (e[0] / na if na else 0.0, e[1] / nb if nb else 0.0)
     return result

@@ -151,5 +151,5 @@ class DeviceVrfProver:
     def drain(self, stream) -> None:
         self.flush(stream)
         for ev, _ in self._inflight:
-            ev.synchronize()
+            S.host_wait(ev)
         self._inflight = []

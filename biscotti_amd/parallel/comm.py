@@ -51,13 +51,18 @@ class Comm:
         `timeout_s` bounds every collective: a rank that dies (the reference's crashed peer) makes
         the survivors' next collective fail within that time instead of hanging, the job exits and
         an elastic launcher (torchrun --max-restarts) restarts it from the persisted chain."""
+        from ..utils.threadcpu import mark_new_threads
+
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
         want_gpu = device != "cpu" and torch.cuda.is_available()
+        mark_new_threads("pre-init")
         if want_gpu:
             torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
             dev = torch.device("cuda", torch.cuda.current_device())
+            torch.empty(1, device=dev)   # the HIP runtime's helper threads start here
+            mark_new_threads("hip-runtime")
         else:
             dev = torch.device("cpu")
         if world > 1 and not dist.is_initialized():
@@ -107,6 +112,9 @@ class Comm:
             # 1-GPU box): the HBM table budget is split between them (ops/bn256.choose_b0)
             global _RANKS_PER_DEVICE
             _RANKS_PER_DEVICE = c.ranks_sharing_device()
+        if world > 1:
+            c.barrier()   # the backend's communicators (and their proxy / progress threads) exist after this
+            mark_new_threads(f"comm-{be}")
         return c
 
     def ranks_sharing_device(self) -> int:

@@ -32,7 +32,7 @@ class _PendingCommitments:
 
     def result(self) -> np.ndarray:
         if self.value is None:
-            self.event.synchronize()
+            S.host_wait(self.event)
             self.value = rt().g1_marshal_jac_batch(self.host.numpy().view(np.uint32))
         return self.value
 

@@ -291,7 +291,7 @@ class SecAggMixin:
         ev = S.record()
 
         def wait():
-            ev.synchronize()
+            S.host_wait(ev)
             return [h.numpy() for h in hs]
         return wait
 
@@ -313,7 +313,7 @@ class SecAggMixin:
         ev = S.record(main)
 
         def result():
-            ev.synchronize()
+            S.host_wait(ev)
             return host.numpy()
         return result
 

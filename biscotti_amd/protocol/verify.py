@@ -261,7 +261,7 @@ class VerifyMixin:
 
                 def load(host=host, ev=ev):
                     if ev is not None:
-                        ev.synchronize()
+                        S.host_wait(ev)
                     return self.crypto.marshal_rows(host)
                 commit_of.fill_lazy(load, {w: i for i, w in enumerate(workers)})
             elif workers:   # every worker's commitment: one batched marshal of the gathered rows

@@ -67,6 +67,23 @@ def wait(dst: torch.cuda.Stream, src: torch.cuda.Stream) -> None:
     dst.wait_event(ev)
 
 
+SPIN_S = 2e-4   # host waits spin this long, then poll with short sleeps
+
+
+def host_wait(ev) -> None:
+    """Wait on the host for a torch event: spin (the round's typical waits are tens to a few hundred us,
+    and a sleeping thread wakes late), then poll with ~50 us sleeps, so a long wait -- ranks sharing a GPU,
+    a collective waiting for a slow rank -- does not burn a core (docs/PERF.md, multi-rank host CPU)."""
+    if ev.query():
+        return
+    import time
+
+    t0 = time.perf_counter()
+    while not ev.query():
+        if time.perf_counter() - t0 > SPIN_S:
+            time.sleep(5e-5)
+
+
 def record(stream: torch.cuda.Stream | None = None) -> torch.cuda.Event:
     """A fresh event recorded on `stream` (default: the current stream), for host-side waits."""
     ev = torch.cuda.Event()

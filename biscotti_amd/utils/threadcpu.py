@@ -7,6 +7,21 @@ from __future__ import annotations
 import os
 
 _TICK = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+_LABELS: dict = {}   # tid -> label of helper threads that inherited the process name (mark_new_threads)
+
+
+def mark_new_threads(label: str) -> None:
+    """Label every thread of this process that has no label yet and is not the main thread: called right
+    after a library starts its helper threads (the HIP runtime at device init, RCCL / gloo at the first
+    collective), so their CPU is attributed to that library instead of to the process name they inherit."""
+    main = str(os.getpid())
+    try:
+        tids = os.listdir("/proc/self/task")
+    except OSError:
+        return
+    for tid in tids:
+        if tid != main and tid not in _LABELS:
+            _LABELS[tid] = label
 
 
 def snapshot() -> dict:
@@ -30,7 +45,11 @@ def snapshot() -> dict:
         rest = st[st.rindex(")") + 2:].split()
         # the process's main thread (the round's host thread) apart from helper threads that inherited its
         # name (HIP runtime, RCCL proxy / socket threads, OpenMP workers)
-        out[tid] = ("main" if tid == main else name, (int(rest[11]) + int(rest[12])) / _TICK)
+        if tid == main:
+            name = "main"
+        elif tid in _LABELS and name in ("python", "python3", "pt_main_thread"):
+            name = _LABELS[tid]
+        out[tid] = (name, (int(rest[11]) + int(rest[12])) / _TICK)
     return out
 
 

@@ -29,7 +29,17 @@ def main():
                     help="fraction of nonzero coefficients (quantised updates after the first rounds: 0.1-0.25)")
     ap.add_argument("--b0", type=int, default=None)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="another build of libbiscotti_hip.so (same-box A/B of kernels)")
     a = ap.parse_args()
+    if a.lib:
+        import ctypes
+
+        from biscotti_amd import native
+        from biscotti_amd.ops import _abi
+
+        lib = ctypes.CDLL(str(Path(a.lib).resolve()))
+        _abi.declare(lib)
+        native._hip = lib
     t0 = time.time()
     key = rt().CommitKey.generate(a.d, 2)
     t1 = time.time()
@@ -46,11 +56,12 @@ def main():
     coeffs = torch.from_numpy(c).cuda()
     allrows = torch.arange(a.workers, dtype=torch.int32, device="cuda")
     rows = allrows[: a.rows].contiguous()
-    res = {"d": a.d, "dist": a.dist, "density": a.density, "b0": eng.b0, "key_gen_s": t1 - t0, "table_build_s": t2 - t1,
+    res = {"lib": a.lib or "default", "d": a.d, "dist": a.dist, "density": a.density, "b0": eng.b0, "key_gen_s": t1 - t0, "table_build_s": t2 - t1,
            "table_gb": eng.table_bytes() / 1e9}
     for name, fn in [
         ("commit_rows_all_workers", lambda: eng.commit_rows(coeffs, allrows)),
         ("shares_approved", lambda: eng.shares(coeffs, rows)),
+        ("shares_witness_only", lambda: eng.shares(coeffs, rows, commit_only=2)),
     ]:
         fn()
         torch.cuda.synchronize()

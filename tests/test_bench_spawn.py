@@ -29,3 +29,42 @@ def test_bench_spawns_ranks_and_reports_them():
     for p in ranks:
         assert p["host_cpu_ms_per_round"] > 0 and p["thread_cpu_ms_per_round"]
         assert p["phase_ms_per_round"] and "engine_stats" in p
+
+
+def test_host_wait_sleeps_through_long_waits():
+    """The round's host waits (utils.streams.host_wait) spin only briefly: a wait of ~60 ms must not burn
+    ~60 ms of the waiting thread's CPU (hipEventSynchronize's busy wait did: 4 ranks sharing one GPU each
+    spent a full core per rank in waits, docs/PERF.md)."""
+    import time
+
+    from biscotti_amd.utils import streams as S
+
+    class Ev:
+        def __init__(self, dt):
+            self.t = time.perf_counter() + dt
+
+        def query(self):
+            return time.perf_counter() >= self.t
+
+    ev = Ev(0.06)
+    c0, w0 = time.thread_time(), time.perf_counter()
+    S.host_wait(ev)
+    cpu, wall = time.thread_time() - c0, time.perf_counter() - w0
+    assert wall >= 0.06 and cpu < 0.3 * wall, (cpu, wall)
+
+
+def test_per_rank_host_cpu_does_not_blow_up_with_ranks():
+    """4 gloo ranks: each rank's host CPU per round stays within the single-rank figure plus an allowance
+    (round 3 measured 19x the single-rank CPU per rank at 4 ranks on one GPU: busy waits)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    out = {}
+    for n in (1, 4):
+        r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--config", "credit4", "--peers", "16",
+                            "--steps", "4", "--warmup", "1", "--rounds", "5"], cwd=ROOT, env=env, capture_output=True,
+                           text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[n] = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    single = out[1]["host_cpu_ms_per_round"]
+    for p in out[4]["per_rank"]:
+        assert p["host_cpu_ms_per_round"] <= 1.25 * single + 30.0, (p["rank"], p["host_cpu_ms_per_round"], single)
