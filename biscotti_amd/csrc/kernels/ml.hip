@@ -635,12 +635,17 @@ extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise(const double
   }
 }
 
+// h_acc / h_node (nullable): the same verdicts written straight into pinned host memory (the host reads them
+// after the kernel's event: no read-back copy); amap / alive / nspec (nullable): the speculative share MSM's
+// row flags set from the block mask (k_set_alive fused: alive[i] = node[amap[i]], 0 where amap[i] < 0)
 extern "C" __global__ void __launch_bounds__(1024) k_krum_vote(const double* scores, const int* inbox, int V, int n,
                                                               int n_accept, int U, int need, const int* lead_rank,
-                                                              int cap, int* acc, int* node) {
+                                                              int cap, int* acc, int* node, int* h_acc, int* h_node,
+                                                              const int* amap, int nspec, int* alive) {
   __shared__ int sigs[1024];
   __shared__ int appr[1024];
   __shared__ int lr[1024];
+  __shared__ int kept[1024];
   __shared__ double sv[4][256];
   const int t = threadIdx.x;
   for (int w = t; w < U; w += 1024) {
@@ -662,6 +667,7 @@ extern "C" __global__ void __launch_bounds__(1024) k_krum_vote(const double* sco
       const int ok = rank < n_accept ? 1 : 0;
       const size_t ge = (size_t)(v0 + vv) * n + i;
       acc[ge] = ok;
+      if (h_acc != nullptr) h_acc[ge] = ok;
       if (ok) atomicAdd(&sigs[inbox[ge]], 1);
     }
   }
@@ -679,7 +685,17 @@ extern "C" __global__ void __launch_bounds__(1024) k_krum_vote(const double* sco
       keep = before < cap;
     }
     node[w] = keep;
+    kept[w] = keep;
+    if (h_node != nullptr) h_node[w] = keep;
   }
+  if (alive != nullptr) {
+    __syncthreads();
+    for (int i = t; i < nspec; i += 1024) {
+      const int j = amap[i];
+      __hip_atomic_store(alive + i, (j >= 0 && j < U && kept[j]) ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (h_acc != nullptr || h_node != nullptr) __threadfence_system();
 }
 
 // ---- large committees (an inbox of more than 256 updates, or more than 1024 candidate rows): the
@@ -771,12 +787,14 @@ extern "C" __global__ void __launch_bounds__(256) k_krum_cap_big(const int* sigs
   node[w] = keep;
 }
 
+extern "C" int bsc_set_alive(const int* accept, const int* src, int n, int* alive, void* stream);
 namespace {
 int krum_vote_any(hipStream_t s, const double* scores, const int* inbox, int V, int n, int n_accept, int U, int need,
-                  const int* lead_rank, int cap, int* acc, int* node, int* ws) {
+                  const int* lead_rank, int cap, int* acc, int* node, int* ws, int* h_out = nullptr,
+                  const int* amap = nullptr, int nspec = 0, int* alive = nullptr) {
   if (U <= 1024 && n <= 256) {
     hipLaunchKernelGGL(k_krum_vote, dim3(1), dim3(1024), 0, s, scores, inbox, V, n, n_accept, U, need, lead_rank,
-                       cap, acc, node);
+                       cap, acc, node, h_out, h_out != nullptr ? h_out + (size_t)V * n : nullptr, amap, nspec, alive);
   } else {
     if (ws == nullptr) return -1;
     hipMemsetAsync(ws, 0, (size_t)U * sizeof(int), s);
@@ -784,6 +802,11 @@ int krum_vote_any(hipStream_t s, const double* scores, const int* inbox, int V, 
                        n_accept, acc, ws);
     hipLaunchKernelGGL(k_krum_cap_big, dim3((U + 255) / 256), dim3(256), 0, s, (const int*)ws, lead_rank, U, need, cap,
                        node);
+    // large committees: the read-back copy and the flag update stay separate launches
+    if (h_out != nullptr && hipMemcpyAsync(h_out, acc, ((size_t)V * n + U) * sizeof(int), hipMemcpyDeviceToHost, s) !=
+                                hipSuccess)
+      return -1;
+    if (alive != nullptr && nspec > 0 && bsc_set_alive(node, amap, nspec, alive, s) != 0) return -1;
   }
   return 0;
 }
@@ -1142,7 +1165,8 @@ constexpr int RW_MAXC = 16;   // coefficients per chunk
 extern "C" __global__ void __launch_bounds__(256) k_recover_w(
     const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask, const int* ycols, const int* xs, int npts,
     const long long* A, const int* basis, int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi,
-    int d, const double* W, double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out) {
+    int d, const double* W, double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out,
+    double* h_W, int* h_status) {
   __shared__ long long agg[RW_CPB][RW_MAXP];
   __shared__ __int128 cf[RW_CPB][RW_MAXC];
   __shared__ int ok[RW_CPB];
@@ -1194,10 +1218,18 @@ extern "C" __global__ void __launch_bounds__(256) k_recover_w(
     const bool good = ok[c] != 0;
     const long long v = good ? (long long)cf[c][j] : 0;
     coeffs[(size_t)k * poly + j] = v;
-    if (j == 0) status[k] = good ? 1 : 0;
+    if (j == 0) {
+      status[k] = good ? 1 : 0;
+      if (h_status != nullptr) h_status[k] = good ? 1 : 0;
+    }
     const int idx = k * poly + j;
-    if (idx < d) W_new[idx] = W[idx] + (double)v / qscale;
+    if (idx < d) {
+      const double w = W[idx] + (double)v / qscale;
+      W_new[idx] = w;
+      if (h_W != nullptr) h_W[idx] = w;   // pinned host mirror: the host reads it after the kernel's event
+    }
   }
+  if (h_W != nullptr || h_status != nullptr) __threadfence_system();
 }
 
 // =====================================================================================
@@ -1343,6 +1375,30 @@ extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2,
                                 double* part, double* gram, unsigned int* count, void* stream) {
   return bsc_gram_stacked_range(X, U1, X2, U2, stride2, D, kchunk, 0, 0, part, gram, count, stream);
 }
+// h_out (nullable): [V * n + U1] pinned host mirror of (acc, node), written by the vote itself (acc and node
+// must be contiguous there too); amap / nspec / alive (nullable): the speculative MSM's row flags set in the
+// same kernel
+extern "C" int bsc_krum_committee_noise2(const double* gram, int U1, int U, const int* nz, const float* sc, int nn,
+                                         const int* inbox, int V, int n, int groupsize, int n_accept, int need,
+                                         const int* lead_rank, int cap, double* scores, int* acc, int* node, int* ws,
+                                         int* h_out, const int* amap, int nspec, int* alive, void* stream) {
+  if (U1 <= 0 || V <= 0 || n <= 0) return 0;
+  if (U > 8192 || U1 > 8192 || n > 4096 || V > 64 || n > U1 || nn <= 0 || nn > 16) return -1;
+  const int T = (U + 15) / 16;
+  hipStream_t s = (hipStream_t)stream;
+  if (n <= 256) {
+    hipLaunchKernelGGL(k_krum_rows_noise, dim3(n, V), dim3(256), 0, s, gram, T, U1, nz, sc, nn, inbox, n, groupsize,
+                       scores);
+  } else {
+    const int np2 = pow2_at_least(n);
+    hipLaunchKernelGGL(k_krum_rows_big<true>, dim3(n, V), dim3(1024), (size_t)np2 * sizeof(double), s, gram, T, U1,
+                       nz, sc, nn, inbox, n, np2, groupsize, scores);
+  }
+  if (krum_vote_any(s, scores, inbox, V, n, n_accept, U1, need, lead_rank, cap, acc, node, ws, h_out, amap, nspec,
+                    alive) != 0)
+    return -1;
+  return (int)hipGetLastError();
+}
 extern "C" int bsc_krum_committee_noise(const double* gram, int U1, int U, const int* nz, const float* sc, int nn,
                                         const int* inbox, int V, int n, int groupsize, int n_accept, int need,
                                         const int* lead_rank, int cap, double* scores, int* acc, int* node, int* ws,
@@ -1423,17 +1479,18 @@ extern "C" int bsc_recover(const long long* ys, int nchunks, int npts, const int
 
 // rstride: int64 elements between consecutive rows of ys (nch * T for a dense [nrows][nch][T] tensor; the
 // packed row length when ys are the ranks' partials inside an all_gather buffer, round.hip)
+// h_W / h_status (nullable): pinned host mirrors of W_new / status written by the kernel (no read-back copies)
 extern "C" int bsc_recover_w_strided(const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask,
                                      const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
                                      int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
                                      const double* W, double qscale, double* W_new, long long* coeffs, int* status,
-                                     long long* agg_out, void* stream) {
+                                     long long* agg_out, double* h_W, int* h_status, void* stream) {
   if (nch <= 0) return 0;
   if (npts > RW_MAXP || poly > RW_MAXC || poly > npts || shift < 0 || shift > 100 || nrows <= 0) return -1;
   if (rstride < (long long)nch * T) return -1;
   hipLaunchKernelGGL(k_recover_w, dim3(nblk(nch, RW_CPB)), dim3(256), 0, (hipStream_t)stream, ys, nrows, rstride, nch,
                      T, mask, ycols, xs, npts, A, basis, poly, shift, inv_lo, inv_hi, d, W, qscale, W_new, coeffs,
-                     status, agg_out);
+                     status, agg_out, h_W, h_status);
   return (int)hipGetLastError();
 }
 
@@ -1442,7 +1499,7 @@ extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, con
                              unsigned long long inv_lo, unsigned long long inv_hi, int d, const double* W, double qscale,
                              double* W_new, long long* coeffs, int* status, long long* agg_out, void* stream) {
   return bsc_recover_w_strided(ys, nrows, (long long)nch * T, nch, T, mask, ycols, xs, npts, A, basis, poly, shift,
-                               inv_lo, inv_hi, d, W, qscale, W_new, coeffs, status, agg_out, stream);
+                               inv_lo, inv_hi, d, W, qscale, W_new, coeffs, status, agg_out, nullptr, nullptr, stream);
 }
 
 extern "C" int bsc_add_rows(const float* delta, int D, const int* rows, int nrows, const double* W, double* W_new,

@@ -394,7 +394,8 @@ __device__ __forceinline__ jac aff_add_aff(const aff& p, const aff& q) {
 //   4. lane m < nm compares the total projectively with miner m's sum.
 extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* coeffs, int d, int poly,
                                                               const uint32_t* tbl_pk, int B0, int NW,
-                                                              const uint32_t* csum, int nm, int nch, int* ok) {
+                                                              const uint32_t* csum, int nm, int nch, int* ok,
+                                                              int* h_ok) {
   __shared__ uint32_t sh[64 * 24];
   __shared__ int dig[16][9];      // signed digit of (coefficient j, window w); NW <= 9 (bsc_chunk_check)
   __shared__ uint32_t items[16 * 9];   // nonzero digits: table entry | sign bit
@@ -450,7 +451,14 @@ extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* 
     if (t < s) st_jac(sh + t * 24, jac_add(ld_jac(sh + t * 24), ld_jac(sh + (t + s) * 24)));
     __syncthreads();
   }
-  if (t < nm) ok[(size_t)t * nch + k] = jac_equal(ld_jac(sh), ld_jac(csum + 24 * ((size_t)t * nch + k))) ? 1 : 0;
+  if (t < nm) {
+    const int v = jac_equal(ld_jac(sh), ld_jac(csum + 24 * ((size_t)t * nch + k))) ? 1 : 0;
+    ok[(size_t)t * nch + k] = v;
+    if (h_ok != nullptr) {   // pinned host mirror: read after the kernel's event, no read-back copy
+      h_ok[(size_t)t * nch + k] = v;
+      __threadfence_system();
+    }
+  }
 }
 
 // ------------------------------------------------------------------ reductions
@@ -510,7 +518,7 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
 // Sum of a strided segment per group: out[g] = sum_{k<n} pts[(g*n + k)*stride + off], one block
 // per group, LDS tree.  Used for the full commitment = sum of chunk commitments.
 extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* pts, int n, int stride, int off,
-                                                               uint32_t* out) {
+                                                               uint32_t* out, uint32_t* hout) {
   __shared__ uint32_t sh[256 * 24];
   const int g = blockIdx.x;
   jac acc = jac_inf();
@@ -528,7 +536,14 @@ extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* 
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) st_jac(out + 24 * (size_t)g, ld_jac(sh));
+  if (threadIdx.x == 0) {
+    const jac r = ld_jac(sh);
+    st_jac(out + 24 * (size_t)g, r);
+    if (hout != nullptr) {   // pinned host mirror (the commitments' read-back without a copy)
+      st_jac(hout + 24 * (size_t)g, r);
+      __threadfence_system();
+    }
+  }
 }
 
 // Jacobian -> kyber marshal (64 B: big-endian affine x || y, Montgomery-decoded; infinity = 0s)
@@ -694,25 +709,36 @@ extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, 
   const int nslab = (d + COMMIT_CB - 1) / COMMIT_CB;
   hipLaunchKernelGGL(k_commit_rows, dim3(nrows * nslab), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows, nrows,
                      tbl_pk, B0, NW, partial);
-  hipLaunchKernelGGL(k_segment_sum, dim3(nrows), dim3(256), 0, (hipStream_t)stream, partial, nslab, 1, 0, out);
+  hipLaunchKernelGGL(k_segment_sum, dim3(nrows), dim3(256), 0, (hipStream_t)stream, partial, nslab, 1, 0, out,
+                     (uint32_t*)nullptr);
   return (int)hipGetLastError();
 }
 
+// hout (nullable): pinned host mirror of out
+extern "C" int bsc_segment_sum_h(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
+                                 uint32_t* hout, void* stream) {
+  if (ngroups <= 0) return 0;
+  hipLaunchKernelGGL(k_segment_sum, dim3(ngroups), dim3(256), 0, (hipStream_t)stream, pts, n, stride, off, out, hout);
+  return (int)hipGetLastError();
+}
 extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
                                void* stream) {
-  if (ngroups <= 0) return 0;
-  hipLaunchKernelGGL(k_segment_sum, dim3(ngroups), dim3(256), 0, (hipStream_t)stream, pts, n, stride, off, out);
-  return (int)hipGetLastError();
+  return bsc_segment_sum_h(pts, ngroups, n, stride, off, out, nullptr, stream);
 }
 
-extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
-                               const uint32_t* csum, int nm, int nch, int* ok, void* stream) {
+// h_ok (nullable): pinned host mirror of ok
+extern "C" int bsc_chunk_check_h(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
+                                 const uint32_t* csum, int nm, int nch, int* ok, int* h_ok, void* stream) {
   if (nch <= 0 || nm <= 0) return 0;
   if (poly < 1 || poly > 16 || nm > 64 || B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65 || NW > 9) return -1;
   if ((long long)nch * poly < d || (long long)(nch - 1) * poly >= d) return -1;
   hipLaunchKernelGGL(k_chunk_check, dim3(nch), dim3(64), 0, (hipStream_t)stream, coeffs, d, poly, tbl_pk, B0, NW,
-                     csum, nm, nch, ok);
+                     csum, nm, nch, ok, h_ok);
   return (int)hipGetLastError();
+}
+extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
+                               const uint32_t* csum, int nm, int nch, int* ok, void* stream) {
+  return bsc_chunk_check_h(coeffs, d, poly, tbl_pk, B0, NW, csum, nm, nch, ok, nullptr, stream);
 }
 
 extern "C" int bsc_marshal(const uint32_t* pts, int n, uint8_t* out, void* stream) {

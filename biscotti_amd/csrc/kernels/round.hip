@@ -33,7 +33,11 @@ extern "C" int bsc_recover_w_strided(const long long* ys, int nrows, long long r
                                      const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
                                      int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
                                      const double* W, double qscale, double* W_new, long long* coeffs, int* status,
-                                     long long* agg_out, void* stream);
+                                     long long* agg_out, double* h_W, int* h_status, void* stream);
+extern "C" int bsc_segment_sum_h(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
+                                 uint32_t* hout, void* stream);
+extern "C" int bsc_chunk_check_h(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
+                                 const uint32_t* csum, int nm, int nch, int* ok, int* h_ok, void* stream);
 extern "C" int bsc_sum_rows_i64(const long long* ys, int R, long long C, const int* rows, int nsel, const int* mask,
                                 long long* out, void* stream);
 extern "C" int bsc_sum_rows2_pos(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
@@ -55,13 +59,60 @@ extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, 
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
                                const uint32_t* csum, int nm, int nch, int* ok, void* stream);
 
+extern "C" int bsc_set_alive(const int* accept, const int* src, int n, int* alive, void* stream);
+
 namespace {
+// resident state of the fused round calls (bsc_round_bind_* / bsc_round_add_*, registered once per run)
+struct Layout {   // one miner layout: which share columns the contributing miners hold, its recovery weights
+  const int *ccols, *wcols, *ycols, *xs, *basis;
+  int nwc, npts, shift;
+  const long long* A;
+  unsigned long long inv_lo, inv_hi;
+  long long* agg;   // [nch][npts] resident output
+  uint32_t* ws;     // [nwc][24] resident witness sums
+};
+struct PreSlot {  // one slot of the pre-step's output ring
+  float* delta;
+  long long* qdelta;
+  float* loss;
+  uint32_t *ccom, *jac, *jac_host;
+  double *part, *gram;
+  hipEvent_t ev_step, ev_ccom, ev_commit, ev_gram;
+};
+struct TaskCfg {  // the softmax task's resident data and the pre-step's constants
+  int bound = 0;
+  hipStream_t gram;
+  const float* X;
+  const int *y, *ntrain, *pid, *rows_arange;
+  const long long* off;
+  int d_in, d_out, B, P, lo, kchunk;
+  unsigned long long seed;
+  float max_norm;
+  double qs;
+  const uint32_t* tbl_wb;
+  const float* noise;       // resident noise table [N][100][d] (nullptr: no noise-aware Gram)
+  int noise_n;
+  unsigned int* counters;
+};
 struct RoundCtx {
   hipStream_t main, side, bg;
   hipEvent_t ev_main, ev_side, ev_readback, ev_audit, ev_pre;
   const uint32_t* tbl_pk;
   int d, poly, T, nch, b0, nw;
   double qscale;
+  // fused-call state
+  double* W_ring[8];
+  int nW = 0, Wk = 0;
+  const void* recent[2] = {nullptr, nullptr};
+  long long* coeffs = nullptr;
+  int *status = nullptr, *ok = nullptr, *h_status = nullptr, *h_ok = nullptr;
+  uint32_t* cs = nullptr;
+  double* h_W = nullptr;
+  Layout layouts[256];
+  int nlayouts = 0;
+  PreSlot pre[8];
+  int npre = 0, pre_k = 0;
+  TaskCfg task;
 };
 #define RC_CHECK(x)                        \
   do {                                     \
@@ -127,10 +178,10 @@ extern "C" int bsc_round_secagg(void* ctx, const uint32_t* pts, int R, const lon
   }
   RC_CHECK(hipStreamWaitEvent(c->bg, c->ev_main, 0));
   RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->bg));
-  RC_CHECK(bsc_recover_w(ys, R, c->nch, c->T, mask, ycols, xs, npts, A, basis, c->poly, shift, inv_lo, inv_hi, c->d, W,
-                         c->qscale, W_new, coeffs, status, agg, c->main));
-  RC_CHECK(hipMemcpyAsync(h_status, status, (size_t)c->nch * sizeof(int), hipMemcpyDeviceToHost, c->main));
-  RC_CHECK(hipMemcpyAsync(h_W, W_new, (size_t)c->d * sizeof(double), hipMemcpyDeviceToHost, c->main));
+  // the recovery writes (status, W_new) into the pinned read-back buffers itself: no copies behind it
+  RC_CHECK(bsc_recover_w_strided(ys, R, (long long)c->nch * c->T, c->nch, c->T, mask, ycols, xs, npts, A, basis,
+                                 c->poly, shift, inv_lo, inv_hi, c->d, W, c->qscale, W_new, coeffs, status, agg, h_W,
+                                 h_status, c->main));
   RC_CHECK(hipEventRecord(c->ev_readback, c->main));
   return 0;
 }
@@ -139,8 +190,7 @@ extern "C" int bsc_round_audit(void* ctx, const long long* coeffs, const uint32_
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return -1;
   RC_CHECK(hipStreamWaitEvent(c->main, c->ev_side, 0));
-  RC_CHECK(bsc_chunk_check(coeffs, c->d, c->poly, c->tbl_pk, c->b0, c->nw, cs, 1, c->nch, ok, c->main));
-  RC_CHECK(hipMemcpyAsync(h_ok, ok, (size_t)c->nch * sizeof(int), hipMemcpyDeviceToHost, c->main));
+  RC_CHECK(bsc_chunk_check_h(coeffs, c->d, c->poly, c->tbl_pk, c->b0, c->nw, cs, 1, c->nch, ok, h_ok, c->main));
   RC_CHECK(hipEventRecord(c->ev_audit, c->main));
   return 0;
 }
@@ -222,11 +272,11 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
     RC_CHECK(bsc_shares_msm(qdelta, c->d, rows_arange, P, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, 1, nullptr,
                             nullptr, 0, ccom, nullptr, cst));
     RC_CHECK(hipEventRecord((hipEvent_t)ev_ccom, cst));
-    RC_CHECK(bsc_segment_sum(ccom, P, c->nch, 1, 0, jac, cst));
+    RC_CHECK(bsc_segment_sum_h(ccom, P, c->nch, 1, 0, jac, jac_host, cst));   // full commitments + host mirror
   } else {   // full commitments only (1024-coefficient slabs; ccom is the slab-partials scratch)
     RC_CHECK(bsc_commit_rows(qdelta, c->d, rows_arange, P, c->tbl_pk, c->b0, c->nw, ccom, jac, cst));
+    RC_CHECK(hipMemcpyAsync(jac_host, jac, (size_t)P * 24 * sizeof(uint32_t), hipMemcpyDeviceToHost, cst));
   }
-  RC_CHECK(hipMemcpyAsync(jac_host, jac, (size_t)P * 24 * sizeof(uint32_t), hipMemcpyDeviceToHost, cst));
   RC_CHECK(hipEventRecord((hipEvent_t)ev_commit, cst));
   if (do_gram) {
     RC_CHECK(bsc_gram_stacked(delta, P, T_rows, U2, stride2, c->d, kchunk, part, gram, counters, gs));
@@ -304,12 +354,235 @@ extern "C" int bsc_round_combine(void* ctx, const unsigned char* recv, int world
   }
   RC_CHECK(bsc_recover_w_strided((const long long*)(recv + 96ll * nch), world, row_bytes / 8, nch, T, nullptr, ycols,
                                  xs, npts, A, basis, c->poly, shift, inv_lo, inv_hi, c->d, W, c->qscale, W_new, coeffs,
-                                 status, agg, c->main));
-  RC_CHECK(hipMemcpyAsync(h_status, status, (size_t)nch * sizeof(int), hipMemcpyDeviceToHost, c->main));
-  RC_CHECK(hipMemcpyAsync(h_W, W_new, (size_t)c->d * sizeof(double), hipMemcpyDeviceToHost, c->main));
+                                 status, agg, h_W, h_status, c->main));
   RC_CHECK(hipMemcpy2DAsync(h_clock, sizeof(long long), recv + 96ll * nch + 8ll * nch * T, (size_t)row_bytes,
                             sizeof(long long), (size_t)world, hipMemcpyDeviceToHost, c->main));
   RC_CHECK(hipEventRecord(c->ev_readback, c->main));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Fused round calls.  The host loop of a round is its critical path; each Python-level launch with its
+// argument marshalling costs 5-60 us of it.  The buffers these calls use are registered once per run
+// (model ring, outputs, miner layouts, pre-step slots, the task), so one call per phase takes a handful of
+// arguments:
+//   bsc_round_after_select   behind the committee's selection (one rank): the speculative rows' flags
+//                            (k_set_alive), the early audit sums, the miners' sums + recovery + read-back,
+//                            the next round's pre-step, the audit -- what NativeSecAgg.secagg + prestep +
+//                            audit and four Python helpers did in ~130 us of host time
+//   bsc_round_select_partials / bsc_round_after_gather   the same on several ranks, split around the
+//                            aggregation's all_gather
+extern "C" int bsc_round_bind_outputs(void* ctx, double* const* W_ring, int nW, long long* coeffs, int* status,
+                                      uint32_t* cs, int* ok, int* h_status, double* h_W, int* h_ok) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || nW < 3 || nW > 8) return -1;
+  for (int i = 0; i < nW; ++i) c->W_ring[i] = W_ring[i];
+  c->nW = nW;
+  c->coeffs = coeffs;
+  c->status = status;
+  c->cs = cs;
+  c->ok = ok;
+  c->h_status = h_status;
+  c->h_W = h_W;
+  c->h_ok = h_ok;
+  return 0;
+}
+
+extern "C" int bsc_round_add_layout(void* ctx, const int* ccols, const int* wcols, int nwc, const int* ycols,
+                                    const int* xs, int npts, const long long* A, const int* basis, int shift,
+                                    unsigned long long inv_lo, unsigned long long inv_hi, long long* agg, uint32_t* ws) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || c->nlayouts >= 256) return -1;
+  Layout& L = c->layouts[c->nlayouts];
+  L.ccols = ccols;
+  L.wcols = wcols;
+  L.nwc = nwc;
+  L.ycols = ycols;
+  L.xs = xs;
+  L.npts = npts;
+  L.A = A;
+  L.basis = basis;
+  L.shift = shift;
+  L.inv_lo = inv_lo;
+  L.inv_hi = inv_hi;
+  L.agg = agg;
+  L.ws = ws;
+  return c->nlayouts++;
+}
+
+extern "C" int bsc_round_bind_task(void* ctx, void* gram_stream, const float* X, const int* y, const long long* off,
+                                   const int* ntrain, const int* pid, int d_in, int d_out, int B, int P,
+                                   unsigned long long seed, float max_norm, double qs, int lo, const uint32_t* tbl_wb,
+                                   const int* rows_arange, const float* noise, int noise_n, int kchunk,
+                                   unsigned int* counters) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || P <= 0 || d_in * d_out + d_out != c->d) return -1;
+  TaskCfg& t = c->task;
+  t.gram = (hipStream_t)gram_stream;
+  t.X = X;
+  t.y = y;
+  t.off = off;
+  t.ntrain = ntrain;
+  t.pid = pid;
+  t.d_in = d_in;
+  t.d_out = d_out;
+  t.B = B;
+  t.P = P;
+  t.seed = seed;
+  t.max_norm = max_norm;
+  t.qs = qs;
+  t.lo = lo;
+  t.tbl_wb = tbl_wb;
+  t.rows_arange = rows_arange;
+  t.noise = noise;
+  t.noise_n = noise_n;
+  t.kchunk = kchunk;
+  t.counters = counters;
+  t.bound = 1;
+  return 0;
+}
+
+extern "C" int bsc_round_add_pre_slot(void* ctx, float* delta, long long* qdelta, float* loss, uint32_t* ccom,
+                                      uint32_t* jac, uint32_t* jac_host, double* part, double* gram, void* ev_step,
+                                      void* ev_ccom, void* ev_commit, void* ev_gram) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || c->npre >= 8) return -1;
+  PreSlot& p = c->pre[c->npre];
+  p.delta = delta;
+  p.qdelta = qdelta;
+  p.loss = loss;
+  p.ccom = ccom;
+  p.jac = jac;
+  p.jac_host = jac_host;
+  p.part = part;
+  p.gram = gram;
+  p.ev_step = (hipEvent_t)ev_step;
+  p.ev_ccom = (hipEvent_t)ev_ccom;
+  p.ev_commit = (hipEvent_t)ev_commit;
+  p.ev_gram = (hipEvent_t)ev_gram;
+  return c->npre++;
+}
+
+// the model ring slot for the next recovered model: never W (its input) and never one of the last two
+// results (one may still feed a queued pre-step), so a dropped aggregate can never overwrite the live model
+// (host-only, testable without a GPU) ring[*k + 1 ...]: the next entry that is neither W nor recent[0..1];
+// advances *k and shifts it into recent.  -1 when none is free (a ring of >= 4 always has one).
+extern "C" int bsc_ring_pick(const void* const* ring, int n, int* k, const void* W, const void** recent) {
+  for (int step = 1; step <= n; ++step) {
+    const int j = (*k + step) % n;
+    const void* cand = ring[j];
+    if (cand != W && cand != recent[0] && cand != recent[1]) {
+      *k = j;
+      recent[0] = recent[1];
+      recent[1] = cand;
+      return j;
+    }
+  }
+  return -1;
+}
+
+extern "C" int bsc_round_pick_W(void* ctx, const double* W) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || c->nW < 3) return -1;
+  return bsc_ring_pick((const void* const*)c->W_ring, c->nW, &c->Wk, W, (const void**)c->recent);
+}
+
+// the next round's pre-step into the next ring slot (noise-aware Gram when do_gram and a noise table is
+// bound; its rows for iteration `it` are the table's rows it % 100); returns the slot
+extern "C" int bsc_round_prestep_slot(void* ctx, const double* W, int it, int do_gram) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || !c->task.bound || c->npre < 3) return -1;
+  c->pre_k = (c->pre_k + 1) % c->npre;
+  const PreSlot& p = c->pre[c->pre_k];
+  const TaskCfg& t = c->task;
+  const bool g = do_gram && t.noise != nullptr;
+  const float* rows = g ? t.noise + (size_t)(it % 100) * c->d : nullptr;
+  RC_CHECK(bsc_round_prestep(ctx, t.gram, t.X, t.y, t.off, t.ntrain, t.pid, W, t.d_in, t.d_out, t.B, t.P, t.seed, it,
+                             t.max_norm, t.qs, t.lo, p.delta, p.qdelta, p.loss, t.tbl_wb, t.rows_arange, p.ccom, p.jac,
+                             p.jac_host, g ? 1 : 0, rows, g ? t.noise_n : 0, 100ll * c->d, t.kchunk, p.part, p.gram,
+                             t.counters, p.ev_step, p.ev_ccom, p.ev_commit, p.ev_gram, 1, nullptr));
+  return c->pre_k;
+}
+
+// the selection's flags for the speculative rows, then (early_slot >= 0) the audit's commitment sums from
+// that pre-step slot's chunk commitments into `cs_out`, then main waits for the MSM (spec_ev)
+static int select_head(RoundCtx* c, const int* node, const int* amap, int* alive, int nspec, const int* spec_rows,
+                       void* spec_ev, int early_slot, void* upload, uint32_t* cs_out) {
+  // node == nullptr: the selection kernel has set the flags itself (k_krum_vote with amap / alive)
+  if (nspec > 0 && node != nullptr) RC_CHECK(bsc_set_alive(node, amap, nspec, alive, c->main));
+  if (early_slot >= 0) {
+    if (early_slot >= c->npre || nspec <= 0) return -1;
+    const PreSlot& p = c->pre[early_slot];
+    RC_CHECK(bsc_round_csum_early(c, p.ccom, p.ev_ccom, spec_rows, nspec, alive, cs_out, upload));
+  }
+  if (spec_ev != nullptr) RC_CHECK(hipStreamWaitEvent(c->main, (hipEvent_t)spec_ev, 0));
+  return 0;
+}
+
+// One rank.  out[0] = model ring slot of the recovered model, out[1] = pre-step slot (-1: none queued).
+// pre_it >= 0 queues the next round's pre-step (iteration pre_it) behind the recovery; audit_now = 0 leaves
+// the audit to a later bsc_round_audit (the caller queues its own pre-step first).
+extern "C" int bsc_round_after_select(void* ctx, const int* node, const int* amap, int* alive, int nspec,
+                                      const int* spec_rows, void* spec_ev, const uint32_t* pts, const long long* ys,
+                                      int early_slot, void* upload, int layout, const double* W, int audit,
+                                      int pre_it, int do_gram, int audit_now, int* out) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || layout < 0 || layout >= c->nlayouts || nspec <= 0 || c->nW < 3) return -1;
+  const Layout& L = c->layouts[layout];
+  RC_CHECK(select_head(c, node, amap, alive, nspec, spec_rows, spec_ev, audit == 2 ? early_slot : -1, upload, c->cs));
+  const int wk = bsc_round_pick_W(ctx, W);
+  if (wk < 0) return -2;
+  double* W_new = c->W_ring[wk];
+  RC_CHECK(bsc_round_secagg(ctx, pts, nspec, ys, alive, L.ccols, L.wcols, L.nwc, L.ycols, L.xs, L.npts, L.A, L.basis,
+                            L.shift, L.inv_lo, L.inv_hi, W, W_new, c->coeffs, c->status, L.agg, c->cs, L.ws,
+                            c->h_status, c->h_W, audit));
+  int ps = -1;
+  if (pre_it >= 0) {
+    ps = bsc_round_prestep_slot(ctx, W_new, pre_it, do_gram);
+    if (ps < 0) return -3;
+  }
+  if (audit != 0 && audit_now) RC_CHECK(bsc_round_audit(ctx, c->coeffs, c->cs, c->ok, c->h_ok));
+  out[0] = wk;
+  out[1] = ps;
+  return 0;
+}
+
+// Several ranks, before the aggregation's all_gather: flags, early audit sums and this rank's partials into
+// the send row (nspec = 0: no local rows).
+extern "C" int bsc_round_select_partials(void* ctx, const int* node, const int* amap, int* alive, int nspec,
+                                         const int* spec_rows, void* spec_ev, const uint32_t* pts, const long long* ys,
+                                         int early_slot, void* upload, int layout, unsigned char* send, long long clock,
+                                         int audit) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || layout < 0 || layout >= c->nlayouts) return -1;
+  const Layout& L = c->layouts[layout];
+  RC_CHECK(select_head(c, node, amap, alive, nspec, spec_rows, nspec > 0 ? spec_ev : nullptr,
+                       audit == 2 && nspec > 0 ? early_slot : -1, upload, (uint32_t*)send));
+  return bsc_round_partials(ctx, nspec > 0 ? pts : nullptr, nspec, nspec > 0 ? ys : nullptr, nspec > 0 ? alive : nullptr,
+                            L.ccols, L.wcols, nspec > 0 ? L.nwc : 0, L.ws, send, clock, nspec > 0 ? audit : (audit ? 1 : 0));
+}
+
+// Several ranks, behind the all_gather into recv: totals + recovery + read-back (clocks included), the next
+// pre-step (no Gram: the caller gathers the deltas and splits the Gram across ranks), the audit.
+extern "C" int bsc_round_after_gather(void* ctx, const unsigned char* recv, int world, long long row_bytes, int layout,
+                                      const double* W, long long* h_clock, int audit, int pre_it, int audit_now,
+                                      int* out) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || layout < 0 || layout >= c->nlayouts) return -1;
+  const Layout& L = c->layouts[layout];
+  const int wk = bsc_round_pick_W(ctx, W);
+  if (wk < 0) return -2;
+  RC_CHECK(bsc_round_combine(ctx, recv, world, row_bytes, L.ycols, L.xs, L.npts, L.A, L.basis, L.shift, L.inv_lo,
+                             L.inv_hi, W, c->W_ring[wk], c->coeffs, c->status, L.agg, c->cs, c->h_status, c->h_W,
+                             h_clock, audit));
+  int ps = -1;
+  if (pre_it >= 0) {
+    ps = bsc_round_prestep_slot(ctx, c->W_ring[wk], pre_it, 0);
+    if (ps < 0) return -3;
+  }
+  if (audit != 0 && audit_now) RC_CHECK(bsc_round_audit(ctx, c->coeffs, c->cs, c->ok, c->h_ok));
+  out[0] = wk;
+  out[1] = ps;
   return 0;
 }
 

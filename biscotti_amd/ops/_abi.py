@@ -49,6 +49,7 @@ SIGNATURES = {
     "bsc_gram_stacked": [P, I, P, I, L, I, I, P, P, P, P],
     "bsc_gram_stacked_range": [P, I, P, I, L, I, I, I, I, P, P, P, P],
     "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P],
+    "bsc_krum_committee_noise2": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, I, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_eval_error_rb": [P, P, I, I, I, P, I, I, P, P, P],
     "bsc_eval_error_t_rb": [P, P, I, I, I, I, P, I, P, P, P],
@@ -71,6 +72,16 @@ SIGNATURES = {
     "bsc_round_row_bytes": [I, I],
     "bsc_round_partials": [P, P, I, P, P, P, P, I, P, P, L, I],
     "bsc_round_combine": [P, P, I, L, P, P, I, P, P, I, U64, U64, P, P, P, P, P, P, P, P, P, I],
+    "bsc_round_bind_outputs": [P, P, I, P, P, P, P, P, P, P],
+    "bsc_round_add_layout": [P, P, P, I, P, P, I, P, P, I, U64, U64, P, P],
+    "bsc_round_bind_task": [P, P, P, P, P, P, P, I, I, I, I, U64, F, D, I, P, P, P, I, I, P],
+    "bsc_round_add_pre_slot": [P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "bsc_round_pick_W": [P, P],
+    "bsc_round_prestep_slot": [P, P, I, I],
+    "bsc_round_after_select": [P, P, P, P, I, P, P, P, P, I, P, I, P, I, I, I, I, P],
+    "bsc_round_select_partials": [P, P, P, P, I, P, P, P, P, I, P, I, P, L, I],
+    "bsc_round_after_gather": [P, P, I, L, I, P, P, I, I, I, P],
+    "bsc_ring_pick": [P, I, P, P, P],
 }
 
 

@@ -347,19 +347,29 @@ class NativeSpec:
 
 
 class NativeSecAgg:
-    """The round's secure aggregation enqueued natively (kernels/round.hip): one call queues the miners'
-    commitment / witness sums (side / background streams), the fused share sums + exact recovery + W
-    update and the read-back (main stream); a second queues the aggregate audit.  Every buffer is
-    resident; the recovered model goes to a ring of W_RING buffers.  A new model never lands in the
-    buffer it is computed from (the engine's W) nor in the last two results (one of them may still feed a
-    queued pre-step): aggregates that are computed and then dropped (a speculative miss, a failed audit,
-    an empty block) can therefore never overwrite the live model.
+    """The round's device choreography, enqueued natively (kernels/round.hip) through a context that holds every
+    resident buffer: the recovered-model ring, the recovery / audit outputs and their pinned read-backs, one
+    entry per miner layout (index columns, exact recovery weights, outputs), the pre-step's slot ring and the
+    softmax task.  They are registered once (add_layout, bind_task), so a phase is ONE call with a handful of
+    arguments -- the round's host thread is its critical path:
 
-    One rank: secagg() does sums + recovery in one call.  Several ranks (one per GPU): partials() writes
-    this rank's partial sums into a packed send row, the caller all_gathers the rows (main stream), and
-    combine() sums the ranks' partials, recovers and reads back (kernels/round.hip)."""
+      after_select     one rank, behind the committee's selection: speculative rows' flags, early audit
+                       sums, the miners' sums + exact recovery + read-back, the next round's pre-step, the audit
+      select_partials  several ranks (one per GPU): flags, early audit sums and this rank's partial sums into
+                       a packed send row; the caller all_gathers the rows (main stream) ...
+      after_gather     ... and this call sums the ranks' partials, recovers, reads back (clocks included),
+                       queues the pre-step and the audit
+      prestep          the pre-step alone (first round, host-decided rounds)
+
+    A recovered model never lands in the buffer it is computed from nor in one of the last two results
+    (bsc_round_pick_W): aggregates that are computed and then dropped (speculative misses, failed audits,
+    empty blocks) cannot overwrite the live model."""
 
     W_RING = 4
+    # a slot is rewritten PRE_SLOTS pre-steps later; a round can queue two (a speculative aggregate that is
+    # dropped, then the host path's), and its commitment table may be read lazily in the next round's VRF
+    # wait (deferred signing): four slots keep every reader clear of the rewrite
+    PRE_SLOTS = 4
 
     def __init__(self, eng: DeviceCommitEngine, main, side, bg, qscale: float):
         self.eng, dev = eng, eng.device
@@ -369,7 +379,6 @@ class NativeSecAgg:
         if not self.ctx:
             raise RuntimeError("bsc_round_create failed")
         self.W_ring = [torch.empty((d,), dtype=torch.float64, device=dev) for _ in range(self.W_RING)]
-        self.k = 0
         self.coeffs = torch.empty((nch, poly), dtype=torch.int64, device=dev)
         self.status = torch.empty((nch,), dtype=torch.int32, device=dev)
         self.cs = torch.empty((nch, 24), dtype=torch.int32, device=dev)
@@ -377,63 +386,118 @@ class NativeSecAgg:
         self.h_status = torch.empty((nch,), dtype=torch.int32, pin_memory=True)
         self.h_W = torch.empty((d,), dtype=torch.float64, pin_memory=True)
         self.h_ok = torch.empty((1, nch), dtype=torch.int32, pin_memory=True)
-        self._by_shape: dict = {}
-        self._recent: list = []   # data pointers of the last two recovered models
+        import ctypes
+
+        ring = (ctypes.c_void_p * self.W_RING)(*[t.data_ptr() for t in self.W_ring])
+        _check(hip().bsc_round_bind_outputs(self.ctx, ring, self.W_RING, _ptr(self.coeffs), _ptr(self.status),
+                                            _ptr(self.cs), _ptr(self.ok), self.h_status.data_ptr(), self.h_W.data_ptr(),
+                                            self.h_ok.data_ptr()), "round_bind_outputs")
+        self._layouts: list = []   # keeps each layout's tensors alive
         self.world = 0            # several ranks: set by gather_buffers()
         self.h_clock = None
+        self._out = (ctypes.c_int * 2)()
+        self.task = None
+        self.slots: list = []
 
-    def _next_W(self, W) -> torch.Tensor:
-        """The ring slot for the next recovered model: not W (the input) and not one of the last two
-        results (see the class docstring)."""
-        avoid = set(self._recent) | {W.data_ptr()}
-        for step in range(1, self.W_RING + 1):
-            k = (self.k + step) % self.W_RING
-            if self.W_ring[k].data_ptr() not in avoid:
-                self.k = k
-                break
-        else:   # unreachable with W_RING >= 4
-            raise RuntimeError("NativeSecAgg: no free model buffer")
-        W_new = self.W_ring[self.k]
-        assert W_new.data_ptr() != W.data_ptr(), "recovered model would alias its input"
-        self._recent = (self._recent + [W_new.data_ptr()])[-2:]
-        return W_new
-
-    def _buf(self, key, shape, dtype):
-        t = self._by_shape.get(key)
-        if t is None:
-            t = self._by_shape[key] = torch.empty(shape, dtype=dtype, device=self.eng.device)
-        return t
-
-    def secagg(self, pts, ys, mask, ccols, wcols, ycols, xs, wts: dict, A_dev, basis_dev, W, audit: int):
-        """Queue sums + recovery + read-back; returns (W_new, coeffs, status, agg) device tensors."""
-        R = pts.shape[0]
+    # ---------------------------------------------------------------- registration (once per run)
+    def add_layout(self, ccols, wcols, ycols, xs, wts: dict, A_dev, basis_dev) -> int:
+        """Register one miner layout (its index columns and exact recovery weights) with resident outputs;
+        returns its id for the per-round calls."""
+        nch, dev = self.eng.nchunks, self.eng.device
         npts, nwc = ycols.numel(), wcols.numel()
-        nch = self.eng.nchunks
-        W_new = self._next_W(W)
-        agg = self._buf(("agg", npts), (nch, npts), torch.int64)
-        ws = self._buf(("ws", nwc), (nwc, 24), torch.int32)
-        err = hip().bsc_round_secagg(self.ctx, _ptr(pts), R, _ptr(ys), _ptr(mask), _ptr(ccols), _ptr(wcols), nwc,
-                                     _ptr(ycols), _ptr(xs), npts, _ptr(A_dev), _ptr(basis_dev), wts["shift"],
-                                     wts["inv_lo"], wts["inv_hi"], _ptr(W), _ptr(W_new), _ptr(self.coeffs),
-                                     _ptr(self.status), _ptr(agg), _ptr(self.cs), _ptr(ws), self.h_status.data_ptr(),
-                                     self.h_W.data_ptr(), int(audit))
-        if err != 0:
-            raise RuntimeError(f"bsc_round_secagg failed ({err})")
-        return W_new, self.coeffs, self.status, agg
+        agg = torch.empty((nch, npts), dtype=torch.int64, device=dev)
+        ws = torch.empty((max(nwc, 1), 24), dtype=torch.int32, device=dev)
+        lid = hip().bsc_round_add_layout(self.ctx, _ptr(ccols), _ptr(wcols), nwc, _ptr(ycols), _ptr(xs), npts, _ptr(A_dev),
+                                         _ptr(basis_dev), wts["shift"], wts["inv_lo"], wts["inv_hi"], _ptr(agg), _ptr(ws))
+        if lid < 0:
+            raise RuntimeError("bsc_round_add_layout failed (too many layouts?)")
+        self._layouts.append((ccols, wcols, ycols, xs, A_dev, basis_dev, agg, ws))
+        return lid
 
-    def csum_early(self, ccom, ccom_event, rows, mask, stream=None) -> None:
-        """Queue the audit's commitment sums now (side stream, behind what main has queued so far -- the
-        selection's flags -- and the pre-step's chunk commitments): cs = sum over the rows r with
-        mask[r] != 0 of ccom[rows[r]].  secagg(.., audit=2) / partials(.., audit=2) then leave them out.
-        Several ranks: the sums are this rank's partial and go straight into its send row."""
-        R = rows.numel()
-        assert ccom.dtype == torch.int32 and ccom.shape[1] == self.eng.nchunks and ccom.shape[-1] == 24
-        assert rows.dtype == torch.int32 and mask.dtype == torch.int32 and mask.numel() == R
-        ev = ccom_event.cuda_event if ccom_event is not None else None
-        out = self.send.data_ptr() if self.world > 1 else _ptr(self.cs)
-        _check(hip().bsc_round_csum_early(self.ctx, _ptr(ccom.contiguous()), ev, _ptr(rows), R, _ptr(mask),
-                                          out, stream.cuda_stream if stream is not None else None),
-               "round_csum_early")
+    def layout_agg(self, lid: int) -> torch.Tensor:
+        return self._layouts[lid][6]
+
+    def bind_task(self, task, gram_stream, noise_table, gram_counters, kchunk: int = 512) -> None:
+        """The softmax task's resident data and the pre-step's slot ring (PRE_SLOTS slots of step outputs, chunk
+        and full commitments, the noise-aware Gram).  noise_table: the resident [N, 100, d] noise table for the
+        one-rank pre-step's Gram (None: no Gram in the pre-step)."""
+        eng, dev = self.eng, self.eng.device
+        P, d = len(task.peers), eng.d
+        U2 = noise_table.shape[0] if noise_table is not None else 0
+        U = P + U2
+        Tt = (U + 15) // 16
+        npairs, nsplit = Tt * (Tt + 1) // 2, (d + kchunk - 1) // kchunk
+        self.pid = torch.tensor(task.peers, dtype=torch.int32, device=dev)
+        self.rows_ar = torch.arange(P, dtype=torch.int32, device=dev)
+        self.task, self.P, self.U2, self.gram_stream = task, P, U2, gram_stream
+        self.noise_table = noise_table
+        _check(hip().bsc_round_bind_task(self.ctx, gram_stream.cuda_stream, _ptr(task.X), _ptr(task.y), _ptr(task.off),
+                                         _ptr(task.ntrain), _ptr(self.pid), task.d_in, task.d_out, task.batch, P,
+                                         task.seed & (2 ** 64 - 1), 100.0, 1e4, task.peers[0], _ptr(eng.tbl_wb),
+                                         _ptr(self.rows_ar), noise_table.data_ptr() if noise_table is not None else None,
+                                         U2, kchunk, _ptr(gram_counters)), "round_bind_task")
+
+        def ev():
+            e = torch.cuda.Event()
+            e.record(gram_stream)   # materialise the handle (re-recorded natively)
+            return e
+        for _ in range(self.PRE_SLOTS):
+            sl = {"delta": torch.empty((P, d), dtype=torch.float32, device=dev),
+                  "qdelta": torch.empty((P, d), dtype=torch.int64, device=dev),
+                  "loss": torch.empty((P,), dtype=torch.float32, device=dev),
+                  "ccom": torch.empty((P, eng.nchunks, 1, 24), dtype=torch.int32, device=dev),
+                  "jac": torch.empty((P, 24), dtype=torch.int32, device=dev),
+                  "host": torch.empty((P, 24), dtype=torch.int32, pin_memory=True),
+                  "part": torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev),
+                  "gram": torch.empty((npairs, 256), dtype=torch.float64, device=dev),
+                  "ev": [ev() for _ in range(4)]}
+            e_step, e_ccom, e_commit, e_gram = sl["ev"]
+            k = hip().bsc_round_add_pre_slot(self.ctx, _ptr(sl["delta"]), _ptr(sl["qdelta"]), _ptr(sl["loss"]),
+                                             _ptr(sl["ccom"]), _ptr(sl["jac"]), sl["host"].data_ptr(), _ptr(sl["part"]),
+                                             _ptr(sl["gram"]), e_step.cuda_event, e_ccom.cuda_event,
+                                             e_commit.cuda_event, e_gram.cuda_event)
+            assert k == len(self.slots), "pre-step slot registration out of order"
+            self.slots.append(sl)
+        torch.cuda.synchronize(dev)
+
+    def _pre_out(self, k: int, W, it: int) -> dict:
+        """The engine's pre-step dict of slot k (the step of every local peer from W for iteration it)."""
+        from ..protocol.crypto_backends import _PendingCommitments
+
+        sl = self.slots[k]
+        e_step, e_ccom, e_commit, e_gram = sl["ev"]
+        pc = _PendingCommitments(sl["host"], e_commit, sl["jac"])
+        pc.ccom, pc.ccom_event, pc.src, pc.slot = sl["ccom"], e_ccom, sl["qdelta"], k   # early audit sums
+        out = {"W": W, "it": it, "delta": sl["delta"], "qdelta": sl["qdelta"], "ev": e_step, "commits": pc, "slot": k}
+        self.task.last_loss = sl["loss"]
+        if self.noise_table is not None and self.world <= 1:
+            out["gram"] = {"gram": sl["gram"], "U1": self.P, "U": self.P + self.U2,
+                           "keep": (sl["delta"], self.noise_table, sl["part"]), "ev": e_gram}
+        return out
+
+    # ---------------------------------------------------------------- per-round calls
+    def prestep(self, W, it: int, do_gram: bool = True) -> dict:
+        """The pre-step alone: the local step of every local peer from W (Gram stream, behind main), the chunk +
+        full commitments (background stream, read back) and, one rank with a noise table, the noise-aware Gram."""
+        k = hip().bsc_round_prestep_slot(self.ctx, _ptr(W), int(it), int(do_gram))
+        if k < 0:
+            raise RuntimeError(f"bsc_round_prestep_slot failed ({k})")
+        return self._pre_out(k, W, it)
+
+    def after_select(self, node, amap, sp, early_slot: int, upload, layout: int, W, audit: int, pre_it: int,
+                     audit_now: bool = True):
+        """One rank: everything behind the committee's selection in one call (see the class docstring).
+        Returns (W_new, pre dict or None)."""
+        o = self._out
+        err = hip().bsc_round_after_select(self.ctx, _ptr(node) if node is not None else None, _ptr(amap),
+                                           _ptr(sp.alive), len(sp.rows),
+                                           _ptr(sp.rows_t), sp.ev.cuda_event, _ptr(sp.pts), _ptr(sp.ys), int(early_slot),
+                                           upload.cuda_stream, int(layout), _ptr(W), int(audit), int(pre_it), 1,
+                                           int(audit_now), o)
+        if err != 0:
+            raise RuntimeError(f"bsc_round_after_select failed ({err})")
+        W_new = self.W_ring[o[0]]
+        return W_new, (self._pre_out(o[1], W_new, pre_it) if o[1] >= 0 else None)
 
     # ---------------------------------------------------------------- several ranks
     def gather_buffers(self, world: int):
@@ -448,92 +512,28 @@ class NativeSecAgg:
             self.world = world
         return self.send, self.recv
 
-    def partials(self, pts, ys, mask, ccols, wcols, clock: int, audit: int) -> None:
-        """Queue this rank's partial sums of its kept rows into the send row (pts / ys / mask None: no
-        local rows).  audit: 0 none, 1 commitment sums here, 2 already queued by csum_early."""
-        assert self.world > 0, "gather_buffers() first"
-        R = 0 if pts is None else pts.shape[0]
-        nwc = wcols.numel() if R else 0
-        ws = self._buf(("ws", nwc), (nwc, 24), torch.int32) if nwc else None
-        _check(hip().bsc_round_partials(self.ctx, _ptr(pts) if R else None, R, _ptr(ys) if R else None,
-                                        _ptr(mask) if R else None, _ptr(ccols), _ptr(wcols) if R else None, nwc,
-                                        _ptr(ws), self.send.data_ptr(), int(clock), int(audit)), "round_partials")
+    def select_partials(self, node, amap, sp, early_slot: int, upload, layout: int, clock: int, audit: int) -> None:
+        """Several ranks, before the all_gather: flags, early audit sums and this rank's partial sums of its kept
+        rows into the send row (sp None: no local rows -- zero partials)."""
+        assert self.world > 1, "gather_buffers() first"
+        n = len(sp.rows) if sp is not None else 0
+        err = hip().bsc_round_select_partials(
+            self.ctx, _ptr(node) if n and node is not None else None, _ptr(amap) if n else None, _ptr(sp.alive) if n else None, n,
+            _ptr(sp.rows_t) if n else None, sp.ev.cuda_event if n else None, _ptr(sp.pts) if n else None,
+            _ptr(sp.ys) if n else None, int(early_slot), upload.cuda_stream, int(layout), self.send.data_ptr(),
+            int(clock), int(audit))
+        if err != 0:
+            raise RuntimeError(f"bsc_round_select_partials failed ({err})")
 
-    def combine(self, ycols, xs, wts: dict, A_dev, basis_dev, W, audit: int):
-        """Behind the all_gather into recv (main stream): ranks' totals, exact recovery, read-back of
-        (status, W_new, clocks).  Returns (W_new, coeffs, status, agg) device tensors."""
-        npts, nch = ycols.numel(), self.eng.nchunks
-        W_new = self._next_W(W)
-        agg = self._buf(("agg", npts), (nch, npts), torch.int64)
-        _check(hip().bsc_round_combine(self.ctx, self.recv.data_ptr(), self.world, self.row_bytes, _ptr(ycols),
-                                       _ptr(xs), npts, _ptr(A_dev), _ptr(basis_dev), wts["shift"], wts["inv_lo"],
-                                       wts["inv_hi"], _ptr(W), _ptr(W_new), _ptr(self.coeffs), _ptr(self.status),
-                                       _ptr(agg), _ptr(self.cs), self.h_status.data_ptr(), self.h_W.data_ptr(),
-                                       self.h_clock.data_ptr(), int(audit)), "round_combine")
-        return W_new, self.coeffs, self.status, agg
-
-    # a slot is rewritten PRE_SLOTS pre-steps later; a round can queue two (a speculative aggregate that is
-    # dropped, then the host path's), and its commitment table may be read lazily in the next round's VRF
-    # wait (deferred signing): four slots keep every reader clear of the rewrite
-    PRE_SLOTS = 4
-
-    def prestep(self, task, W, it: int, gram_stream, noise_rows, gram_counters, kchunk: int = 512,
-                chunked: bool = True, commit_stream=None) -> dict:
-        """The next round's pre-step of a SoftmaxTask in ONE native call (bsc_round_prestep): the local step of
-        every local peer on the Gram stream, the per-chunk + full commitments (read back) on the background
-        stream and, with noise_rows (the noise table's rows of this iteration), the noise-aware Krum's Gram.
-        Outputs and events rotate over PRE_SLOTS resident slots (a slot is rewritten three rounds later, after
-        every consumer of its round).  Returns the engine's pre-step dict."""
-        from ..ops import ml as K
-        from ..protocol.crypto_backends import _PendingCommitments
-
-        eng, dev = self.eng, self.eng.device
-        P, d = len(task.peers), eng.d
-        U2 = noise_rows.shape[0] if noise_rows is not None else 0
-        U = P + U2
-        Tt = (U + 15) // 16
-        npairs, nsplit = Tt * (Tt + 1) // 2, (d + kchunk - 1) // kchunk
-        ring = self.__dict__.get("_pre_ring")
-        if ring is None:
-            def ev():
-                e = torch.cuda.Event()
-                e.record(gram_stream)   # materialise the handle (re-recorded natively)
-                return e
-
-            ring = self._pre_ring = {"k": 0, "pid": torch.tensor(task.peers, dtype=torch.int32, device=dev),
-                                     "rows": torch.arange(P, dtype=torch.int32, device=dev), "slots": [
-                {"delta": torch.empty((P, d), dtype=torch.float32, device=dev),
-                 "qdelta": torch.empty((P, d), dtype=torch.int64, device=dev),
-                 "loss": torch.empty((P,), dtype=torch.float32, device=dev),
-                 "ccom": torch.empty((P, eng.nchunks, 1, 24), dtype=torch.int32, device=dev),
-                 "jac": torch.empty((P, 24), dtype=torch.int32, device=dev),
-                 "host": torch.empty((P, 24), dtype=torch.int32, pin_memory=True),
-                 "part": torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev),
-                 "gram": torch.empty((npairs, 256), dtype=torch.float64, device=dev),
-                 "ev": [ev() for _ in range(4)]} for _ in range(self.PRE_SLOTS)]}
-            torch.cuda.synchronize(dev)
-        ring["k"] = (ring["k"] + 1) % self.PRE_SLOTS
-        sl = ring["slots"][ring["k"]]
-        e_step, e_ccom, e_commit, e_gram = sl["ev"]
-        assert sl["part"].shape == (nsplit, npairs, 256), "Gram shape changed between rounds"
-        _check(hip().bsc_round_prestep(
-            self.ctx, gram_stream.cuda_stream, _ptr(task.X), _ptr(task.y), _ptr(task.off), _ptr(task.ntrain),
-            _ptr(ring["pid"]), _ptr(W), task.d_in, task.d_out, task.batch, P, task.seed & (2 ** 64 - 1), int(it),
-            100.0, 1e4, task.peers[0], _ptr(sl["delta"]), _ptr(sl["qdelta"]), _ptr(sl["loss"]), _ptr(eng.tbl_wb),
-            _ptr(ring["rows"]), _ptr(sl["ccom"]), _ptr(sl["jac"]), sl["host"].data_ptr(), int(noise_rows is not None),
-            noise_rows.data_ptr() if noise_rows is not None else None, U2,
-            noise_rows.stride(0) if noise_rows is not None else 0, kchunk, _ptr(sl["part"]), _ptr(sl["gram"]),
-            _ptr(gram_counters), e_step.cuda_event, e_ccom.cuda_event, e_commit.cuda_event, e_gram.cuda_event,
-            int(chunked), commit_stream.cuda_stream if commit_stream is not None else None), "round_prestep")
-        pc = _PendingCommitments(sl["host"], e_commit, sl["jac"])
-        if chunked:   # per-chunk commitments for the early audit sums
-            pc.ccom, pc.ccom_event, pc.src = sl["ccom"], e_ccom, sl["qdelta"]
-        out = {"W": W, "it": it, "delta": sl["delta"], "qdelta": sl["qdelta"], "ev": e_step, "commits": pc}
-        task.last_loss = sl["loss"]
-        if noise_rows is not None:
-            out["gram"] = {"gram": sl["gram"], "U1": P, "U": U, "keep": (sl["delta"], noise_rows, sl["part"]),
-                           "ev": e_gram}
-        return out
+    def after_gather(self, layout: int, W, audit: int, pre_it: int, audit_now: bool = True):
+        """Several ranks, behind the all_gather into recv: (W_new, pre-step slot k or -1); the pre dict needs
+        the caller's Gram gather (the deltas cross ranks)."""
+        o = self._out
+        err = hip().bsc_round_after_gather(self.ctx, self.recv.data_ptr(), self.world, self.row_bytes, int(layout),
+                                           _ptr(W), self.h_clock.data_ptr(), int(audit), int(pre_it), int(audit_now), o)
+        if err != 0:
+            raise RuntimeError(f"bsc_round_after_gather failed ({err})")
+        return self.W_ring[o[0]], o[1]
 
     SPEC_SLOTS = 3
 
@@ -582,10 +582,12 @@ class NativeSecAgg:
             return out
         return wait
 
-    def audit(self):
-        """Queue the aggregate audit on main; returns the callable giving ok int32 [1, nchunks]."""
-        _check(hip().bsc_round_audit(self.ctx, _ptr(self.coeffs), _ptr(self.cs), _ptr(self.ok), self.h_ok.data_ptr()),
-               "round_audit")
+    def audit(self, queue: bool = True):
+        """Queue the aggregate audit on main (queue=False: a fused call queued it already); returns the
+        callable giving ok int32 [1, nchunks]."""
+        if queue:
+            _check(hip().bsc_round_audit(self.ctx, _ptr(self.coeffs), _ptr(self.cs), _ptr(self.ok),
+                                         self.h_ok.data_ptr()), "round_audit")
 
         def result():
             _check(hip().bsc_round_wait(self.ctx, 1), "round_wait")

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from ..native import hip
-from ..utils import d2h_into, pinned
+from ..utils import pinned
 from ..utils import streams as S
 
 PHILOX_M0, PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
@@ -518,10 +518,12 @@ def gram_adopt(pre: dict, gathered: torch.Tensor) -> None:
 
 
 def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accept: int, need: int, lead_rank,
-                               cap: int, on_accept=None):
+                               cap: int, on_accept=None, flags=None):
     """Noise-aware committee Krum, phase 2: the noised rows x_a = delta_a + mean_s sc[a, s] t_{nz[a, s]}
     are never materialised -- their inner products are assembled from the phase-1 Gram.  nz int32 /
-    sc fp32 [U1, nn] (nz indexes the stacked noise rows); the rest as krum_committee_async."""
+    sc fp32 [U1, nn] (nz indexes the stacked noise rows); the rest as krum_committee_async.  The vote kernel
+    writes its verdicts straight into the pinned read-back buffer; flags = (amap, alive): it also sets the
+    speculative share MSM's row flags from the block mask (alive[i] = node[amap[i]])."""
     U1, U = pre["U1"], pre["U"]
     V, n = inbox.shape
     nn = nz.shape[1]
@@ -547,12 +549,13 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
     out = torch.empty((V * n + U1,), dtype=torch.int32, device=dev)
     acc, node = out[: V * n], out[V * n:]
     ws = torch.empty((U1,), dtype=torch.int32, device=dev) if (U1 > 1024 or n > 256) else None
-    _check(hip().bsc_krum_committee_noise(_p(pre["gram"]), U1, U, _p(nz.contiguous()), _p(sc.contiguous()), nn,
-                                          _p(inbox.contiguous()), V, n, groupsize, n_accept, need,
-                                          _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _p(ws),
-                                          _stream()), "krum_committee_noise")
     host = pinned("krum_noise", out.shape, torch.int32)
-    d2h_into(host, out)
+    amap, alive = flags if flags is not None else (None, None)
+    _check(hip().bsc_krum_committee_noise2(_p(pre["gram"]), U1, U, _p(nz.contiguous()), _p(sc.contiguous()), nn,
+                                           _p(inbox.contiguous()), V, n, groupsize, n_accept, need,
+                                           _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _p(ws),
+                                           host.data_ptr(), _p(amap), alive.numel() if alive is not None else 0,
+                                           _p(alive), _stream()), "krum_committee_noise")
     ev = S.record()
     if on_accept is not None:
         on_accept(node)

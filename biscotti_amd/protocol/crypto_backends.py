@@ -170,7 +170,7 @@ class DeviceCrypto:
         chunked: the per-chunk commitments C_k (the commitment lanes of the share MSM) are computed
         first and kept (pending.ccom [n, nch, 1, 24], ready at pending.ccom_event): the full
         commitment is their sum, and the aggregate audit sums them over the kept rows long before the
-        share MSM ends (NativeSecAgg.csum_early)."""
+        share MSM ends (the early audit sums of NativeSecAgg.after_select)."""
         n = qdelta.shape[0]
         if n == 0:
             return _Ready(np.zeros((0, 64), np.uint8))

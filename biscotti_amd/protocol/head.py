@@ -240,23 +240,10 @@ class RoundHeadMixin:
         adopts them if that block carries W (same device tensor) and discards them otherwise.  Every rank
         queues it at the same point (the recovery is replicated), so the Gram's gather lines up."""
         main, gs = S.current(), self.gram_stream
-        if self._native is not None and type(self.task).__name__ == "SoftmaxTask" and self.cfg.audit_aggregate:
-            # step + chunk commitments (+ one rank: the Krum Gram) in one native call (resident output ring)
-            nk = self._noise_krum()
-            single = self.comm.world == 1
-            with S.use(gs):
-                cnt = K._tile_counters(self.dev, 1024)
-            out = self._native.prestep(self.task, W, it, gs, self.noise_rows.rows(it) if nk and single else None, cnt)
-            if nk and single:
-                out["gram"]["xrow"] = self.flat
-            elif nk:
-                # several ranks: the deltas' all_gather and this rank's share of the Gram's tiles, on the Gram
-                # stream behind the step (every rank queues this at the same point)
-                with S.use(gs):
-                    g = self._gram_rows(out["delta"], None, it)
-                    g["ev"] = S.record()
-                out["gram"] = g
-            return out
+        if self._native_prestep_ok():
+            # step + chunk commitments (+ one rank: the Krum Gram) in one native call (resident slot ring)
+            out = self._native.prestep(W, it, do_gram=self._noise_krum() and self.comm.world == 1)
+            return self._finish_pre(out, it)
         S.wait(gs, main)
         with S.use(gs):
             delta, qdelta = self.task.step(W, it, list(self.local))
@@ -271,6 +258,36 @@ class RoundHeadMixin:
             # before the noisers are drawn, and the main stream's evaluation does not wait for it
             with S.use(gs):
                 g = self._gram_rows(delta, None, it)
+                g["ev"] = S.record()
+            out["gram"] = g
+        return out
+
+    def _native_prestep_ok(self) -> bool:
+        """The pre-step runs natively (NativeSecAgg: softmax task, aggregate audit on); the task and the slot
+        ring are bound at the first use."""
+        na = self._native
+        if na is None or type(self.task).__name__ != "SoftmaxTask" or not self.cfg.audit_aggregate:
+            return False
+        if na.task is None:
+            gs = self.gram_stream
+            with S.use(gs):
+                cnt = K._tile_counters(self.dev, 1024)
+            nk = self._noise_krum() and self.comm.world == 1
+            na.bind_task(self.task, gs, self.noise_rows.table if nk else None, cnt)
+        return True
+
+    def _finish_pre(self, out: dict, it: int) -> dict:
+        """A native pre-step's Gram: one rank -- computed in the call (its row map added here); several ranks --
+        the deltas' all_gather and this rank's share of the Gram's tiles, on the Gram stream behind the step
+        (every rank gets here at the same point of the round)."""
+        if not self._noise_krum():
+            out.pop("gram", None)
+            return out
+        if self.comm.world == 1:
+            out["gram"]["xrow"] = self.flat
+        else:
+            with S.use(self.gram_stream):
+                g = self._gram_rows(out["delta"], None, it)
                 g["ev"] = S.record()
             out["gram"] = g
         return out
@@ -310,7 +327,7 @@ class RoundHeadMixin:
         if not spec_workers:
             return
         side = self.side_stream
-        # the audit's commitment sums come from the pre-step's chunk commitments (NativeSecAgg.csum_early):
+        # the audit's commitment sums come from the pre-step's chunk commitments (the early audit sums of NativeSecAgg.after_select):
         # the MSM then computes the witness lanes only
         no_commit = getattr(pre["commits"], "ccom", None) is not None and cfg.kzg_audit == "off"
         rows = [w - self.lo for w in spec_workers]

@@ -58,7 +58,9 @@ class SecAggMixin:
         return contributing, part
 
     def _spec_aggregate(self, spec, pred, node) -> dict:
-        """Queue the secure aggregation of the rows the committee's selection kept -- masked share-value
+        """Python path (host crypto, the KZG audit's per-rank inputs) of the device-selection aggregation; GPU
+        rounds otherwise take _spec_aggregate_native.  Queue the secure aggregation of the rows the committee's
+        selection kept -- masked share-value
         sums, the cross-rank combination, exact recovery (main stream), the audit's commitment sums +
         check (side stream), the witness sums (background stream) -- right behind the selection
         kernels, before the host has read the selection.  Every rank queues it at the same point (the
@@ -68,23 +70,13 @@ class SecAggMixin:
         contributing, part = pred
         sp = spec[1] if spec is not None else None
         pts = ys = alive = None
-        early_cs = False
         if sp is not None:
             sp.launch()
             pts, ys, alive = sp.pts, sp.ys, sp.alive
-            cfg = self.cfg
-            pc = getattr(self, "_cur_commits", None)
-            if self._native is not None and cfg.audit_aggregate and cfg.kzg_audit == "off" and pc is not None \
-                    and getattr(pc, "ccom", None) is not None and pc.src is sp.qdelta:
-                # the audit's commitment sums from the pre-step's chunk commitments, queued before main waits
-                # for the MSM: they run while the MSM is still busy, not after it
-                # on the (high-priority, otherwise idle) upload stream: the side stream still runs the MSM
-                self._native.csum_early(pc.ccom, pc.ccom_event, sp.rows_t, alive, self.upload_stream)
-                early_cs = True
-            elif sp.no_commit and cfg.audit_aggregate:
+            if sp.no_commit and self.cfg.audit_aggregate:
                 raise RuntimeError("speculative MSM without commitment slots but no chunk commitments to audit with")
             S.current().wait_event(sp.ev)          # the MSM's shares
-        agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration), early_cs=early_cs)
+        agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration))
         agg["contributing"], agg["part"], agg["accepted"], agg["node"] = list(contributing), dict(part), None, node
         return agg
 
@@ -109,12 +101,15 @@ class SecAggMixin:
             offs = np.cumsum([0] + [len(x) for x in parts])
             A_dev = h2d(wts["A"].reshape(-1), torch.int64, self.dev)
             sl = [idx[offs[i]:offs[i + 1]] for i in range(5)]
-            hit = (sl[:4], (ycols - 10).tolist(), (wts, A_dev, sl[4]))
+            # the native round calls know the layout by an id (its columns, weights and outputs registered once)
+            lid = self._native.add_layout(sl[0], sl[1], sl[2], sl[3], wts, A_dev, sl[4]) \
+                if self._native is not None else None
+            hit = (sl[:4], (ycols - 10).tolist(), (wts, A_dev, sl[4]), lid)
             if len(self._agg_idx) < 256:
                 self._agg_idx[key] = hit
         return hit
 
-    def _aggregate(self, pts, ys, rowsel, contributing, part, now, early_cs: bool = False) -> dict:
+    def _aggregate(self, pts, ys, rowsel, contributing, part, now) -> dict:
         """Secure aggregation of this rank's kept rows, combined over ranks, then exact recovery.
 
         Every miner sums the shares it received (aggregateSecret, kyber.go:244-287) and the leader
@@ -130,14 +125,7 @@ class SecAggMixin:
         T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
         audit = cfg.audit_aggregate
         kzg = cfg.kzg_audit != "off"
-        if self._native is not None and not isinstance(rowsel, list) and not kzg:
-            # the device-selection path (replicated on every rank, so every rank takes this branch together:
-            # the collective below lines up); a rank without local rows adds zero partials
-            if comm.world > 1:
-                return self._aggregate_native_multi(pts, ys, rowsel, contributing, part, now, early_cs)
-            if pts is not None:
-                return self._aggregate_native(pts, ys, rowsel, contributing, part, now, early_cs)
-        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
+        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev), _ = self._agg_index(contributing, part)
         kzg_in = None   # this rank's (commitment sums, witness sums, share sums) for the KZG audit
         main = S.current() if self.gpu else None
         single = comm.world == 1
@@ -230,46 +218,50 @@ class SecAggMixin:
                 out["kzg_events"] = [S.record(main), S.record(self.side_stream), S.record(self.bg_stream)]
         return out
 
-    def _aggregate_native(self, pts, ys, mask, contributing, part, now, early_cs: bool = False) -> dict:
-        """_aggregate's one-rank device path in two native calls (kernels/round.hip): the miners' sums, the
-        recovery and its read-back, then -- after the next round's pre-step is queued on the Gram stream
-        -- the aggregate audit.  Same kernels, same streams, same order as the Python path."""
-        cfg = self.cfg
-        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
-        na = self._native
-        W_new, coeffs, status, agg = na.secagg(pts.contiguous(), ys.contiguous(), mask, ccols, wcols, ycols_t, xs_t,
-                                               wts, A_dev, basis_dev, self.W,
-                                               (2 if early_cs else 1) if cfg.audit_aggregate else 0)
-        S.hold(pts, ys, mask)   # read on the side and background streams
-        readback = na.readback()
-        if self._pipelined() and getattr(self.task, "stateless_step", False):
-            self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)
-        audit_ok = na.audit() if cfg.audit_aggregate else None
-        return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
-                "clock": None, "now": now, "readback": readback}
-
-    def _aggregate_native_multi(self, pts, ys, mask, contributing, part, now, early_cs: bool = False) -> dict:
-        """_aggregate on several ranks (one per GPU) in two native calls around ONE all_gather of packed
-        rows (kernels/round.hip): this rank's partial share / commitment sums of its kept rows and its
-        clock straight into its send row, the collective on the main stream, then the ranks' totals, the
-        exact recovery and its read-back; the audit as on one rank."""
-        cfg, comm = self.cfg, self.comm
-        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev) = self._agg_index(contributing, part)
-        na = self._native
-        send, recv = na.gather_buffers(comm.world)
-        audit = (2 if early_cs else 1) if cfg.audit_aggregate else 0
-        if pts is not None:
-            pts, ys = pts.contiguous(), ys.contiguous()
-            S.hold(pts, ys, mask)   # read on the side and background streams
-        na.partials(pts, ys, mask, ccols, wcols, now, audit)
-        comm.all_gather_into(recv, send)
-        W_new, coeffs, status, agg = na.combine(ycols_t, xs_t, wts, A_dev, basis_dev, self.W, audit)
-        readback = na.readback(clocks=True)
-        if self._pipelined() and getattr(self.task, "stateless_step", False):
-            self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)
-        audit_ok = na.audit() if cfg.audit_aggregate else None
-        return {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
-                "clock": True, "now": now, "readback": readback}
+    def _spec_aggregate_native(self, sp, pred, node, amap, flags_set: bool = False) -> dict:
+        """_spec_aggregate through the fused native calls (kernels/round.hip): one rank -- ONE call queues the
+        speculative rows' flags, the early audit sums, the miners' sums + exact recovery + read-back, the next
+        round's pre-step and the audit; several ranks -- one call up to this rank's partial sums in the packed
+        send row, the all_gather (main stream), one call for the totals, recovery, read-back, pre-step and
+        audit.  Same kernels, streams and order as the Python path it replaces."""
+        cfg, comm, na = self.cfg, self.comm, self._native
+        contributing, part = pred
+        _, xs_list, _, lid = self._agg_index(contributing, part)
+        audit = 1 if cfg.audit_aggregate else 0
+        early = -1
+        if sp is not None:
+            sp.launch()
+            pc = getattr(self, "_cur_commits", None)
+            if audit and pc is not None and getattr(pc, "slot", None) is not None and pc.src is sp.qdelta:
+                early, audit = pc.slot, 2   # the audit's sums from the pre-step's chunk commitments, early
+            elif sp.no_commit and audit:
+                raise RuntimeError("speculative MSM without commitment slots but no chunk commitments to audit with")
+        nxt = self.fsm.iteration + 1            # fsm: the round being aggregated
+        want_pre = self._pipelined() and getattr(self.task, "stateless_step", False)
+        native_pre = want_pre and self._native_prestep_ok()
+        now = self._now(self.fsm.iteration)
+        sel = None if flags_set else node   # None: the vote kernel has set the rows' flags already
+        if comm.world == 1:
+            W_new, pre = na.after_select(sel, amap, sp, early, self.upload_stream, lid, self.W, audit,
+                                         nxt if native_pre else -1, audit_now=not (want_pre and not native_pre))
+            readback, clock = na.readback(), None
+        else:
+            na.select_partials(sel, amap, sp, early, self.upload_stream, lid, now, audit)
+            comm.all_gather_into(na.recv, na.send)
+            W_new, k = na.after_gather(lid, self.W, audit, nxt if native_pre else -1,
+                                       audit_now=not (want_pre and not native_pre))
+            pre = self._finish_pre(na._pre_out(k, W_new, nxt), nxt) if k >= 0 else None
+            readback, clock = na.readback(clocks=True), True
+        if pre is not None:
+            if comm.world == 1:
+                pre = self._finish_pre(pre, nxt)
+            self._pre = pre
+        elif want_pre:
+            self._pre = self._queue_pre_step(W_new, nxt)
+        audit_ok = na.audit(queue=want_pre and not native_pre) if audit else None
+        return {"W_new": W_new, "status": na.status, "agg": na.layout_agg(lid), "xs": list(xs_list),
+                "audit_ok": audit_ok, "clock": clock, "now": now, "readback": readback,
+                "contributing": list(contributing), "part": dict(part), "accepted": None, "node": node}
 
     # ------------------------------------------------------------------ read-backs and the audit
     def _d2h_async(self, *ts: torch.Tensor):

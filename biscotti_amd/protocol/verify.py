@@ -163,12 +163,13 @@ class VerifyMixin:
         U = X.shape[0] if X is not None else pre["U1"]
         st = static if static is not None and static["U"] == U else self._krum_static(xrow, U, plan, live, inboxes, spec)
         n, clip, need, cap = st["n"], st["clip"], st["need"], st["cap"]
-        on_accept = self._on_accept(spec, st["amap"], plan, live, box)
+        on_accept, flags = self._on_accept(spec, st["amap"], plan, live, box)
         if pre is not None:
             if "ev" in pre and self.gpu:   # produced on the Gram stream
                 S.current().wait_event(pre["ev"])
+            box["flags_set"] = flags is not None
             return K.krum_committee_noise_async(pre, nz, sc, st["inbox"], n - clip, n - clip, need, st["rank"], cap,
-                                                on_accept=on_accept)
+                                                on_accept=on_accept, flags=flags)
         return K.krum_committee_async(X, st["inbox"], n - clip, n - clip, need, st["rank"], cap, on_accept=on_accept)
 
     def _on_accept(self, spec, amap_t, plan, live, box):
@@ -176,18 +177,27 @@ class VerifyMixin:
         leader's block mask (rows outside it are cancelled) and the aggregation of the kept rows is
         queued -- on EVERY rank, with or without local rows, so the aggregation's collective lines up;
         its handle lands in box['sa'].  amap_t: device int32 [n speculative rows], speculative row -> Krum
-        row (-1: dropped)."""
+        row (-1: dropped).  Returns (on_accept, flags): flags = (amap, alive) when the selection kernel
+        itself should set the rows' flags (the fused native path), else None."""
         sp = spec[1] if spec is not None else None
         pred = self._predict_miners(plan, live) if self.gpu and self.cfg.secure_agg else None
+        # the fused native path (one call behind the selection) takes every device-selection round it can
+        fused = pred is not None and self._native is not None and self.cfg.kzg_audit == "off" and \
+            (sp is not None or self.comm.world > 1)
 
         def on_accept(node):
             with self.timer.phase("verify.queue_agg"):
+                if fused:
+                    box["sa"] = self._spec_aggregate_native(sp, pred, node, amap_t, box.get("flags_set", False))
+                    return
                 if sp is not None:
                     B.set_alive(node, amap_t, sp.alive)
                     sp.launch()   # no-op when the MSM already runs speculatively
                 if pred is not None:
                     box["sa"] = self._spec_aggregate(spec, pred, node)
-        return on_accept
+        # the fused path lets the noise-aware Krum's vote kernel set the speculative rows' flags itself
+        flags = (amap_t, sp.alive) if fused and sp is not None and amap_t is not None else None
+        return on_accept, flags
 
     def _verify(self, X: torch.Tensor, inbox: list, it: int, verifier: int) -> list[bool]:
         """One verifier's decision on its inbox rows X: RONI (VerifyUpdateRONI, main.go:191-233) or a

@@ -114,25 +114,30 @@ def test_rank_failure_restarts_from_chain_file(tmp_path):
 
 
 def test_native_secagg_model_ring_never_aliases_the_live_model():
-    """NativeSecAgg's recovered-model ring: aggregates computed and then dropped (speculative misses,
-    failed audits, empty blocks) keep the engine's W unchanged for several rounds; the next model must never
-    land in W's buffer nor in one of the last two results (a queued pre-step may still read it)."""
-    import torch
+    """NativeSecAgg's recovered-model ring (kernels/round.hip bsc_ring_pick, host code: runs without a GPU):
+    aggregates computed and then dropped (speculative misses, failed audits, empty blocks) keep the engine's W
+    unchanged for several rounds; the next model must never land in W's buffer nor in one of the last two
+    results (a queued pre-step may still read it)."""
+    import ctypes
 
-    from biscotti_amd.ops.bn256 import NativeSecAgg
+    from biscotti_amd.native import hip
 
-    na = object.__new__(NativeSecAgg)
-    na.W_ring = [torch.zeros(4, dtype=torch.float64) for _ in range(NativeSecAgg.W_RING)]
-    na.k, na._recent = 0, []
-    W = na.W_ring[1]                # the live model sits in a ring slot (adopted earlier)
+    lib = hip()
+    ring = (ctypes.c_void_p * 4)(0x1000, 0x2000, 0x3000, 0x4000)
+    k, recent = ctypes.c_int(0), (ctypes.c_void_p * 2)()
+
+    def pick(W):
+        j = lib.bsc_ring_pick(ring, 4, ctypes.byref(k), W, recent)
+        assert j >= 0
+        return ring[j]
+    W = ring[1]                       # the live model sits in a ring slot (adopted earlier)
     last = []
-    for _ in range(12):             # twelve dropped aggregates in a row
-        out = na._next_W(W)
-        assert out.data_ptr() != W.data_ptr()
-        assert out.data_ptr() not in last[-2:]
-        last.append(out.data_ptr())
-    W = na._next_W(W)               # adopted: becomes the live model
+    for _ in range(12):               # twelve dropped aggregates in a row
+        out = pick(W)
+        assert out != W and out not in last[-2:]
+        last.append(out)
+    W = pick(W)                       # adopted: becomes the live model
     for _ in range(6):
-        out = na._next_W(W)
-        assert out.data_ptr() != W.data_ptr()
+        out = pick(W)
+        assert out != W
         W = out

@@ -26,15 +26,15 @@ def _run_exact(eng, rounds=4):
         return d, q
     eng.task.step = spy
     if eng._native is not None:
-        # the one-rank pre-step runs natively (NativeSecAgg.prestep): record its quantised updates too
-        pre_fn = eng._native.prestep
+        # the pre-step runs natively (NativeSecAgg.prestep / after_select): record its quantised updates too
+        pre_fn = eng._native._pre_out
 
-        def pre_spy(task, W, it, *a, **kw):
-            out = pre_fn(task, W, it, *a, **kw)
+        def pre_spy(k, W, it):
+            out = pre_fn(k, W, it)
             torch.cuda.current_stream().wait_event(out["ev"])   # the step runs on the Gram stream
-            seen.update({(it, p): out["qdelta"][i].clone() for i, p in enumerate(task.peers)})
+            seen.update({(it, p): out["qdelta"][i].clone() for i, p in enumerate(eng.task.peers)})
             return out
-        eng._native.prestep = pre_spy
+        eng._native._pre_out = pre_spy
     res = []
     for _ in range(rounds):
         W0 = eng.W.clone()
