@@ -1,10 +1,10 @@
-# Same-box A/B of the working tree (new) against exp/base (a copy of the last commit's package, built
+# Same-box A/B of the working tree (new) against ab_base (scripts/make_ab_base.sh: a copy of an earlier commit's package, built
 # libraries included): driver-style benches, alternating order per repetition, then one long run each.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out
 R=$PWD
 run() {  # $1 = variant, $2 = steps, $3 = warmup, $4 = tag
-  if [ $1 = base ]; then D=$R/exp/base; else D=$R; fi
+  if [ $1 = base ]; then D=$R/ab_base; else D=$R; fi
   (cd $D && timeout -k 10 300 python bench.py --steps $2 --warmup $3) > gpurun_out/abt_$1_$4.txt 2>&1 || { echo "FAIL $1 $4"; tail -5 gpurun_out/abt_$1_$4.txt; return 1; }
   grep '^{' gpurun_out/abt_$1_$4.txt | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); p=d['phase_ms_per_round']; print('$1 $4', round(d['ms_per_step'],3), 'drain', round(d.get('drain_ms',0),2), 'rb', round(p['recover.readback'],3), 'audit', round(p['recover.audit'],3), 'idle', round(p.get('recover.idle',0),3), 'qa', round(p['verify.queue_agg'],3), 'pv', round(p['pre_vrf'],3))"
 }

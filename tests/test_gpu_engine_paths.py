@@ -190,8 +190,10 @@ def test_mnist_label_flip_rejection_floor_default_noise():
     eng = _engine(num_nodes=100, poisoning=0.3, epsilon=1.0, seed=7)
     pois = {p for p in range(100) if eng.fsm.is_poisoner(p)}
     seen = kept = 0
+    attack = []
     for _ in range(30):
         r = eng.run_round()
+        attack.append(r.attack_rate)
         if r.iteration < 10:
             continue
         judged = set().union(*r.inboxes.values()) if r.inboxes else set()
@@ -202,3 +204,10 @@ def test_mnist_label_flip_rejection_floor_default_noise():
     assert ok, why
     assert seen > 0
     assert kept <= 0.25 * seen, (kept, seen)
+    # the attack's effect (get17AttackRate: digit-1 error) over rounds 20-29, next to the rejection floor
+    last10 = sum(attack[-10:]) / 10
+    print("digit-1 error, rounds 20-29:", round(last10, 4), "rejection", round(1 - kept / seen, 4))
+    assert last10 <= DIGIT1_ERR_CEILING, last10
+
+
+DIGIT1_ERR_CEILING = 0.75   # this deterministic run measures 0.647 (rejection 0.756), docs/ROBUSTNESS.md
