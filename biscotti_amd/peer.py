@@ -17,6 +17,11 @@ injects such a crash deterministically.
 At exit rank 0 prints the chain with PrintChain's format (blockchain.go:43-54) to stdout, which
 is what localTest.sh compares between peers.
 
+``--rpc-peer`` (with ``-i k -t N`` and a ``-f`` peers file, or local ports 8000+i) runs the reference's own
+deployment instead: this process is ONE peer that exchanges every protocol message with the others over Go
+net/rpc + gob (protocol/rpcpeer.py: noise requests, VerifyUpdateKRUM, RegisterSecret, the leader's GetUpdateList /
+GetMinerPart and RegisterBlock flooding) -- no collective group, so it can run among reference peers.
+
 Talking to peers outside the job (reference peers included) uses the reference's own transport, Go
 net/rpc + gob (parallel/netrpc.py): ``--rpc-listen HOST:PORT`` serves the ``Peer`` RPC methods on
 rank 0 over the job's chain (RegisterPeer hands it to joiners, RegisterBlock accepts extensions,
@@ -41,11 +46,15 @@ def main(argv=None) -> int:
     ap.add_argument("--print-chain", default="rank0", choices=["rank0", "all", "none"])
     ap.add_argument("--rpc-listen", default=None, help="HOST:PORT: serve the Peer net/rpc methods (rank 0)")
     ap.add_argument("--rpc-flood", default="", help="comma list of HOST:PORT peers that receive every block")
+    ap.add_argument("--rpc-peer", action="store_true",
+                    help="run as one peer over net/rpc (the reference's deployment; needs -i and -t)")
     ns = ap.parse_args(argv)
     cfg = config_from_args(ns)
     if cfg.num_nodes <= 0 or not cfg.dataset:
         ap.print_usage()
         return 1
+    if ns.rpc_peer:
+        return _rpc_peer_main(cfg, ns)
     if "WORLD_SIZE" not in os.environ and cfg.node_index >= 0:
         # one process per peer (reference deployment)
         os.environ["WORLD_SIZE"] = str(cfg.num_nodes)
@@ -104,6 +113,36 @@ def main(argv=None) -> int:
     comm.barrier()
     eng.close()
     comm.shutdown()
+    return 0
+
+
+def _rpc_peer_main(cfg, ns) -> int:
+    """One peer of a net/rpc deployment (DistSys/main.go: a process per peer, addresses from the peers file or
+    127.0.0.1:8000+i): runs --rounds rounds, prints the chain (PrintChain) like localTest.sh compares."""
+    import dataclasses
+
+    from .protocol.rpcpeer import RpcPeer
+
+    if cfg.node_index < 0:
+        raise SystemExit("--rpc-peer needs -i <index>")
+    if cfg.peers_file:
+        with open(cfg.peers_file) as f:
+            addrs = [ln.strip() for ln in f if ln.strip()][: cfg.num_nodes]
+    else:
+        addrs = [f"127.0.0.1:{8000 + i}" for i in range(cfg.num_nodes)]
+    cfg = dataclasses.replace(cfg, device="cpu")
+    peer = RpcPeer(cfg, cfg.node_index, addrs, timeout_s=cfg.comm_timeout_s if cfg.comm_timeout_s < 300 else 30.0)
+    try:
+        import time
+
+        time.sleep(1.0)   # every peer's server is up before the first round's messages (announceToNetwork)
+        for _ in range(ns.rounds or cfg.max_iterations):
+            peer.run_round()
+        if ns.print_chain != "none":
+            sys.stdout.write(peer.fsm.chain.print_chain())
+            sys.stdout.flush()
+    finally:
+        peer.close()
     return 0
 
 
