@@ -15,6 +15,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "wave_prio.h"
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -65,7 +67,12 @@ constexpr int SM_THREADS = 256;
 extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
     const float* X, const int* y, const long long* off, const int* ntrain, const int* pid, const double* W, int D_IN,
     int D_OUT, int B, int P, unsigned long long seed, int iteration, float max_norm, double qscale, float* delta,
-    long long* qdelta, float* loss, int lo) {
+    long long* qdelta, float* loss, int lo, int* ones, int nones) {
+  BSC_SET_PRIO(BSC_PRIO_AHEAD);
+  // ones (optional): the next speculative MSM's row flags, set to 1 here (the MSM waits for this step anyway)
+  // instead of by an upload or a kernel of their own in front of the MSM
+  if (ones != nullptr && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < nones; i += blockDim.x) ones[i] = 1;
   __shared__ float xs[16 * SM_MAXK];  // minibatch rows, transformed; rows >= B are zero
   __shared__ float red[4][16][16];    // per-wave partial logits
   __shared__ float G[16][16];         // (softmax - onehot) / B
@@ -472,6 +479,7 @@ __device__ __forceinline__ double gram_at(const double* gram, int T, int a, int 
 extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, int U, int D, int kchunk, int T,
                                                               double* part, double* gram, unsigned int* count,
                                                               const float* X2, int U1, long long stride2, int pair0) {
+  BSC_SET_PRIO(BSC_PRIO_AHEAD);
   __shared__ double red[4][256];
   __shared__ unsigned int last;
   // this launch covers the tile pairs [pair0, pair0 + gridDim.x) (several ranks split one Gram); part and
@@ -606,6 +614,7 @@ extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise(const double
                                                                    const int* inbox, int n, int groupsize,
                                                                    double* scores) {
   __shared__ double row[256];
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ double kept[256];
   __shared__ double xaa;
   const int i = blockIdx.x, v = blockIdx.y, t = threadIdx.x;
@@ -642,6 +651,7 @@ extern "C" __global__ void __launch_bounds__(1024) k_krum_vote(const double* sco
                                                               int n_accept, int U, int need, const int* lead_rank,
                                                               int cap, int* acc, int* node, int* h_acc, int* h_node,
                                                               const int* amap, int nspec, int* alive) {
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ int sigs[1024];
   __shared__ int appr[1024];
   __shared__ int lr[1024];
@@ -993,6 +1003,7 @@ extern "C" __global__ void __launch_bounds__(256) k_eval_error(const float* X, c
 extern "C" __global__ void __launch_bounds__(256) k_eval_error_t(const float* Xt, const int* y, int N, int KG, int D_IN,
                                                                 int D_OUT, const double* W, int split,
                                                                 unsigned int* err) {
+  BSC_SET_PRIO(BSC_PRIO_AHEAD);
   // 4 waves per tile split the K loop (latency: the evaluation is read one round later and must be done by
   // then under the share MSM's load), then reduce the logits through LDS
   __shared__ float red[4][4][64];
@@ -1167,6 +1178,7 @@ extern "C" __global__ void __launch_bounds__(256) k_recover_w(
     const long long* A, const int* basis, int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi,
     int d, const double* W, double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out,
     double* h_W, int* h_status) {
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ long long agg[RW_CPB][RW_MAXP];
   __shared__ __int128 cf[RW_CPB][RW_MAXC];
   __shared__ int ok[RW_CPB];
@@ -1280,15 +1292,23 @@ extern "C" int bsc_sum_rows_i64(const long long* ys, int R, long long C, const i
   return (int)hipGetLastError();
 }
 
+extern "C" int bsc_softmax_step_ones(const float* X, const int* y, const long long* off, const int* ntrain,
+                                     const int* pid, const double* W, int D_IN, int D_OUT, int B, int P,
+                                     unsigned long long seed, int iteration, float max_norm, double qscale, float* delta,
+                                     long long* qdelta, float* loss, int lo, int* ones, int nones, void* stream) {
+  if (D_IN <= 0 || D_OUT > 16 || B > 16) return -1;
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(k_softmax_step, dim3(P), dim3(SM_THREADS), 0, (hipStream_t)stream, X, y, off, ntrain, pid, W, D_IN,
+                     D_OUT, B, P, seed, iteration, max_norm, qscale, delta, qdelta, loss, lo, ones, nones);
+  return (int)hipGetLastError();
+}
+
 extern "C" int bsc_softmax_step(const float* X, const int* y, const long long* off, const int* ntrain,
                                 const int* pid, const double* W, int D_IN, int D_OUT, int B, int P, unsigned long long seed,
                                 int iteration, float max_norm, double qscale, float* delta, long long* qdelta,
                                 float* loss, int lo, void* stream) {
-  if (D_IN <= 0 || D_OUT > 16 || B > 16) return -1;
-  if (P <= 0) return 0;
-  hipLaunchKernelGGL(k_softmax_step, dim3(P), dim3(SM_THREADS), 0, (hipStream_t)stream, X, y, off, ntrain, pid, W, D_IN,
-                     D_OUT, B, P, seed, iteration, max_norm, qscale, delta, qdelta, loss, lo);
-  return (int)hipGetLastError();
+  return bsc_softmax_step_ones(X, y, off, ntrain, pid, W, D_IN, D_OUT, B, P, seed, iteration, max_norm, qscale, delta,
+                               qdelta, loss, lo, nullptr, 0, stream);
 }
 
 extern "C" int bsc_logreg_step(const double* X, const double* y, const long long* off, const int* nrows,

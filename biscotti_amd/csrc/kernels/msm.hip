@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "bn256_dev.h"
+#include "wave_prio.h"
 
 using namespace bn;
 
@@ -188,11 +189,32 @@ extern "C" __global__ void __launch_bounds__(64) k_fb_table(const uint32_t* base
 // share values only -- slot T is left untouched (the caller has the chunk commitments already), so a
 // group is T lanes instead of T+1 and no wave runs the commitment lane's extra c_0 addition.
 // out_y: int64 [nrows][nchunks][T].
-extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
-    const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
-    int poly, int T, int B0, int NW, int commit_only, const int* alive, const int* compact, int group_rows,
-    uint32_t* out_pts, long long* out_y) {
+// The row list comes from device memory (rows) or from the kernel's argument block (RowArg, <= ROWARG_MAX
+// rows): the speculative MSM is launched the moment its rows are known, with no upload in front of it.
+#define ROWARG_MAX 248
+struct RowArg {
+  int r[ROWARG_MAX];
+};
+struct RowsPtr {
+  const int* p;
+  __device__ __forceinline__ int operator[](int i) const { return p[i]; }
+};
+struct RowsArg {
+  const RowArg* a;
+  __device__ __forceinline__ int operator[](int i) const { return a->r[i]; }
+};
+
+template <class Rows>
+__device__ __forceinline__ void shares_msm_body(const long long* coeffs, int d, Rows rows, int nrows,
+                                                const uint32_t* tbl_pk, const uint32_t* tbl_wb, int poly, int T,
+                                                int B0, int NW, int commit_only, const int* alive,
+                                                const int* compact, int group_rows, uint32_t* out_pts,
+                                                long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
+  // both share MSMs of a round end on its critical path: the speculative one gates the recovery, the pre-step's
+  // commitment MSM (commit_only == 1) the block build (the block carries the commitments); the commitment MSM is
+  // latency-bound (one lane per (row, chunk), ~1 wave per SIMD) and, launched first, wins the age tie-break
+  BSC_SET_PRIO(BSC_PRIO_SPEC);
   const int S = commit_only == 1 ? 1 : T + 1;   // output slots per (row, chunk)
   const int SL = commit_only == 2 ? T : S;      // lanes per (row, chunk)
   // compact (optional): [count, row...] -- only the listed rows are computed, packed densely over the
@@ -278,6 +300,22 @@ extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
     for (int j = L - 1; j >= 0; --j) y = y * (unsigned long long)x + (unsigned long long)c[j];
     out_y[((size_t)r * nchunks + k) * T + slot] = (long long)y;
   }
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_shares_msm(
+    const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
+    int poly, int T, int B0, int NW, int commit_only, const int* alive, const int* compact, int group_rows,
+    uint32_t* out_pts, long long* out_y) {
+  shares_msm_body(coeffs, d, RowsPtr{rows}, nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, compact,
+                  group_rows, out_pts, out_y);
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_shares_msm_ka(
+    const long long* coeffs, int d, RowArg rows, int nrows, const uint32_t* tbl_pk, const uint32_t* tbl_wb,
+    int poly, int T, int B0, int NW, int commit_only, const int* alive, int group_rows, uint32_t* out_pts,
+    long long* out_y) {
+  shares_msm_body(coeffs, d, RowsArg{&rows}, nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, nullptr,
+                  group_rows, out_pts, out_y);
 }
 
 // ------------------------------------------------------------------ full-vector commitments
@@ -396,6 +434,7 @@ extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* 
                                                               const uint32_t* tbl_pk, int B0, int NW,
                                                               const uint32_t* csum, int nm, int nch, int* ok,
                                                               int* h_ok) {
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ uint32_t sh[64 * 24];
   __shared__ int dig[16][9];      // signed digit of (coefficient j, window w); NW <= 9 (bsc_chunk_check)
   __shared__ uint32_t items[16 * 9];   // nonzero digits: table entry | sign bit
@@ -486,6 +525,7 @@ extern "C" __global__ void __launch_bounds__(128) k_sum_rows(const uint32_t* pts
 extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
                                                              int nrows, const int* cols, int ncols,
                                                              const int* row_mask, int mask_by_pos, uint32_t* out) {
+  if (mask_by_pos) BSC_SET_PRIO(BSC_PRIO_AHEAD);   // the early commitment sums; witness sums stay background
   // 16 columns x 16 row lanes per block: each lane's serial chain is nrows/16 additions, then a
   // 4-level LDS tree (the sums sit on the round's critical path: latency, not throughput, matters)
   __shared__ uint32_t sh[16][16][24];
@@ -519,6 +559,7 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
 // per group, LDS tree.  Used for the full commitment = sum of chunk commitments.
 extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* pts, int n, int stride, int off,
                                                                uint32_t* out, uint32_t* hout) {
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);   // the full commitments: the round's block build waits for them (a latency chain)
   __shared__ uint32_t sh[256 * 24];
   const int g = blockIdx.x;
   jac acc = jac_inf();
@@ -627,6 +668,23 @@ extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, i
   return (int)hipGetLastError();
 }
 
+// rows_host: n <= ROWARG_MAX row indices (host memory), passed by value in the kernel's arguments
+extern "C" int bsc_shares_msm_ka(const long long* coeffs, int d, const int* rows_host, int nrows, const uint32_t* tbl_pk,
+                                 const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
+                                 const int* alive, int group_rows, uint32_t* out_pts, long long* out_y, void* stream) {
+  if (B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65) return -1;
+  if (commit_only < 0 || commit_only > 2 || nrows > ROWARG_MAX || nrows < 0) return -1;
+  const int nchunks = (d + poly - 1) / poly;
+  const int SL = commit_only == 1 ? 1 : commit_only == 2 ? T : T + 1;
+  const long long n = (long long)nrows * nchunks * SL;
+  if (n <= 0) return 0;
+  RowArg ra;
+  for (int i = 0; i < nrows; ++i) ra.r[i] = rows_host[i];
+  hipLaunchKernelGGL(k_shares_msm_ka, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, coeffs, d, ra,
+                     nrows, tbl_pk, tbl_wb, poly, T, B0, NW, commit_only, alive, group_rows, out_pts, out_y);
+  return (int)hipGetLastError();
+}
+
 // compact = [count, r0, r1, ...]: the rows r with alive[r] != 0, ascending (one block, n <= 4096)
 extern "C" __global__ void __launch_bounds__(1024) k_alive_compact(const int* alive, int n, int* compact) {
   __shared__ int cnt[1024];
@@ -662,6 +720,7 @@ extern "C" int bsc_alive_compact(const int* alive, int n, int* compact, void* st
 // selection -- e.g. a peer the pre-step computed that turned out not to be a worker -- and is dropped).
 // Device-scope stores: a share MSM still running on another stream skips the rows cleared here.
 extern "C" __global__ void k_set_alive(const int* accept, const int* src, int n, int* alive) {
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int j = src[i];

@@ -5,7 +5,7 @@
 // bsc_round_secagg  -- the miners' sums and the leader's recovery (aggregateSecret + recoverSecret,
 //                      DistSys/kyber.go:244-287,809-857) for the rows the selection kept:
 //                        side: chunk-commitment sums of the kept rows (the audit's input)
-//                        bg:   witness sums (no consumer on the protocol path)
+//                        wit:  witness sums (no consumer on the protocol path; own low-priority stream)
 //                        main: fused share sums + exact recovery + W update (k_recover_w), then the
 //                              read-back of (status, W_new) into pinned memory, event `readback`
 // bsc_round_audit   -- verifyCommitment on the aggregate (kyber.go:564-577): main waits for the side
@@ -46,10 +46,14 @@ extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, i
                               const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
                               const int* alive, const int* compact, int group_rows, uint32_t* out_pts,
                               long long* out_y, void* stream);
-extern "C" int bsc_softmax_step(const float* X, const int* y, const long long* off, const int* ntrain,
-                                const int* pid, const double* W, int D_IN, int D_OUT, int B, int P, unsigned long long seed,
-                                int iteration, float max_norm, double qscale, float* delta, long long* qdelta,
-                                float* loss, int lo, void* stream);
+extern "C" int bsc_softmax_step_ones(const float* X, const int* y, const long long* off, const int* ntrain,
+                                     const int* pid, const double* W, int D_IN, int D_OUT, int B, int P,
+                                     unsigned long long seed, int iteration, float max_norm, double qscale, float* delta,
+                                     long long* qdelta, float* loss, int lo, int* ones, int nones, void* stream);
+extern "C" int bsc_shares_msm_ka(const long long* coeffs, int d, const int* rows_host, int nrows, const uint32_t* tbl_pk,
+                                 const uint32_t* tbl_wb, int poly, int T, int B0, int NW, int commit_only,
+                                 const int* alive, int group_rows, uint32_t* out_pts, long long* out_y, void* stream);
+#define ROWARG_MAX 248   // msm.hip: rows passed in the MSM kernel's arguments
 extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
                                 double* part, double* gram, unsigned int* count, void* stream);
 extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
@@ -96,6 +100,7 @@ struct TaskCfg {  // the softmax task's resident data and the pre-step's constan
 };
 struct RoundCtx {
   hipStream_t main, side, bg;
+  hipStream_t wit;   // the miners' witness sums (no consumer in the round; default: bg)
   hipEvent_t ev_main, ev_side, ev_readback, ev_audit, ev_pre;
   const uint32_t* tbl_pk;
   int d, poly, T, nch, b0, nw;
@@ -113,12 +118,34 @@ struct RoundCtx {
   PreSlot pre[8];
   int npre = 0, pre_k = 0;
   TaskCfg task;
+  // the speculative MSM's output ring (bsc_round_set_spec_ring): per slot the rows' flags (cap entries), an
+  // event on the background stream after the slot's last reader (the witness sums), whether the next
+  // pre-step has set the flags already; spec_k = the slot of the last launch
+  int* spec_alive[8];
+  hipEvent_t spec_done[8];
+  bool spec_used[8], spec_filled[8];
+  int nspec = 0, spec_cap = 0, spec_k = -1;
 };
 #define RC_CHECK(x)                        \
   do {                                     \
     const int e_ = (int)(x);               \
     if (e_ != 0) return e_;                \
   } while (0)
+// the speculative slot whose flags `mask` is (-1: not a speculative slot's)
+static int spec_slot_of(const RoundCtx* c, const int* mask) {
+  for (int i = 0; i < c->nspec; ++i)
+    if (c->spec_alive[i] == mask) return i;
+  return -1;
+}
+// after the witness sums over a speculative slot: the slot's last reader is queued (witness stream)
+static int spec_mark_read(RoundCtx* c, const int* mask) {
+  const int s = spec_slot_of(c, mask);
+  if (s >= 0) {
+    RC_CHECK(hipEventRecord(c->spec_done[s], c->wit));
+    c->spec_used[s] = true;
+  }
+  return 0;
+}
 }  // namespace
 
 extern "C" void* bsc_round_create(void* main, void* side, void* bg, const uint32_t* tbl_pk, int d, int poly, int T,
@@ -127,6 +154,7 @@ extern "C" void* bsc_round_create(void* main, void* side, void* bg, const uint32
   c->main = (hipStream_t)main;
   c->side = (hipStream_t)side;
   c->bg = (hipStream_t)bg;
+  c->wit = c->bg;
   c->tbl_pk = tbl_pk;
   c->d = d;
   c->poly = poly;
@@ -144,6 +172,15 @@ extern "C" void* bsc_round_create(void* main, void* side, void* bg, const uint32
   return c;
 }
 
+// The witness sums' own stream: on the background stream they queued the pre-step's commitments -- which the
+// round's block carries -- behind ~0.5 ms of low-priority sums (the block build then waited for them).
+extern "C" int bsc_round_set_witness_stream(void* ctx, void* stream) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || stream == nullptr) return -1;
+  c->wit = (hipStream_t)stream;
+  return 0;
+}
+
 extern "C" void bsc_round_destroy(void* ctx) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return;
@@ -152,6 +189,7 @@ extern "C" void bsc_round_destroy(void* ctx) {
   hipEventDestroy(c->ev_readback);
   hipEventDestroy(c->ev_audit);
   hipEventDestroy(c->ev_pre);
+  for (int i = 0; i < c->nspec; ++i) hipEventDestroy(c->spec_done[i]);
   delete c;
 }
 
@@ -176,8 +214,9 @@ extern "C" int bsc_round_secagg(void* ctx, const uint32_t* pts, int R, const lon
     RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, ccols, c->nch, mask, cs, c->side));
     RC_CHECK(hipEventRecord(c->ev_side, c->side));
   }
-  RC_CHECK(hipStreamWaitEvent(c->bg, c->ev_main, 0));
-  RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->bg));
+  RC_CHECK(hipStreamWaitEvent(c->wit, c->ev_main, 0));
+  RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->wit));
+  RC_CHECK(spec_mark_read(c, mask));
   // the recovery writes (status, W_new) into the pinned read-back buffers itself: no copies behind it
   RC_CHECK(bsc_recover_w_strided(ys, R, (long long)c->nch * c->T, c->nch, c->T, mask, ycols, xs, npts, A, basis,
                                  c->poly, shift, inv_lo, inv_hi, c->d, W, c->qscale, W_new, coeffs, status, agg, h_W,
@@ -216,29 +255,60 @@ extern "C" int bsc_round_csum_early(void* ctx, const uint32_t* ccom, void* ev_cc
   return 0;
 }
 
-// The next round's speculative share MSM (head.py _spec_head_launch) in one call: the side stream waits for
-// the pre-step (ev_wait: its quantised updates), uploads the row list and the all-ones alive flags from
-// pinned staging (host [2n] int32: rows, then ones) into rows_dev [2n], and runs the MSM over them into
-// resident pts / ys.  The caller rotates staging / device buffers over enough slots that a slot is
-// rewritten only after its MSM and every consumer of its outputs are done.
-// The upload goes through `up` (a high-priority stream on every CU, event ev_up): on the CU-masked, low-
-// priority side stream the copy kernel waited ~150 us for a free slot behind the pre-step's MSM.
-extern "C" int bsc_round_spec_msm(void* ctx, void* ev_wait, const long long* coeffs, const int* rows_host,
-                                  int* rows_dev, int n, const uint32_t* tbl_wb, int commit_only, int group_rows,
-                                  uint32_t* pts, long long* ys, void* up, void* ev_up) {
+// The speculative MSM's slot ring: nslots slots whose row flags are alive[k] (cap entries each).  Registered
+// once; the pre-steps then set the next slot's flags to 1 inside the local step (which the MSM waits for).
+extern "C" int bsc_round_set_spec_ring(void* ctx, int* const* alive, int nslots, int cap) {
   RoundCtx* c = (RoundCtx*)ctx;
-  if (c == nullptr || n <= 0) return -1;
-  if (ev_wait != nullptr) RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_wait, 0));
-  if (up != nullptr && ev_up != nullptr) {
-    RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, (hipStream_t)up));
-    RC_CHECK(hipEventRecord((hipEvent_t)ev_up, (hipStream_t)up));
-    RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_up, 0));
-  } else {
-    RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, 2 * (size_t)n * sizeof(int), hipMemcpyHostToDevice, c->side));
+  if (c == nullptr || nslots < 3 || nslots > 8 || cap <= 0) return -1;
+  for (int i = 0; i < c->nspec; ++i) hipEventDestroy(c->spec_done[i]);
+  c->nspec = 0;
+  for (int i = 0; i < nslots; ++i) {
+    c->spec_alive[i] = alive[i];
+    RC_CHECK(hipEventCreateWithFlags(&c->spec_done[i], hipEventDisableTiming));
+    c->spec_used[i] = c->spec_filled[i] = false;
+    c->nspec = i + 1;
   }
-  RC_CHECK(bsc_shares_msm(coeffs, c->d, rows_dev, n, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, commit_only,
-                          rows_dev + n, nullptr, group_rows, pts, ys, c->side));
+  c->spec_cap = cap;
+  c->spec_k = -1;
   return 0;
+}
+
+// The next round's speculative share MSM (head.py _spec_head_launch) into ring slot `slot` (which must be the
+// next one): the side stream waits for the pre-step (ev_wait: its quantised updates) and for the slot's last
+// reader, sets the slot's flags unless a pre-step did, and runs the MSM over rows_host (pinned, n rows) into
+// pts / ys.  Up to ROWARG_MAX rows travel in the kernel's arguments, so nothing stands between the launch and
+// the MSM (an upload's copy kernel waited 20-120 us for a CU slot behind the round's work); the device copy
+// of the row list (rows_dev: the early audit sums read it) then goes up on `up` (high priority; event ev_up),
+// which is also where those sums run.  More rows: the copy first, and the MSM reads rows_dev.
+extern "C" int bsc_round_spec_msm2(void* ctx, int slot, void* ev_wait, const long long* coeffs, const int* rows_host,
+                                   int n, const uint32_t* tbl_wb, int commit_only, int group_rows, uint32_t* pts,
+                                   long long* ys, int* rows_dev, void* up, void* ev_up, void* ev_flags) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || n <= 0 || c->nspec == 0 || n > c->spec_cap || up == nullptr || ev_up == nullptr ||
+      ev_flags == nullptr)
+    return -1;
+  if (slot != (c->spec_k + 1) % c->nspec) return -5;
+  c->spec_k = slot;
+  int* alive = c->spec_alive[slot];
+  hipStream_t st = (hipStream_t)up;
+  if (ev_wait != nullptr) RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_wait, 0));
+  if (c->spec_used[slot]) RC_CHECK(hipStreamWaitEvent(c->side, c->spec_done[slot], 0));
+  if (!c->spec_filled[slot]) RC_CHECK(hipMemsetD32Async((hipDeviceptr_t)alive, 1, (size_t)n, c->side));
+  c->spec_filled[slot] = false;
+  // the flags are set from here on: the selection's writes to them (main) wait for this
+  RC_CHECK(hipEventRecord((hipEvent_t)ev_flags, c->side));
+  if (n <= ROWARG_MAX) {
+    RC_CHECK(bsc_shares_msm_ka(coeffs, c->d, rows_host, n, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, commit_only,
+                               alive, group_rows, pts, ys, c->side));
+    RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
+    RC_CHECK(hipEventRecord((hipEvent_t)ev_up, st));
+    return 0;
+  }
+  RC_CHECK(hipMemcpyAsync(rows_dev, rows_host, (size_t)n * sizeof(int), hipMemcpyHostToDevice, st));
+  RC_CHECK(hipEventRecord((hipEvent_t)ev_up, st));
+  RC_CHECK(hipStreamWaitEvent(c->side, (hipEvent_t)ev_up, 0));
+  return bsc_shares_msm(coeffs, c->d, rows_dev, n, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw, commit_only, alive,
+                        nullptr, group_rows, pts, ys, c->side);
 }
 
 // The next round's pre-step (head.py _queue_pre_step) in one call, queued behind everything on main so far
@@ -249,23 +319,20 @@ extern "C" int bsc_round_spec_msm(void* ctx, void* ev_wait, const long long* coe
 //   background:  behind the step, the per-chunk commitments of every row (ccom, event ev_ccom), their
 //                per-row sums = the full commitments (jac), read back into pinned jac_host, event ev_commit
 // Outputs are resident (the caller rotates them over slots); events are caller-owned and re-recorded.
-extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, const int* y, const long long* off,
-                                 const int* ntrain, const int* pid, const double* W, int d_in, int d_out, int B, int P,
-                                 unsigned long long seed, int iteration, float max_norm, double qscale, int lo,
-                                 float* delta, long long* qdelta, float* loss, const uint32_t* tbl_wb,
-                                 const int* rows_arange, uint32_t* ccom, uint32_t* jac, uint32_t* jac_host,
-                                 int do_gram, const float* T_rows, int U2, long long stride2, int kchunk, double* part,
-                                 double* gram, unsigned int* counters, void* ev_step, void* ev_ccom, void* ev_commit,
-                                 void* ev_gram, int chunked, void* commit_stream) {
-  RoundCtx* c = (RoundCtx*)ctx;
+static int prestep_impl(RoundCtx* c, hipStream_t gs, const float* X, const int* y, const long long* off,
+                        const int* ntrain, const int* pid, const double* W, int d_in, int d_out, int B, int P,
+                        unsigned long long seed, int iteration, float max_norm, double qscale, int lo, float* delta,
+                        long long* qdelta, float* loss, const uint32_t* tbl_wb, const int* rows_arange, uint32_t* ccom,
+                        uint32_t* jac, uint32_t* jac_host, int do_gram, const float* T_rows, int U2, long long stride2,
+                        int kchunk, double* part, double* gram, unsigned int* counters, void* ev_step, void* ev_ccom,
+                        void* ev_commit, void* ev_gram, int chunked, hipStream_t cst, int* ones, int nones,
+                        hipEvent_t ones_wait) {
   if (c == nullptr || P <= 0 || d_in * d_out + d_out != c->d) return -1;
-  hipStream_t gs = (hipStream_t)gram_stream;
-  // the commitments' stream (default: background; an A/B passes one masked to the CUs the MSM leaves)
-  hipStream_t cst = commit_stream != nullptr ? (hipStream_t)commit_stream : c->bg;
   RC_CHECK(hipEventRecord(c->ev_pre, c->main));
   RC_CHECK(hipStreamWaitEvent(gs, c->ev_pre, 0));
-  RC_CHECK(bsc_softmax_step(X, y, off, ntrain, pid, W, d_in, d_out, B, P, seed, iteration, max_norm, qscale, delta,
-                            qdelta, loss, lo, gs));
+  if (ones_wait != nullptr) RC_CHECK(hipStreamWaitEvent(gs, ones_wait, 0));
+  RC_CHECK(bsc_softmax_step_ones(X, y, off, ntrain, pid, W, d_in, d_out, B, P, seed, iteration, max_norm, qscale, delta,
+                                 qdelta, loss, lo, ones, nones, gs));
   RC_CHECK(hipEventRecord((hipEvent_t)ev_step, gs));
   RC_CHECK(hipStreamWaitEvent(cst, (hipEvent_t)ev_step, 0));
   if (chunked) {
@@ -283,6 +350,24 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
     RC_CHECK(hipEventRecord((hipEvent_t)ev_gram, gs));
   }
   return 0;
+}
+
+extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, const int* y, const long long* off,
+                                 const int* ntrain, const int* pid, const double* W, int d_in, int d_out, int B, int P,
+                                 unsigned long long seed, int iteration, float max_norm, double qscale, int lo,
+                                 float* delta, long long* qdelta, float* loss, const uint32_t* tbl_wb,
+                                 const int* rows_arange, uint32_t* ccom, uint32_t* jac, uint32_t* jac_host,
+                                 int do_gram, const float* T_rows, int U2, long long stride2, int kchunk, double* part,
+                                 double* gram, unsigned int* counters, void* ev_step, void* ev_ccom, void* ev_commit,
+                                 void* ev_gram, int chunked, void* commit_stream) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr) return -1;
+  // the commitments' stream (default: background; an A/B passes one masked to the CUs the MSM leaves)
+  hipStream_t cst = commit_stream != nullptr ? (hipStream_t)commit_stream : c->bg;
+  return prestep_impl(c, (hipStream_t)gram_stream, X, y, off, ntrain, pid, W, d_in, d_out, B, P, seed, iteration,
+                      max_norm, qscale, lo, delta, qdelta, loss, tbl_wb, rows_arange, ccom, jac, jac_host, do_gram,
+                      T_rows, U2, stride2, kchunk, part, gram, counters, ev_step, ev_ccom, ev_commit, ev_gram, chunked,
+                      cst, nullptr, 0, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -324,8 +409,9 @@ extern "C" int bsc_round_partials(void* ctx, const uint32_t* pts, int R, const l
       RC_CHECK(hipEventRecord(c->ev_side, c->side));
     }
     if (nwc > 0 && ws != nullptr) {
-      RC_CHECK(hipStreamWaitEvent(c->bg, c->ev_main, 0));
-      RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->bg));
+      RC_CHECK(hipStreamWaitEvent(c->wit, c->ev_main, 0));
+      RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->wit));
+      RC_CHECK(spec_mark_read(c, mask));
     }
     RC_CHECK(bsc_sum_rows_i64(ys, R, (long long)nch * T, nullptr, R, mask, ys_slot, c->main));
   } else {
@@ -497,10 +583,20 @@ extern "C" int bsc_round_prestep_slot(void* ctx, const double* W, int it, int do
   const TaskCfg& t = c->task;
   const bool g = do_gram && t.noise != nullptr;
   const float* rows = g ? t.noise + (size_t)(it % 100) * c->d : nullptr;
-  RC_CHECK(bsc_round_prestep(ctx, t.gram, t.X, t.y, t.off, t.ntrain, t.pid, W, t.d_in, t.d_out, t.B, t.P, t.seed, it,
-                             t.max_norm, t.qs, t.lo, p.delta, p.qdelta, p.loss, t.tbl_wb, t.rows_arange, p.ccom, p.jac,
-                             p.jac_host, g ? 1 : 0, rows, g ? t.noise_n : 0, 100ll * c->d, t.kchunk, p.part, p.gram,
-                             t.counters, p.ev_step, p.ev_ccom, p.ev_commit, p.ev_gram, 1, nullptr));
+  // the next speculative slot's flags are set inside the step (after the slot's last reader)
+  int* ones = nullptr;
+  hipEvent_t ones_wait = nullptr;
+  if (c->nspec > 0) {
+    const int ns = (c->spec_k + 1) % c->nspec;
+    ones = c->spec_alive[ns];
+    ones_wait = c->spec_used[ns] ? c->spec_done[ns] : nullptr;
+    c->spec_filled[ns] = true;
+  }
+  RC_CHECK(prestep_impl(c, t.gram, t.X, t.y, t.off, t.ntrain, t.pid, W, t.d_in, t.d_out, t.B, t.P, t.seed, it,
+                        t.max_norm, t.qs, t.lo, p.delta, p.qdelta, p.loss, t.tbl_wb, t.rows_arange, p.ccom, p.jac,
+                        p.jac_host, g ? 1 : 0, rows, g ? t.noise_n : 0, 100ll * c->d, t.kchunk, p.part, p.gram,
+                        t.counters, p.ev_step, p.ev_ccom, p.ev_commit, p.ev_gram, 1, c->bg, ones, c->spec_cap,
+                        ones_wait));
   return c->pre_k;
 }
 

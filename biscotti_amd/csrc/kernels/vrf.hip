@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "wave_prio.h"
+
 namespace {
 
 __constant__ static const unsigned long long K512[80] = {
@@ -548,7 +550,12 @@ extern "C" __global__ void __launch_bounds__(192) k_vrf_prove(const uint32_t* __
                                                              const uint8_t* __restrict__ alphas,
                                                              const int* __restrict__ alpha_idx, int alpha_len, int n,
                                                              const uint32_t* __restrict__ btab, uint32_t* scratch,
-                                                             uint8_t* __restrict__ pi, uint8_t* __restrict__ beta) {
+                                                             uint8_t* __restrict__ pi, uint8_t* __restrict__ beta,
+                                                             int urgent) {
+  // a batch of rounds' proofs nothing reads fills the issue slots the round's kernels leave (priority 0); the
+  // run's final flush is what the run's end waits for (urgent: highest priority -- at 0 or 1 it ran ~2x
+  // longer under the share MSMs, drain 0.9 -> 1.9 ms)
+  if (urgent) BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ int s_ok[VTRY][VP];          // phase 1: counter j of proof p decoded
   __shared__ int s_win[VP];               // the winning counter slot (-1: none yet)
   __shared__ uint32_t s_h[VP][20];        // decoded H (affine x, y) of the winner
@@ -766,36 +773,19 @@ extern "C" __global__ void __launch_bounds__(192) k_vrf_prove(const uint32_t* __
   }
 }
 
-extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
-                             int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
-                             void* stream);
-
-extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
-                             int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
-                             void* stream);
-
-// One round's proofs in one call (per-round launches, ops/vrf.py): the staging words [key rows (n) | zeros
-// (n) | the 32-byte message (8 words)] go up from pinned memory, the prover runs, `ev` is recorded -- a
-// resident slot per call, no allocation, ~10 us of the caller's time instead of a Python launch path.
-extern "C" int bsc_vrf_prove_round(const uint32_t* keys, const int* staging_host, int* staging_dev, int n,
-                                   const uint32_t* btab, uint32_t* scratch, uint8_t* pi, void* stream, void* ev) {
+// urgent != 0: the run's end waits for these proofs (highest wave priority)
+extern "C" int bsc_vrf_prove_p(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
+                               int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi,
+                               uint8_t* beta, int urgent, void* stream) {
   if (n <= 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  if (hipMemcpyAsync(staging_dev, staging_host, (2 * (size_t)n + 8) * sizeof(int), hipMemcpyHostToDevice, st) !=
-      hipSuccess)
-    return -1;
-  const int rc = bsc_vrf_prove(keys, staging_dev, (const uint8_t*)(staging_dev + 2 * n), staging_dev + n, 32, n, btab,
-                               scratch, pi, nullptr, stream);
-  if (rc != 0) return rc;
-  return ev != nullptr ? (int)hipEventRecord((hipEvent_t)ev, st) : 0;
+  if (alpha_len < 0 || alpha_len > 1024) return -1;
+  hipLaunchKernelGGL(k_vrf_prove, dim3((n + VP - 1) / VP), dim3(192), 0, (hipStream_t)stream, keys, key_idx, alphas,
+                     alpha_idx, alpha_len, n, btab, scratch, pi, beta, urgent);
+  return (int)hipGetLastError();
 }
 
 extern "C" int bsc_vrf_prove(const uint32_t* keys, const int* key_idx, const uint8_t* alphas, const int* alpha_idx,
                              int alpha_len, int n, const uint32_t* btab, uint32_t* scratch, uint8_t* pi, uint8_t* beta,
                              void* stream) {
-  if (n <= 0) return 0;
-  if (alpha_len < 0 || alpha_len > 1024) return -1;
-  hipLaunchKernelGGL(k_vrf_prove, dim3((n + VP - 1) / VP), dim3(192), 0, (hipStream_t)stream, keys, key_idx, alphas,
-                     alpha_idx, alpha_len, n, btab, scratch, pi, beta);
-  return (int)hipGetLastError();
+  return bsc_vrf_prove_p(keys, key_idx, alphas, alpha_idx, alpha_len, n, btab, scratch, pi, beta, 0, stream);
 }

@@ -1237,8 +1237,9 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       .def("make_secagg_block", [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w,
                                    std::vector<i64> nodes, std::vector<py::bytes> comms, i64 now) {
         std::vector<Bytes> cs;
+        cs.reserve(comms.size());
         for (auto& c : comms) cs.push_back(B(c));
-        return f.make_secagg_block(std::vector<double>(w.data(), w.data() + w.size()), nodes, cs, now);
+        return f.make_secagg_block(w.data(), size_t(w.size()), nodes, std::move(cs), now);
       })
       .def("make_plain_block", [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w,
                                   const std::vector<Update>& ups, i64 now) {

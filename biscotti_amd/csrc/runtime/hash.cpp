@@ -95,7 +95,17 @@ void Sha256::block(const u8* p) {
 
 void Sha256::update(const u8* p, size_t n) {
   total += n;
-  if (blen == 0 && n >= 64 && have_sha_ni()) {  // whole blocks straight from the input
+  if (blen > 0 && blen + n >= 64) {   // complete the buffered block first
+    const size_t take = 64 - blen;
+    memcpy(buf + blen, p, take);
+    block(buf);
+    blen = 0;
+    p += take;
+    n -= take;
+  }
+  if (blen == 0 && n >= 64 && have_sha_ni()) {  // then whole blocks straight from the input, in one call
+    // (a block hash's input starts with 42 bytes of hash + timestamp, so the ~75 KB of gob behind them
+    // would otherwise go block by block through the buffer: one state load / shuffle / store per 64 bytes)
     const size_t nb = n / 64;
     sha256_ni_blocks(h, p, nb);
     p += nb * 64;

@@ -188,13 +188,66 @@ Bytes gob_encode_blockdata(const BlockData& d) {
   return out;
 }
 
+// bytes put_f64s writes for the values of v (the count excluded)
+static size_t f64s_payload_len(const std::vector<double>& v) {
+  size_t n = 0;
+  for (double x : v) {
+    u64 bits;
+    memcpy(&bits, &x, 8);
+    const u64 r = __builtin_bswap64(bits);
+    n += r < 128 ? 1 : size_t(9 - (__builtin_clzll(r) >> 3));
+  }
+  return n;
+}
+
 // ------------------------------------------------------------------ Block
+// sha256(prev_hash || timestamp || gob(data)) -- the same bytes as hashing gob_encode_blockdata(data), but
+// the ~70 KB of GlobalW values are encoded straight into the hash in L1-sized pieces (no message buffer):
+// the gob message's length prefix comes from a length pass over the values.  The block hash sits on the
+// round's host path between the recovery's read-back and the next round's speculative launch.
 Bytes Block::compute_hash() const {
   Sha256 s;
   s.update(prev_hash);
   std::string ts = std::to_string(timestamp);
   s.update(reinterpret_cast<const u8*>(ts.data()), ts.size());
-  s.update(gob_encode_blockdata(data));
+  const BlockData& d = data;
+  Bytes head, tail;   // the message payload = head | GlobalW values | tail
+  head.reserve(32);
+  int last = -1;
+  auto field = [&](Bytes& p, int idx) { gob_put_uint(p, u64(idx - last)); last = idx; };
+  gob_put_int(head, T_BLOCKDATA);
+  if (d.iteration != 0) { field(head, 0); gob_put_int(head, d.iteration); }
+  size_t wlen = 0;
+  if (!d.global_w.empty()) {
+    field(head, 1);
+    gob_put_uint(head, d.global_w.size());
+    wlen = f64s_payload_len(d.global_w);
+  }
+  if (!d.deltas.empty()) {
+    field(tail, 2);
+    gob_put_uint(tail, d.deltas.size());
+    for (auto& u : d.deltas) encode_update(tail, u);
+  }
+  gob_put_uint(tail, 0);
+  s.update(gob_type_prefix());
+  Bytes len;
+  gob_put_uint(len, head.size() + wlen + tail.size());
+  s.update(len);
+  s.update(head);
+  constexpr size_t CH = 448;   // values per piece: <= 448 * 9 bytes, plus the 8-byte store's slack
+  u8 buf[CH * 9 + 8];
+  const size_t nw = d.global_w.size();
+  for (size_t i = 0; i < nw; i += CH) {
+    u8* o = buf;
+    const size_t e = std::min(nw, i + CH);
+    for (size_t k = i; k < e; ++k) {
+      u64 bits;
+      memcpy(&bits, &d.global_w[k], 8);
+      o = gob_uint_raw(o, __builtin_bswap64(bits));
+    }
+    s.update(buf, size_t(o - buf));
+  }
+  s.update(tail);
   Bytes out(32);
   s.final(out.data());
   return out;
@@ -304,11 +357,14 @@ Blockchain Blockchain::with_genesis(size_t nf) {
   return c;
 }
 Block Blockchain::make_block(const BlockData& d, const std::map<i64, i64>& stake, i64 now_unix) const {
+  return make_block(BlockData(d), std::map<i64, i64>(stake), now_unix);
+}
+Block Blockchain::make_block(BlockData&& d, std::map<i64, i64>&& stake, i64 now_unix) const {
   Block b;
   b.timestamp = d.deltas.empty() ? 0 : now_unix;
-  b.data = d;
+  b.data = std::move(d);
   b.prev_hash = latest().hash;
-  b.stake = stake;
+  b.stake = std::move(stake);
   b.set_hash();
   return b;
 }

@@ -63,6 +63,7 @@ struct Blockchain {
   static Block genesis(size_t num_features);
   // NewBlock semantics: timestamp 0 for empty blocks, else `now_unix` (block.go:30-44)
   Block make_block(const BlockData& d, const std::map<i64, i64>& stake, i64 now_unix) const;
+  Block make_block(BlockData&& d, std::map<i64, i64>&& stake, i64 now_unix) const;   // no copies
   const Block& latest() const { return blocks.back(); }
   // getBlock(iteration) (blockchain.go:77-96): index iteration+1 if present
   const Block* get(i64 iteration) const;

@@ -337,20 +337,28 @@ std::map<i64, std::vector<i64>> RoundFSM::route_updates(const std::vector<i64>& 
 
 Block RoundFSM::make_secagg_block(const std::vector<double>& new_w, const std::vector<i64>& node_list,
                                   const std::vector<Bytes>& commitments, i64 now_unix) {
+  return make_secagg_block(new_w.data(), new_w.size(), node_list, std::vector<Bytes>(commitments), now_unix);
+}
+
+Block RoundFSM::make_secagg_block(const double* new_w, size_t n, const std::vector<i64>& node_list,
+                                  std::vector<Bytes>&& commitments, i64 now_unix) {
   if (commitments.size() != node_list.size()) fail("make_secagg_block: commitments/node_list mismatch");
   BlockData d;
   d.iteration = iteration;
-  d.global_w = node_list.empty() ? chain.latest().data.global_w : new_w;
+  if (node_list.empty())
+    d.global_w = chain.latest().data.global_w;
+  else
+    d.global_w.assign(new_w, new_w + n);
   std::map<i64, i64> st = stake;
+  d.deltas.resize(node_list.size());
   for (size_t k = 0; k < node_list.size(); ++k) {
     st[node_list[k]] += cfg.stake_unit;
-    Update u;
+    Update& u = d.deltas[k];
     u.iteration = iteration;
-    u.commitment = commitments[k];
+    u.commitment = std::move(commitments[k]);
     u.accepted = true;
-    d.deltas.push_back(u);
   }
-  return chain.make_block(d, st, now_unix);
+  return chain.make_block(std::move(d), std::move(st), now_unix);
 }
 
 Block RoundFSM::make_plain_block(const std::vector<double>& new_w, const std::vector<Update>& updates, i64 now_unix) {

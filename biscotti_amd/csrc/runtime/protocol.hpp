@@ -134,6 +134,9 @@ class RoundFSM {
   // Block creation.  Secure-agg: deltas = [{Iteration, Commitment, Accepted}] per node, +stake.
   Block make_secagg_block(const std::vector<double>& new_w, const std::vector<i64>& node_list,
                           const std::vector<Bytes>& commitments, i64 now_unix);
+  // the same from a raw model pointer (the pinned read-back of the recovery): one copy of W, into the block
+  Block make_secagg_block(const double* new_w, size_t n, const std::vector<i64>& node_list,
+                          std::vector<Bytes>&& commitments, i64 now_unix);
   // Plain path (createBlock): full updates, stake +/- per Accepted flag.
   Block make_plain_block(const std::vector<double>& new_w, const std::vector<Update>& updates, i64 now_unix);
   Block make_empty_block();

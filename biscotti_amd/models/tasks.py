@@ -97,6 +97,7 @@ class SoftmaxTask:
         def result():
             err, att = both()
             return {"test_error": err, "attack_rate": att}
+        result.ready = getattr(both, "ready", lambda: True)
         return result
 
     def train_error(self, W: torch.Tensor, peer: int, iteration: int) -> float:

@@ -24,7 +24,9 @@ SIGNATURES = {
     "bsc_sum_rows2": [P, I, P, I, P, I, P, P, P],
     "bsc_sum_rows2_pos": [P, I, P, I, P, I, P, P, P],
     "bsc_round_csum_early": [P, P, P, P, I, P, P, P],
-    "bsc_round_spec_msm": [P, P, P, P, P, I, P, I, I, P, P, P, P],
+    "bsc_round_spec_msm2": [P, I, P, P, P, I, P, I, I, P, P, P, P, P, P],
+    "bsc_round_set_spec_ring": [P, P, I, I],
+    "bsc_round_set_witness_stream": [P, P],
     "bsc_round_prestep": [P, P, P, P, P, P, P, P, I, I, I, I, U64, I, F, D, I, P, P, P, P, P, P, P, P,
                           I, P, I, L, I, P, P, P, P, P, P, P, I, P],
     "bsc_commit_rows": [P, I, P, I, P, I, I, P, P, P],
@@ -37,6 +39,7 @@ SIGNATURES = {
     "bsc_chunk_check": [P, I, I, P, I, I, P, I, I, P, P],
     # vrf.hip
     "bsc_vrf_prove": [P, P, P, P, I, I, P, P, P, P, P],
+    "bsc_vrf_prove_p": [P, P, P, P, I, I, P, P, P, P, I, P],
     # kzg.hip
     "bsc_kzg_blocks": [I, I],
     "bsc_kzg_rlc": [P, P, P, P, I, I, I, P, I, I, U64, P, P, P],

@@ -337,6 +337,7 @@ class NativeSpec:
         self.qdelta, self.rows, self.rows_t, self.alive, self.pts, self.ys = qdelta, rows, rows_t, alive, pts, ys
         self.no_commit, self.deferred = no_commit, False
         self.ev = None
+        self.ev_flags = None   # the rows' flags are set (the selection's writes wait for it)
         self._S = S
 
     def record(self, side) -> None:
@@ -371,13 +372,15 @@ class NativeSecAgg:
     # wait (deferred signing): four slots keep every reader clear of the rewrite
     PRE_SLOTS = 4
 
-    def __init__(self, eng: DeviceCommitEngine, main, side, bg, qscale: float):
+    def __init__(self, eng: DeviceCommitEngine, main, side, bg, qscale: float, witness=None):
         self.eng, dev = eng, eng.device
         d, nch, poly = eng.d, eng.nchunks, eng.poly
         self.ctx = hip().bsc_round_create(main.cuda_stream, side.cuda_stream, bg.cuda_stream, _ptr(eng.tbl_pk), d, poly,
                                           eng.T, eng.b0, eng.nw, float(qscale))
         if not self.ctx:
             raise RuntimeError("bsc_round_create failed")
+        if witness is not None:   # the miners' witness sums off the background stream (its commitments first)
+            _check(hip().bsc_round_set_witness_stream(self.ctx, witness.cuda_stream), "round_set_witness_stream")
         self.W_ring = [torch.empty((d,), dtype=torch.float64, device=dev) for _ in range(self.W_RING)]
         self.coeffs = torch.empty((nch, poly), dtype=torch.int64, device=dev)
         self.status = torch.empty((nch,), dtype=torch.int32, device=dev)
@@ -458,6 +461,7 @@ class NativeSecAgg:
                                              e_commit.cuda_event, e_gram.cuda_event)
             assert k == len(self.slots), "pre-step slot registration out of order"
             self.slots.append(sl)
+        self._spec_ring_for(P)   # every local peer can be a speculative row
         torch.cuda.synchronize(dev)
 
     def _pre_out(self, k: int, W, it: int) -> dict:
@@ -536,40 +540,52 @@ class NativeSecAgg:
         return self.W_ring[o[0]], o[1]
 
     SPEC_SLOTS = 3
+    ROWARG_MAX = 248   # kernels/msm.hip: speculative rows that travel in the MSM kernel's arguments
 
-    def spec_msm(self, qdelta, rows: list, ev_wait, no_commit: bool, group_rows: int, up=None) -> "NativeSpec":
-        """The speculative share MSM of qdelta[rows] on the side stream, behind ev_wait (a torch event: the
-        pre-step), in one native call with resident outputs (a ring of SPEC_SLOTS: a slot is reused three
-        rounds later, long after its round read it).  Returns the handle the engine's aggregation uses
-        (pts, ys, alive, rows_t, ev)."""
-        eng, n = self.eng, len(rows)
+    def _spec_ring_for(self, cap: int) -> dict:
+        """The speculative MSM's resident output ring (SPEC_SLOTS slots of cap rows: shares, share values, the
+        device row list + the rows' flags, pinned row staging), registered with the native context -- from then
+        on each pre-step sets the next slot's flags inside its step."""
         ring = self.__dict__.get("_spec_ring")
-        if ring is None or ring["cap"] < n:
-            cap, dev = max(n, qdelta.shape[0]), eng.device
-            ring = self._spec_ring = {"cap": cap, "k": 0, "slots": [
-                {"pts": torch.empty((cap, eng.nchunks, eng.T + 1, 24), dtype=torch.int32, device=dev),
-                 "ys": torch.empty((cap, eng.nchunks, eng.T), dtype=torch.int64, device=dev),
-                 "rows": torch.empty((2 * cap,), dtype=torch.int32, device=dev),
-                 "host": torch.empty((2 * cap,), dtype=torch.int32, pin_memory=True)}
-                for _ in range(self.SPEC_SLOTS)]}
-        ring["k"] = (ring["k"] + 1) % self.SPEC_SLOTS
-        sl = ring["slots"][ring["k"]]
-        ev_up = None
-        if up is not None:
-            ev_up = sl.get("ev_up")
-            if ev_up is None:
-                ev_up = sl["ev_up"] = torch.cuda.Event()
-                ev_up.record(up)   # materialise the handle (re-recorded natively)
-        h = sl["host"].numpy()
-        h[:n] = rows
-        h[n:2 * n] = 1
+        if ring is not None and ring["cap"] >= cap:
+            return ring
+        import ctypes
+
+        eng, dev = self.eng, self.eng.device
+        ring = self._spec_ring = {"cap": cap, "k": -1, "slots": [
+            {"pts": torch.empty((cap, eng.nchunks, eng.T + 1, 24), dtype=torch.int32, device=dev),
+             "ys": torch.empty((cap, eng.nchunks, eng.T), dtype=torch.int64, device=dev),
+             "rows": torch.empty((2 * cap,), dtype=torch.int32, device=dev),   # [row list | flags]
+             "host": torch.empty((cap,), dtype=torch.int32, pin_memory=True)}
+            for _ in range(self.SPEC_SLOTS)]}
+        alive = (ctypes.c_void_p * self.SPEC_SLOTS)(*[sl["rows"].data_ptr() + 4 * cap for sl in ring["slots"]])
+        _check(hip().bsc_round_set_spec_ring(self.ctx, alive, self.SPEC_SLOTS, cap), "round_set_spec_ring")
+        return ring
+
+    def spec_msm(self, qdelta, rows: list, ev_wait, no_commit: bool, group_rows: int, up) -> "NativeSpec":
+        """The speculative share MSM of qdelta[rows] on the side stream, behind ev_wait (a torch event: the
+        pre-step), in one native call with resident outputs (a ring of SPEC_SLOTS: a slot is rewritten three
+        launches later, after its witness sums -- the native side waits for them).  The row list travels in
+        the kernel's arguments; its device copy (for the early audit sums) goes up on `up`.  Returns the handle
+        the engine's aggregation uses (pts, ys, alive, rows_t, ev)."""
+        eng, n = self.eng, len(rows)
+        ring = self._spec_ring_for(max(n, qdelta.shape[0]))
+        k = ring["k"] = (ring["k"] + 1) % self.SPEC_SLOTS
+        sl, cap = ring["slots"][k], ring["cap"]
+        ev_up, ev_flags = sl.get("ev_up"), sl.get("ev_flags")
+        if ev_up is None:
+            ev_up, ev_flags = sl["ev_up"], sl["ev_flags"] = torch.cuda.Event(), torch.cuda.Event()
+            ev_up.record(up)   # materialise the handles (re-recorded natively)
+            ev_flags.record(up)
+        sl["host"].numpy()[:n] = rows
         pts, ys = sl["pts"][:n], sl["ys"][:n]
-        _check(hip().bsc_round_spec_msm(self.ctx, ev_wait.cuda_event if ev_wait is not None else None,
-                                        _ptr(qdelta), sl["host"].data_ptr(), _ptr(sl["rows"]), n, _ptr(eng.tbl_wb),
-                                        2 if no_commit else 0, int(group_rows), _ptr(pts), _ptr(ys),
-                                        up.cuda_stream if up is not None else None,
-                                        ev_up.cuda_event if ev_up is not None else None), "round_spec_msm")
-        return NativeSpec(qdelta, rows, sl["rows"][:n], sl["rows"][n:2 * n], pts, ys, no_commit)
+        _check(hip().bsc_round_spec_msm2(self.ctx, k, ev_wait.cuda_event if ev_wait is not None else None,
+                                         _ptr(qdelta), sl["host"].data_ptr(), n, _ptr(eng.tbl_wb), 2 if no_commit else 0,
+                                         int(group_rows), _ptr(pts), _ptr(ys), _ptr(sl["rows"]), up.cuda_stream,
+                                         ev_up.cuda_event, ev_flags.cuda_event), "round_spec_msm2")
+        sp = NativeSpec(qdelta, rows, sl["rows"][:n], sl["rows"][cap:cap + n], pts, ys, no_commit)
+        sp.ev_flags = ev_flags
+        return sp
 
     def readback(self, clocks: bool = False):
         """Callable: waits for the recovery's read-back -> [status, W_new(, every rank's clock)] numpy views

@@ -611,6 +611,7 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True, Xt=None)
         S.host_wait(ev)
         e = host.tolist()
         return (e[0] / na if na else 0.0, e[1] / nb if nb else 0.0)
+    result.ready = ev.query   # the read-back has landed (result() will not wait)
     return result
 
 

@@ -58,7 +58,8 @@ class DeviceVrfProver:
         return self._launch(np.asarray(self._rows(seeds), np.int32), list(uniq),
                             np.asarray([uniq[a] for a in alphas], np.int32), beta)
 
-    def _launch(self, rows: np.ndarray, alphas: list, alpha_idx: np.ndarray, beta: bool = False, reuse: bool = False):
+    def _launch(self, rows: np.ndarray, alphas: list, alpha_idx: np.ndarray, beta: bool = False, reuse: bool = False,
+                urgent: bool = False):
         n = int(rows.size)
         if self._keys_dev is None:
             self._keys_dev = self._upload(np.concatenate(self._keys))
@@ -77,9 +78,9 @@ class DeviceVrfProver:
                                      torch.empty((cap, 80), dtype=torch.uint8, device=self.device))
         scratch, pi = buf[0][: max(n, 1)], buf[1][:n]
         bt = torch.empty((n, 64), dtype=torch.uint8, device=self.device) if beta else None
-        err = hip().bsc_vrf_prove(self._keys_dev.data_ptr(), idx.data_ptr(), al.data_ptr(), idx[n:].data_ptr(),
-                                  self.ALPHA_LEN, n, self.btab.data_ptr(), scratch.data_ptr(), pi.data_ptr(),
-                                  bt.data_ptr() if bt is not None else None, S.raw())
+        err = hip().bsc_vrf_prove_p(self._keys_dev.data_ptr(), idx.data_ptr(), al.data_ptr(), idx[n:].data_ptr(),
+                                    self.ALPHA_LEN, n, self.btab.data_ptr(), scratch.data_ptr(), pi.data_ptr(),
+                                    bt.data_ptr() if bt is not None else None, int(urgent), S.raw())
         if err != 0:
             raise RuntimeError(f"HIP launch of vrf_prove failed with hipError {err}")
         self.proofs += n
@@ -111,7 +112,9 @@ class DeviceVrfProver:
         if len(self._queue) >= self.batch_rounds:
             self.flush(stream)
 
-    def flush(self, stream) -> None:
+    def flush(self, stream, urgent: bool = False) -> None:
+        """Launch the queued rounds' proofs.  urgent: the caller's next step waits for them (the run's final
+        flush) -- they run at the highest wave priority instead of filling the round's idle issue slots."""
         if not self._queue:
             return
         q, self._queue = self._queue, []
@@ -128,9 +131,9 @@ class DeviceVrfProver:
                 up = self._upload(buf)
                 scratch = torch.empty((n, 320), dtype=torch.int32, device=self.device)
                 pi = torch.empty((n, 80), dtype=torch.uint8, device=self.device)
-                err = hip().bsc_vrf_prove(self._keys_dev.data_ptr(), up.data_ptr(), up[2 * n:].data_ptr(),
-                                          up[n:].data_ptr(), self.ALPHA_LEN, n, self.btab.data_ptr(),
-                                          scratch.data_ptr(), pi.data_ptr(), None, S.raw())
+                err = hip().bsc_vrf_prove_p(self._keys_dev.data_ptr(), up.data_ptr(), up[2 * n:].data_ptr(),
+                                            up[n:].data_ptr(), self.ALPHA_LEN, n, self.btab.data_ptr(),
+                                            scratch.data_ptr(), pi.data_ptr(), None, int(urgent), S.raw())
                 if err != 0:
                     raise RuntimeError(f"HIP launch of vrf_prove failed with hipError {err}")
                 self.proofs += n
@@ -142,14 +145,14 @@ class DeviceVrfProver:
         rows = np.concatenate([r for r, _ in q])
         alpha_idx = np.repeat(np.arange(len(q), dtype=np.int32), [r.size for r, _ in q])
         with S.use(stream):   # uploads, scratch and the launch all on the prover's stream
-            pi, _ = self._launch(rows, [a for _, a in q], alpha_idx, reuse=True)
+            pi, _ = self._launch(rows, [a for _, a in q], alpha_idx, reuse=True, urgent=urgent)
             ev = S.record(stream)
         self._inflight.append((ev, pi))
         # keep the last few batches alive until their kernels finished (the proofs are discarded)
         self._inflight = [x for x in self._inflight if not x[0].query()] if len(self._inflight) > 2 else self._inflight
 
     def drain(self, stream) -> None:
-        self.flush(stream)
+        self.flush(stream, urgent=True)
         for ev, _ in self._inflight:
             S.host_wait(ev)
         self._inflight = []

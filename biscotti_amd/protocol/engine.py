@@ -147,7 +147,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self._native = None
         if self.gpu:
             self._native = B.NativeSecAgg(self.crypto.eng, self.main_stream, self.side_stream, self.bg_stream,
-                                          10.0 ** cfg.precision)
+                                          10.0 ** cfg.precision, witness=self.witness_stream)
             if self.comm.world > 1:
                 self._native.gather_buffers(self.comm.world)
         if cfg.pkey_file:
@@ -213,8 +213,11 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         lo, hi = torch.cuda.Stream.priority_range()
         self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
         self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, SIDE_STREAM_SKIP_EVERY)
-        # work no consumer in the round waits for (the miners' witness sums, the commitments)
+        # work the round's end waits for at most (the pre-step's commitments: the block carries them)
         self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
+        # work no consumer in the round waits for (the miners' witness sums): on bg they queued the
+        # commitments behind them
+        self.witness_stream = torch.cuda.Stream(device=self.dev, priority=lo)
         # long device work nothing in a round waits for -- the VRF proofs (kernels/vrf.hip) and the KZG
         # audit sums (kernels/kzg.hip) -- gets a stream of its own
         self.vrf_stream = torch.cuda.Stream(device=self.dev, priority=lo)
@@ -254,13 +257,19 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             self.vrf_dev.proofs = 0
 
     # ------------------------------------------------------------------ lifecycle
-    def _resolve_evals(self) -> None:
-        """Read the queued evaluations of earlier rounds (lazy_eval) into their results and log them."""
-        evs, self._evals = self._evals, []
-        for res, f in evs:
+    def _resolve_evals(self, wait: bool = True) -> None:
+        """Read the queued evaluations of earlier rounds (lazy_eval) into their results and log them, in round
+        order.  wait=False: only those whose read-back has landed (the last round's evaluation is queued just
+        before the next round starts; waiting for it there held the round's host thread ~0.13 ms)."""
+        evs = self._evals
+        k = 0
+        while k < len(evs) and (wait or getattr(evs[k][1], "ready", lambda: True)()):
+            res, f = evs[k]
             ev = f()
             res.test_error, res.attack_rate = ev["test_error"], ev["attack_rate"]
             self._log_round(res)
+            k += 1
+        del evs[:k]
 
     def drain(self, final: bool = True) -> None:
         """Join work that belongs to rounds already returned: the last host VRF batch and, when final,
@@ -352,8 +361,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             if head.get("vrf_proofs") is not None:
                 self.vrf_dev.submit(*head["vrf_proofs"], self.vrf_stream)
                 if last or it == cfg.max_iterations - 1:
-                    self.vrf_dev.flush(self.vrf_stream)
-            self._resolve_evals()
+                    self.vrf_dev.flush(self.vrf_stream, urgent=True)   # the run's end waits for these
+            self._resolve_evals(wait=len(self._evals) > 3)   # a bounded backlog: the host rings hold 4
             if krum_pre is not None and cfg.verification and inboxes and cfg.defense == "KRUM":
                 kst = head.get("kst") or self._krum_static(krum_pre["xrow"], krum_pre["U1"], plan, live, inboxes, head["spec"],
                                         head.get("arrivals"))

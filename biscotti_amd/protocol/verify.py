@@ -164,6 +164,9 @@ class VerifyMixin:
         st = static if static is not None and static["U"] == U else self._krum_static(xrow, U, plan, live, inboxes, spec)
         n, clip, need, cap = st["n"], st["clip"], st["need"], st["cap"]
         on_accept, flags = self._on_accept(spec, st["amap"], plan, live, box)
+        if self.gpu and spec is not None and getattr(spec[1], "ev_flags", None) is not None:
+            # the speculative rows' flags are set (side stream) before the selection writes them
+            S.current().wait_event(spec[1].ev_flags)
         if pre is not None:
             if "ev" in pre and self.gpu:   # produced on the Gram stream
                 S.current().wait_event(pre["ev"])

@@ -32,6 +32,13 @@ def main():
               f"{sum(ds[-q:]) / q:8.1f}")
     gaps = [(rec[i + 1]["e"] - rec[i]["e"]) / 1e3 for i in range(len(rec) - 1)]
     print("recovery-to-recovery us:", [round(g) for g in gaps])
+    # per round: every share MSM launched inside it (queue, start after the previous recovery, duration)
+    print("round  wall  share MSMs (queue:start+duration us)")
+    for i in range(len(rec) - 1):
+        t0, t1 = rec[i]["e"], rec[i + 1]["e"]
+        ms = [r for r in rows if r["n"] == "k_shares_msm" and t0 <= r["s"] < t1]
+        print(f"{i + 1:5d} {(t1 - t0) / 1e3:6.0f}  " + " ".join(f"q{r['Queue_Id']}:{(r['s'] - t0) / 1e3:.0f}+{r['d']:.0f}"
+                                                       for r in ms))
     for i in range(a, min(b, len(rec) - 1)):
         t0 = rec[i]["e"]
         print(f"--- round {i + 1} (t=0: end of recovery {i}), next recovery ends at {(rec[i + 1]['e'] - t0) / 1e3:.0f} us")

@@ -46,8 +46,8 @@ def test_host_wait_sleeps_through_long_waits():
         def query(self):
             return time.perf_counter() >= self.t
 
-    ev = Ev(0.06)
     c0, w0 = time.thread_time(), time.perf_counter()
+    ev = Ev(0.06)
     S.host_wait(ev)
     cpu, wall = time.thread_time() - c0, time.perf_counter() - w0
     assert wall >= 0.06 and cpu < 0.3 * wall, (cpu, wall)
