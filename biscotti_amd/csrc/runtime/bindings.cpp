@@ -519,6 +519,35 @@ static py::array_t<int64_t> select_noisers_impl(const std::map<i64, i64>& stake,
   return res;
 }
 
+// Jacobian rows (device layout: [*, 24] Montgomery u32 limbs; rows idx[0..n) of `jac`, or the first n when idx
+// is null) -> 64-byte kyber marshals in `out` [n, 64], with ONE inversion (Montgomery's trick)
+static void marshal_jac_rows(const uint32_t* jac, const int64_t* idx, size_t n, uint8_t* out) {
+  std::vector<G1> pts(n);
+  for (size_t i = 0; i < n; ++i) pts[i] = g1_from_jac_u32(jac + 24 * size_t(idx != nullptr ? idx[i] : int64_t(i)));
+  const MontField& F = Fp();
+  std::vector<U256> pre(n);
+  U256 acc = F.one;
+  for (size_t i = 0; i < n; ++i) {
+    pre[i] = acc;
+    if (!pts[i].is_inf()) F.mul(acc, acc, pts[i].z);
+  }
+  U256 inv;
+  F.inv_mont(inv, acc);
+  std::memset(out, 0, n * 64);
+  for (size_t k = n; k-- > 0;) {
+    if (pts[k].is_inf()) continue;
+    U256 zi, zi2, zi3, ax, ay;
+    F.mul(zi, inv, pre[k]);
+    F.mul(inv, inv, pts[k].z);
+    F.sqr(zi2, zi);
+    F.mul(zi3, zi2, zi);
+    F.mul(ax, pts[k].x, zi2);
+    F.mul(ay, pts[k].y, zi3);
+    F.from_mont(ax).to_be(out + 64 * k);
+    F.from_mont(ay).to_be(out + 64 * k + 32);
+  }
+}
+
 PYBIND11_MODULE(_biscotti_rt, m) {
   m.doc() = "biscotti_amd native host runtime (crypto, ledger, protocol FSM)";
 
@@ -578,30 +607,7 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     if (jac.ndim() != 2 || jac.shape(1) != 24) throw std::runtime_error("expected [n, 24] uint32");
     const size_t n = size_t(jac.shape(0));
     py::array_t<uint8_t> out({py::ssize_t(n), py::ssize_t(64)});
-    std::vector<G1> pts(n);
-    for (size_t i = 0; i < n; ++i) pts[i] = g1_from_jac_u32(jac.data(py::ssize_t(i), 0));
-    const MontField& F = Fp();
-    std::vector<U256> pre(n);
-    U256 acc = F.one;
-    for (size_t i = 0; i < n; ++i) {
-      pre[i] = acc;
-      if (!pts[i].is_inf()) F.mul(acc, acc, pts[i].z);
-    }
-    U256 inv;
-    F.inv_mont(inv, acc);
-    std::memset(out.mutable_data(), 0, n * 64);
-    for (size_t k = n; k-- > 0;) {
-      if (pts[k].is_inf()) continue;
-      U256 zi, zi2, zi3, ax, ay;
-      F.mul(zi, inv, pre[k]);
-      F.mul(inv, inv, pts[k].z);
-      F.sqr(zi2, zi);
-      F.mul(zi3, zi2, zi);
-      F.mul(ax, pts[k].x, zi2);
-      F.mul(ay, pts[k].y, zi3);
-      F.from_mont(ax).to_be(out.mutable_data(py::ssize_t(k), 0));
-      F.from_mont(ay).to_be(out.mutable_data(py::ssize_t(k), 32));
-    }
+    marshal_jac_rows(jac.data(), nullptr, n, out.mutable_data());
     return out;
   });
   m.def("g1_sum_jac_u32", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> jac) {
@@ -1239,6 +1245,22 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         std::vector<Bytes> cs;
         cs.reserve(comms.size());
         for (auto& c : comms) cs.push_back(B(c));
+        return f.make_secagg_block(w.data(), size_t(w.size()), nodes, std::move(cs), now);
+      })
+      // the same with the commitments as device-layout Jacobian rows (the pre-step's pinned read-back): only the
+      // block's rows are marshalled (one inversion), in C++, on the round's block-build path
+      .def("make_secagg_block_jac", [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w,
+                                       std::vector<i64> nodes,
+                                       py::array_t<uint32_t, py::array::c_style | py::array::forcecast> jac,
+                                       std::vector<int64_t> rows, i64 now) {
+        if (jac.ndim() != 2 || jac.shape(1) != 24) throw std::runtime_error("expected [n, 24] uint32");
+        if (rows.size() != nodes.size()) throw std::runtime_error("rows/node_list mismatch");
+        for (int64_t r : rows)
+          if (r < 0 || r >= jac.shape(0)) throw std::runtime_error("commitment row out of range");
+        std::vector<uint8_t> m(rows.size() * 64);
+        marshal_jac_rows(jac.data(), rows.data(), rows.size(), m.data());
+        std::vector<Bytes> cs(rows.size());
+        for (size_t k = 0; k < rows.size(); ++k) cs[k].assign(m.begin() + 64 * k, m.begin() + 64 * (k + 1));
         return f.make_secagg_block(w.data(), size_t(w.size()), nodes, std::move(cs), now);
       })
       .def("make_plain_block", [](RoundFSM& f, py::array_t<double, py::array::c_style | py::array::forcecast> w,

@@ -568,22 +568,25 @@ class NativeSecAgg:
         launches later, after its witness sums -- the native side waits for them).  The row list travels in
         the kernel's arguments; its device copy (for the early audit sums) goes up on `up`.  Returns the handle
         the engine's aggregation uses (pts, ys, alive, rows_t, ev)."""
-        eng, n = self.eng, len(rows)
+        n = len(rows)
         ring = self._spec_ring_for(max(n, qdelta.shape[0]))
         k = ring["k"] = (ring["k"] + 1) % self.SPEC_SLOTS
         sl, cap = ring["slots"][k], ring["cap"]
-        ev_up, ev_flags = sl.get("ev_up"), sl.get("ev_flags")
-        if ev_up is None:
-            ev_up, ev_flags = sl["ev_up"], sl["ev_flags"] = torch.cuda.Event(), torch.cuda.Event()
+        lp = sl.get("launch")
+        if lp is None:   # the slot's pointers and event handles, resolved once (the launch sits on the round's path)
+            ev_up, ev_flags = torch.cuda.Event(), torch.cuda.Event()
             ev_up.record(up)   # materialise the handles (re-recorded natively)
             ev_flags.record(up)
-        sl["host"].numpy()[:n] = rows
-        pts, ys = sl["pts"][:n], sl["ys"][:n]
+            lp = sl["launch"] = (sl["host"].numpy(), sl["host"].data_ptr(), _ptr(sl["pts"]), _ptr(sl["ys"]),
+                                 _ptr(sl["rows"]), ev_up, ev_flags, ev_up.cuda_event, ev_flags.cuda_event,
+                                 _ptr(self.eng.tbl_wb))
+        h_np, h_ptr, pts_p, ys_p, rows_p, ev_up, ev_flags, ev_up_h, ev_flags_h, wb_p = lp
+        h_np[:n] = rows
         _check(hip().bsc_round_spec_msm2(self.ctx, k, ev_wait.cuda_event if ev_wait is not None else None,
-                                         _ptr(qdelta), sl["host"].data_ptr(), n, _ptr(eng.tbl_wb), 2 if no_commit else 0,
-                                         int(group_rows), _ptr(pts), _ptr(ys), _ptr(sl["rows"]), up.cuda_stream,
-                                         ev_up.cuda_event, ev_flags.cuda_event), "round_spec_msm2")
-        sp = NativeSpec(qdelta, rows, sl["rows"][:n], sl["rows"][cap:cap + n], pts, ys, no_commit)
+                                         qdelta.data_ptr(), h_ptr, n, wb_p, 2 if no_commit else 0, int(group_rows),
+                                         pts_p, ys_p, rows_p, up.cuda_stream, ev_up_h, ev_flags_h), "round_spec_msm2")
+        # the handle's views, after the launch
+        sp = NativeSpec(qdelta, rows, sl["rows"][:n], sl["rows"][cap:cap + n], sl["pts"][:n], sl["ys"][:n], no_commit)
         sp.ev_flags = ev_flags
         return sp
 

@@ -100,6 +100,9 @@ class _CommitTable(dict):
     def __init__(self):
         super().__init__()
         self._table, self.row, self._load = None, {}, None
+        # (pinned [n, 24] device-layout Jacobian rows, their read-back event): set when the table is the
+        # pre-step's commitments -- the block build then marshals only its own rows natively
+        self.jac = None
 
     @property
     def table(self):

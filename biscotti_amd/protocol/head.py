@@ -320,19 +320,17 @@ class RoundHeadMixin:
         if got is None:
             return
         plan, ibs, arrivals, spec_workers, cands = got[:5]
-        plan = PlanView(plan)
-        workers = plan.workers
-        inboxes = dict(zip(plan.verifiers, ibs))
-        cand = set(cands)
         if not spec_workers:
             return
         side = self.side_stream
         # the audit's commitment sums come from the pre-step's chunk commitments (the early audit sums of NativeSecAgg.after_select):
         # the MSM then computes the witness lanes only
         no_commit = getattr(pre["commits"], "ccom", None) is not None and cfg.kzg_audit == "off"
-        rows = [w - self.lo for w in spec_workers]
+        lo = self.lo
+        rows = [w - lo for w in spec_workers]
         if self._native is not None:
-            # one native call: wait for the step, upload rows + flags, launch (resident output ring)
+            # one native call: wait for the step, launch with the rows in the kernel's arguments (resident output
+            # ring); the plan's Python views are built after the launch
             sp = self._native.spec_msm(pre["qdelta"], rows, pre["ev"], no_commit, SPEC_GROUP_ROWS, self.upload_stream)
             sp.record(side)
         else:
@@ -341,6 +339,10 @@ class RoundHeadMixin:
             with S.use(self.upload_stream):
                 sp = self.crypto.shares_async(pre["qdelta"], rows, side, group_rows=SPEC_GROUP_ROWS,
                                               no_commit=no_commit)
+        plan = PlanView(plan)
+        workers = plan.workers
+        inboxes = dict(zip(plan.verifiers, ibs))
+        cand = set(cands)
         self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
                            "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
                            "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}

@@ -380,13 +380,21 @@ class SecAggMixin:
                         W_np[i] = Wn[i] + v / 10.0 ** cfg.precision
             self.log.info("recovery fell back to least squares for %d chunks", int((st == 0).sum()))
         with tm.phase("recover.block"):
-            block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
+            jac = getattr(commit_of, "jac", None)
+            if jac is not None and commit_of._table is None:
+                # the commitments are still the pre-step's Jacobian rows: only the block's are marshalled (one
+                # inversion, natively) -- the signing marshals the whole table later, off this path
+                S.host_wait(jac[1])
+                block = fsm.make_secagg_block_jac(W_np, node_list, jac[0].numpy().view(np.uint32),
+                                                  [commit_of.row[w] for w in node_list], now)
+            else:
+                block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
         self._W_next = W_new if st.all() and self.gpu else None
-        # the next round's VRF outputs first (a native seed set: ~10 us to submit; started later they are not
-        # ready at the next round's noiser lottery), then its share MSM
-        self._early_vrf_submit(block.hash)
+        # the next round's share MSM first (its end gates the next recovery), then its VRF outputs (a native seed
+        # set, ~12 us to submit; the noiser lottery reads them ~0.3 ms later)
         if self._W_next is not None:
             self._spec_head_launch(block)
+        self._early_vrf_submit(block.hash)
         if audit_ok is not None:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()

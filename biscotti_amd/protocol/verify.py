@@ -269,6 +269,8 @@ class VerifyMixin:
             if single:
                 if local_workers:
                     commit_of.fill_lazy(pending_commits.result, row_of)
+                    if getattr(pending_commits, "value", 1) is None and getattr(pending_commits, "host", None) is not None:
+                        commit_of.jac = (pending_commits.host, pending_commits.event)
             elif head.get("commit_gather") is not None:   # gathered with the noisers (noise-aware path)
                 host, ev = head["commit_gather"]
 

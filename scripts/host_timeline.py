@@ -76,6 +76,12 @@ def main():
             wrap(eng.crypto, m[7:], m)
         elif m.startswith("fsm."):
             wrap(eng.fsm, m[4:], m)
+        elif m.startswith("native."):
+            wrap(eng._native, m[7:], m)
+        elif m.startswith("mod:"):   # mod:package.module.function (a module-level name the engine calls)
+            import importlib
+            mod, fn = m[4:].rsplit(".", 1)
+            wrap(importlib.import_module(mod), fn, m[4:])
         else:
             wrap(eng, m, m)
     for _ in range(a.warm):

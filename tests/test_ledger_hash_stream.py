@@ -58,3 +58,28 @@ def test_secagg_block_hash_matches_gob():
     assert np.array_equal(np.asarray(b.data.global_w), W) and b.data.n_deltas == 3
     e = fsm.make_secagg_block(W, [], [], 12345)   # empty block: the latest block's W, timestamp 0
     assert bytes(e.hash) == _expected(e) and e.timestamp == 0 and not np.any(np.asarray(e.data.global_w))
+
+
+def test_secagg_block_from_jacobian_rows():
+    """make_secagg_block_jac (the block's commitments marshalled natively from the pre-step's device-layout
+    Jacobian rows) builds the same block as make_secagg_block with the marshals g1_marshal_jac_batch gives."""
+    from biscotti_amd.protocol.config import RunConfig
+
+    R = rt()
+    one = np.array([0xa1f76999, 0xe7a35393, 0xdf4a4a61, 0x11a4772e, 0x9e7b23de, 0x55901347, 0xb55c7806, 0x704afe1c],
+                   np.uint32)   # Montgomery 1 (bn256_dev.h ONE): Z of an affine point in Jacobian form
+    pts = [R.g1_base_mul(k * 7919 + 3) for k in range(12)]
+    jac = np.stack([np.concatenate([np.asarray(R.g1_affine_mont_u32(p), np.uint32).reshape(-1)[:16], one])
+                    for p in pts])
+    jac[5] = 0   # the point at infinity (Z = 0)
+    ref = R.g1_marshal_jac_batch(jac)
+    assert bytes(ref[0]) == bytes(pts[0]) and not np.any(ref[5])
+    cfg = RunConfig(dataset="mnist", num_nodes=20)
+    fsm = R.RoundFSM(cfg.protocol(R), 7850)
+    fsm.begin_round([1] * 20)
+    W = np.random.default_rng(5).standard_normal(7850)
+    nodes, rows = [2, 4, 9, 11], [7, 0, 5, 11]
+    a = fsm.make_secagg_block_jac(W, nodes, jac, rows, 777)
+    b = fsm.make_secagg_block(W, nodes, [bytes(ref[r]) for r in rows], 777)
+    assert bytes(a.hash) == bytes(b.hash) == _expected(a)
+    assert [bytes(u.commitment) for u in a.data.deltas] == [bytes(ref[r]) for r in rows]
