@@ -82,12 +82,15 @@ class RunConfig:
     #                      at block build): the chain must not change (tests)
     #   spec_head_shared   GPU: the next round's share MSM at block build also when several ranks share one
     #                      GPU (off there by default: rehearsals of the one-rank-per-GPU path force it)
+    #   spec_all_candidates GPU: the speculative share MSM covers every candidate (every approved worker's
+    #                      shares, as each reference worker computes its own), not only the leader's first
+    #                      arrivals up to the adaptive horizon (head.py SPEC_MARGIN): the chain must not change
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
     churn_round_s: ClassVar[float] = 25.44
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
-                                  "spec_head_shared")
+                                  "spec_head_shared", "spec_all_candidates")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

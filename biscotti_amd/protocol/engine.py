@@ -427,6 +427,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             self.drain(final=False)
             self._pending_roles = (head["fut_noise"], head["fut_roles"])
         self.stats["total_updates"] += n_up
+        if n_up:
+            self._note_block_depth(head, self._last_nodes)
         accepted_map = v["accepted_map"]
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=n_up == 0,
                           node_list=self._last_nodes, approved=list(approved), verifiers=list(plan.verifiers),

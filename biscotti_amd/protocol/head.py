@@ -22,6 +22,12 @@ from ..utils import h2d, h2d_many
 from ..utils import streams as S
 
 SPEC_GROUP_ROWS = 8   # speculative MSM rows per group, in leader arrival order (late cancellation)
+# The leader's block closes at its first NUM_SAMPLES/2 approved arrivals (main.go:360): shares of candidates
+# further down its arrival order are never aggregated.  The speculative MSM covers the candidates up to a
+# horizon in that order -- the leader's cap plus SPEC_MARGIN, and at least SPEC_SLACK past the deepest block
+# row of the last SPEC_WINDOW rounds (rejections push the block deeper) -- instead of every candidate (~94 at
+# 100 peers, 2.7x the block); a block that reaches past it is topped up by the host path (spec_misses).
+SPEC_MARGIN, SPEC_SLACK, SPEC_WINDOW = 16, 8, 8
 
 
 class PlanView:
@@ -120,7 +126,7 @@ class RoundHeadMixin:
             cand = set()
             if sn is not None:
                 # launched at the previous block's build (_spec_head_launch), from this very plan
-                cand, spec, head["arrivals"] = sn["cand"], sn["spec"], sn["arrivals"]
+                cand, spec, head["arrivals"], head["krank"] = sn["cand"], sn["spec"], sn["arrivals"], sn.get("krank")
                 if sn.get("kst") is not None:
                     head["kst"] = sn["kst"]   # Krum's static tables, built in the previous round's audit wait
                 self.stats["spec_head"] = self.stats.get("spec_head", 0) + 1
@@ -320,6 +326,16 @@ class RoundHeadMixin:
         if got is None:
             return
         plan, ibs, arrivals, spec_workers, cands = got[:5]
+        # candidates in the leader's arrival order up to the horizon (replicated on every rank)
+        cset = set(cands)
+        order = [w for w in arrivals if w in cset]
+        krank = {w: i for i, w in enumerate(order)}
+        horizon = self._spec_horizon(len(order))
+        keep = None
+        if horizon < len(order):
+            keep = [i for i, w in enumerate(spec_workers) if krank.get(w, 1 << 30) < horizon]
+            spec_workers = [spec_workers[i] for i in keep]
+            cands = order[:horizon]
         if not spec_workers:
             return
         side = self.side_stream
@@ -328,6 +344,7 @@ class RoundHeadMixin:
         no_commit = getattr(pre["commits"], "ccom", None) is not None and cfg.kzg_audit == "off"
         lo = self.lo
         rows = [w - lo for w in spec_workers]
+        self.stats["spec_rows"] = self.stats.get("spec_rows", 0) + len(rows)   # speculative MSM rows launched
         if self._native is not None:
             # one native call: wait for the step, launch with the rows in the kernel's arguments (resident output
             # ring); the plan's Python views are built after the launch
@@ -345,13 +362,34 @@ class RoundHeadMixin:
         cand = set(cands)
         self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
                            "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
-                           "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre}
+                           "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre, "krank": krank}
         if krum and ibs:
             n = len(ibs[0])
-            up = h2d_many([(got[5], torch.int32), (got[6], torch.int32), (got[7], torch.int32)], self.dev)
+            amap = got[7] if keep is None else got[7][keep]   # speculative row -> Krum row, for the kept rows
+            up = h2d_many([(got[5], torch.int32), (got[6], torch.int32), (amap, torch.int32)], self.dev)
             self._spec_next["kst"] = {"U": g["U1"], "n": n, "clip": self.fsm.krum_clip(n),
                                       "need": len(plan.verifiers) // 2, "cap": self.fsm.leader_cap_size(),
                                       "inbox": up[0], "rank": up[1], "amap": up[2]}
+
+    def _spec_horizon(self, ncand: int) -> int:
+        """How far down the leader's arrival order of candidates the speculative MSM reaches (replicated: the
+        leader's cap and the committed blocks' depths are the same on every rank)."""
+        cap = self.fsm.leader_cap_size()
+        if cap <= 0 or self.cfg.has("spec_all_candidates"):
+            return ncand
+        depths = getattr(self, "_spec_depths", None) or [0]
+        return min(ncand, max(cap + SPEC_MARGIN, max(depths) + SPEC_SLACK))
+
+    def _note_block_depth(self, head: dict, node_list) -> None:
+        """After a block: how far down the leader's candidate arrival order its rows reached (the horizon's
+        input for the next rounds)."""
+        kr = head.get("krank")
+        if not kr or not node_list:
+            return
+        d = 1 + max(kr.get(w, len(kr)) for w in node_list)
+        hist = self.__dict__.setdefault("_spec_depths", [])
+        hist.append(d)
+        del hist[:-SPEC_WINDOW]
 
     def _early_vrf_submit(self, block_hash) -> None:
         """Start the next round's noiser VRF outputs as soon as the block that seeds them is built, before

@@ -390,11 +390,12 @@ class SecAggMixin:
             else:
                 block = fsm.make_secagg_block(W_np, node_list, [commit_of[w] for w in node_list], now)
         self._W_next = W_new if st.all() and self.gpu else None
-        # the next round's share MSM first (its end gates the next recovery), then its VRF outputs (a native seed
-        # set, ~12 us to submit; the noiser lottery reads them ~0.3 ms later)
+        # the next round's VRF outputs first (a native seed set: ~12 us to submit; started after the speculative
+        # launch they were not ready at the next round's noiser lottery: vrf_join 0.04 -> 0.1 ms), then its
+        # share MSM
+        self._early_vrf_submit(block.hash)
         if self._W_next is not None:
             self._spec_head_launch(block)
-        self._early_vrf_submit(block.hash)
         if audit_ok is not None:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()

@@ -211,3 +211,26 @@ def test_mnist_label_flip_rejection_floor_default_noise():
 
 
 DIGIT1_ERR_CEILING = 0.75   # this deterministic run measures 0.647 (rejection 0.756), docs/ROBUSTNESS.md
+
+
+@pytest.mark.parametrize("poisoning", [0.0, 0.3])
+def test_spec_horizon_same_chain_as_every_candidate(poisoning):
+    """The speculative share MSM covers the leader's candidate arrivals up to an adaptive horizon (head.py
+    SPEC_MARGIN) instead of every candidate: the chain is byte-identical to computing every candidate's shares
+    (ablation spec_all_candidates) -- blocks reaching past the horizon are topped up by the host path -- and it
+    launches fewer rows."""
+    out = []
+    for abl in ("", "spec_all_candidates"):
+        eng = _engine(num_nodes=100, poisoning=poisoning, epsilon=1.0, seed=11, ablation=abl)
+        hashes = [bytes(eng.run_round().block_hash) for _ in range(8)]
+        eng.drain()
+        ok, why = eng.fsm.chain.verify()
+        stats = dict(eng.stats)
+        eng.close()
+        assert ok, why
+        out.append((hashes, stats))
+    (h0, s0), (h1, s1) = out
+    assert h0 == h1
+    assert s0.get("spec_head", 0) >= 6 and s1.get("spec_head", 0) >= 6
+    assert s0["spec_rows"] < 0.8 * s1["spec_rows"], (s0["spec_rows"], s1["spec_rows"])
+    print("rows launched", s0["spec_rows"], "vs", s1["spec_rows"], "misses", s0.get("spec_misses", 0))
