@@ -25,8 +25,9 @@ SPEC_GROUP_ROWS = 8   # speculative MSM rows per group, in leader arrival order 
 # The leader's block closes at its first NUM_SAMPLES/2 approved arrivals (main.go:360): shares of candidates
 # further down its arrival order are never aggregated.  The speculative MSM covers the candidates up to a
 # horizon in that order -- the leader's cap plus SPEC_MARGIN, and at least SPEC_SLACK past the deepest block
-# row of the last SPEC_WINDOW rounds (rejections push the block deeper) -- instead of every candidate (~94 at
-# 100 peers, 2.7x the block); a block that reaches past it is topped up by the host path (spec_misses).
+# row of the last SPEC_WINDOW rounds (rejections push the block deeper; every candidate until SPEC_WINDOW blocks
+# are known) -- instead of every candidate (~94 at 100 peers, 2.7x the block); a block that reaches past it is
+# topped up by the host path (spec_misses).
 SPEC_MARGIN, SPEC_SLACK, SPEC_WINDOW = 16, 8, 8
 
 
@@ -375,9 +376,9 @@ class RoundHeadMixin:
         """How far down the leader's arrival order of candidates the speculative MSM reaches (replicated: the
         leader's cap and the committed blocks' depths are the same on every rank)."""
         cap = self.fsm.leader_cap_size()
-        if cap <= 0 or self.cfg.has("spec_all_candidates"):
-            return ncand
-        depths = getattr(self, "_spec_depths", None) or [0]
+        depths = getattr(self, "_spec_depths", None) or []
+        if cap <= 0 or len(depths) < SPEC_WINDOW or self.cfg.has("spec_all_candidates"):
+            return ncand   # every candidate until a window of blocks shows how deep they reach
         return min(ncand, max(cap + SPEC_MARGIN, max(depths) + SPEC_SLACK))
 
     def _note_block_depth(self, head: dict, node_list) -> None:
