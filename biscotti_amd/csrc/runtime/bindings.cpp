@@ -1320,7 +1320,11 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       // order, this rank's candidate workers [lo, hi) sorted by arrival, every candidate sorted), or None
       // when the run is over.  Candidates: every update some verifier judges, or every worker when
       // floor(nv/2) == 0 signatures suffice (main.go:1686).
-      .def("spec_plan", [](RoundFSM& f, const Block& b, i64 lo, i64 hi, std::vector<i64> xrow, i64 U) -> py::object {
+      // horizon >= 0: only the first `horizon` candidates in the leader's arrival order are speculative rows (the
+      // candidate list, this rank's rows and the Krum row map are cut to them); the tuple then ends with the full
+      // candidate arrival order
+      .def("spec_plan", [](RoundFSM& f, const Block& b, i64 lo, i64 hi, std::vector<i64> xrow, i64 U,
+                           i64 horizon) -> py::object {
         RoundFSM s = f.successor(b);
         const i64 n = s.cfg.num_nodes;
         std::vector<u8> live(size_t(n), 1);
@@ -1337,13 +1341,18 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         auto arrivals = s.leader_arrivals();
         std::vector<i64> rank(size_t(n), i64(1) << 30);
         for (size_t i = 0; i < arrivals.size(); ++i) rank.at(size_t(arrivals[i])) = i64(i);
+        std::vector<i64> order;   // the candidates in the leader's arrival order
+        for (i64 w : arrivals)
+          if (cand.at(size_t(w))) order.push_back(w);
+        if (horizon >= 0 && horizon < i64(order.size()))
+          for (size_t i = size_t(horizon); i < order.size(); ++i) cand[size_t(order[i])] = 0;
         std::vector<i64> spec, cands;
         for (i64 w : plan.workers)
           if (cand.at(size_t(w)) && w >= lo && w < hi) spec.push_back(w);
         std::stable_sort(spec.begin(), spec.end(), [&](i64 a, i64 c) { return rank[size_t(a)] < rank[size_t(c)]; });
         for (i64 w = 0; w < n; ++w)
           if (cand[size_t(w)]) cands.push_back(w);
-        if (xrow.empty()) return py::make_tuple(plan, inboxes, arrivals, spec, cands);
+        if (xrow.empty()) return py::make_tuple(plan, inboxes, arrivals, spec, cands, order);
         // Krum's static tables for this plan (verify.py _krum_static): every verifier's inbox as rows of the
         // selection input (xrow: peer -> row, -1 none), each row's leader-arrival rank, speculative row -> row
         if (xrow.size() != size_t(n)) throw std::runtime_error("spec_plan: xrow must map every peer");
@@ -1364,8 +1373,9 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         py::array_t<int32_t> src(py::ssize_t(spec.size()));
         int32_t* sr = src.mutable_data();
         for (size_t i = 0; i < spec.size(); ++i) sr[i] = int32_t(xrow.at(size_t(spec[i])));
-        return py::make_tuple(plan, inboxes, arrivals, spec, cands, inbox, rk, src);
-      }, py::arg("block"), py::arg("lo"), py::arg("hi"), py::arg("xrow") = std::vector<i64>{}, py::arg("U") = 0);
+        return py::make_tuple(plan, inboxes, arrivals, spec, cands, inbox, rk, src, order);
+      }, py::arg("block"), py::arg("lo"), py::arg("hi"), py::arg("xrow") = std::vector<i64>{}, py::arg("U") = 0,
+         py::arg("horizon") = -1);
   m.def("select_roles", [](const std::map<i64, i64>& stake, py::bytes h, i64 nv, i64 na, i64 n) {
     std::vector<i64> v, mm;
     select_roles(stake, B(h), nv, na, n, &v, &mm);

@@ -127,7 +127,7 @@ class RoundHeadMixin:
             cand = set()
             if sn is not None:
                 # launched at the previous block's build (_spec_head_launch), from this very plan
-                cand, spec, head["arrivals"], head["krank"] = sn["cand"], sn["spec"], sn["arrivals"], sn.get("krank")
+                cand, spec, head["arrivals"], head["cand_order"] = sn["cand"], sn["spec"], sn["arrivals"], sn.get("cand_order")
                 if sn.get("kst") is not None:
                     head["kst"] = sn["kst"]   # Krum's static tables, built in the previous round's audit wait
                 self.stats["spec_head"] = self.stats.get("spec_head", 0) + 1
@@ -322,21 +322,14 @@ class RoundHeadMixin:
         krum = g is not None and cfg.defense == "KRUM"
         # with the noise-aware Krum input, the same call also returns Krum's static tables (verify.py
         # _krum_static) for the successor plan: they go up in one copy below, off the next round's path
-        got = self.fsm.spec_plan(block, self.local.start, self.local.stop, *((self._xrow_list(g["xrow"]), g["U1"])
-                                                                             if krum else ()))
+        # the candidates up to the horizon in the leader's arrival order (replicated on every rank)
+        got = self.fsm.spec_plan(block, self.local.start, self.local.stop,
+                                 self._xrow_list(g["xrow"]) if krum else [], g["U1"] if krum else 0,
+                                 self._spec_horizon())
         if got is None:
             return
         plan, ibs, arrivals, spec_workers, cands = got[:5]
-        # candidates in the leader's arrival order up to the horizon (replicated on every rank)
-        cset = set(cands)
-        order = [w for w in arrivals if w in cset]
-        krank = {w: i for i, w in enumerate(order)}
-        horizon = self._spec_horizon(len(order))
-        keep = None
-        if horizon < len(order):
-            keep = [i for i, w in enumerate(spec_workers) if krank.get(w, 1 << 30) < horizon]
-            spec_workers = [spec_workers[i] for i in keep]
-            cands = order[:horizon]
+        order = got[-1]
         if not spec_workers:
             return
         side = self.side_stream
@@ -363,31 +356,31 @@ class RoundHeadMixin:
         cand = set(cands)
         self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
                            "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
-                           "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre, "krank": krank}
+                           "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre, "cand_order": order}
         if krum and ibs:
             n = len(ibs[0])
-            amap = got[7] if keep is None else got[7][keep]   # speculative row -> Krum row, for the kept rows
-            up = h2d_many([(got[5], torch.int32), (got[6], torch.int32), (amap, torch.int32)], self.dev)
+            up = h2d_many([(got[5], torch.int32), (got[6], torch.int32), (got[7], torch.int32)], self.dev)
             self._spec_next["kst"] = {"U": g["U1"], "n": n, "clip": self.fsm.krum_clip(n),
                                       "need": len(plan.verifiers) // 2, "cap": self.fsm.leader_cap_size(),
                                       "inbox": up[0], "rank": up[1], "amap": up[2]}
 
-    def _spec_horizon(self, ncand: int) -> int:
-        """How far down the leader's arrival order of candidates the speculative MSM reaches (replicated: the
-        leader's cap and the committed blocks' depths are the same on every rank)."""
+    def _spec_horizon(self) -> int:
+        """How far down the leader's arrival order of candidates the speculative MSM reaches, -1: every candidate
+        (replicated: the leader's cap and the committed blocks' depths are the same on every rank)."""
         cap = self.fsm.leader_cap_size()
         depths = getattr(self, "_spec_depths", None) or []
         if cap <= 0 or len(depths) < SPEC_WINDOW or self.cfg.has("spec_all_candidates"):
-            return ncand   # every candidate until a window of blocks shows how deep they reach
-        return min(ncand, max(cap + SPEC_MARGIN, max(depths) + SPEC_SLACK))
+            return -1   # every candidate until a window of blocks shows how deep they reach
+        return max(cap + SPEC_MARGIN, max(depths) + SPEC_SLACK)
 
     def _note_block_depth(self, head: dict, node_list) -> None:
         """After a block: how far down the leader's candidate arrival order its rows reached (the horizon's
         input for the next rounds)."""
-        kr = head.get("krank")
-        if not kr or not node_list:
+        order = head.get("cand_order")
+        if not order or not node_list:
             return
-        d = 1 + max(kr.get(w, len(kr)) for w in node_list)
+        nl = set(node_list)
+        d = 1 + max((i for i, w in enumerate(order) if w in nl), default=len(order))
         hist = self.__dict__.setdefault("_spec_depths", [])
         hist.append(d)
         del hist[:-SPEC_WINDOW]

@@ -233,7 +233,9 @@ def test_spec_plan_matches_python_composition(nv, lo, hi):
         arr = list(shadow.leader_arrivals())
         rank = {w: i for i, w in enumerate(arr)}
         spec = sorted((w for w in workers if lo <= w < hi and w in cand), key=lambda w: rank.get(w, 1 << 30))
-        plan, ibs2, arr2, spec2, cands2 = eng.fsm.spec_plan(blk, lo, hi)
+        plan, ibs2, arr2, spec2, cands2, order2 = eng.fsm.spec_plan(blk, lo, hi)
+        order = [w for w in arr if w in cand]
+        assert list(order2) == order
         assert (list(plan.verifiers), list(plan.miners), list(plan.workers), plan.iteration) == \
             (list(p.verifiers), list(p.miners), workers, p.iteration)
         assert [list(x) for x in ibs2] == ibs and list(arr2) == arr and list(spec2) == spec
@@ -249,6 +251,13 @@ def test_spec_plan_matches_python_composition(nv, lo, hi):
                 want_rank[xl[w]] = i
         np.testing.assert_array_equal(got[6], want_rank)
         np.testing.assert_array_equal(got[7], np.array([xl[w] for w in spec], np.int32))
+        # a horizon keeps the first h candidates in the leader's arrival order (head.py SPEC_MARGIN)
+        h = max(1, len(order) // 2)
+        gh = eng.fsm.spec_plan(blk, lo, hi, xl, 12, h)
+        keep = set(order[:h])
+        spec_h = [w for w in spec if w in keep]
+        assert list(gh[3]) == spec_h and list(gh[4]) == sorted(keep) and list(gh[8]) == order
+        np.testing.assert_array_equal(gh[7], np.array([xl[w] for w in spec_h], np.int32))
     eng.close()
 
 
