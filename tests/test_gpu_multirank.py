@@ -129,3 +129,21 @@ def test_gpu_one_rank_per_gpu_fast_path_over_rccl(world):
             assert st.get(k, 0) >= rounds - 1, (r, k, st)
         assert st.get("spec_misses", 0) == 0 and st.get("audit_failures", 0) == 0, st
     assert s1.get("spec_head", 0) >= rounds - 1, s1
+
+
+def test_gpu_spec_horizon_two_ranks_100_peers_over_rccl():
+    """The headline size (100 peers) on two RCCL ranks with the speculative head forced on: after 8 blocks
+    the speculative MSM covers only the candidates up to the replicated horizon (head.py SPEC_MARGIN), every
+    rank takes the same fast / top-up decisions, and the chain equals one process's byte for byte."""
+    rounds = 12
+    kw = dict(num_nodes=100, dataset="mnist", seed=17, deterministic_time=True, max_iterations=100,
+              ablation="spec_head_shared")
+    single, s1 = _run_stats(1, kw, rounds)[0]
+    out = _run_stats(2, kw, rounds, backend="nccl")
+    for r in range(2):
+        hashes, st = out[r]
+        assert hashes == single, f"rank {r} chain differs"
+        assert st.get("spec_head", 0) >= rounds - 1 and st.get("audit_failures", 0) == 0, (r, st)
+    assert out[0][1].get("spec_misses", 0) == out[1][1].get("spec_misses", 0) == s1.get("spec_misses", 0)
+    # each rank launches its own peers' rows: together the single process's rows
+    assert out[0][1]["spec_rows"] + out[1][1]["spec_rows"] == s1["spec_rows"], (out[0][1], out[1][1], s1)
