@@ -25,10 +25,10 @@ SPEC_GROUP_ROWS = 8   # speculative MSM rows per group, in leader arrival order 
 # The leader's block closes at its first NUM_SAMPLES/2 approved arrivals (main.go:360): shares of candidates
 # further down its arrival order are never aggregated.  The speculative MSM covers the candidates up to a
 # horizon in that order -- the leader's cap plus SPEC_MARGIN, and at least SPEC_SLACK past the deepest block
-# row of the last SPEC_WINDOW rounds (rejections push the block deeper; every candidate until SPEC_WINDOW blocks
-# are known) -- instead of every candidate (~94 at 100 peers, 2.7x the block); a block that reaches past it is
-# topped up by the host path (spec_misses).
-SPEC_MARGIN, SPEC_SLACK, SPEC_WINDOW = 16, 8, 8
+# row of the last SPEC_WINDOW rounds (rejections push the block deeper; every candidate until SPEC_MIN_HISTORY
+# blocks are known, more slack while the window fills) -- instead of every candidate (~94 at 100 peers, 2.7x the
+# block); a block that reaches past it is topped up by the host path (spec_misses).
+SPEC_MARGIN, SPEC_SLACK, SPEC_WINDOW, SPEC_MIN_HISTORY = 16, 8, 8, 3
 
 
 class PlanView:
@@ -369,9 +369,10 @@ class RoundHeadMixin:
         (replicated: the leader's cap and the committed blocks' depths are the same on every rank)."""
         cap = self.fsm.leader_cap_size()
         depths = getattr(self, "_spec_depths", None) or []
-        if cap <= 0 or len(depths) < SPEC_WINDOW or self.cfg.has("spec_all_candidates"):
-            return -1   # every candidate until a window of blocks shows how deep they reach
-        return max(cap + SPEC_MARGIN, max(depths) + SPEC_SLACK)
+        if cap <= 0 or len(depths) < SPEC_MIN_HISTORY or self.cfg.has("spec_all_candidates"):
+            return -1   # every candidate until a few blocks show how deep they reach
+        # a short history gets more slack: 2 rows per missing block of the window
+        return max(cap + SPEC_MARGIN, max(depths) + SPEC_SLACK + 2 * (SPEC_WINDOW - len(depths)))
 
     def _note_block_depth(self, head: dict, node_list) -> None:
         """After a block: how far down the leader's candidate arrival order its rows reached (the horizon's

@@ -222,7 +222,7 @@ def test_spec_horizon_same_chain_as_every_candidate(poisoning):
     out = []
     for abl in ("", "spec_all_candidates"):
         eng = _engine(num_nodes=100, poisoning=poisoning, epsilon=1.0, seed=11, ablation=abl)
-        hashes = [bytes(eng.run_round().block_hash) for _ in range(8)]   # the horizon applies after 8 blocks
+        hashes = [bytes(eng.run_round().block_hash) for _ in range(8)]   # the horizon applies after 3 blocks
         rows8 = eng.stats.get("spec_rows", 0)
         hashes += [bytes(eng.run_round().block_hash) for _ in range(6)]
         eng.stats["spec_rows_late"] = eng.stats.get("spec_rows", 0) - rows8
