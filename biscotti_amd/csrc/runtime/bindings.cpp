@@ -198,8 +198,11 @@ struct VrfJob {
   }
 };
 
+static void marshal_jac_rows(const uint32_t* jac, const int64_t* idx, size_t n, uint8_t* out);
+
 struct SignJob {
   std::vector<Bytes> msgs, bases, out;
+  std::vector<uint32_t> jac;   // messages still as device-layout Jacobian rows: marshalled on the job's thread
   std::vector<Scalar> keys;
   std::vector<int> key_of, ids;
   int threads = 1;
@@ -284,6 +287,13 @@ static void start_sign_job(SignJob* jp) {
 }
 
 static void run_sign_job(SignJob& j) {
+  if (!j.jac.empty()) {   // the messages: commitments marshalled here, off the round's thread
+    const size_t nj = j.jac.size() / 24;
+    std::vector<uint8_t> m(nj * 64);
+    marshal_jac_rows(j.jac.data(), nullptr, nj, m.data());
+    j.msgs.resize(nj);
+    for (size_t k = 0; k < nj; ++k) j.msgs[k].assign(m.begin() + 64 * k, m.begin() + 64 * (k + 1));
+  }
   // nonce points in parallel, ONE inversion for all their marshals, responses in parallel
   const size_t n = j.msgs.size();
   std::vector<Scalar> vs(n);
@@ -731,6 +741,36 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     start_sign_job(job.get());
     return job;
   }, py::arg("table"), py::arg("rows"), py::arg("sks"), py::arg("key_of"), py::arg("nonce_base"),
+     py::arg("nonce_ids"), py::arg("threads"), py::arg("after_vrf") = nullptr);
+  // the same with the table as device-layout Jacobian rows [n, 24] uint32 (the pre-step's read-back): the
+  // signed rows are copied now and marshalled on the job's thread
+  m.def("schnorr_sign_rows_jac_async", [](py::array_t<uint32_t, py::array::c_style | py::array::forcecast> jac,
+                                          std::vector<int> rows, std::vector<py::bytes> sks, std::vector<int> key_of,
+                                          std::vector<py::bytes> nonce_base, std::vector<int> nonce_ids, int threads,
+                                          std::shared_ptr<VrfJob> after_vrf) {
+    if (jac.ndim() != 2 || jac.shape(1) != 24) throw std::runtime_error("schnorr_sign_rows_jac: expected [n, 24]");
+    const size_t n = rows.size();
+    if (key_of.size() != n || nonce_ids.size() != n || nonce_base.size() != sks.size())
+      throw std::runtime_error("schnorr_sign_rows_jac: length mismatch");
+    auto job = std::make_shared<SignJob>();
+    job->jac.resize(n * 24);
+    for (size_t i = 0; i < n; ++i) {
+      if (rows[i] < 0 || rows[i] >= jac.shape(0)) throw std::runtime_error("schnorr_sign_rows_jac: bad row");
+      std::memcpy(job->jac.data() + 24 * i, jac.data(rows[i], 0), 24 * sizeof(uint32_t));
+    }
+    for (auto& x : sks) job->keys.push_back(Scalar::from_be(B(x)));
+    for (auto& x : nonce_base) job->bases.push_back(B(x));
+    for (int k : key_of)
+      if (k < 0 || size_t(k) >= job->keys.size()) throw std::runtime_error("schnorr_sign_rows_jac: bad key index");
+    job->key_of = key_of;
+    job->ids = nonce_ids;
+    job->threads = threads;
+    job->out.resize(n);
+    (void)gen_table();
+    job->after_vrf = std::move(after_vrf);
+    start_sign_job(job.get());
+    return job;
+  }, py::arg("jac"), py::arg("rows"), py::arg("sks"), py::arg("key_of"), py::arg("nonce_base"),
      py::arg("nonce_ids"), py::arg("threads"), py::arg("after_vrf") = nullptr);
   m.def("client_key_from_entropy", [](py::bytes e) {
     auto kp = client_key_from_entropy(B(e));

@@ -411,9 +411,18 @@ class VerifyMixin:
                         rmap[list(rowmap)] = list(rowmap.values())
                         bases = [_seed_bytes(cfg.seed, f"nonce-{i}", v) for v, i in nonce_keys]
                         sign["sl"] = (vidx[kk], jj)
-                        sign["job"] = R.schnorr_sign_rows_async(commit_of.table, rmap[ws].tolist(), sks, kk.tolist(),
-                                                                bases,
-                                                                ws.tolist(), SIGN_THREADS, after_vrf)
+                        jac = getattr(commit_of, "jac", None)
+                        if jac is not None and commit_of._table is None:
+                            # the commitments are still the pre-step's Jacobian rows: the job marshals the signed
+                            # ones on its own thread (the round's thread skips the table's ~30 us marshal)
+                            S.host_wait(jac[1])
+                            sign["job"] = R.schnorr_sign_rows_jac_async(jac[0].numpy().view(np.uint32),
+                                                                        rmap[ws].tolist(), sks, kk.tolist(), bases,
+                                                                        ws.tolist(), SIGN_THREADS, after_vrf)
+                        else:
+                            sign["job"] = R.schnorr_sign_rows_async(commit_of.table, rmap[ws].tolist(), sks,
+                                                                    kk.tolist(), bases, ws.tolist(), SIGN_THREADS,
+                                                                    after_vrf)
                 sign["prep"] = _prep_sign
                 if defer_sign:   # prepared in the next round's VRF wait, started once its outputs are known
                     self._pre_vrf_work.append(_prep_sign)

@@ -276,6 +276,29 @@ def test_schnorr_sign_rows_matches_message_list(rt):
         rt.schnorr_sign_rows_async(table, [12], [keys[0][0]], [0], bases[:1], [1], 1).result_array()
 
 
+def test_schnorr_sign_rows_jac_matches_marshalled_rows(rt):
+    """Signing device-layout Jacobian commitment rows (marshalled on the job's thread: the deferred verifier
+    signatures) equals signing their marshals."""
+    import os
+
+    import numpy as np
+
+    one = np.array([0xa1f76999, 0xe7a35393, 0xdf4a4a61, 0x11a4772e, 0x9e7b23de, 0x55901347, 0xb55c7806, 0x704afe1c],
+                   np.uint32)   # Montgomery 1: an affine point's Z in Jacobian form
+    pts = [rt.g1_base_mul(3 + 101 * k) for k in range(8)]
+    jac = np.stack([np.concatenate([np.asarray(rt.g1_affine_mont_u32(p), np.uint32).reshape(-1)[:16], one])
+                    for p in pts])
+    table = rt.g1_marshal_jac_batch(jac)
+    keys = [rt.client_key_from_entropy(os.urandom(32)) for _ in range(2)]
+    rows, key_of, ids = [4, 0, 7, 4], [1, 0, 1, 0], [3, 4, 5, 6]
+    bases = [os.urandom(32) for _ in range(2)]
+    want = rt.schnorr_sign_rows_async(table, rows, [k[0] for k in keys], key_of, bases, ids, 2).result_array()
+    got = rt.schnorr_sign_rows_jac_async(jac, rows, [k[0] for k in keys], key_of, bases, ids, 2).result_array()
+    assert np.array_equal(got, want)
+    with pytest.raises(RuntimeError):
+        rt.schnorr_sign_rows_jac_async(jac, [8], [keys[0][0]], [0], bases[:1], [1], 1)
+
+
 def test_concurrent_native_jobs_share_the_pool(rt):
     """VRF and signing jobs running at once (and a foreground batch) give the serial results."""
     import os
