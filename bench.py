@@ -224,6 +224,7 @@ def main() -> int:
     comm.barrier()
     elapsed = time.perf_counter() - t0
     drain_s = time.perf_counter() - t_drain
+    drain_parts = dict(getattr(eng, "drain_parts_ms", None) or {})
     # device memory segments the caching allocator had to hipMalloc inside the timed window
     seg_new = (torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) - seg0) if eng.gpu else 0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
@@ -320,6 +321,7 @@ def main() -> int:
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
             "drain_ms": 1e3 * drain_s,          # inside the timed window: joins of the last rounds' work
+            "drain_parts_ms": drain_parts,
             "device_segments_allocated_timed": seg_new,
             "round_wall_ms": [round(1e3 * w, 3) for w in walls],
             "host_cpu_ms_per_round": 1e3 * host_cpu / max(a.steps, 1),

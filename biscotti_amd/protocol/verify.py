@@ -398,7 +398,7 @@ class VerifyMixin:
                 sks = [self.sk[v] for v in local_vs]
                 nonce_keys = [(v, it) for v in local_vs]
 
-                def _prep_sign(after_vrf=None, sign=sign):
+                def _prep_sign(after_vrf=None, sign=sign, threads=SIGN_THREADS):
                     # message i = row rows[i] of the commitment table, signed with sks[key_of[i]], nonce id =
                     # the worker; (sl_v, sl_j) = its (verifier, inbox slot) in the signature matrix
                     from .engine import _seed_bytes
@@ -418,11 +418,10 @@ class VerifyMixin:
                             S.host_wait(jac[1])
                             sign["job"] = R.schnorr_sign_rows_jac_async(jac[0].numpy().view(np.uint32),
                                                                         rmap[ws].tolist(), sks, kk.tolist(), bases,
-                                                                        ws.tolist(), SIGN_THREADS, after_vrf)
+                                                                        ws.tolist(), threads, after_vrf)
                         else:
                             sign["job"] = R.schnorr_sign_rows_async(commit_of.table, rmap[ws].tolist(), sks,
-                                                                    kk.tolist(), bases, ws.tolist(), SIGN_THREADS,
-                                                                    after_vrf)
+                                                                    kk.tolist(), bases, ws.tolist(), threads, after_vrf)
                 sign["prep"] = _prep_sign
                 if defer_sign:   # prepared in the next round's VRF wait, started once its outputs are known
                     self._pre_vrf_work.append(_prep_sign)
