@@ -191,7 +191,44 @@ __device__ fe fe_mul(const fe& f, const fe& g) {
   for (int i = 0; i < 10; ++i) r.v[i] = (uint32_t)h[i];
   return r;
 }
-__device__ __forceinline__ fe fe_sq(const fe& a) { return fe_mul(a, a); }
+// f^2 with the 45 symmetric cross products taken once (doubled): 55 limb products instead of fe_mul's 100.
+// Same radix conventions as fe_mul: an odd-odd limb pair carries a factor 2 (25-bit limbs), a wrap past
+// limb 9 a factor 19; every partial product stays below 2^60 and every column below 2^64.
+__device__ fe fe_sq(const fe& f) {
+  uint32_t f19[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) f19[i] = 19 * f.v[i];
+  unsigned long long h[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) h[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    // the diagonal term (i, i)
+    const uint32_t ad = (i & 1) ? 2 * f.v[i] : f.v[i];
+    const uint32_t bd = (2 * i >= 10) ? f19[i] : f.v[i];
+    h[(2 * i) % 10] += (unsigned long long)ad * bd;
+#pragma unroll
+    for (int j = i + 1; j < 10; ++j) {   // (i, j) and (j, i) together
+      const uint32_t a = ((i & 1) && (j & 1)) ? 4 * f.v[i] : 2 * f.v[i];
+      const uint32_t b = (i + j >= 10) ? f19[j] : f.v[j];
+      h[(i + j) % 10] += (unsigned long long)a * b;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned long long c = h[i] >> fw(i);
+    h[i] &= (1ull << fw(i)) - 1;
+    if (i < 9) h[i + 1] += c;
+    else h[0] += 19 * c;
+  }
+  const unsigned long long c = h[0] >> 26;
+  h[0] &= (1ull << 26) - 1;
+  h[1] += c;
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) r.v[i] = (uint32_t)h[i];
+  return r;
+}
 __device__ fe fe_sqn(fe a, int n) {
 #pragma unroll 1
   for (int i = 0; i < n; ++i) a = fe_sq(a);

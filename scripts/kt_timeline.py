@@ -36,7 +36,7 @@ def main():
     print("round  wall  share MSMs (queue:start+duration us)")
     for i in range(len(rec) - 1):
         t0, t1 = rec[i]["e"], rec[i + 1]["e"]
-        ms = [r for r in rows if r["n"] == "k_shares_msm" and t0 <= r["s"] < t1]
+        ms = [r for r in rows if r["n"].startswith("k_shares_msm") and t0 <= r["s"] < t1]
         print(f"{i + 1:5d} {(t1 - t0) / 1e3:6.0f}  " + " ".join(f"q{r['Queue_Id']}:{(r['s'] - t0) / 1e3:.0f}+{r['d']:.0f}"
                                                        for r in ms))
     for i in range(a, min(b, len(rec) - 1)):
