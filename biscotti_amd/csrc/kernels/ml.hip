@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "wave_prio.h"
+BSC_PRIO_SETTER(bsc_wave_prio_ml)
 
 namespace {
 

@@ -23,6 +23,7 @@
 
 #include "bn256_dev.h"
 #include "wave_prio.h"
+BSC_PRIO_SETTER(bsc_wave_prio_msm)
 
 using namespace bn;
 

@@ -181,6 +181,16 @@ extern "C" int bsc_round_set_witness_stream(void* ctx, void* stream) {
   return 0;
 }
 
+extern "C" int bsc_wave_prio_ml(int on);
+extern "C" int bsc_wave_prio_msm(int on);
+extern "C" int bsc_wave_prio_vrf(int on);
+// the round kernels' wave priority classes (kernels/wave_prio.h) on or off, in every kernel file
+extern "C" int bsc_wave_prio(int on) {
+  RC_CHECK(bsc_wave_prio_ml(on));
+  RC_CHECK(bsc_wave_prio_msm(on));
+  return bsc_wave_prio_vrf(on);
+}
+
 extern "C" void bsc_round_destroy(void* ctx) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return;

@@ -12,4 +12,18 @@
 // proofs (the run's final flush: CRITICAL), KZG audit sums.
 // The argument must be a constant; call it before the kernel's main work, under a wave-uniform condition (a
 // kernel argument) if any, since s_setprio is a scalar instruction.
-#define BSC_SET_PRIO(p) __builtin_amdgcn_s_setprio(p)
+//
+// The classes apply to one rank per process driving its GPU alone (bsc_wave_prio(1), the default).  With
+// several ranks the engine turns them off (bsc_wave_prio(0)): RCCL's collective kernels run at the default
+// priority and spin on their peers' flags, and under prio-2 share MSMs of two ranks sharing a GPU a collective
+// stalled for 0.1-0.3 s (2-rank RCCL rehearsal).  Each kernel file holds its own flag (one per translation
+// unit) and exports its setter; kernels read it once, wave-uniformly.
+static __device__ int bsc_prio_on = 1;
+#define BSC_SET_PRIO(p)                                  \
+  do {                                                   \
+    if (bsc_prio_on) __builtin_amdgcn_s_setprio(p);      \
+  } while (0)
+#define BSC_PRIO_SETTER(name)                                                                      \
+  extern "C" int name(int on) {                                                                    \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(bsc_prio_on), &on, sizeof(int), 0, hipMemcpyHostToDevice); \
+  }

@@ -27,6 +27,7 @@ SIGNATURES = {
     "bsc_round_spec_msm2": [P, I, P, P, P, I, P, I, I, P, P, P, P, P, P],
     "bsc_round_set_spec_ring": [P, P, I, I],
     "bsc_round_set_witness_stream": [P, P],
+    "bsc_wave_prio": [I],
     "bsc_round_prestep": [P, P, P, P, P, P, P, P, I, I, I, I, U64, I, F, D, I, P, P, P, P, P, P, P, P,
                           I, P, I, L, I, P, P, P, P, P, P, P, I, P],
     "bsc_commit_rows": [P, I, P, I, P, I, I, P, P, P],

@@ -327,6 +327,11 @@ def cu_masked_stream(device, skip_every: int = 4):
     return torch.cuda.ExternalStream(ptr, device=device), used.value
 
 
+def set_wave_priorities(on: bool) -> None:
+    """The round kernels' wave priority classes (kernels/wave_prio.h) on or off, process-wide."""
+    _check(hip().bsc_wave_prio(1 if on else 0), "wave_prio")
+
+
 class NativeSpec:
     """Handle of a speculative share MSM launched by NativeSecAgg.spec_msm (same surface as the engine's
     _SpecShares: the MSM is already running; `ev` marks its end on the side stream)."""

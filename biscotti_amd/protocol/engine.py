@@ -146,6 +146,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         # on any number of ranks
         self._native = None
         if self.gpu:
+            # wave priority classes (kernels/wave_prio.h): one rank drives its GPU alone; with several ranks the
+            # collectives' kernels must not queue behind prio-2 share MSMs
+            B.set_wave_priorities(self.comm.world == 1)
             self._native = B.NativeSecAgg(self.crypto.eng, self.main_stream, self.side_stream, self.bg_stream,
                                           10.0 ** cfg.precision, witness=self.witness_stream)
             if self.comm.world > 1:
