@@ -314,3 +314,39 @@ def test_route_view_matches_route_shares_and_leader_view():
             assert part == {m: dict(routes[m])[nodes[0]] for m in contrib}
         fsm.iteration -= 1   # undo the probe's begin_round
     eng.close()
+
+
+def test_spec_horizon_policy():
+    """head.py's speculative horizon: every candidate (-1) until SPEC_MIN_HISTORY blocks are known, then the
+    leader's cap + SPEC_MARGIN or the deepest recent block row + SPEC_SLACK (+2 per missing window block),
+    whichever is further; block depths are kept for the last SPEC_WINDOW blocks."""
+    from types import SimpleNamespace
+
+    from biscotti_amd.protocol import head as H
+
+    class Cfg:
+        def __init__(self, abl=""):
+            self.abl = abl
+
+        def has(self, a):
+            return a == self.abl
+
+    eng = SimpleNamespace(fsm=SimpleNamespace(leader_cap_size=lambda: 35), cfg=Cfg())
+    horizon = H.RoundHeadMixin._spec_horizon
+    note = H.RoundHeadMixin._note_block_depth
+    assert horizon(eng) == -1
+    order = list(range(100, 194))   # candidates in leader arrival order
+    for depth in (40, 44, 38):
+        note(eng, {"cand_order": order}, [order[depth - 1], order[3]])
+    assert eng._spec_depths == [40, 44, 38]
+    # 3 of 8 window blocks known: max(35 + 16, 44 + 8 + 2 * 5)
+    assert horizon(eng) == max(35 + H.SPEC_MARGIN, 44 + H.SPEC_SLACK + 2 * (H.SPEC_WINDOW - 3)) == 62
+    for _ in range(10):
+        note(eng, {"cand_order": order}, [order[29]])
+    assert len(eng._spec_depths) == H.SPEC_WINDOW and horizon(eng) == 35 + H.SPEC_MARGIN
+    note(eng, {"cand_order": order}, [order[79]])   # a deep block widens the next horizons
+    assert horizon(eng) == 80 + H.SPEC_SLACK
+    eng.cfg = Cfg("spec_all_candidates")
+    assert horizon(eng) == -1
+    eng.cfg, eng.fsm = Cfg(), SimpleNamespace(leader_cap_size=lambda: 0)   # no leader cap: every candidate
+    assert horizon(eng) == -1
