@@ -327,6 +327,9 @@ def main() -> int:
             "host_cpu_ms_per_round": 1e3 * host_cpu / max(a.steps, 1),
             "thread_cpu_ms_per_round": mine["thread_cpu_ms_per_round"],
             "engine_stats": stats0,
+            # per committed block: how deep in the leader's candidate arrival order its rows reached, of how many
+            # candidates, and the leader's cap (the speculative horizon's input)
+            "spec_depths": [list(x) for x in getattr(eng, "spec_depth_log", [])][:a.warmup + a.steps],
             "table_gb": (eng.crypto.eng.table_bytes() / 1e9) if hasattr(getattr(eng, "crypto", None), "eng") else 0.0,
             "b0": getattr(getattr(getattr(eng, "crypto", None), "eng", None), "b0", None),
             "baseline_test_acc": ref_acc,

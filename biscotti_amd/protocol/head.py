@@ -385,6 +385,9 @@ class RoundHeadMixin:
         hist = self.__dict__.setdefault("_spec_depths", [])
         hist.append(d)
         del hist[:-SPEC_WINDOW]
+        log = self.__dict__.setdefault("spec_depth_log", [])   # (depth, candidates, leader cap) per block, for bench
+        if len(log) < 4096:
+            log.append((d, len(order), self.fsm.leader_cap_size()))
 
     def _early_vrf_submit(self, block_hash) -> None:
         """Start the next round's noiser VRF outputs as soon as the block that seeds them is built, before
