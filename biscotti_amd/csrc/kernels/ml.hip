@@ -15,6 +15,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#define BSC_PRIO_FLAG bsc_prio_on_ml
 #include "wave_prio.h"
 BSC_PRIO_SETTER(bsc_wave_prio_ml)
 

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "bn256_dev.h"
+#define BSC_PRIO_FLAG bsc_prio_on_msm
 #include "wave_prio.h"
 BSC_PRIO_SETTER(bsc_wave_prio_msm)
 

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define BSC_PRIO_FLAG bsc_prio_on_vrf
 #include "wave_prio.h"
 BSC_PRIO_SETTER(bsc_wave_prio_vrf)
 

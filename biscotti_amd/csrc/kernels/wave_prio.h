@@ -17,13 +17,19 @@
 // several ranks the engine turns them off (bsc_wave_prio(0)): RCCL's collective kernels run at the default
 // priority and spin on their peers' flags, and under prio-2 share MSMs of two ranks sharing a GPU a collective
 // stalled for 0.1-0.3 s (2-rank RCCL rehearsal).  Each kernel file holds its own flag (one per translation
-// unit) and exports its setter; kernels read it once, wave-uniformly.
-static __device__ int bsc_prio_on = 1;
+// unit, named by BSC_PRIO_FLAG before the include) and exports its setter; kernels read it once,
+// wave-uniformly.  The flag has external linkage on purpose: a `static` __device__ variable that the host
+// addresses is externalised with default visibility and read through the GOT (two dependent scalar loads at
+// every kernel's entry); a plain one is protected and costs one PC-relative load.
+#ifndef BSC_PRIO_FLAG
+#error "define BSC_PRIO_FLAG (a per-file name) before including wave_prio.h"
+#endif
+__device__ int BSC_PRIO_FLAG = 1;
 #define BSC_SET_PRIO(p)                                  \
   do {                                                   \
-    if (bsc_prio_on) __builtin_amdgcn_s_setprio(p);      \
+    if (BSC_PRIO_FLAG) __builtin_amdgcn_s_setprio(p);    \
   } while (0)
-#define BSC_PRIO_SETTER(name)                                                                      \
-  extern "C" int name(int on) {                                                                    \
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(bsc_prio_on), &on, sizeof(int), 0, hipMemcpyHostToDevice); \
+#define BSC_PRIO_SETTER(name)                                                                        \
+  extern "C" int name(int on) {                                                                      \
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(BSC_PRIO_FLAG), &on, sizeof(int), 0, hipMemcpyHostToDevice); \
   }
