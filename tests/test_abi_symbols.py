@@ -36,3 +36,17 @@ def test_every_declared_symbol_is_exported():
     lib = ctypes.CDLL(str(path))
     missing = sorted(n for n in _abi.SIGNATURES if not hasattr(lib, n))
     assert not missing, f"declared in _abi.SIGNATURES but not exported by {path.name}: {missing}"
+
+
+def test_no_static_device_variables_in_kernels():
+    """A `static __device__`/`__constant__` variable that the host addresses is externalised with default
+    visibility and read through the GOT (two dependent scalar loads per kernel entry, measured ~0.04 ms/round on
+    the wave-priority flags); kernel files use externally linked, per-file names instead (wave_prio.h)."""
+    bad = []
+    for p in sorted((_ROOT / "biscotti_amd" / "csrc" / "kernels").glob("*")):
+        if p.suffix in (".hip", ".h", ".hpp"):
+            for i, line in enumerate(p.read_text().splitlines(), 1):
+                if re.search(r"\bstatic\s+__(device|constant)__\s+(?!__forceinline__|inline)[\w:<>]+\s+\w+\s*[=;\[]",
+                             line):
+                    bad.append(f"{p.name}:{i}: {line.strip()}")
+    assert not bad, bad
