@@ -88,19 +88,46 @@ PRESETS = {
 
 
 def _host_threads() -> int:
-    """Native crypto pool per rank: the CPUs this job may use (cgroup quota, else the affinity mask)
-    shared by the node's local ranks, 4..16 (16 = one rank on a 16-CPU share of the 1-GPU box)."""
+    """Native crypto pool per rank: what the job's CPU quota leaves after every local rank's round thread,
+    HIP runtime and RCCL threads (utils/threadcpu.pool_threads)."""
     import os
 
-    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 16)
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if q != "max":
-            cpus = min(cpus, max(1, int(int(q) / int(per))))
-    except (OSError, ValueError):
-        pass
-    local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-    return max(4, min(16, cpus // max(1, local)))
+    from biscotti_amd.utils.threadcpu import pool_threads
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return pool_threads(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))), world)
+
+
+def _pct(vals: list) -> tuple:
+    v = sorted(vals)
+    return (round(1e3 * v[len(v) // 2], 4), round(1e3 * v[-1], 4)) if v else (None, None)
+
+
+def _pct_by_name(calls: list) -> dict:
+    """{collective: {n, p50_ms, max_ms}} of the host time inside each collective call."""
+    by: dict = {}
+    for name, s in calls:
+        by.setdefault(name, []).append(s)
+    out = {}
+    for name, v in sorted(by.items()):
+        p50, mx = _pct(v)
+        out[name] = {"n": len(v), "p50_ms": p50, "max_ms": mx}
+    return out
+
+
+def _phase_p50_max(round_phases: list) -> dict:
+    """{phase: [median ms, worst-round ms]} over the timed rounds (phases a round did not enter count 0)."""
+    keys = sorted({k for p in round_phases for k in p})
+    return {k: list(_pct([p.get(k, 0.0) for p in round_phases])) for k in keys}
+
+
+def _outliers(walls: list) -> dict:
+    if not walls:
+        return {}
+    med = sorted(walls)[len(walls) // 2]
+    return {"round_wall_p50_ms": round(1e3 * med, 4), "round_wall_max_ms": round(1e3 * max(walls), 4),
+            "rounds_over_3x_median": sum(w > 3 * med for w in walls),
+            "rounds_over_5x_median": sum(w > 5 * med for w in walls)}
 
 
 def _spawn_ranks(n: int) -> int:
@@ -133,6 +160,9 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=100, help="rounds the accuracy is quoted at (MAX_ITERATIONS)")
     ap.add_argument("--trace", default=None)
     ap.add_argument("--fedsys", action="store_true", help="same as --config fedsys")
+    ap.add_argument("--emulate-world", type=int, default=0, metavar="N",
+                    help="run rank 0 of an N-rank job alone on this GPU (other ranks' collective slots filled with "
+                         "rank 0's data): the per-rank cost of an N-GPU job, never a scaling number")
     ap.add_argument("--phase-sync", action="store_true",
                     help="synchronise the GPU at every phase boundary (per-phase GPU attribution, slower)")
     a = ap.parse_args()
@@ -158,11 +188,16 @@ def main() -> int:
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
-    comm = Comm.init()
+    if a.emulate_world > 1:
+        if world != 1 or a.gpus != 1:
+            raise SystemExit("--emulate-world runs one process on one GPU (--gpus 1, no torchrun)")
+        comm = Comm.emulated(a.emulate_world)
+    else:
+        comm = Comm.init()
     if comm.device.type == "cuda":
         # the GPU path does little CPU tensor work; idle-spinning OpenMP workers would only steal the
         # cgroup CPU quota from the native crypto pool
-        torch.set_num_threads(min(4, torch.get_num_threads()))
+        torch.set_num_threads(min(4, torch.get_num_threads()) if comm.world == 1 else 1)
     # lazy_eval: each round's two evaluation numbers are read back one round later (the kernels still run
     # inside the round); the accuracies below are read after drain()
     kw = dict(num_nodes=100, dataset="mnist", seed=a.seed, max_iterations=10**9, trace_file=a.trace,
@@ -202,9 +237,12 @@ def main() -> int:
 
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     th0 = threadcpu.snapshot()
+    cg0 = threadcpu.cgroup_cpu_stat()
+    comm.take_calls()
     t0 = time.perf_counter()
     last = None
     phases: dict = {}
+    round_phases: list = []
     results = []
     walls = []
     seg0 = torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) if eng.gpu else 0
@@ -215,6 +253,7 @@ def main() -> int:
         last = eng.run_round(last=k == a.steps - 1) if hasattr(eng, "drain") else eng.run_round()
         walls.append(time.perf_counter() - tr)
         results.append(last)
+        round_phases.append(last.phases)
         for k, v in last.phases.items():
             phases[k] = phases.get(k, 0.0) + v
     t_drain = time.perf_counter()
@@ -229,6 +268,8 @@ def main() -> int:
     seg_new = (torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) - seg0) if eng.gpu else 0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     th1 = threadcpu.snapshot()
+    cg = threadcpu.cgroup_delta(cg0, threadcpu.cgroup_cpu_stat())
+    calls = comm.take_calls()
     host_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)   # every thread of this rank
     stats0 = {k: v for k, v in getattr(eng, "stats", {}).items() if isinstance(v, (int, float))}
     per_step = 1e3 / max(a.steps, 1)
@@ -238,15 +279,23 @@ def main() -> int:
             "thread_cpu_ms_per_round": {k: round(v * per_step, 3)
                                         for k, v in list(threadcpu.delta_by_group(th0, th1).items())[:10]},
             "phase_ms_per_round": {k: round(v * per_step, 4) for k, v in sorted(phases.items())},
-            "engine_stats": stats0, "elapsed_s": elapsed}
+            "engine_stats": stats0, "elapsed_s": elapsed,
+            # stall attribution (docs/PERF.md, multi-rank stalls): the cgroup's CFS throttling over the timed window,
+            # the host time inside each collective call, per-phase median / worst round, and the round outliers
+            "cgroup_cpu_stat_delta": cg, "cpu_quota": threadcpu.cpu_quota(),
+            "collective_ms": _pct_by_name(calls),
+            "phase_ms_p50_max": _phase_p50_max(round_phases),
+            "round_wall_ms": [round(1e3 * w, 3) for w in walls],
+            **_outliers(walls)}
     per_rank = [mine]
-    if comm.world > 1:
+    real_world = 1 if comm.emulating else comm.world
+    if real_world > 1:
         import torch.distributed as dist
 
         per_rank = [None] * comm.world
         dist.all_gather_object(per_rank, mine)
     t = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
-    if comm.world > 1:
+    if real_world > 1:
         import torch.distributed as dist
 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -301,18 +350,21 @@ def main() -> int:
         headline = a.config == "headline"
         out = {
             "metric": ("sec/round (block commit) + final test acc, MNIST 100 peers" if headline else
-                       f"sec/round + final test acc, {a.config}"),
+                       f"sec/round + final test acc, {a.config}")
+                      + (f" [emulated rank 0 of {comm.world}: per-rank cost, not a scaling number]"
+                         if comm.emulating else ""),
             "value": s_per_round,
             "unit": "s/round",
-            "n_gpus": comm.world,
+            "n_gpus": real_world,
+            "emulated_world": comm.world if comm.emulating else None,
             "device": comm.device.type,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": 1e3 * s_per_round,
             "higher_is_better": False,
             "scaling": "strong",
-            "vs_baseline": s_per_round / ref_s if ref_s else None,
-            "speedup_vs_baseline": ref_s / s_per_round if ref_s else None,
+            "vs_baseline": s_per_round / ref_s if ref_s and not comm.emulating else None,
+            "speedup_vs_baseline": ref_s / s_per_round if ref_s and not comm.emulating else None,
             "final_test_acc": acc,
             "test_acc_last10_mean": last10[0],
             "accuracy_rounds": R,
@@ -326,6 +378,12 @@ def main() -> int:
             "round_wall_ms": [round(1e3 * w, 3) for w in walls],
             "host_cpu_ms_per_round": 1e3 * host_cpu / max(a.steps, 1),
             "thread_cpu_ms_per_round": mine["thread_cpu_ms_per_round"],
+            "cgroup_cpu_stat_delta": mine["cgroup_cpu_stat_delta"],
+            "cpu_quota": mine["cpu_quota"],
+            "host_threads": cfg.host_threads,
+            "collective_ms": mine["collective_ms"],
+            "phase_ms_p50_max": mine["phase_ms_p50_max"],
+            **_outliers(walls),
             "engine_stats": stats0,
             # per committed block: how deep in the leader's candidate arrival order its rows reached, of how many
             # candidates, and the leader's cap (the speculative horizon's input)
@@ -343,7 +401,10 @@ def main() -> int:
                                                    "lfw": "softmax regression 8742x2 (17486 params, SoftmaxModel)"}
                        .get(cfg.dataset, "logistic regression (25)"),
                        "peers": cfg.num_nodes, "global_batch": cfg.num_nodes * cfg.batch_size, "seq_len": 1,
-                       "parallelism": f"dp{comm.world} (virtual peers: {math.ceil(cfg.num_nodes / comm.world)}/GPU)",
+                       "parallelism": (f"emulated rank 0 of dp{comm.world} (virtual peers: "
+                                       f"{len(comm.peer_range(cfg.num_nodes))} on this GPU; collectives not timed)"
+                                       if comm.emulating else
+                                       f"dp{comm.world} (virtual peers: {math.ceil(cfg.num_nodes / comm.world)}/GPU)"),
                        "verifiers": cfg.num_verifiers, "aggregators": cfg.num_miners, "noisers": cfg.num_noisers,
                        "epsilon": cfg.epsilon, "ns_percent": cfg.perc_samples, "poisoning": cfg.poisoning,
                        "churn": cfg.churn, "secure_agg": cfg.secure_agg, "verification": cfg.verification,
@@ -359,7 +420,7 @@ def main() -> int:
             out["attack_rate_last10_mean_std"] = ms(att10)
         for k, v in ref_extra.items():
             out[f"baseline_{k}"] = v
-        if comm.world > 1:
+        if real_world > 1:
             out["per_rank"] = per_rank
         print(json.dumps(out), flush=True)
     comm.barrier()

@@ -1004,7 +1004,7 @@ extern "C" __global__ void __launch_bounds__(256) k_eval_error(const float* X, c
 // coalesced 256-byte load: the row-strided gathers and the per-element transform of k_eval_error are gone.
 extern "C" __global__ void __launch_bounds__(256) k_eval_error_t(const float* Xt, const int* y, int N, int KG, int D_IN,
                                                                 int D_OUT, const double* W, int split,
-                                                                unsigned int* err) {
+                                                                unsigned int* err, unsigned int* err_host) {
   BSC_SET_PRIO(BSC_PRIO_AHEAD);
   // 4 waves per tile split the K loop (latency: the evaluation is read one round later and must be done by
   // then under the share MSM's load), then reduce the logits through LDS
@@ -1066,6 +1066,20 @@ extern "C" __global__ void __launch_bounds__(256) k_eval_error_t(const float* Xt
   if (i == 0) {
     if (cnt0) atomicAdd(err, cnt0);
     if (cnt1) atomicAdd(err + 1, cnt1);
+  }
+  // err_host: the last tile to finish (counter err[2]) copies the two counts into pinned host memory and
+  // resets err[0..2] for the next launch -- no fill and no copy blit around the kernel on the stream (each
+  // waited ~20-40 us for a CU slot behind the share MSMs).  err[0..2] must be zero before the first launch.
+  if (err_host != nullptr) {
+    __threadfence();   // this wave's counts are visible before its tile is counted as done
+    if (lane == 0 && atomicAdd(err + 2, 1u) == gridDim.x - 1) {
+      __threadfence();
+      const unsigned int e0 = atomicExch(err, 0u), e1 = atomicExch(err + 1, 0u);
+      atomicExch(err + 2, 0u);
+      err_host[0] = e0;
+      err_host[1] = e1;
+      __threadfence_system();
+    }
   }
 }
 
@@ -1463,14 +1477,14 @@ extern "C" int bsc_eval_error_rb(const float* X, const int* y, int N, int D_IN, 
 extern "C" int bsc_eval_error_t_rb(const float* Xt, const int* y, int N, int KG, int D_IN, int D_OUT, const double* W,
                                    int split, unsigned int* err, unsigned int* err_host, void* stream) {
   if (D_OUT > 16 || D_IN <= 0 || KG * 4 < D_IN) return -1;
-  if (hipMemsetAsync(err, 0, 2 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) return -1;
-  if (N > 0) {
-    hipLaunchKernelGGL(k_eval_error_t, dim3((N + 15) / 16), dim3(256), 0, (hipStream_t)stream, Xt, y, N, KG, D_IN, D_OUT,
-                       W, split, err);
-    const int rc = (int)hipGetLastError();
-    if (rc != 0) return rc;
+  if (N <= 0) {
+    if (hipMemsetAsync(err, 0, 3 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) return -1;
+    return (int)hipMemcpyAsync(err_host, err, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, (hipStream_t)stream);
   }
-  return (int)hipMemcpyAsync(err_host, err, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, (hipStream_t)stream);
+  // err: 3 zeroed counters (two error counts + tiles done); the kernel's last tile writes err_host and re-zeroes
+  hipLaunchKernelGGL(k_eval_error_t, dim3((N + 15) / 16), dim3(256), 0, (hipStream_t)stream, Xt, y, N, KG, D_IN, D_OUT,
+                     W, split, err, err_host);
+  return (int)hipGetLastError();
 }
 
 extern "C" int bsc_noise_table(int nnoisers, int D, unsigned long long seed, float* tbl, void* stream) {

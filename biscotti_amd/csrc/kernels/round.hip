@@ -695,8 +695,12 @@ extern "C" int bsc_round_after_gather(void* ctx, const unsigned char* recv, int 
 // Host wait for an event: spin for SPIN_NS (the round's waits are tens to a few hundred us, and a sleeping
 // thread wakes late), then poll with short sleeps -- a long wait (ranks sharing a GPU, a collective behind a
 // slow rank) does not burn a core the way hipEventSynchronize's busy wait does (docs/PERF.md, multi-rank CPU).
+static long long g_spin_ns = 200000;   // bsc_set_host_spin_ns: the engine spins longer with one rank per process
+
+extern "C" void bsc_set_host_spin_ns(long long ns) { g_spin_ns = ns < 0 ? 0 : ns; }
+
 static int host_wait(hipEvent_t ev) {
-  constexpr long long SPIN_NS = 200000;
+  const long long SPIN_NS = g_spin_ns;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipEventQuery(ev);

@@ -73,6 +73,7 @@ SIGNATURES = {
     "bsc_round_secagg": [P, P, I, P, P, P, P, I, P, P, I, P, P, I, U64, U64, P, P, P, P, P, P, P, P, P, I],
     "bsc_round_audit": [P, P, P, P, P],
     "bsc_round_wait": [P, I],
+    "bsc_set_host_spin_ns": [L],
     "bsc_round_row_bytes": [I, I],
     "bsc_round_partials": [P, P, I, P, P, P, P, I, P, P, L, I],
     "bsc_round_combine": [P, P, I, L, P, P, I, P, P, I, U64, U64, P, P, P, P, P, P, P, P, P, I],
@@ -86,10 +87,15 @@ SIGNATURES = {
     "bsc_round_select_partials": [P, P, P, P, I, P, P, P, P, I, P, I, P, L, I],
     "bsc_round_after_gather": [P, P, I, L, I, P, P, I, I, I, P],
     "bsc_ring_pick": [P, I, P, P, P],
+    # gather.hip
+    "bsc_vg_limits": [P],
+    "bsc_vg_pack": [P, L, L, L, P, I, I, P, P, P, I, P],
+    "bsc_vg_unpack": [P, L, I, I, L, L, L, I, I, I, I, P, I, P, P, P, P, P],
 }
 
 
-RESTYPES = {"bsc_stream_create_cumask": C.c_void_p, "bsc_round_create": C.c_void_p, "bsc_round_destroy": None}
+RESTYPES = {"bsc_stream_create_cumask": C.c_void_p, "bsc_round_create": C.c_void_p, "bsc_round_destroy": None,
+            "bsc_set_host_spin_ns": None}
 
 
 def declare(lib) -> None:

@@ -461,14 +461,16 @@ def gram_split(U: int, rank: int, world: int) -> tuple[int, int, int, int]:
     return p0, min(npairs, p0 + chunk), chunk, npairs
 
 
-def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | None = None) -> dict:
+def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | None = None, out=None) -> dict:
     """Noise-aware committee Krum, phase 1: f64 Gram of the stacked rows [X; T_rows].
 
     X fp32 [U1, d] (the workers' deltas, contiguous); T_rows fp32 [U2, d] with contiguous rows (a
     strided view of the resident noise table at this iteration).  Runs before the noisers are known.
     split = (rank, world): this rank computes only its share of the tile pairs (gram_split) into rows
     [rank * chunk, ...) of a [world * chunk, 256] buffer; the caller all_gathers the ranks' slots
-    (gram_slot) and calls gram_adopt.  Returns the handle krum_committee_noise_async consumes."""
+    (gram_slot) and calls gram_adopt.  out (GPU, split): this rank's [chunk, 256] slot is written there
+    instead (the packed verification row, ops/gather.py).  Returns the handle krum_committee_noise_async
+    consumes."""
     U1, D = X.shape
     U2 = T_rows.shape[0]
     assert X.is_contiguous() and T_rows.stride(1) == 1 and T_rows.shape[1] == D
@@ -491,14 +493,22 @@ def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | No
     nsplit = (D + kchunk - 1) // kchunk
     dev = X.device
     part = torch.empty((nsplit, max(1, p1 - p0), 256), dtype=torch.float64, device=dev)
-    gram = torch.empty((chunk * (split[1] if split else 1), 256), dtype=torch.float64, device=dev)
+    if out is not None:
+        assert split is not None and out.dtype == torch.float64 and tuple(out.shape) == (chunk, 256)
+        gram = out
+        base = out.data_ptr() - p0 * 256 * 8   # the kernel indexes its output by the global pair index
+    else:
+        gram = torch.empty((chunk * (split[1] if split else 1), 256), dtype=torch.float64, device=dev)
+        base = gram.data_ptr()
     _check(hip().bsc_gram_stacked_range(_p(X), U1, T_rows.data_ptr(), U2, T_rows.stride(0), D, kchunk, p0, p1,
-                                        _p(part), _p(gram), _p(_tile_counters(dev, max(1, p1 - p0))), _stream()),
+                                        _p(part), base, _p(_tile_counters(dev, max(1, p1 - p0))), _stream()),
            "gram_stacked")
-    out = {"gram": gram, "U1": U1, "U": U, "keep": (X, T_rows, part)}
+    res = {"gram": gram, "U1": U1, "U": U, "keep": (X, T_rows, part)}
     if split is not None:
-        out["split"] = (rank, chunk, npairs)
-    return out
+        res["split"] = (rank, chunk, npairs)
+        if out is not None:
+            res["packed"] = True
+    return res
 
 
 def gram_slot(pre: dict) -> torch.Tensor:
@@ -597,7 +607,9 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True, Xt=None)
     host = pinned("eval", (2,), torch.int32, depth=4)
     err = _EVAL_DEV.get(host.data_ptr())
     if err is None:
-        err = _EVAL_DEV[host.data_ptr()] = torch.empty((2,), dtype=torch.int32, device=X.device)
+        # [errors of rows < split, errors of the rest, tiles done]: zero before the first launch, and
+        # k_eval_error_t's last tile re-zeroes it when it writes the host copy
+        err = _EVAL_DEV[host.data_ptr()] = torch.zeros((4,), dtype=torch.int32, device=X.device)
     if Xt is not None:   # cached pre-transformed tiles (k_eval_error_t)
         assert Xt.shape[0] == (N + 15) // 16 and Xt.shape[1] * 4 >= d_in and Xt.shape[2] == 64
         _check(hip().bsc_eval_error_t_rb(_p(Xt), _p(y), N, Xt.shape[1], d_in, d_out, _p(W), int(split), _p(err),

@@ -22,7 +22,9 @@ and the plumbing configuration.
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+import time
+from collections import deque
+from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
@@ -42,6 +44,10 @@ class Comm:
     rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    # (collective, host seconds inside the call) of every collective since the last take_calls(): with RCCL the
+    # call returns once the kernel is queued, so a long one means the host thread itself was held (a CFS quota
+    # throttle, the GIL, a full queue); with gloo it is the whole exchange
+    calls: deque = field(default_factory=lambda: deque(maxlen=16384))
 
     # ------------------------------------------------------------------ setup
     @staticmethod
@@ -117,6 +123,29 @@ class Comm:
             mark_new_threads(f"comm-{be}")
         return c
 
+    @staticmethod
+    def emulated(world: int, device: str | None = None) -> "Comm":
+        """Rank 0 of a `world`-rank job, alone in this process (bench.py --emulate-world): the engine hosts
+        rank 0's peers and does exactly rank 0's work -- its local step, commitments and VRF outputs, its
+        slice of the Gram tiles, its partial sums, then the replicated recovery, audit and block -- while
+        every collective fills the other ranks' slots with rank 0's own contribution (deterministic, the
+        same bytes an all_gather would deliver in shape, not in value).  Measures what one rank of an
+        N-GPU job costs per round on a one-GPU box; collective latency is not included."""
+        from ..utils.threadcpu import mark_new_threads
+
+        mark_new_threads("pre-init")
+        if device != "cpu" and torch.cuda.is_available():
+            dev = torch.device("cuda", torch.cuda.current_device())
+            torch.empty(1, device=dev)
+            mark_new_threads("hip-runtime")
+        else:
+            dev = torch.device("cpu")
+        return Comm(int(world), 0, dev, "emulated")
+
+    @property
+    def emulating(self) -> bool:
+        return self.backend == "emulated"
+
     def ranks_sharing_device(self) -> int:
         """Ranks whose GPU is this rank's GPU (same host, same device UUID), from one all_gather_object
         at start-up -- HIP_VISIBLE_DEVICES isolation, shared boxes and multi-node jobs all count right."""
@@ -133,7 +162,7 @@ class Comm:
         return sum(1 for o in everyone if o[:2] == me[:2])
 
     def shutdown(self) -> None:
-        if self.world > 1 and dist.is_initialized():
+        if self.world > 1 and not self.emulating and dist.is_initialized():
             dist.destroy_process_group()
 
     # ------------------------------------------------------------------ ownership
@@ -151,10 +180,44 @@ class Comm:
         return max(len(self.peer_range(num_peers, r)) for r in range(self.world))
 
     # ------------------------------------------------------------------ collectives
+    # ------------------------------------------------------------------ the collectives' stream
+    def _comm_stream(self):
+        """ONE stream for every RCCL collective of this communicator.  torch issues a synchronous collective on
+        the caller's current stream, and the round issues them from two streams (the deltas' gather for the
+        split Gram on the Gram stream, the verification and aggregation gathers on the main stream): two
+        kernels of one communicator could then run concurrently, or in a different order on each rank --
+        undefined for RCCL (ranks' channel FIFOs pair up op by op), seen as 50-330 ms stalls of the 2-rank
+        rehearsal (docs/PERF.md).  Collectives run here in issue order, which every rank shares."""
+        st = getattr(self, "_cstream", None)
+        if st is None and self.backend == "nccl":
+            st = self._cstream = torch.cuda.Stream(device=self.device,
+                                                   priority=torch.cuda.Stream.priority_range()[1])
+        return st
+
+    def _ordered(self, fn):
+        """Run fn() (one collective) on the comm stream, ordered after the caller's stream and before its
+        later work."""
+        cs = self._comm_stream()
+        if cs is None:
+            return fn()
+        from ..utils import streams as S
+
+        cur = S.current()
+        S.wait(cs, cur)
+        with S.use(cs):
+            r = fn()
+        S.wait(cur, cs)
+        return r
+
+    def take_calls(self) -> list:
+        out = list(self.calls)
+        self.calls.clear()
+        return out
+
     def barrier(self) -> None:
-        if self.world > 1:
+        if self.world > 1 and not self.emulating:
             if self.backend == "nccl":
-                dist.barrier(device_ids=[self.device.index])
+                self._ordered(lambda: dist.barrier(device_ids=[self.device.index]))
             else:
                 dist.barrier()
 
@@ -165,7 +228,12 @@ class Comm:
             return t.unsqueeze(0)
         flat = t.reshape(-1)
         out = torch.empty((self.world * flat.numel(),), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, flat)
+        t0 = time.perf_counter()
+        if self.emulating:
+            out.view(self.world, -1).copy_(flat.unsqueeze(0).expand(self.world, -1))
+        else:
+            self._ordered(lambda: dist.all_gather_into_tensor(out, flat))
+        self.calls.append(("all_gather", time.perf_counter() - t0))
         return out.view(self.world, *t.shape)
 
     def all_gather_into(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
@@ -174,7 +242,17 @@ class Comm:
         if self.world == 1:
             out[0].copy_(t)
             return out
-        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1))
+        t0 = time.perf_counter()
+        if self.emulating:
+            flat = out.view(self.world, -1)
+            if t.data_ptr() == flat[0].data_ptr():   # in place: rank 0's row is the source
+                flat[1:].copy_(flat[0:1].expand(self.world - 1, -1))
+            else:
+                flat.copy_(t.reshape(1, -1).expand(self.world, -1))
+        else:
+            src = t.contiguous().view(-1)
+            self._ordered(lambda: dist.all_gather_into_tensor(out.view(-1), src))
+        self.calls.append(("all_gather_into", time.perf_counter() - t0))
         return out
 
     def all_gather_packed(self, parts: list[torch.Tensor]) -> list[torch.Tensor]:
@@ -194,6 +272,8 @@ class Comm:
         return out
 
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
-        if self.world > 1:
-            dist.broadcast(t, src)
+        if self.world > 1 and not self.emulating:
+            t0 = time.perf_counter()
+            self._ordered(lambda: dist.broadcast(t, src))
+            self.calls.append(("broadcast", time.perf_counter() - t0))
         return t

@@ -476,9 +476,12 @@ def read_message(stream, limit: int = MAX_MESSAGE) -> bytes:
 
 
 def _read_exact(stream, n: int) -> bytes:
+    """n bytes, read in pieces of at most 1 MB: a declared length is only a claim, so memory grows with the
+    bytes that actually arrive instead of being reserved up front (a buffered socket file's read(n) allocates
+    n bytes at once)."""
     buf = bytearray()
     while len(buf) < n:
-        chunk = stream.read(n - len(buf))
+        chunk = stream.read(min(n - len(buf), 1 << 20))
         if not chunk:
             raise EOFError("gob: stream ended inside a message")
         buf += chunk

@@ -40,14 +40,14 @@ def _send(sock, data: bytes) -> None:
 
 
 class _ValueReader:
-    """Reads values (skipping type definitions) off a gob stream."""
+    """Reads values (skipping type definitions) off a gob stream; messages over `limit` bytes are refused."""
 
-    def __init__(self, stream):
-        self.stream, self.dec = stream, G.Decoder()
+    def __init__(self, stream, limit: int = G.MAX_MESSAGE):
+        self.stream, self.dec, self.limit = stream, G.Decoder(), limit
 
     def next(self):
         while True:
-            payload = G.read_message(self.stream)
+            payload = G.read_message(self.stream, self.limit)
             r = G._Reader(payload)
             if r.int() < 0:
                 self.dec.feed_message(payload)
@@ -59,18 +59,21 @@ class RpcServer:
     """net/rpc server: handlers maps "Peer.Method" -> (arg schema, reply schema, fn(args) -> reply).  One
     thread per connection, calls on a connection served in order (Go serves them concurrently; the
     reference's clients issue one call per connection).  At most `max_conns` connections are served at
-    once (further ones are closed on accept) and a connection idle for `idle_s` is dropped, so a peer
-    cannot exhaust the server's threads; gob messages are size-bounded (gob.read_message)."""
+    once; further ones wait in the listen backlog until a slot frees (a verifier holds one connection per
+    worker until its Krum threshold, so closing them would starve the threshold -- size max_conns from the
+    peer count, `conns_for`).  A connection idle for `idle_s` is dropped, and gob messages over
+    `max_message` bytes are refused before their body is read, so a peer cannot exhaust the server's
+    threads or memory."""
 
-    def __init__(self, handlers: dict, host: str = "127.0.0.1", port: int = 0, max_conns: int = 64,
-                 idle_s: float = 120.0):
+    def __init__(self, handlers: dict, host: str = "127.0.0.1", port: int = 0, max_conns: int = 256,
+                 idle_s: float = 120.0, max_message: int = G.MAX_MESSAGE):
         self.handlers = handlers
         self._slots = threading.BoundedSemaphore(max_conns)
-        self.idle_s = idle_s
+        self.idle_s, self.max_message = idle_s, max_message
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self.sock.bind((host, port))
-        self.sock.listen(64)
+        self.sock.listen(max(128, 2 * max_conns))
         self.addr = self.sock.getsockname()
         self._stop = False
         self._thr = threading.Thread(target=self._accept, daemon=True)
@@ -88,19 +91,20 @@ class RpcServer:
 
     def _accept(self) -> None:
         while not self._stop:
+            # a free slot first: while every slot is busy, new connections queue in the kernel's backlog
+            if not self._slots.acquire(timeout=0.25):
+                continue
             try:
                 conn, _ = self.sock.accept()
             except OSError:
+                self._slots.release()
                 return
-            if not self._slots.acquire(blocking=False):
-                conn.close()   # too many open connections
-                continue
             conn.settimeout(self.idle_s)
             threading.Thread(target=self._serve, args=(conn,), daemon=True).start()
 
     def _serve(self, conn) -> None:
         f = conn.makefile("rb")
-        rd, enc = _ValueReader(f), G.Encoder()
+        rd, enc = _ValueReader(f, self.max_message), G.Encoder()
         try:
             while True:
                 try:
@@ -132,6 +136,18 @@ class RpcServer:
 
 class RpcError(RuntimeError):
     pass
+
+
+def conns_for(num_nodes: int) -> int:
+    """Connections a peer's server may hold at once: every other peer's VerifyUpdateKRUM (held until the Krum
+    threshold) plus its concurrent RequestNoise / RegisterSecret / RegisterBlock calls."""
+    return 2 * max(1, int(num_nodes)) + 16
+
+
+def message_limit(dim: int, num_nodes: int) -> int:
+    """Largest gob message a peer expects: a block of every peer's update (three float64 vectors of `dim`,
+    <= 9 bytes per gob float, plus commitments and signatures) dominates; 1 MB of envelope slack."""
+    return (1 << 20) + 32 * max(1, int(dim)) * (max(1, int(num_nodes)) + 1)
 
 
 def call(addr: str, method: str, arg_schema, args, timeout: float = 30.0):
@@ -204,15 +220,20 @@ class PeerService:
     them between rounds (take_blocks) -- the reference's asynchronous processBlock, without a second
     writer racing the round's commit.  live=False (a follower / the `serve` CLI): the service owns the
     chain and appends extensions itself.  Per-iteration state (inboxes, decisions, shares, updates) is
-    kept for the last KEEP_ITERATIONS iterations only."""
+    kept for the last KEEP_ITERATIONS iterations only, measured from this peer's OWN progress (its chain's next
+    iteration, or `progress()`): a message more than AHEAD_ITERATIONS past it is refused, so no remote
+    Iteration field can evict the current round's state (the reference's RegisterUpdate / processBlock
+    likewise judge staleness against the peer's own iterationCount)."""
 
     KEEP_ITERATIONS = 4
+    AHEAD_ITERATIONS = 4
     MAX_QUEUED_BLOCKS = 64
 
     def __init__(self, rt, chain, peer_id: int = 0, sk: bytes | None = None, noise=None, krum_thresh: int = 1,
                  krum_timeout_s: float = 10.0, lock: threading.Lock | None = None, live: bool = False,
-                 dim: int | None = None):
+                 dim: int | None = None, progress=None):
         self.rt, self.chain, self.id, self.sk, self.noise = rt, chain, peer_id, sk, noise
+        self._progress = progress
         self.lock = lock or threading.Lock()
         self.live, self.dim = live, dim
         self.peers: list = []           # addresses announced through RegisterPeer
@@ -224,22 +245,35 @@ class PeerService:
         self._updates: dict = {}        # iteration -> [Update values]
         self._blocks: list = []         # live: verified blocks waiting for the engine (take_blocks)
         self.block_log: list = []       # (iteration, outcome) of every RegisterBlock, newest last (bounded)
-        self._newest = -1
 
     def _note(self, it: int, what: str) -> None:
         self.block_log.append((it, what))
         del self.block_log[:-256]
 
-    def _prune(self, it: int) -> None:
-        """Forget per-iteration state older than the newest iteration seen minus KEEP_ITERATIONS (caller holds
-        the lock)."""
-        if it <= self._newest:
-            return
-        self._newest = it
-        lo = it - self.KEEP_ITERATIONS
+    def current_iteration(self) -> int:
+        """The iteration this peer is working on: progress(), else its chain's latest block + 1."""
+        if self._progress is not None:
+            return int(self._progress())
+        return int(self.chain.latest().data.iteration) + 1
+
+    def _admit(self, it: int) -> None:
+        """Refuse a message whose iteration is outside [current - KEEP, current + AHEAD] and forget state
+        older than current - KEEP (caller holds the lock).  The window moves with this peer's own progress
+        only: the largest Iteration a remote peer sends decides nothing."""
+        cur = self.current_iteration()
+        lo = cur - self.KEEP_ITERATIONS
         for d in (self._inbox, self._decided, self._secrets, self._updates):
             for k in [k for k in d if k < lo]:
                 del d[k]
+        if it < lo:
+            raise ValueError(f"stale message for iteration {it} (this peer is at {cur})")
+        if it > cur + self.AHEAD_ITERATIONS:
+            raise ValueError(f"message for iteration {it} too far ahead (this peer is at {cur})")
+
+    def secrets_of(self, it: int) -> dict:
+        """{NodeID: MinerPartRPC value} stored for iteration it (a copy)."""
+        with self.lock:
+            return dict(self._secrets.get(it, {}))
 
     def handlers(self) -> dict:
         return {
@@ -334,20 +368,23 @@ class PeerService:
         if self.dim is not None and len(row) != self.dim:
             raise ValueError(f"update of length {len(row)}: the model has {self.dim} parameters")
         with self._cv:
-            self._prune(it)
-            if it < self._newest - self.KEEP_ITERATIONS:
-                raise ValueError(f"stale update for iteration {it}")
+            self._admit(it)
             box = self._inbox.setdefault(it, [])
             box.append(u)
             if len(box) >= self.krum_thresh:
                 self._cv.notify_all()
             deadline = time.monotonic() + self.krum_timeout_s
             while it not in self._decided:
+                if it not in self._inbox:   # this peer moved past the iteration while we waited
+                    raise ValueError(f"stale update for iteration {it}")
                 if len(self._inbox[it]) >= self.krum_thresh or time.monotonic() >= deadline:
                     self._decide(it, K, torch)
                     break
                 self._cv.wait(timeout=max(0.0, deadline - time.monotonic()))
-            ok = self._decided[it].get(int(u.get("SourceID") or 0), False)
+            dec = self._decided.get(it)
+            if dec is None:
+                raise ValueError(f"stale update for iteration {it}")
+            ok = dec.get(int(u.get("SourceID") or 0), False)
         if not ok:
             raise ValueError("update rejected by Multi-Krum")
         if self.sk is None:
@@ -374,14 +411,14 @@ class PeerService:
     def register_secret(self, part: dict) -> bool:
         with self.lock:
             it = int(part.get("Iteration") or 0)
-            self._prune(it)
+            self._admit(it)
             self._secrets.setdefault(it, {})[int(part.get("NodeID") or 0)] = part
             return True
 
     def register_update(self, u: dict) -> bool:
         with self.lock:
             it = int(u.get("Iteration") or 0)
-            self._prune(it)
+            self._admit(it)
             self._updates.setdefault(it, []).append(u)
             return True
 
@@ -453,7 +490,8 @@ def main(argv=None) -> int:
     R = rt()
     if a.cmd == "serve":
         chain = R.Blockchain.load(a.chain_file) if a.chain_file else R.Blockchain.with_genesis(0)
-        srv = RpcServer(PeerService(R, chain).handlers(), a.host, a.port).start()
+        srv = RpcServer(PeerService(R, chain).handlers(), a.host, a.port,
+                        max_message=message_limit(len(chain.latest().data.global_w), 256)).start()
         print(f"serving {len(chain)} blocks on {srv.addr[0]}:{srv.addr[1]}", flush=True)
         t0 = time.time()
         while not a.seconds or time.time() - t0 < a.seconds:

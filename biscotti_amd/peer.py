@@ -82,7 +82,8 @@ def main(argv=None) -> int:
         svc = netrpc.PeerService(eng.R, eng.fsm.chain, peer_id=me, sk=eng.sk[me],
                                  noise=lambda it: eng.task.noise_scale(eng.sigma) * _noise_row(eng, me, it),
                                  krum_thresh=max(1, eng.pc.krum_thresh), live=True, dim=eng.d)
-        srv = netrpc.RpcServer(svc.handlers(), host, int(port)).start()
+        srv = netrpc.RpcServer(svc.handlers(), host, int(port), max_conns=netrpc.conns_for(cfg.num_nodes),
+                               max_message=netrpc.message_limit(eng.d, cfg.num_nodes)).start()
         eng.log.info("serving Peer net/rpc on %s:%d", *srv.addr)
     n = 0
     while ns.rounds is None or n < ns.rounds:

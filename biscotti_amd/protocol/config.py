@@ -59,6 +59,9 @@ class RunConfig:
     resume: bool = False
     device: str | None = None       # "cpu" forces the CPU path
     log_every_peer: bool = False    # one Train Error line per local peer (reference style)
+    phase_log: bool = False         # the reference's role / phase lines (Verifiers are, Getting noise from, Sending
+    #                                 update to verifiers / miners, Got share for, Sending block of iteration) so its
+    #                                 parseLogs.py phase breakdown works on our logs (protocol/golog.py)
     deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
     phase_sync: bool = False        # device sync at phase boundaries (diagnostics: per-phase GPU times)
     audit_aggregate: bool = True    # check the recovered aggregate against the miners' summed chunk
@@ -85,12 +88,14 @@ class RunConfig:
     #   spec_all_candidates GPU: the speculative share MSM covers every candidate (every approved worker's
     #                      shares, as each reference worker computes its own), not only the leader's first
     #                      arrivals up to the adaptive horizon (head.py SPEC_MARGIN): the chain must not change
+    #   short_spin         GPU: host waits spin 200 us before polling with sleeps also with one rank (the
+    #                      multi-rank setting; one rank spins up to 5 ms: a sleeping thread wakes late)
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
     churn_round_s: ClassVar[float] = 25.44
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
-                                  "spec_head_shared", "spec_all_candidates")
+                                  "spec_head_shared", "spec_all_candidates", "short_spin")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""
@@ -251,6 +256,8 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--device", default=None)
     ap.add_argument("--log-every-peer", action="store_true")
+    ap.add_argument("--phase-log", action="store_true",
+                    help="write the reference's role and phase log lines (parseLogs.py breakdowns)")
     ap.add_argument("--deterministic-time", action="store_true")
     ap.add_argument("--phase-sync", action="store_true",
                     help="synchronise the device at every phase boundary (per-phase GPU times; slower)")

@@ -38,7 +38,7 @@ from ..native import rt
 from ..ops import bn256 as B
 from ..ops import ml as K
 from ..parallel.comm import Comm
-from ..utils import JsonlWriter, PhaseTimer, fast_info, flush_logs, get_logger
+from ..utils import JsonlWriter, PhaseTimer, StampedPhaseTimer, fast_info, flush_logs, get_logger
 from ..utils import streams as S
 from .config import RunConfig
 from .crypto_backends import DeviceCrypto, HostCrypto
@@ -101,8 +101,13 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.trace = JsonlWriter(cfg.trace_file if self.comm.rank == 0 else None)
         # phase_sync: synchronise the device at every phase boundary so GPU time lands in its phase
         # (diagnostics); off, phase times are host-side and the device pipeline runs undisturbed
-        self.timer = PhaseTimer(sync=(lambda: torch.cuda.synchronize(self.dev))
-                                if self.gpu and cfg.phase_sync else None)
+        self.timer = (StampedPhaseTimer if cfg.phase_log else PhaseTimer)(
+            sync=(lambda: torch.cuda.synchronize(self.dev)) if self.gpu and cfg.phase_sync else None)
+        self.golog = None
+        if cfg.phase_log:
+            from .golog import GoPhaseLog
+
+            self.golog = GoPhaseLog(self.log, self.lo, self.N, log_dir=cfg.log_dir, world=self.comm.world)
         # ---- data / model
         from ..data import dataset_dims
         from ..models import make_task
@@ -149,6 +154,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             # wave priority classes (kernels/wave_prio.h): one rank drives its GPU alone; with several ranks the
             # collectives' kernels must not queue behind prio-2 share MSMs
             B.set_wave_priorities(self.comm.world == 1)
+            S.set_spin(5e-3 if self.comm.world == 1 and not cfg.has("short_spin") else 2e-4)
             self._native = B.NativeSecAgg(self.crypto.eng, self.main_stream, self.side_stream, self.bg_stream,
                                           10.0 ** cfg.precision, witness=self.witness_stream)
             if self.comm.world > 1:
@@ -314,6 +320,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         """Join the pre-opened round's native VRF jobs and drain the device.  Idempotent; also registered
         with atexit so interpreter teardown never races native threads."""
         flush_logs(self.log)
+        if self.golog is not None:
+            self.golog.flush()
         self.drain()
         head, self._head = self._head, None
         if head:
@@ -426,7 +434,16 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 self.W = W_dev
             elif n_up:
                 self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
-            eval_pending = self.task.evaluate_async(self.W)   # queued ahead of the next round's MSMs
+            if self.gpu:
+                # on the witness stream (low priority; nothing in the round waits for either): on the main
+                # stream the evaluation sat between the audit and the next round's Krum kernels
+                ws = self.witness_stream
+                S.wait(ws, S.current())
+                S.hold(self.W)   # read on another stream: kept for two rounds
+                with S.use(ws):
+                    eval_pending = self.task.evaluate_async(self.W)
+            else:
+                eval_pending = self.task.evaluate_async(self.W)
         with tm.phase("next_head"):
             self._head = self._open_round()   # next round's committee + VRF outputs start now
         if self._idle_work is not None:  # every rank, same point: the collective stays aligned
@@ -446,6 +463,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         if n_up:
             self._note_block_depth(head, self._last_nodes)
         accepted_map = v["accepted_map"]
+        if self.golog is not None:
+            self.golog.round(it, plan, tm.take_stamps(), noisers, approved, cfg.secure_agg, cfg.noising)
         res = RoundResult(iteration=it, block_hash=bytes(block.hash), empty=n_up == 0,
                           node_list=self._last_nodes, approved=list(approved), verifiers=list(plan.verifiers),
                           miners=list(plan.miners), test_error=ev["test_error"], attack_rate=ev["attack_rate"],

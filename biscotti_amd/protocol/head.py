@@ -230,10 +230,17 @@ class RoundHeadMixin:
         comm = self.comm
         X = comm.all_gather(buf).reshape(-1, d) if comm.world > 1 else buf
         # several ranks: each computes 1/world of the Gram's tile pairs; the tiles travel with the
-        # commitments + noiser ids in the verification all_gather (_gather_verify_inputs)
+        # commitments + noiser ids in the verification all_gather (_gather_verify_inputs) -- on a GPU written
+        # straight into this rank's row of the packed gather buffer (ops/gather.py)
+        vg = self._vgather() if comm.world > 1 else None
+        if vg is not None and S.current().stream_id != self.gram_stream.stream_id:
+            # a discarded pre-step may still write this iteration's slot on the Gram stream
+            S.wait(S.current(), self.gram_stream)
         g = K.gram_stacked_async(X.contiguous(), self.noise_rows.rows(it),
-                                 split=(comm.rank, comm.world) if comm.world > 1 else None)
+                                 split=(comm.rank, comm.world) if comm.world > 1 else None,
+                                 out=vg.gram_out(it) if vg is not None else None)
         g["xrow"] = self.flat
+        g["it"] = it
         return g
 
     # ------------------------------------------------------------------ cross-round pipelining

@@ -67,7 +67,8 @@ class RpcPeer:
                                  krum_thresh=max(1, self.pc.krum_thresh), krum_timeout_s=timeout_s, live=True,
                                  dim=self.d)
         h, p = self.addrs[self.id].rsplit(":", 1) if port is None else (host, port)
-        self.srv = N.RpcServer(self.svc.handlers(), h, int(p)).start()
+        self.srv = N.RpcServer(self.svc.handlers(), h, int(p), max_conns=N.conns_for(self.N),
+                               max_message=N.message_limit(self.d, self.N)).start()
         self.W = np.asarray(self.fsm.chain.latest().data.global_w, np.float64)
         self.log: list = []   # (iteration, event) -- what this peer did in each round
 
@@ -136,8 +137,7 @@ class RpcPeer:
         thresh = max(1, fsm.leader_cap_size()) if cfg.verification else max(1, self.pc.krum_thresh // 2)
         deadline = time.monotonic() + self.timeout
         while time.monotonic() < deadline:
-            with self.svc.lock:
-                have = len(self.svc._secrets.get(it, {}))
+            have = len(self.svc.secrets_of(it))
             if have >= thresh:
                 break
             time.sleep(0.01)
@@ -150,9 +150,9 @@ class RpcPeer:
             parts = get_secret_shares(miners, node_list, self.timeout)
             if len(parts) == len(miners):
                 W_new = recover_from_parts(R, parts, cfg.poly_size, self.d, self.W, cfg.precision)
-                with self.svc.lock:
-                    mine = self.svc._secrets.get(it, {})
-                    comms = [bytes(mine[w].get("CommitmentUpdate") or bytes(64)) for w in node_list]
+                mine = self.svc.secrets_of(it)
+                comms = [bytes(mine[w].get("CommitmentUpdate") or bytes(64)) if w in mine else bytes(64)
+                         for w in node_list]
                 now = it + 1 if cfg.deterministic_time else int(time.time())
                 block = fsm.make_secagg_block(W_new, node_list, comms, now)
         if block is None:   # no quorum before the deadline: the reference's empty block
@@ -162,10 +162,13 @@ class RpcPeer:
         return block
 
     def _await_block(self, it: int):
+        """The first flooded block of iteration `it` that verified and extends this peer's chain (processBlock,
+        main.go:1238-1330); the empty block after the deadline."""
         deadline = time.monotonic() + 3 * self.timeout
+        tip = bytes(self.fsm.chain.latest().hash)
         while time.monotonic() < deadline:
             for it_b, kind, b in self.svc.take_blocks():
-                if int(it_b) == it and kind == "ahead":
+                if int(it_b) == it and kind == "ahead" and bytes(b.prev_hash) == tip:
                     return b
             time.sleep(0.005)
         return self.fsm.make_empty_block()

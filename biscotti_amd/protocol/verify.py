@@ -219,10 +219,50 @@ class VerifyMixin:
         return [bool(a) for a in acc.cpu().tolist()]
 
     # ------------------------------------------------------------------ the verification phase
+    def _vgather(self):
+        """The packed verification gather (ops/gather.py) for several ranks on GPUs with the noise-aware Krum,
+        when its kernels' argument blocks hold this layout; None otherwise (the tensor path below)."""
+        vg = self.__dict__.get("_vg")
+        if vg is None:
+            vg = False
+            if self.gpu and self.comm.world > 1 and self._noise_krum():
+                from ..ops.gather import VerifyGather
+
+                nn_ = self.cfg.num_noisers
+                if VerifyGather.fits(self.maxlocal, nn_, self.N):
+                    U = self.comm.world * self.maxlocal + self.N
+                    _, _, chunk, npairs = K.gram_split(U, self.comm.rank, self.comm.world)
+                    vg = VerifyGather(self.comm, self.maxlocal, self.crypto.point_width, nn_, chunk, npairs, self.N,
+                                      self.dev)
+            self._vg = vg
+        return vg or None
+
+    def _gather_verify_packed(self, vg, head: dict, noisers: dict):
+        """_gather_verify_inputs with the packed row: one pack kernel, the in-place all_gather, one unpack
+        kernel (the workers' commitment rows land in pinned memory)."""
+        pre = head["krum_pre"]
+        nz_np, sc_np = self._noise_ids_np(noisers, head["local_workers"])
+        rows = self.crypto.commit_rows_tensor(head["pending_commits"]).to(self.dev)
+        src = [-1] * self.maxlocal
+        row_of = head["row_of"]
+        for w in head["local_workers"]:
+            src[w - self.lo] = row_of[w]
+        if self.gpu and "ev" in pre:   # the Gram slot is written on the Gram stream
+            S.current().wait_event(pre["ev"])
+        gram, nz, sc, host, ev = vg.exchange(pre["it"], rows.contiguous(), src, nz_np, sc_np,
+                                             [self.flat[w] for w in head["workers"]])
+        pre["gram"] = gram
+        pre.pop("split", None)
+        head["commit_gather"] = (host, ev)
+        return nz, sc
+
     def _gather_verify_inputs(self, head: dict, noisers: dict):
         """Several ranks, noise-aware Krum: ONE all_gather of every rank's [commitment rows | noiser ids
         | noiser weights] in the flat layout (each rank computed only its own workers' VRF outputs), the
         commitments' read-back queued right behind it.  Returns (nz, sc) [U1, nn] on the device."""
+        pre = head.get("krum_pre")
+        if pre is not None and pre.get("packed"):
+            return self._gather_verify_packed(self._vgather(), head, noisers)
         nz_np, sc_np = self._noise_ids_np(noisers, head["local_workers"])
         nz_l, sc_l = h2d_many([(nz_np, torch.int32), (sc_np, torch.float32)], self.dev)
         parts = [self._local_commit_buf(head), nz_l, sc_l]

@@ -83,6 +83,22 @@ def fast_info(lg: logging.Logger, where: str, msg: str) -> None:
         h.flush()
 
 
+def fast_info_at(lg: logging.Logger, where: str, msg: str, when: float) -> None:
+    """fast_info with the line's timestamp given (wall-clock seconds): lines written after the fact for
+    instants recorded earlier in the round (protocol/golog.py)."""
+    if not lg.isEnabledFor(logging.INFO):
+        return
+    h = lg.handlers[0] if lg.handlers else None
+    if not isinstance(h, _BatchingHandler) or not isinstance(h.formatter, _GoFormatter):
+        lg.info("%s", msg)
+        return
+    t = time.gmtime(when)
+    h.lines.append(f"{h.formatter.prefix}{t.tm_hour:02d}:{t.tm_min:02d}:{t.tm_sec:02d}.{int((when % 1) * 1e6):06d} "
+                   f"{where}: {msg}")
+    if len(h.lines) >= h.max_lines or time.monotonic() - h.t_last > h.max_delay:
+        h.flush()
+
+
 def flush_logs(lg: logging.Logger) -> None:
     for h in lg.handlers:
         h.flush()
@@ -126,6 +142,8 @@ class _Phase:
 class PhaseTimer:
     """Accumulates wall time per protocol phase; ``sync`` makes GPU work visible to the clock."""
 
+    stamps = None
+
     def __init__(self, sync=None):
         self.t: dict[str, float] = {}
         self.sync = sync
@@ -135,6 +153,40 @@ class PhaseTimer:
 
     def reset(self) -> dict[str, float]:
         out, self.t = self.t, {}
+        return out
+
+
+class _StampedPhase(_Phase):
+    __slots__ = ("w",)
+
+    def __enter__(self):
+        super().__enter__()
+        self.w = time.time() - (time.perf_counter() - self.s)   # wall clock of the same instant
+        return self
+
+    def __exit__(self, *exc):
+        super().__exit__(*exc)
+        end = self.w + (time.perf_counter() - self.s)
+        st = self.timer.stamps
+        first = st.get(self.name)
+        st[self.name] = (first[0] if first else self.w, end)
+        return False
+
+
+class StampedPhaseTimer(PhaseTimer):
+    """A PhaseTimer that also keeps each phase's wall-clock (first start, last end) of the current round in
+    ``stamps`` (the reference's phase log lines are written from them, protocol/golog.py).  The plain timer
+    pays nothing for this."""
+
+    def __init__(self, sync=None):
+        super().__init__(sync)
+        self.stamps: dict = {}
+
+    def phase(self, name: str) -> _Phase:
+        return _StampedPhase(self, name)
+
+    def take_stamps(self) -> dict:
+        out, self.stamps = self.stamps, {}
         return out
 
 

@@ -67,7 +67,22 @@ def wait(dst: torch.cuda.Stream, src: torch.cuda.Stream) -> None:
     dst.wait_event(ev)
 
 
-SPIN_S = 2e-4   # host waits spin this long, then poll with short sleeps
+SPIN_S = 2e-4   # host waits spin this long, then poll with short sleeps (set_spin)
+
+
+def set_spin(seconds: float) -> None:
+    """How long host waits spin before they poll with sleeps -- these and the native round's waits
+    (bsc_set_host_spin_ns).  The engine spins long with one rank per process (a sleeping thread wakes
+    late; the GPU's one host thread has nothing else to do) and briefly with several (ranks sharing the
+    CPU quota)."""
+    global SPIN_S
+    SPIN_S = float(seconds)
+    try:
+        from ..native import hip
+
+        hip().bsc_set_host_spin_ns(int(seconds * 1e9))
+    except (ImportError, OSError, AttributeError):
+        pass
 
 
 def host_wait(ev) -> None:

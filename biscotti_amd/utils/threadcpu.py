@@ -53,6 +53,88 @@ def snapshot() -> dict:
     return out
 
 
+def _cgroup_dirs() -> list:
+    """This process's cgroup-v2 directory and its ancestors up to /sys/fs/cgroup (a CFS quota may sit on
+    any of them: on the GPU box the process's own group has no cpu controller, its parent has cpu.max)."""
+    out = []
+    try:
+        rel = open("/proc/self/cgroup").read().strip().split("\n")[0].split(":", 2)[2]
+    except (OSError, IndexError):
+        rel = ""
+    parts = [p for p in rel.split("/") if p]
+    while True:
+        out.append("/sys/fs/cgroup" + "".join("/" + p for p in parts))
+        if not parts:
+            return out
+        parts.pop()
+
+
+def cgroup_cpu_stat() -> dict:
+    """CPU counters of the nearest cgroup that throttles this process: nr_periods, nr_throttled,
+    throttled_usec (cgroup v2 cpu.stat, or v1 cpu,cpuacct).  A CFS quota (cpu.max) that the job's threads
+    exhaust inside a 100 ms period stops EVERY thread of the group until the period ends -- a 10-100 ms
+    stall of whichever rank holds a collective.  Empty when no such counters exist."""
+    cands = [d + "/cpu.stat" for d in _cgroup_dirs()] + ["/sys/fs/cgroup/cpu/cpu.stat",
+                                                         "/sys/fs/cgroup/cpu,cpuacct/cpu.stat"]
+    for p in cands:
+        out = {}
+        try:
+            with open(p) as f:
+                for ln in f:
+                    k, _, v = ln.partition(" ")
+                    if k in ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec"):
+                        out[k] = int(v)
+                    elif k == "throttled_time":   # v1: nanoseconds
+                        out["throttled_usec"] = int(v) // 1000
+        except (OSError, ValueError):
+            continue
+        if "nr_throttled" in out:
+            return out
+    return {}
+
+
+def cgroup_delta(a: dict, b: dict) -> dict:
+    return {k: b[k] - a.get(k, 0) for k in b}
+
+
+def cpu_quota() -> float | None:
+    """CPUs the tightest CFS quota over this process's cgroup and its ancestors allows (cpu.max), or None
+    when unlimited / unknown."""
+    best = None
+    for d in _cgroup_dirs():
+        try:
+            q, per = open(d + "/cpu.max").read().split()[:2]
+        except (OSError, ValueError):
+            continue
+        if q != "max":
+            c = int(q) / int(per)
+            best = c if best is None else min(best, c)
+    if best is not None:
+        return best
+    try:   # cgroup v1
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def pool_threads(local_ranks: int, world: int, cpus: float | None = None) -> int:
+    """Native crypto pool size per rank so that every thread the node's local ranks keep busy fits the CPUs
+    the job may use (the CFS quota, else the affinity mask): per rank, the round's host thread and the HIP
+    runtime's threads take one CPU each and, with several ranks, RCCL's proxy / service threads two more
+    (measured 1.2-2 cores per rank on the RCCL rehearsal, docs/PERF.md); the pool gets the rest, 2..16.  A
+    pool that overshoots the quota gets every thread of the job throttled for the rest of the CFS period --
+    the 50-280 ms multi-rank stalls of round 4."""
+    if cpus is None:
+        aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 16)
+        q = cpu_quota()
+        cpus = aff if q is None else min(aff, q)
+    local = max(1, int(local_ranks))
+    reserve = 2 + (2 if world > 1 else 0)
+    return int(max(2, min(16, (int(cpus) - local * reserve) // local)))
+
+
 def _group(name: str) -> str:
     """Thread groups: names are truncated to 15 characters and often numbered (``bsc-pool``,
     ``python``/``pt_main_thread``, ``HIP ...``, ``NCCL``/``rccl`` threads, ``gloo`` ...)."""

@@ -68,3 +68,42 @@ def test_per_rank_host_cpu_does_not_blow_up_with_ranks():
     single = out[1]["host_cpu_ms_per_round"]
     for p in out[4]["per_rank"]:
         assert p["host_cpu_ms_per_round"] <= 1.25 * single + 30.0, (p["rank"], p["host_cpu_ms_per_round"], single)
+
+
+def test_pool_sizing_fits_the_quota_across_local_ranks():
+    """The native pools of all local ranks plus each rank's round thread, HIP runtime and RCCL threads fit the
+    job's CPU quota (a pool that overshoots it got every thread throttled for the rest of the CFS period: the
+    52-278 ms stalls of the 2-rank RCCL rehearsal, docs/PERF.md) -- checked at 8 local ranks under small and
+    large quotas; the floor (2 threads) applies only where even the reserve does not fit."""
+    from biscotti_amd.utils.threadcpu import pool_threads
+
+    for local, quota in ((8, 128), (8, 64), (8, 40), (8, 48), (4, 16), (2, 16), (1, 16), (1, 8)):
+        world = local
+        pool = pool_threads(local, world, cpus=quota)
+        reserve = 2 + (2 if world > 1 else 0)
+        assert 2 <= pool <= 16
+        if quota >= local * (reserve + 2):
+            assert local * (pool + reserve) <= quota, (local, quota, pool)
+    assert pool_threads(2, 2, cpus=16) == 4           # the rehearsal box: 16 CPUs, 2 ranks (was 8 each)
+    assert pool_threads(1, 1, cpus=16) == 14
+    assert pool_threads(8, 8, cpus=128) == 12
+    assert pool_threads(8, 8, cpus=16) == 2           # oversubscribed quota: the floor
+
+
+def test_bench_emulate_world_runs_rank0_alone():
+    """--emulate-world N: one process runs rank 0's share of an N-rank job (its own peers, its Gram slice, its
+    partial sums, the replicated recovery and block); the line says so and never claims N GPUs."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    r = subprocess.run([sys.executable, "bench.py", "--emulate-world", "4", "--config", "credit4", "--steps", "3",
+                        "--warmup", "1", "--rounds", "4"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["emulated_world"] == 4
+    assert "emulated" in out["metric"] and out["vs_baseline"] is None
+    assert out["config"]["parallelism"].startswith("emulated rank 0 of dp4")
+    assert out["chain_valid"] is True and out["engine_stats"]["audit_failures"] == 0
+    # rank 0 of 4 hosts 1 of the 4 peers; the round still issued its collectives (emulated)
+    assert "(virtual peers: 1 on this GPU" in out["config"]["parallelism"]
+    assert out["collective_ms"]

@@ -425,3 +425,21 @@ def test_eval_errors_cached_tiles_match_reference():
     assert abs(a - ref_a) <= 1.0 / split and abs(b - ref_b) <= 1.0 / (2347 - split)
     a0, b0 = K.eval_errors_async(Xc, y.cuda(), split, W.cuda(), 784, 10)()   # the gather kernel
     assert abs(a - a0) <= 1.0 / split and abs(b - b0) <= 1.0 / (2347 - split)
+
+
+def test_eval_errors_cached_tiles_repeated_launches():
+    """The cached-tile evaluation resets its own counters (its last tile writes the host copy and re-zeroes
+    them): back-to-back launches over the rotating buffers, each with a different model, each match the
+    reference, including results read only after later launches were queued."""
+    X, y, off, nt, pid, W = _fed(P=1, n=1000)
+    split = 700
+    Xc, yc = X.cuda(), y.cuda()
+    Xt = K.eval_tiles(Xc, transform=True)
+    g = torch.Generator().manual_seed(5)
+    Ws = [W + 0.05 * k * torch.randn(W.shape, generator=g, dtype=W.dtype) for k in range(7)]
+    pending = [K.eval_errors_async(Xc, yc, split, Wk.cuda(), 784, 10, Xt=Xt) for Wk in Ws[:3]]
+    got = [f() for f in pending] + [K.eval_errors_async(Xc, yc, split, Wk.cuda(), 784, 10, Xt=Xt)() for Wk in Ws[3:]]
+    for Wk, (a, b) in zip(Ws, got):
+        ra = K.eval_error(X[:split], y[:split], Wk, 784, 10)
+        rb = K.eval_error(X[split:], y[split:], Wk, 784, 10)
+        assert abs(a - ra) <= 1.0 / split and abs(b - rb) <= 1.0 / (1000 - split)

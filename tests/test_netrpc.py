@@ -219,3 +219,82 @@ def test_peer_cli_serves_and_floods(tmp_path):
         assert len(follower_chain) == 4 and follower_chain.verify()[0]
     finally:
         follower.close()
+
+
+def test_far_future_iteration_cannot_evict_current_round(rt):
+    """pruning follows this peer's own progress (its chain), not the largest Iteration a remote
+    peer sends -- a forged far-future message is refused and the current round's shares survive."""
+    g = rt.g1_generator()
+    svc = N.PeerService(rt, rt.Blockchain.with_genesis(25), peer_id=3, krum_thresh=2, krum_timeout_s=2.0)
+    srv = N.RpcServer(svc.handlers()).start()
+    addr = f"127.0.0.1:{srv.addr[1]}"
+    try:
+        assert svc.current_iteration() == 0
+        part = {"CommitmentUpdate": g, "Iteration": 0, "NodeID": 5,
+                "PolyMap": {0: {"Commitment": g, "Secrets": [{"X": -10, "Y": 1}], "Witnesses": [g]}}}
+        assert N.call(addr, "Peer.RegisterSecret", G.MinerPartRPC, part) is True
+        with pytest.raises(N.RpcError, match="too far ahead"):
+            N.call(addr, "Peer.RegisterSecret", G.MinerPartRPC, dict(part, Iteration=10**9, NodeID=6))
+        with pytest.raises(N.RpcError, match="too far ahead"):
+            N.call(addr, "Peer.VerifyUpdateKRUM", G.Update,
+                   {"SourceID": 1, "Iteration": 10**9, "Commitment": bytes(64), "NoisedDelta": [0.0] * 25})
+        assert N.call(addr, "Peer.GetUpdateList", G.INT, 0) == [5]
+        assert set(svc.secrets_of(0)) == {5}
+        # within the window ahead (a peer one round ahead of this one) is accepted
+        assert N.call(addr, "Peer.RegisterSecret", G.MinerPartRPC, dict(part, Iteration=2, NodeID=7)) is True
+        assert set(svc.secrets_of(0)) == {5}
+    finally:
+        srv.close()
+
+
+def test_verifier_threshold_above_old_connection_cap(rt):
+    """a verifier holds one connection per worker until its Krum threshold; 80 concurrent
+    VerifyUpdateKRUM calls (more than the 64 connections the server used to allow) all reach the threshold and
+    get a decision before the deadline, and extra connections wait in the backlog instead of being closed."""
+    import threading
+    import time
+
+    sk, _ = rt.client_key_from_entropy(b"\x09" * 32)
+    n = 80
+    svc = N.PeerService(rt, rt.Blockchain.with_genesis(25), peer_id=0, sk=sk, krum_thresh=n, krum_timeout_s=60.0)
+    srv = N.RpcServer(svc.handlers(), max_conns=N.conns_for(n)).start()
+    addr = f"127.0.0.1:{srv.addr[1]}"
+    rng = np.random.default_rng(1)
+    out = {}
+
+    def send(i):
+        u = {"SourceID": i, "Iteration": 0, "Commitment": bytes([i % 256]) * 64,
+             "NoisedDelta": list(rng.normal(0, 0.01, 25))}
+        try:
+            out[i] = N.call(addr, "Peer.VerifyUpdateKRUM", G.Update, u, timeout=60.0)
+        except N.RpcError as e:
+            out[i] = str(e)
+        except OSError as e:
+            out[i] = ("socket", str(e))
+    t0 = time.monotonic()
+    try:
+        ts = [threading.Thread(target=send, args=(i,)) for i in range(n)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        srv.close()
+    assert time.monotonic() - t0 < 30.0, "the threshold was not reached: the deadline decided"
+    assert not [v for v in out.values() if isinstance(v, tuple)], "a connection was dropped"
+    acc = [v for v in out.values() if isinstance(v, bytes)]
+    assert len(acc) == n - n // 2, len(acc)
+    # a server with fewer slots than the threshold queues the rest: the late callers get a decision (the
+    # deadline's), never a closed socket
+    svc2 = N.PeerService(rt, rt.Blockchain.with_genesis(25), peer_id=0, sk=sk, krum_thresh=6, krum_timeout_s=1.0)
+    srv2 = N.RpcServer(svc2.handlers(), max_conns=3).start()
+    addr, out = f"127.0.0.1:{srv2.addr[1]}", {}
+    try:
+        ts = [threading.Thread(target=send, args=(i,)) for i in range(6)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        srv2.close()
+    assert len(out) == 6 and not [v for v in out.values() if isinstance(v, tuple)], out

@@ -279,7 +279,7 @@ def test_cli_defaults_match_runconfig():
     assert RunConfig().fail_point() == (-1, 0)
     import dataclasses
 
-    assert len(dataclasses.fields(RunConfig)) < 50
+    assert len(dataclasses.fields(RunConfig)) <= 50   # 49 + phase_log (the reference's phase lines, round 5)
     import pytest
 
     with pytest.raises(ValueError):
