@@ -480,7 +480,8 @@ __device__ __forceinline__ double gram_at(const double* gram, int T, int a, int 
 // pre-sampled vectors of this iteration (a strided view of the resident noise table)
 extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, int U, int D, int kchunk, int T,
                                                               double* part, double* gram, unsigned int* count,
-                                                              const float* X2, int U1, long long stride2, int pair0) {
+                                                              const float* X2, int U1, long long stride2, int pair0,
+                                                              const double* nn, int tn0) {
   BSC_SET_PRIO(BSC_PRIO_AHEAD);
   __shared__ double red[4][256];
   __shared__ unsigned int last;
@@ -495,6 +496,17 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
     ++ti;
   }
   const int tj = ti + rem;
+  if (nn != nullptr && ti >= tn0) {
+    // both tiles hold noise rows only (rows >= U1): the noisers' pre-sampled vectors repeat with the iteration
+    // modulo 100 (client_obj.py:61-63,97-98), so this block of the Gram was computed at setup, by this kernel
+    // (bit-identical entries), into the dense [U2, U2] table nn of this iteration: copy, no split-K
+    if (sp == 0) {
+      const int U2 = U - U1, e = threadIdx.x;
+      const int a = ti * 16 + (e >> 4) - U1, b = tj * 16 + (e & 15) - U1;
+      gram[(size_t)pair * 256 + e] = (a < U2 && b < U2) ? nn[(size_t)a * U2 + b] : 0.0;
+    }
+    return;
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = ti * 16 + (lane & 15), j = tj * 16 + (lane & 15), kk = lane >> 4;
   const bool va = i < U, vb = j < U;
@@ -1378,7 +1390,7 @@ extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, cons
   hipStream_t s = (hipStream_t)stream;
   // count: npairs zeroed counters (re-armed by the kernel itself)
   hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part, gram, count,
-                     (const float*)nullptr, U, 0ll, 0);
+                     (const float*)nullptr, U, 0ll, 0, (const double*)nullptr, 0);
   if (n <= 256) {
     hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, gram, T, inbox, n, groupsize, scores);
   } else {
@@ -1391,9 +1403,11 @@ extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, cons
 }
 // Tile pairs [p0, p1) of the stacked Gram only (p1 <= 0: all of them): several ranks split one Gram's tiles
 // and exchange the reduced tiles (engine: the verification all_gather).  part: [nsplit, p1 - p0, 256].
+// nn (nullable): this iteration's dense [U2, U2] Gram of the noise rows (setup, bsc_gram_noise_table); the tile
+// pairs of noise rows only are copied from it instead of computed.
 extern "C" int bsc_gram_stacked_range(const float* X, int U1, const float* X2, int U2, long long stride2, int D,
                                       int kchunk, int p0, int p1, double* part, double* gram, unsigned int* count,
-                                      void* stream) {
+                                      const double* nn, void* stream) {
   const int U = U1 + U2;
   if (U <= 0) return 0;
   if (U > 8192 || kchunk <= 0) return -1;
@@ -1404,12 +1418,12 @@ extern "C" int bsc_gram_stacked_range(const float* X, int U1, const float* X2, i
   if (p0 == p1) return 0;
   const int nsplit = (D + kchunk - 1) / kchunk;
   hipLaunchKernelGGL(k_gram_pairs, dim3(p1 - p0, nsplit), dim3(256), 0, (hipStream_t)stream, X, U, D, kchunk, T, part,
-                     gram, count, X2, U1, stride2, p0);
+                     gram, count, X2, U1, stride2, p0, nn, (U1 + 15) / 16);
   return (int)hipGetLastError();
 }
 extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
-                                double* part, double* gram, unsigned int* count, void* stream) {
-  return bsc_gram_stacked_range(X, U1, X2, U2, stride2, D, kchunk, 0, 0, part, gram, count, stream);
+                                double* part, double* gram, unsigned int* count, const double* nn, void* stream) {
+  return bsc_gram_stacked_range(X, U1, X2, U2, stride2, D, kchunk, 0, 0, part, gram, count, nn, stream);
 }
 // h_out (nullable): [V * n + U1] pinned host mirror of (acc, node), written by the vote itself (acc and node
 // must be contiguous there too); amap / nspec / alive (nullable): the speculative MSM's row flags set in the

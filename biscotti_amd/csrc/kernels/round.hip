@@ -55,7 +55,7 @@ extern "C" int bsc_shares_msm_ka(const long long* coeffs, int d, const int* rows
                                  const int* alive, int group_rows, uint32_t* out_pts, long long* out_y, void* stream);
 #define ROWARG_MAX 248   // msm.hip: rows passed in the MSM kernel's arguments
 extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
-                                double* part, double* gram, unsigned int* count, void* stream);
+                                double* part, double* gram, unsigned int* count, const double* nn, void* stream);
 extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
                                void* stream);
 extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
@@ -96,6 +96,7 @@ struct TaskCfg {  // the softmax task's resident data and the pre-step's constan
   const uint32_t* tbl_wb;
   const float* noise;       // resident noise table [N][100][d] (nullptr: no noise-aware Gram)
   int noise_n;
+  const double* nn_tab;     // [100][N][N] Gram of each iteration's noise rows (nullptr: computed every round)
   unsigned int* counters;
 };
 struct RoundCtx {
@@ -336,7 +337,7 @@ static int prestep_impl(RoundCtx* c, hipStream_t gs, const float* X, const int* 
                         uint32_t* jac, uint32_t* jac_host, int do_gram, const float* T_rows, int U2, long long stride2,
                         int kchunk, double* part, double* gram, unsigned int* counters, void* ev_step, void* ev_ccom,
                         void* ev_commit, void* ev_gram, int chunked, hipStream_t cst, int* ones, int nones,
-                        hipEvent_t ones_wait) {
+                        hipEvent_t ones_wait, const double* nn) {
   if (c == nullptr || P <= 0 || d_in * d_out + d_out != c->d) return -1;
   RC_CHECK(hipEventRecord(c->ev_pre, c->main));
   RC_CHECK(hipStreamWaitEvent(gs, c->ev_pre, 0));
@@ -356,7 +357,7 @@ static int prestep_impl(RoundCtx* c, hipStream_t gs, const float* X, const int* 
   }
   RC_CHECK(hipEventRecord((hipEvent_t)ev_commit, cst));
   if (do_gram) {
-    RC_CHECK(bsc_gram_stacked(delta, P, T_rows, U2, stride2, c->d, kchunk, part, gram, counters, gs));
+    RC_CHECK(bsc_gram_stacked(delta, P, T_rows, U2, stride2, c->d, kchunk, part, gram, counters, nn, gs));
     RC_CHECK(hipEventRecord((hipEvent_t)ev_gram, gs));
   }
   return 0;
@@ -377,7 +378,7 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
   return prestep_impl(c, (hipStream_t)gram_stream, X, y, off, ntrain, pid, W, d_in, d_out, B, P, seed, iteration,
                       max_norm, qscale, lo, delta, qdelta, loss, tbl_wb, rows_arange, ccom, jac, jac_host, do_gram,
                       T_rows, U2, stride2, kchunk, part, gram, counters, ev_step, ev_ccom, ev_commit, ev_gram, chunked,
-                      cst, nullptr, 0, nullptr);
+                      cst, nullptr, 0, nullptr, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -532,9 +533,19 @@ extern "C" int bsc_round_bind_task(void* ctx, void* gram_stream, const float* X,
   t.rows_arange = rows_arange;
   t.noise = noise;
   t.noise_n = noise_n;
+  t.nn_tab = nullptr;
   t.kchunk = kchunk;
   t.counters = counters;
   t.bound = 1;
+  return 0;
+}
+
+// The [100][N][N] Gram of each iteration's noise rows (built at setup, ml.py NoiseRows.gram_table): the pre-step's
+// noise-aware Gram copies its noise x noise tiles from it instead of computing them (nullptr: compute).
+extern "C" int bsc_round_set_nn_table(void* ctx, const double* nn) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || !c->task.bound) return -1;
+  c->task.nn_tab = nn;
   return 0;
 }
 
@@ -606,7 +617,7 @@ extern "C" int bsc_round_prestep_slot(void* ctx, const double* W, int it, int do
                         t.max_norm, t.qs, t.lo, p.delta, p.qdelta, p.loss, t.tbl_wb, t.rows_arange, p.ccom, p.jac,
                         p.jac_host, g ? 1 : 0, rows, g ? t.noise_n : 0, 100ll * c->d, t.kchunk, p.part, p.gram,
                         t.counters, p.ev_step, p.ev_ccom, p.ev_commit, p.ev_gram, 1, c->bg, ones, c->spec_cap,
-                        ones_wait));
+                        ones_wait, g && t.nn_tab ? t.nn_tab + (size_t)(it % 100) * t.noise_n * t.noise_n : nullptr));
   return c->pre_k;
 }
 

@@ -50,8 +50,8 @@ SIGNATURES = {
     "bsc_dp_noise": [P, I, I, P, I, P, U64, I, P, P],
     "bsc_krum": [P, I, I, I, P, P, P, P, I, I, P],
     "bsc_krum_committee": [P, I, I, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, P, P],
-    "bsc_gram_stacked": [P, I, P, I, L, I, I, P, P, P, P],
-    "bsc_gram_stacked_range": [P, I, P, I, L, I, I, I, I, P, P, P, P],
+    "bsc_gram_stacked": [P, I, P, I, L, I, I, P, P, P, P, P],
+    "bsc_gram_stacked_range": [P, I, P, I, L, I, I, I, I, P, P, P, P, P],
     "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P],
     "bsc_krum_committee_noise2": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, I, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
@@ -83,6 +83,7 @@ SIGNATURES = {
     "bsc_round_add_pre_slot": [P, P, P, P, P, P, P, P, P, P, P, P, P],
     "bsc_round_pick_W": [P, P],
     "bsc_round_prestep_slot": [P, P, I, I],
+    "bsc_round_set_nn_table": [P, P],
     "bsc_round_after_select": [P, P, P, P, I, P, P, P, P, I, P, I, P, I, I, I, I, P],
     "bsc_round_select_partials": [P, P, P, P, I, P, P, P, P, I, P, I, P, L, I],
     "bsc_round_after_gather": [P, P, I, L, I, P, P, I, I, I, P],

@@ -425,6 +425,9 @@ class NativeSecAgg:
     def layout_agg(self, lid: int) -> torch.Tensor:
         return self._layouts[lid][6]
 
+    def layout_ws(self, lid: int) -> torch.Tensor:
+        return self._layouts[lid][7]
+
     def bind_task(self, task, gram_stream, noise_table, gram_counters, kchunk: int = 512) -> None:
         """The softmax task's resident data and the pre-step's slot ring (PRE_SLOTS slots of step outputs, chunk
         and full commitments, the noise-aware Gram).  noise_table: the resident [N, 100, d] noise table for the
@@ -468,6 +471,12 @@ class NativeSecAgg:
             self.slots.append(sl)
         self._spec_ring_for(P)   # every local peer can be a speculative row
         torch.cuda.synchronize(dev)
+
+    def set_nn_table(self, tab) -> None:
+        """The pre-step's noise-aware Gram copies its noise x noise tiles from tab ([100, N, N] fp64, None: computes
+        them): see NoiseRows.gram_table."""
+        self.nn_tab = tab
+        _check(hip().bsc_round_set_nn_table(self.ctx, _ptr(tab) if tab is not None else None), "round_set_nn_table")
 
     def _pre_out(self, k: int, W, it: int) -> dict:
         """The engine's pre-step dict of slot k (the step of every local peer from W for iteration it)."""

@@ -243,6 +243,41 @@ class NoiseRows:
             self._rows, self._m = torch.from_numpy(_gauss(r[0], r[1])), m
         return self._rows
 
+    def gram_table(self, kchunk: int = 512) -> torch.Tensor:
+        """GPU: [100, N, N] fp64, entry [m, a, b] = <rows(m)[a], rows(m)[b]> as k_gram_pairs computes it (the same
+        kernel, K split and reduction order, so the noise-aware Gram's noise x noise tiles copied from here are
+        bit-identical to computed ones).  The noisers' vectors repeat with the iteration mod 100
+        (client_obj.py:61-63,97-98): built once (~8 MB at N = 100), a setup cost instead of ~23 % of every
+        round's Gram tiles."""
+        tab = getattr(self, "_gram_tab", None)
+        if tab is not None:
+            return tab
+        assert self.table is not None, "the noise Gram table lives on the GPU"
+        N, D, dev = self.N, self.D, self.device
+        T = (N + 15) // 16
+        npairs, nsplit = T * (T + 1) // 2, (D + kchunk - 1) // kchunk
+        part = torch.empty((nsplit, npairs, 256), dtype=torch.float64, device=dev)
+        tiles = torch.empty((npairs, 256), dtype=torch.float64, device=dev)
+        cnt = _tile_counters(dev, npairs)
+        # (pair, e) -> (a, b) of the dense matrix, both triangles
+        pr = torch.tensor(_pair_tiles(T), dtype=torch.long)
+        e = torch.arange(256)
+        a = (pr[:, 0, None] * 16 + e[None, :] // 16).reshape(-1)
+        b = (pr[:, 1, None] * 16 + e[None, :] % 16).reshape(-1)
+        ok = (a < N) & (b < N)
+        src = torch.nonzero(ok).flatten().to(dev)
+        ia, ib = a[ok].to(dev), b[ok].to(dev)
+        tab = torch.empty((100, N, N), dtype=torch.float64, device=dev)
+        for m in range(100):
+            rows = self.table[:, m, :]
+            _check(hip().bsc_gram_stacked_range(None, 0, rows.data_ptr(), N, rows.stride(0), D, kchunk, 0, 0,
+                                                _p(part), _p(tiles), _p(cnt), None, _stream()), "gram_noise_table")
+            flat = tiles.view(-1).index_select(0, src)
+            tab[m].index_put_((ia, ib), flat)
+            tab[m].index_put_((ib, ia), flat)
+        self._gram_tab = tab
+        return tab
+
 
 # ---------------------------------------------------------------------------- K5 Multi-Krum
 def krum_async(X, groupsize: int, n_accept: int, ksplit: int = 256, on_accept=None):
@@ -461,7 +496,8 @@ def gram_split(U: int, rank: int, world: int) -> tuple[int, int, int, int]:
     return p0, min(npairs, p0 + chunk), chunk, npairs
 
 
-def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | None = None, out=None) -> dict:
+def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | None = None, out=None,
+                       nn=None) -> dict:
     """Noise-aware committee Krum, phase 1: f64 Gram of the stacked rows [X; T_rows].
 
     X fp32 [U1, d] (the workers' deltas, contiguous); T_rows fp32 [U2, d] with contiguous rows (a
@@ -469,8 +505,9 @@ def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | No
     split = (rank, world): this rank computes only its share of the tile pairs (gram_split) into rows
     [rank * chunk, ...) of a [world * chunk, 256] buffer; the caller all_gathers the ranks' slots
     (gram_slot) and calls gram_adopt.  out (GPU, split): this rank's [chunk, 256] slot is written there
-    instead (the packed verification row, ops/gather.py).  Returns the handle krum_committee_noise_async
-    consumes."""
+    instead (the packed verification row, ops/gather.py).  nn (GPU): this iteration's dense [U2, U2] Gram of
+    T_rows (NoiseRows.gram_table): the noise x noise tiles are copied from it, not computed.  Returns the
+    handle krum_committee_noise_async consumes."""
     U1, D = X.shape
     U2 = T_rows.shape[0]
     assert X.is_contiguous() and T_rows.stride(1) == 1 and T_rows.shape[1] == D
@@ -501,7 +538,8 @@ def gram_stacked_async(X, T_rows, kchunk: int = 512, split: tuple[int, int] | No
         gram = torch.empty((chunk * (split[1] if split else 1), 256), dtype=torch.float64, device=dev)
         base = gram.data_ptr()
     _check(hip().bsc_gram_stacked_range(_p(X), U1, T_rows.data_ptr(), U2, T_rows.stride(0), D, kchunk, p0, p1,
-                                        _p(part), base, _p(_tile_counters(dev, max(1, p1 - p0))), _stream()),
+                                        _p(part), base, _p(_tile_counters(dev, max(1, p1 - p0))),
+                                        nn.data_ptr() if nn is not None else None, _stream()),
            "gram_stacked")
     res = {"gram": gram, "U1": U1, "U": U, "keep": (X, T_rows, part)}
     if split is not None:
@@ -605,11 +643,12 @@ def eval_errors_async(X, y, split: int, W, d_in, d_out, transform=True, Xt=None)
     # afterwards (the next round's head).  Device and host buffers rotate together (lazy_eval reads the
     # host copy up to a few rounds later).
     host = pinned("eval", (2,), torch.int32, depth=4)
-    err = _EVAL_DEV.get(host.data_ptr())
+    key = (host.data_ptr(), Xt is not None)   # the two kernels keep their own accumulators: only the tiled one
+    err = _EVAL_DEV.get(key)                  # leaves its counters zeroed after a launch
     if err is None:
         # [errors of rows < split, errors of the rest, tiles done]: zero before the first launch, and
         # k_eval_error_t's last tile re-zeroes it when it writes the host copy
-        err = _EVAL_DEV[host.data_ptr()] = torch.zeros((4,), dtype=torch.int32, device=X.device)
+        err = _EVAL_DEV[key] = torch.zeros((4,), dtype=torch.int32, device=X.device)
     if Xt is not None:   # cached pre-transformed tiles (k_eval_error_t)
         assert Xt.shape[0] == (N + 15) // 16 and Xt.shape[1] * 4 >= d_in and Xt.shape[2] == 64
         _check(hip().bsc_eval_error_t_rb(_p(Xt), _p(y), N, Xt.shape[1], d_in, d_out, _p(W), int(split), _p(err),

@@ -230,7 +230,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         # long device work nothing in a round waits for -- the VRF proofs (kernels/vrf.hip) and the KZG
         # audit sums (kernels/kzg.hip) -- gets a stream of its own
         self.vrf_stream = torch.cuda.Stream(device=self.dev, priority=lo)
-        # the pre-step and its Krum Gram (_queue_pre_step): beside the main stream, so the evaluation and
+        # the pre-step and its Krum Gram (NativeSecAgg pre-step): beside the main stream, so the evaluation and
         # the audit queued there do not wait for it.  High priority: the Gram is on the next round's critical
         # path (Krum waits for it) and is released together with the speculative MSM; at low priority the MSM
         # took the CUs first and the Gram ran 5x slower (200 -> 1000 us; verify.krum_wait 0.32 -> 0.02 ms,
@@ -252,6 +252,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             M = cfg.num_miners
             for perm in itertools.permutations(range(M)):
                 self._agg_index(list(range(M)), {i: perm[i] for i in range(M)})
+        if self.gpu and self._noise_krum():
+            self._noise_gram_table()   # the 100 periodic noise Grams (~8 MB), built now rather than in round 1
         if self.vrf_dev is not None:
             # the key material of every peer this rank proves for (secret scalar, nonce prefix, public key:
             # a fixed-base multiplication each) -- the host batches and the device prover share the cache

@@ -91,9 +91,9 @@ class RoundHeadMixin:
                     fut_roles = R.vrf_prove_batch_async(roles, latest_hash, 8, fut_noise)
         head.update(fut_noise=fut_noise, fut_roles=fut_roles)
         tm, it = self.timer, plan.iteration
-        # the local step (and the commitments) may already be in flight: queued behind the recovery of the
-        # model this head starts from (_queue_pre_step), for every local peer.  The decision is the same
-        # on every rank (the pre-step is queued at the same point everywhere): the Gram gather depends on it.
+        # the local step (and the commitments) may already be in flight: the native pre-step queued behind the
+        # recovery of the model this head starts from, for every local peer.  The decision is the same on every
+        # rank (the pre-step is queued at the same point everywhere): the Gram gather depends on it.
         pre, self._pre = self._pre, None
         use_pre = pre is not None and pre["it"] == it and pre["W"] is self.W
         with tm.phase("local_step"):
@@ -236,51 +236,33 @@ class RoundHeadMixin:
         if vg is not None and S.current().stream_id != self.gram_stream.stream_id:
             # a discarded pre-step may still write this iteration's slot on the Gram stream
             S.wait(S.current(), self.gram_stream)
+        nn = self._noise_gram_table()
         g = K.gram_stacked_async(X.contiguous(), self.noise_rows.rows(it),
                                  split=(comm.rank, comm.world) if comm.world > 1 else None,
-                                 out=vg.gram_out(it) if vg is not None else None)
+                                 out=vg.gram_out(it) if vg is not None else None,
+                                 nn=nn[it % 100] if nn is not None else None)
         g["xrow"] = self.flat
         g["it"] = it
         return g
+
+    def _noise_gram_table(self):
+        """GPU: the [100, N, N] Gram of each iteration's noise rows (NoiseRows.gram_table, built at setup), whose
+        tiles the noise-aware Gram copies instead of computing; None on the CPU or with the
+        noise_gram_each_round ablation."""
+        if not (self.gpu and self.noise_rows is not None and self.noise_rows.table is not None) or \
+                self.cfg.has("noise_gram_each_round"):
+            return None
+        return self.noise_rows.gram_table()
 
     # ------------------------------------------------------------------ cross-round pipelining
     def _pipelined(self) -> bool:
         return self.gpu and not self.cfg.has("no_pipeline")
 
-    def _queue_pre_step(self, W: torch.Tensor, it: int) -> dict:
-        """The next round's local step for EVERY local peer (its workers are not known before the next
-        block's roles) and their commitments (background stream), queued right behind the recovery of
-        W -- the GPU runs them while the host reads W back, builds and commits the block; the next head
-        adopts them if that block carries W (same device tensor) and discards them otherwise.  Every rank
-        queues it at the same point (the recovery is replicated), so the Gram's gather lines up."""
-        main, gs = S.current(), self.gram_stream
-        if self._native_prestep_ok():
-            # step + chunk commitments (+ one rank: the Krum Gram) in one native call (resident slot ring)
-            out = self._native.prestep(W, it, do_gram=self._noise_krum() and self.comm.world == 1)
-            return self._finish_pre(out, it)
-        S.wait(gs, main)
-        with S.use(gs):
-            delta, qdelta = self.task.step(W, it, list(self.local))
-            ev = S.record()
-            out = {"W": W, "it": it, "delta": delta, "qdelta": qdelta, "ev": ev,
-                   "commits": self.crypto.commitments_async(
-                       qdelta, self.bg_stream, chunked=self._native is not None and self.cfg.audit_aggregate)}
-        S.hold(delta, qdelta)
-        if self._noise_krum():
-            # the noise-aware Krum's d-dimensional phase over EVERY peer's delta (the workers are not known
-            # yet) and this iteration's noise rows, on the same stream right behind the step: done long
-            # before the noisers are drawn, and the main stream's evaluation does not wait for it
-            with S.use(gs):
-                g = self._gram_rows(delta, None, it)
-                g["ev"] = S.record()
-            out["gram"] = g
-        return out
-
     def _native_prestep_ok(self) -> bool:
-        """The pre-step runs natively (NativeSecAgg: softmax task, aggregate audit on); the task and the slot
-        ring are bound at the first use."""
+        """The pre-step runs natively (NativeSecAgg, softmax tasks); the task and the slot ring are bound at the
+        first use."""
         na = self._native
-        if na is None or type(self.task).__name__ != "SoftmaxTask" or not self.cfg.audit_aggregate:
+        if na is None or type(self.task).__name__ != "SoftmaxTask":
             return False
         if na.task is None:
             gs = self.gram_stream
@@ -288,6 +270,8 @@ class RoundHeadMixin:
                 cnt = K._tile_counters(self.dev, 1024)
             nk = self._noise_krum() and self.comm.world == 1
             na.bind_task(self.task, gs, self.noise_rows.table if nk else None, cnt)
+            if nk:
+                na.set_nn_table(self._noise_gram_table())
         return True
 
     def _finish_pre(self, out: dict, it: int) -> dict:

@@ -22,23 +22,22 @@ from ..utils import d2h_into, h2d
 from ..utils import streams as S
 
 
-class SecAggMixin:
-    # ------------------------------------------------------------------ off-critical-path work
-    def _background(self, fn, *inputs):
-        """Run `fn` on the background stream behind everything queued so far on the main stream.
-        Nothing on the round's critical path reads the result: its inputs and outputs are
-        stream-ordered on the background stream, so the main stream never waits for it (it overlaps
-        the next round's head).  Without a GPU it runs inline."""
-        if not self.gpu:
-            return fn()
-        main = S.current()
-        bg = self.bg_stream
-        S.wait(bg, main)
-        with S.use(bg):
-            out = fn()
-        S.hold(*[t for t in inputs if isinstance(t, torch.Tensor)])
-        return out
+class _Rows:
+    """Share rows the host path aggregates on the GPU, in the shape of a speculative MSM's handle (NativeSpec): the
+    rows' keep flags are set (alive), the tensors are final once `ev` has passed."""
 
+    no_commit = False
+    qdelta = None   # never the pre-step's rows: the audit sums come from the rows' commitment slots
+
+    def __init__(self, pts, ys, alive, rows_t, ev):
+        self.pts, self.ys, self.alive, self.rows_t, self.ev = pts, ys, alive, rows_t, ev
+        self.rows = list(range(pts.shape[0]))
+
+    def launch(self) -> None:
+        return None
+
+
+class SecAggMixin:
     # ------------------------------------------------------------------ device-side aggregation
     def _predict_miners(self, plan, live):
         """(contributing miners, share part of each) exactly as leader_view / route_shares report them
@@ -56,29 +55,6 @@ class SecAggMixin:
         if self.pc.shares_per_miner * len(contributing) < self.cfg.poly_size:
             return None   # too few live miners for a quorum (leader_view): the round's block is empty
         return contributing, part
-
-    def _spec_aggregate(self, spec, pred, node) -> dict:
-        """Python path (host crypto, the KZG audit's per-rank inputs) of the device-selection aggregation; GPU
-        rounds otherwise take _spec_aggregate_native.  Queue the secure aggregation of the rows the committee's
-        selection kept -- masked share-value
-        sums, the cross-rank combination, exact recovery (main stream), the audit's commitment sums +
-        check (side stream), the witness sums (background stream) -- right behind the selection
-        kernels, before the host has read the selection.  Every rank queues it at the same point (the
-        selection is replicated), so its collective lines up.  The host later adopts it if the
-        approvals, miners and parts match (_secure_aggregation).  node: device int32 mask over the
-        Krum rows (the leader's block)."""
-        contributing, part = pred
-        sp = spec[1] if spec is not None else None
-        pts = ys = alive = None
-        if sp is not None:
-            sp.launch()
-            pts, ys, alive = sp.pts, sp.ys, sp.alive
-            if sp.no_commit and self.cfg.audit_aggregate:
-                raise RuntimeError("speculative MSM without commitment slots but no chunk commitments to audit with")
-            S.current().wait_event(sp.ev)          # the MSM's shares
-        agg = self._aggregate(pts, ys, alive, contributing, part, self._now(self.fsm.iteration))
-        agg["contributing"], agg["part"], agg["accepted"], agg["node"] = list(contributing), dict(part), None, node
-        return agg
 
     def _agg_index(self, contributing, part):
         """Resident index tensors of one miner layout (a handful recur: the parts are a permutation of
@@ -110,124 +86,76 @@ class SecAggMixin:
         return hit
 
     def _aggregate(self, pts, ys, rowsel, contributing, part, now) -> dict:
-        """Secure aggregation of this rank's kept rows, combined over ranks, then exact recovery.
+        """CPU (host crypto) secure aggregation of this rank's kept rows, combined over ranks, then exact recovery;
+        GPU rounds aggregate through the native calls (_spec_aggregate_native).
 
-        Every miner sums the shares it received (aggregateSecret, kyber.go:244-287) and the leader
-        recovers from the miners' sums (kyber.go:809-857).  Each rank sums its own workers' share
-        columns (one kernel) and ONE all_gather hands every rank all partials; the fused recovery kernel
-        adds them up.  The chunk-commitment sums (identical for every miner: same node list) travel in
-        the same buffer for the audit; the witness sums, which no consumer on the protocol path reads,
-        stay per-rank partials on the background stream (the KZG audit reads them when on).
+        Every miner sums the shares it received (aggregateSecret, kyber.go:244-287) and the leader recovers from
+        the miners' sums (kyber.go:809-857).  Each rank sums its own workers' share columns and ONE all_gather
+        hands every rank all partials (share sums, chunk-commitment sums for the audit, the clocks); the witness
+        sums stay per-rank partials (the KZG audit reads them when on).
 
-        pts [R, nch, T+1, pw] / ys [R, nch, T] (None: no local rows); rowsel: device int32 mask [R]
-        or a host list of row indices.  Returns the handles _finish_secagg consumes."""
+        pts [R, nch, T+1, 64] / ys [R, nch, T] (None: no local rows); rowsel: a list of row indices.  Returns the
+        handles _finish_secagg consumes."""
+        assert not self.gpu, "GPU rounds aggregate natively"
         cfg, comm = self.cfg, self.comm
         T, nch, pw, pdt = self.T, self.nchunks, self.crypto.point_width, self.crypto.point_dtype
         audit = cfg.audit_aggregate
         kzg = cfg.kzg_audit != "off"
-        (ccols, wcols, ycols_t, xs_t), xs_list, (wts, A_dev, basis_dev), _ = self._agg_index(contributing, part)
+        (ccols, wcols, ycols_t, xs_t), xs_list, _, _ = self._agg_index(contributing, part)
         kzg_in = None   # this rank's (commitment sums, witness sums, share sums) for the KZG audit
-        main = S.current() if self.gpu else None
-        single = comm.world == 1
-        ys_part = None   # this rank's share sums (several ranks / host path); one rank fuses them below
-        ys_fused = mask_fused = None   # one rank, GPU: the share sums are fused into the recovery kernel
-        cs_part = None
-        if pts is not None and (not isinstance(rowsel, list) or rowsel):
+        ys_part = cs_part = None
+        if pts is not None and rowsel:
             flat = pts.view(pts.shape[0], nch * (T + 1), pw)
-            if self.gpu:
-                rows_t = None if not isinstance(rowsel, list) else h2d(rowsel, torch.int32, self.dev)
-                mask = rowsel if rows_t is None else None
-                if single:
-                    ys_fused = ys
-                    if mask is not None:
-                        mask_fused = mask
-                    else:
-                        sel = np.zeros(ys.shape[0], np.int32)
-                        sel[np.asarray(rowsel)] = 1
-                        mask_fused = h2d(sel, torch.int32, self.dev)
-                else:
-                    ys_part = K.sum_rows_i64(ys, rows=rows_t, mask=mask)   # [nch, T], one kernel
-                if audit or kzg:
-                    # the commitment sums on the side stream (the MSM's stream, now done with these rows)
-                    st = self.side_stream
-                    S.wait(st, main)
-                    with S.use(st):
-                        cs_part = B.sum_rows(flat, rows_t, ccols, check=False, row_mask=mask)
-                    S.hold(pts, ccols, mask if mask is not None else rows_t)
-                # the miners' witness sums: no consumer on the protocol path (background stream); the KZG
-                # audit, when on, reads them from there
-                ws_part = self._background(lambda: B.sum_rows(flat, rows_t, wcols, check=False, row_mask=mask),
-                                           flat, wcols, mask if mask is not None else rows_t)
-                if kzg:
-                    kzg_in = (cs_part, ws_part, None if single else ys_part.index_select(1, ycols_t.long()))
-            else:
-                rows_l = list(rowsel)
-                ys_part = ys[rows_l].sum(0)
-                if audit or kzg:
-                    cs_part = self.crypto.sum_rows(flat[rows_l][:, ccols.long()])
-                if kzg:
-                    kzg_in = (cs_part, self.crypto.sum_rows(flat[rows_l][:, wcols.long()]),
-                              ys_part.index_select(1, ycols_t.long()))
-        if ys_part is None and ys_fused is None:   # no local rows: nothing to add
-            ys_part = torch.zeros((nch, T), dtype=torch.int64, device=self.dev)
+            rows_l = list(rowsel)
+            ys_part = ys[rows_l].sum(0)
+            if audit or kzg:
+                cs_part = self.crypto.sum_rows(flat[rows_l][:, ccols.long()])
+            if kzg:
+                kzg_in = (cs_part, self.crypto.sum_rows(flat[rows_l][:, wcols.long()]),
+                          ys_part.index_select(1, ycols_t.long()))
+        if ys_part is None:   # no local rows: nothing to add
+            ys_part = torch.zeros((nch, T), dtype=torch.int64)
         if audit and cs_part is None:   # no local rows: the neutral element (point at infinity)
-            cs_part = torch.zeros((nch, pw), dtype=pdt, device=self.dev)
+            cs_part = torch.zeros((nch, pw), dtype=pdt)
         # ---- combine over ranks: ONE all_gather (share sums, commitment sums, clock)
         clock = None
-        ys_src = None
         if comm.world > 1:
-            if self.gpu and audit:
-                S.wait(main, self.side_stream)   # the commitment sums travel in the gather
-            parts = [ys_part.reshape(1, -1), torch.full((1, 1), now, dtype=torch.int64, device=self.dev)]
+            parts = [ys_part.reshape(1, -1), torch.full((1, 1), now, dtype=torch.int64)]
             if audit:
                 parts.append(cs_part.reshape(1, -1))
             got = comm.all_gather_packed(parts)
-            ys_src = got[0].view(comm.world, nch, T)      # the recovery kernel sums the ranks' partials
+            ys_src = got[0].view(comm.world, nch, T)
             clock = got[1].reshape(comm.world)
-            if audit:
-                cs_all = got[2].view(comm.world, nch, pw)
-                cs_tot = B.sum_rows(cs_all.contiguous(), None, None, check=False) if self.gpu else \
-                    self.crypto.sum_rows(cs_all)
+            cs_tot = self.crypto.sum_rows(got[2].view(comm.world, nch, pw)) if audit else None
         else:
-            ys_src = ys_part.reshape(1, nch, T) if ys_part is not None else None
+            ys_src = ys_part.reshape(1, nch, T)
             cs_tot = cs_part
-        if self.gpu:
-            src = ys_fused if ys_fused is not None else ys_src
-            W_new, coeffs, status, agg = K.recover_rows(src.contiguous(), mask_fused if ys_fused is not None else None,
-                                                        ycols_t, xs_t, wts, A_dev, basis_dev, cfg.poly_size, self.d,
-                                                        self.W, 10.0 ** cfg.precision)
-        else:
-            agg = ys_src.sum(0).index_select(1, ycols_t.long()).contiguous()   # [nch, npts]
-            W_new, coeffs, status = K.recover(agg, xs_t.cpu(), cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
-        # the recovered model (and the clocks) are read back right behind the recovery, AHEAD of the
-        # audit queued next on the same stream: the block is built while the audit still runs
+        agg = ys_src.sum(0).index_select(1, ycols_t.long()).contiguous()   # [nch, npts]
+        W_new, coeffs, status = K.recover(agg, xs_t.cpu(), cfg.poly_size, self.d, self.W, 10.0 ** cfg.precision)
         readback = self._d2h_async(status, W_new, *((clock,) if clock is not None else ()))
-        if self._pipelined() and getattr(self.task, "stateless_step", False):
-            # every rank recovers the same W_new, so each one queues its own local peers' next step (on the
-            # Gram stream, behind the recovery but not behind the audit queued next on main)
-            self._pre = self._queue_pre_step(W_new, self.fsm.iteration + 1)   # fsm: the round being aggregated
         audit_ok = self._audit(coeffs, cs_tot.reshape(1, nch, pw)) if audit else None
         out = {"W_new": W_new, "status": status, "agg": agg, "xs": list(xs_list), "audit_ok": audit_ok,
                "clock": clock, "now": now, "readback": readback}
         if kzg_in is not None:
-            # each rank audits its own partial aggregate (verifySecret is linear in (C, W, y)); staged only
-            # once the aggregate is adopted (_finish_secagg), behind the work that produced these sums
+            # each rank audits its own partial aggregate (verifySecret is linear in (C, W, y))
             cs_k, ws_k, y_k = kzg_in
-            out["kzg_in"] = (cs_k, ws_k, agg if y_k is None else y_k, xs_t)
-            if self.gpu:
-                out["kzg_events"] = [S.record(main), S.record(self.side_stream), S.record(self.bg_stream)]
+            out["kzg_in"] = (cs_k, ws_k, agg if comm.world == 1 else y_k, xs_t)
         return out
 
     def _spec_aggregate_native(self, sp, pred, node, amap, flags_set: bool = False) -> dict:
-        """_spec_aggregate through the fused native calls (kernels/round.hip): one rank -- ONE call queues the
-        speculative rows' flags, the early audit sums, the miners' sums + exact recovery + read-back, the next
-        round's pre-step and the audit; several ranks -- one call up to this rank's partial sums in the packed
+        """The GPU secure aggregation through the fused native calls (kernels/round.hip) -- behind the committee's
+        selection (sp: the speculative MSM) or on the host-decided path (sp: _Rows) alike.  One rank: ONE call
+        queues the rows' flags, the early audit sums, the miners' sums + exact recovery + read-back, the next
+        round's pre-step and the audit; several ranks: one call up to this rank's partial sums in the packed
         send row, the all_gather (main stream), one call for the totals, recovery, read-back, pre-step and
-        audit.  Same kernels, streams and order as the Python path it replaces."""
+        audit.  With the KZG audit on, this rank's partial aggregate (commitment, witness and share sums) is
+        copied out of the resident buffers for it (_kzg_capture)."""
         cfg, comm, na = self.cfg, self.comm, self._native
         contributing, part = pred
-        _, xs_list, _, lid = self._agg_index(contributing, part)
-        audit = 1 if cfg.audit_aggregate else 0
+        (_, _, ycols_t, xs_t), xs_list, _, lid = self._agg_index(contributing, part)
+        kzg = cfg.kzg_audit != "off"
+        run_audit = cfg.audit_aggregate
+        audit = 1 if (run_audit or kzg) else 0   # the KZG audit reads the commitment sums too
         early = -1
         if sp is not None:
             sp.launch()
@@ -236,78 +164,80 @@ class SecAggMixin:
                 early, audit = pc.slot, 2   # the audit's sums from the pre-step's chunk commitments, early
             elif sp.no_commit and audit:
                 raise RuntimeError("speculative MSM without commitment slots but no chunk commitments to audit with")
+        if kzg and getattr(self, "_kzg_copied", None) is not None:
+            S.current().wait_event(self._kzg_copied)   # the last aggregate's copies before its buffers are rewritten
         nxt = self.fsm.iteration + 1            # fsm: the round being aggregated
-        want_pre = self._pipelined() and getattr(self.task, "stateless_step", False)
-        native_pre = want_pre and self._native_prestep_ok()
+        # the next round's pre-step behind the recovery (softmax tasks: binds the task at the first use)
+        pre_it = nxt if (self._pipelined() and getattr(self.task, "stateless_step", False)
+                         and self._native_prestep_ok()) else -1
         now = self._now(self.fsm.iteration)
-        sel = None if flags_set else node   # None: the vote kernel has set the rows' flags already
+        sel = None if flags_set else node   # None: the vote kernel (or the host path) has set the rows' flags
         if comm.world == 1:
-            W_new, pre = na.after_select(sel, amap, sp, early, self.upload_stream, lid, self.W, audit,
-                                         nxt if native_pre else -1, audit_now=not (want_pre and not native_pre))
+            W_new, pre = na.after_select(sel, amap, sp, early, self.upload_stream, lid, self.W, audit, pre_it,
+                                         audit_now=run_audit)
             readback, clock = na.readback(), None
+            if pre is not None:
+                pre = self._finish_pre(pre, nxt)
         else:
             na.select_partials(sel, amap, sp, early, self.upload_stream, lid, now, audit)
             comm.all_gather_into(na.recv, na.send)
-            W_new, k = na.after_gather(lid, self.W, audit, nxt if native_pre else -1,
-                                       audit_now=not (want_pre and not native_pre))
+            W_new, k = na.after_gather(lid, self.W, audit, pre_it, audit_now=run_audit)
             pre = self._finish_pre(na._pre_out(k, W_new, nxt), nxt) if k >= 0 else None
             readback, clock = na.readback(clocks=True), True
         if pre is not None:
-            if comm.world == 1:
-                pre = self._finish_pre(pre, nxt)
             self._pre = pre
-        elif want_pre:
-            self._pre = self._queue_pre_step(W_new, nxt)
-        audit_ok = na.audit(queue=want_pre and not native_pre) if audit else None
-        return {"W_new": W_new, "status": na.status, "agg": na.layout_agg(lid), "xs": list(xs_list),
-                "audit_ok": audit_ok, "clock": clock, "now": now, "readback": readback,
-                "contributing": list(contributing), "part": dict(part), "accepted": None, "node": node}
+        out = {"W_new": W_new, "status": na.status, "agg": na.layout_agg(lid), "xs": list(xs_list),
+               "audit_ok": na.audit(queue=False) if run_audit else None, "clock": clock, "now": now,
+               "readback": readback, "contributing": list(contributing), "part": dict(part), "accepted": None,
+               "node": node}
+        if kzg:
+            out["kzg_in"], out["kzg_events"] = self._kzg_capture(lid, ycols_t, xs_t), []
+        return out
+
+    def _kzg_capture(self, lid: int, ycols_t, xs_t):
+        """This rank's partial aggregate for the KZG audit, copied (audit stream) out of the native round's resident
+        buffers once the streams that wrote them are done: chunk-commitment sums, witness sums and share sums at
+        the contributing points ([nch, npts]: the recovered aggregate on one rank, this rank's send-row partials
+        on several).  The next aggregation waits for the copies (_kzg_copied) before rewriting the buffers."""
+        na, nch = self._native, self.nchunks
+        st = self.vrf_stream
+        for src in (S.current(), self.side_stream, self.upload_stream, self.witness_stream):
+            S.wait(st, src)
+        with S.use(st):
+            if self.comm.world == 1:
+                cs, ys = na.cs.clone(), na.layout_agg(lid).clone()
+            else:
+                row = na.send
+                cs = row[: 96 * nch].view(torch.int32).view(nch, 24).clone()
+                ys = row[96 * nch: 96 * nch + 8 * nch * self.T].view(torch.int64).view(nch, self.T) \
+                    .index_select(1, ycols_t.long())
+            ws = na.layout_ws(lid).clone()
+            self._kzg_copied = S.record(st)
+        return cs, ws, ys, xs_t
+
+    def _native_rows_aggregate(self, pts, ys, rowsel: list, pred, ev) -> dict:
+        """The host-decided path's GPU aggregation (no device selection, a speculative miss, a prediction mismatch):
+        rows `rowsel` of the share tensors pts / ys (None: no local rows) through the same native calls, with the
+        rows' flags set here instead of by the selection kernel."""
+        rows = None
+        if pts is not None and rowsel:
+            keep = np.zeros(pts.shape[0], np.int32)
+            keep[np.asarray(rowsel, np.int64)] = 1
+            rows = _Rows(pts, ys, h2d(keep, torch.int32, self.dev),
+                         h2d(np.arange(pts.shape[0], dtype=np.int32), torch.int32, self.dev), ev)
+        return self._spec_aggregate_native(rows, pred, None, None, flags_set=True)
 
     # ------------------------------------------------------------------ read-backs and the audit
     def _d2h_async(self, *ts: torch.Tensor):
-        """Queue the copies now (on the current stream, behind what produced the tensors and ahead of
-        anything queued later); the returned callable waits for them and gives numpy arrays."""
-        if not self.gpu:
-            out = [t.numpy() for t in ts]
-            return lambda: out
-        hs = []
-        for i, t in enumerate(ts):
-            # persistent pinned buffers per (slot, shape, dtype): a round reads its copies before the next
-            # round queues new ones into the same buffer
-            key = (i, tuple(t.shape), t.dtype)
-            h = self._pinned.get(key)
-            if h is None:
-                h = self._pinned[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-            d2h_into(h, t.contiguous())
-            hs.append(h)
-        ev = S.record()
-
-        def wait():
-            S.host_wait(ev)
-            return [h.numpy() for h in hs]
-        return wait
+        """CPU: the tensors as numpy arrays behind a callable (the GPU path reads back natively)."""
+        out = [t.numpy() for t in ts]
+        return lambda: out
 
     def _audit(self, coeffs: torch.Tensor, csum: torch.Tensor):
-        """Queue the aggregate audit (recovered chunks vs the miners' summed chunk commitments); returns a
-        callable giving ok int32 [n_miners, nchunks].  On the GPU the check runs on the main stream (high
-        priority, every CU: the MSM is done by now) while the host builds the block (gob + SHA-256)."""
-        if not self.gpu:
-            ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
-            return lambda: ok
-        main = S.current()
-        S.wait(main, self.side_stream)   # the commitment sums
-        ok = self.crypto.check_aggregate(coeffs, csum)
-        key = ("audit", tuple(ok.shape), ok.dtype)
-        host = self._pinned.get(key)
-        if host is None:
-            host = self._pinned[key] = torch.empty(ok.shape, dtype=ok.dtype, pin_memory=True)
-        d2h_into(host, ok.contiguous())
-        ev = S.record(main)
-
-        def result():
-            S.host_wait(ev)
-            return host.numpy()
-        return result
+        """CPU: the aggregate audit (recovered chunks vs the miners' summed chunk commitments) behind a callable
+        giving ok int32 [n_miners, nchunks] (the GPU path runs it natively: bsc_round_audit)."""
+        ok = self.crypto.check_aggregate(coeffs.cpu(), csum.cpu())
+        return lambda: ok
 
     # ------------------------------------------------------------------ secure aggregation path
     def _secure_aggregation(self, plan, live, approved, qdelta, local_workers, row_of, commit_of,
@@ -337,7 +267,7 @@ class SecAggMixin:
         # computed; every rank takes this branch together (replicated decisions)
         with tm.phase("shares"):
             local_used = [w for w in node_list if w in self.local]
-            pts = ys = None
+            pts = ys = ev = None
             rowsel: list = []
             if local_used:
                 spec_row = {w: i for i, w in enumerate(spec[0])} if spec is not None else {}
@@ -345,16 +275,18 @@ class SecAggMixin:
                 if spec is not None and all(w in spec_row for w in local_used) and not spec[1].no_commit:
                     sp = spec[1]
                     sp.launch()
-                    pts, ys = sp.pts, sp.ys
-                    if self.gpu:
-                        S.current().wait_event(sp.ev)
+                    pts, ys, ev = sp.pts, sp.ys, sp.ev
                     rowsel = [spec_row[w] for w in local_used]   # rows of the speculative tensors
                 else:
                     sel = h2d([row_of[w] for w in local_used], torch.long, self.dev)
                     pts, ys = self.crypto.shares(qdelta.index_select(0, sel).contiguous())
                     rowsel = list(range(len(local_used)))
+                    ev = S.record() if self.gpu else None
         with tm.phase("recover"):
-            agg = self._aggregate(pts, ys, rowsel, contributing, part_of, self._now(plan.iteration))
+            if self.gpu:
+                agg = self._native_rows_aggregate(pts, ys, rowsel, (contributing, part_of), ev)
+            else:
+                agg = self._aggregate(pts, ys, rowsel, contributing, part_of, self._now(plan.iteration))
             return self._finish_secagg(plan, node_list, commit_of, agg)
 
     def _finish_secagg(self, plan, node_list, commit_of, h):

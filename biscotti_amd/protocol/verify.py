@@ -184,20 +184,18 @@ class VerifyMixin:
         itself should set the rows' flags (the fused native path), else None."""
         sp = spec[1] if spec is not None else None
         pred = self._predict_miners(plan, live) if self.gpu and self.cfg.secure_agg else None
-        # the fused native path (one call behind the selection) takes every device-selection round it can
-        fused = pred is not None and self._native is not None and self.cfg.kzg_audit == "off" and \
-            (sp is not None or self.comm.world > 1)
+        # the native aggregation behind the selection: every GPU round with a predictable miner layout and local
+        # speculative rows (one rank) or any rows at all (several ranks: the collective lines up on every rank);
+        # the rest takes the host-decided path after the approvals
+        fused = pred is not None and self._native is not None and (sp is not None or self.comm.world > 1)
 
         def on_accept(node):
             with self.timer.phase("verify.queue_agg"):
                 if fused:
                     box["sa"] = self._spec_aggregate_native(sp, pred, node, amap_t, box.get("flags_set", False))
-                    return
-                if sp is not None:
+                elif sp is not None:   # no aggregate behind the selection: cancel the rows the block drops
                     B.set_alive(node, amap_t, sp.alive)
-                    sp.launch()   # no-op when the MSM already runs speculatively
-                if pred is not None:
-                    box["sa"] = self._spec_aggregate(spec, pred, node)
+                    sp.launch()
         # the fused path lets the noise-aware Krum's vote kernel set the speculative rows' flags itself
         flags = (amap_t, sp.alive) if fused and sp is not None and amap_t is not None else None
         return on_accept, flags
@@ -242,7 +240,10 @@ class VerifyMixin:
         kernel (the workers' commitment rows land in pinned memory)."""
         pre = head["krum_pre"]
         nz_np, sc_np = self._noise_ids_np(noisers, head["local_workers"])
-        rows = self.crypto.commit_rows_tensor(head["pending_commits"]).to(self.dev)
+        if head["local_workers"]:
+            rows = self.crypto.commit_rows_tensor(head["pending_commits"]).to(self.dev)
+        else:   # no local worker this round (committee members, churn): every slot of the row is zeros
+            rows = torch.zeros((1, self.crypto.point_width), dtype=torch.int32, device=self.dev)
         src = [-1] * self.maxlocal
         row_of = head["row_of"]
         for w in head["local_workers"]:

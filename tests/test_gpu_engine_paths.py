@@ -210,7 +210,7 @@ def test_mnist_label_flip_rejection_floor_default_noise():
     assert last10 <= DIGIT1_ERR_CEILING, last10
 
 
-DIGIT1_ERR_CEILING = 0.75   # this deterministic run measures 0.647 (rejection 0.756), docs/ROBUSTNESS.md
+DIGIT1_ERR_CEILING = 0.70   # this deterministic run measures 0.647 (rejection 0.756): + 0.05, docs/ROBUSTNESS.md
 
 
 @pytest.mark.parametrize("poisoning", [0.0, 0.3])

@@ -443,3 +443,30 @@ def test_eval_errors_cached_tiles_repeated_launches():
         ra = K.eval_error(X[:split], y[:split], Wk, 784, 10)
         rb = K.eval_error(X[split:], y[split:], Wk, 784, 10)
         assert abs(a - ra) <= 1.0 / split and abs(b - rb) <= 1.0 / (1000 - split)
+
+
+@pytest.mark.parametrize("U1", [16, 23, 100])
+def test_noise_gram_table_tiles_bit_identical(U1):
+    """The noise-aware Gram with its noise x noise tiles copied from the setup table of the 100 periodic noise
+    Grams (NoiseRows.gram_table) equals the Gram that computes them, bit for bit -- whole, and split over 3
+    ranks' tile ranges -- for delta blocks that do and do not end on a tile boundary."""
+    N, D = 37, 7850
+    nr = K.NoiseRows(N, D, 11, "cuda")
+    tab = nr.gram_table()
+    assert tab.shape == (100, N, N) and torch.equal(tab[5], tab[5].T)
+    g = torch.Generator().manual_seed(U1)
+    X = (0.01 * torch.randn((U1, D), generator=g)).float().cuda()
+    for it in (0, 5, 199):
+        ref = K.gram_stacked_async(X, nr.rows(it))["gram"]
+        got = K.gram_stacked_async(X, nr.rows(it), nn=tab[it % 100])["gram"]
+        torch.cuda.synchronize()
+        assert torch.equal(ref, got), (it, (ref - got).abs().max().item())
+        parts = [K.gram_stacked_async(X, nr.rows(it), split=(r, 3), nn=tab[it % 100]) for r in range(3)]
+        torch.cuda.synchronize()
+        U = U1 + N
+        _, _, chunk, npairs = K.gram_split(U, 0, 3)
+        full = torch.cat([p["gram"][r * chunk:(r + 1) * chunk] for r, p in enumerate(parts)])[:npairs]
+        assert torch.equal(ref, full)
+    # the table's entries are the dense noise Gram (fp64 products of fp32 rows, summed exactly enough)
+    rows = nr.rows(7).double()
+    assert torch.allclose(tab[7], rows @ rows.T, rtol=1e-12, atol=1e-9)
