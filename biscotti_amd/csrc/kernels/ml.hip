@@ -70,7 +70,9 @@ extern "C" __global__ void __launch_bounds__(SM_THREADS) k_softmax_step(
     const float* X, const int* y, const long long* off, const int* ntrain, const int* pid, const double* W, int D_IN,
     int D_OUT, int B, int P, unsigned long long seed, int iteration, float max_norm, double qscale, float* delta,
     long long* qdelta, float* loss, int lo, int* ones, int nones) {
-  BSC_SET_PRIO(BSC_PRIO_AHEAD);
+  // the next round's speculative share MSM waits for this step (and the Gram behind it on the same stream):
+  // a short latency chain at the front of the round
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   // ones (optional): the next speculative MSM's row flags, set to 1 here (the MSM waits for this step anyway)
   // instead of by an upload or a kernel of their own in front of the MSM
   if (ones != nullptr && blockIdx.x == 0)
@@ -482,7 +484,9 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
                                                               double* part, double* gram, unsigned int* count,
                                                               const float* X2, int U1, long long stride2, int pair0,
                                                               const double* nn, int tn0) {
-  BSC_SET_PRIO(BSC_PRIO_AHEAD);
+  // high: at priority 1 the pre-step's commitment MSM squeezed it to ~220 us, and its resident workgroups kept
+  // the speculative share MSM from being dispatched until it ended (docs/PERF.md round 5); its work is ~10 us
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ double red[4][256];
   __shared__ unsigned int last;
   // this launch covers the tile pairs [pair0, pair0 + gridDim.x) (several ranks split one Gram); part and

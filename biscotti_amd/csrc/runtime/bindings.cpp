@@ -8,6 +8,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <future>
 #include <random>
 #include <thread>
@@ -430,6 +431,12 @@ static G1 g1_from_jac_u32(const uint32_t* p) {
   return g;
 }
 
+// the IFMA batch path unless BISCOTTI_VRF_SCALAR is set (same-box A/Bs) or the CPU lacks it
+static bool vrf_batch_enabled() {
+  static const bool on = vrf_beta_batch_supported() && std::getenv("BISCOTTI_VRF_SCALAR") == nullptr;
+  return on;
+}
+
 // One VRF batch on the native dispatcher: pass 1 computes every output (H, Gamma = x*H, beta), pass 2
 // the proofs unless outputs_only (the device prover makes them, kernels/vrf.hip).
 static std::shared_ptr<VrfJob> vrf_submit(const std::vector<Bytes>& seeds, const Bytes& alpha, int threads,
@@ -451,8 +458,20 @@ static std::shared_ptr<VrfJob> vrf_submit(const std::vector<Bytes>& seeds, const
     try {
       // pass 1: every output (H, Gamma = x*H, beta); pass 2: the proofs (k*B, k*H, c, s) unless
       // they are produced elsewhere (outputs_only: the device prover, kernels/vrf.hip)
-      if (jp->outputs_only) {
-        parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+      const size_t n = jp->seeds.size();
+      if (jp->outputs_only && vrf_batch_enabled() && n >= 2 * size_t(std::max(1, threads))) {
+        // eight outputs per AVX-512 IFMA batch (vrf_ifma.cpp, ~5x the outputs per core) once each thread would
+        // otherwise compute two or more one by one: ~100 outputs on 14 threads take one batch's time
+        parallel_for((n + 7) / 8, threads, [&](size_t b) {
+          const size_t o = 8 * b, m = std::min<size_t>(8, n - o);
+          const VrfKey* ks[8];
+          Bytes outs[8];
+          for (size_t i = 0; i < m; ++i) ks[i] = &VrfKey::cached(jp->seeds[o + i]);
+          vrf_beta_batch(ks, int(m), jp->alpha, outs);
+          for (size_t i = 0; i < m; ++i) jp->out[o + i].first = std::move(outs[i]);
+        });
+      } else if (jp->outputs_only) {
+        parallel_for(n, threads, [&](size_t i) {
           jp->out[i].first = vrf_beta(VrfKey::cached(jp->seeds[i]), jp->alpha);
         });
       } else {
@@ -1018,6 +1037,20 @@ PYBIND11_MODULE(_biscotti_rt, m) {
   });
   m.def("vrf_base_table", [] { return P(vrf_base_table_bytes()); });
   m.def("vrf_beta", [](py::bytes seed, py::bytes alpha) { return P(vrf_beta(VrfKey::cached(B(seed)), B(alpha))); });
+  m.def("vrf_beta_batch_supported", [] { return vrf_beta_batch_supported(); });
+  m.def("vrf_beta_batch", [](std::vector<py::bytes> seeds, py::bytes alpha) {
+    std::vector<const VrfKey*> ks;
+    for (auto& s : seeds) ks.push_back(&VrfKey::cached(B(s)));
+    const Bytes a = B(alpha);
+    std::vector<Bytes> out(ks.size());
+    {
+      py::gil_scoped_release rel;
+      vrf_beta_batch(ks.data(), int(ks.size()), a, out.data());
+    }
+    py::list res;
+    for (auto& o : out) res.append(P(o));
+    return res;
+  });
   py::class_<VrfSeedSet, std::shared_ptr<VrfSeedSet>>(m, "VrfSeedSet")
       .def(py::init([](std::vector<py::bytes> seeds) {
         auto st = std::make_shared<VrfSeedSet>();
@@ -1161,6 +1194,11 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       .def("__len__", [](const Blockchain& c) { return c.blocks.size(); })
       .def("block", [](const Blockchain& c, size_t i) { return c.blocks.at(i); })
       .def("latest", [](const Blockchain& c) { return c.latest(); })
+      // the latest block's hash alone (latest() copies the whole block, GlobalW included, into a new object)
+      .def("latest_hash", [](const Blockchain& c) {
+        const Bytes& h = c.latest().hash;
+        return py::bytes(reinterpret_cast<const char*>(h.data()), h.size());
+      })
       .def("get", [](const Blockchain& c, i64 it) -> py::object {
         const Block* b = c.get(it);
         if (!b) return py::none();

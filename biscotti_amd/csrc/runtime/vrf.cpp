@@ -510,6 +510,23 @@ Bytes challenge_str(const Bytes& Y, const Bytes& H, const Bytes& G, const Bytes&
 
 }  // namespace
 
+// the scalar field code for vrf_ifma.cpp (per-lane encodings and constants of the batched path)
+namespace vrf_detail {
+void fe51_tobytes(u8 out[32], const u64 v[5]) {
+  Fe a;
+  memcpy(a.v, v, sizeof(a.v));
+  fe_tobytes(out, a);
+}
+void fe51_frombytes(u64 v[5], const u8 in[32]) {
+  const Fe a = fe_frombytes(in);
+  memcpy(v, a.v, sizeof(a.v));
+}
+void fe51_consts(u64 d[5], u64 sqrtm1[5]) {
+  memcpy(d, D().v, 5 * sizeof(u64));
+  memcpy(sqrtm1, SQRTM1().v, 5 * sizeof(u64));
+}
+}  // namespace vrf_detail
+
 Bytes ed25519_public_from_seed(const Bytes& seed32) {
   if (seed32.size() != 32) fail("ed25519: seed must be 32 bytes");
   u8 x[32], prefix[32];

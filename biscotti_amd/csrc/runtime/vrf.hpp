@@ -38,6 +38,10 @@ Bytes vrf_finish(const VrfKey& key, const VrfStage& stage);
 // The output alone (no proof, no encoding of H): the noiser lottery's input when the proofs are
 // produced elsewhere (kernels/vrf.hip).
 Bytes vrf_beta(const VrfKey& key, const Bytes& alpha);
+// vrf_beta of n keys (same alpha) eight at a time on AVX-512 IFMA lanes (vrf_ifma.cpp); CPUs without IFMA
+// (vrf_beta_batch_supported() false) take vrf_beta per key.  out: n outputs.
+bool vrf_beta_batch_supported();
+void vrf_beta_batch(const VrfKey* const* keys, int n, const Bytes& alpha, Bytes* out);
 // The fixed-base table of B (64 signed radix-16 windows x 8 multiples, cached form) as 512 x 4
 // canonical 32-byte field encodings (Y+X, Y-X, 2Z, 2dT): the device prover's k*B table.
 Bytes vrf_base_table_bytes();

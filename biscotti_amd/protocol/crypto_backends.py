@@ -217,7 +217,7 @@ class DeviceCrypto:
 
     def shares(self, qdelta: torch.Tensor):
         rows = torch.arange(qdelta.shape[0], dtype=torch.int32, device=qdelta.device)
-        return self.eng.shares(qdelta, rows)
+        return self.eng.shares(qdelta, rows, check_rows=False)   # arange: in range (and no stream sync)
 
     def shares_async(self, qdelta: torch.Tensor, rows: list, stream, launch: bool = True,
                      group_rows: int = 0, no_commit: bool = False) -> "_SpecShares":

@@ -254,6 +254,12 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 self._agg_index(list(range(M)), {i: perm[i] for i in range(M)})
         if self.gpu and self._noise_krum():
             self._noise_gram_table()   # the 100 periodic noise Grams (~8 MB), built now rather than in round 1
+        if self.gpu and cfg.secure_agg:
+            # the host-decided path's share MSM (a speculative miss): its torch kernels (row gather, arange)
+            # are loaded at their first launch -- tens of ms in the first round that misses otherwise
+            q = torch.zeros((2, self.d), dtype=torch.int64, device=self.dev)
+            self.crypto.shares(q.index_select(0, torch.arange(2, dtype=torch.long, device=self.dev)).contiguous())
+            torch.cuda.synchronize(self.dev)
         if self.vrf_dev is not None:
             # the key material of every peer this rank proves for (secret scalar, nonce prefix, public key:
             # a fixed-base multiplication each) -- the host batches and the device prover share the cache

@@ -54,7 +54,7 @@ class RoundHeadMixin:
         head = {"live": live, "plan": plan}
         if plan.done:
             return head
-        latest_hash = fsm.chain.latest().hash
+        latest_hash = fsm.chain.latest_hash()
         workers = [w for w in plan.workers if live[w]]
         local_workers = [w for w in workers if w in self.local]
         # stake None: the noiser lottery reads the FSM's stake natively (unchanged until the block commits)
@@ -362,6 +362,8 @@ class RoundHeadMixin:
         depths = getattr(self, "_spec_depths", None) or []
         if cap <= 0 or len(depths) < SPEC_MIN_HISTORY or self.cfg.has("spec_all_candidates"):
             return -1   # every candidate until a few blocks show how deep they reach
+        if self.cfg.has("spec_tight"):
+            return cap
         # a short history gets more slack: 2 rows per missing block of the window
         return max(cap + SPEC_MARGIN, max(depths) + SPEC_SLACK + 2 * (SPEC_WINDOW - len(depths)))
 

@@ -30,8 +30,8 @@ struct f6 {
 };
 
 // p in 48-bit limbs, p' = -p^-1 mod 2^48
-__device__ __constant__ static const double P48[6] = {189503643146855.0, 35965000243292.0, 242232013277393.0,
-                                                      187451826151812.0, 2081416447993.0, 36789.0};
+__device__ __constant__ static const double P48[6] = {189581434066535.0, 35964808206428.0, 242038291007697.0,
+                                                      187397689598340.0, 2075721435129.0, 36789.0};
 static constexpr double PPRIME = 273780527585961.0;
 static constexpr double TWO48 = 281474976710656.0;          // 2^48
 static constexpr double INV48 = 1.0 / 281474976710656.0;    // 2^-48

@@ -218,9 +218,9 @@ def test_spec_horizon_same_chain_as_every_candidate(poisoning):
     """The speculative share MSM covers the leader's candidate arrivals up to an adaptive horizon (head.py
     SPEC_MARGIN) instead of every candidate: the chain is byte-identical to computing every candidate's shares
     (ablation spec_all_candidates) -- blocks reaching past the horizon are topped up by the host path -- and it
-    launches fewer rows."""
+    launches fewer rows.  spec_tight (horizon = the leader's cap) makes the host top-up path frequent: same chain."""
     out = []
-    for abl in ("", "spec_all_candidates"):
+    for abl in ("", "spec_all_candidates", "spec_tight"):
         eng = _engine(num_nodes=100, poisoning=poisoning, epsilon=1.0, seed=11, ablation=abl)
         hashes = [bytes(eng.run_round().block_hash) for _ in range(8)]   # the horizon applies after 3 blocks
         rows8 = eng.stats.get("spec_rows", 0)
@@ -232,9 +232,11 @@ def test_spec_horizon_same_chain_as_every_candidate(poisoning):
         eng.close()
         assert ok, why
         out.append((hashes, stats))
-    (h0, s0), (h1, s1) = out
-    assert h0 == h1
+    (h0, s0), (h1, s1), (h2, s2) = out
+    assert h0 == h1 == h2
+    if poisoning:
+        assert s2.get("spec_misses", 0) > 0, s2   # rejections among the first cap arrivals: the host path ran
     assert s0.get("spec_head", 0) >= 6 and s1.get("spec_head", 0) >= 6
     assert s0["spec_rows_late"] < 0.9 * s1["spec_rows_late"], (s0["spec_rows_late"], s1["spec_rows_late"])
     print("rows launched after the window", s0["spec_rows_late"], "vs", s1["spec_rows_late"], "misses",
-          s0.get("spec_misses", 0))
+          s0.get("spec_misses", 0), "tight misses", s2.get("spec_misses", 0))

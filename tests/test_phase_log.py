@@ -34,7 +34,8 @@ def test_phase_log_lines_parse_into_the_trace_phases(tmp_path):
     assert [k for k, _ in aggr] == list(range(10))
     for (k, got), t in zip(aggr, trace):
         want = t.get("t_shares", 0.0) + t.get("t_recover", 0.0) + t["t_block"]
-        assert got is not None and abs(got - want) < 1e-3 + 0.02 * want, (k, got, want)
+        # the log's span also covers the host work between those phases (a few ms more on a loaded CPU)
+        assert got is not None and want - 1e-3 <= got <= 1.1 * want + 5e-3, (k, got, want)
     # the reference parser's fixed offset (parseLogs.py:184: line[48:len(line)-1]) reads the miner ids
     miners_lines = [ln for ln in lines if "Miners are" in ln]
     assert [[int(x) for x in ln[48:len(ln) - 1].split(" ")] for ln in miners_lines] == [list(r.miners) for r in res]

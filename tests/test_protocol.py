@@ -348,5 +348,7 @@ def test_spec_horizon_policy():
     assert horizon(eng) == 80 + H.SPEC_SLACK
     eng.cfg = Cfg("spec_all_candidates")
     assert horizon(eng) == -1
+    eng.cfg = Cfg("spec_tight")
+    assert horizon(eng) == 35
     eng.cfg, eng.fsm = Cfg(), SimpleNamespace(leader_cap_size=lambda: 0)   # no leader cap: every candidate
     assert horizon(eng) == -1
