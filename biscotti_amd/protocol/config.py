@@ -92,6 +92,8 @@ class RunConfig:
     #                      multi-rank setting; one rank spins up to 5 ms: a sleeping thread wakes late)
     #   noise_gram_each_round GPU: the noise-aware Gram computes its noise x noise tiles every round instead of
     #                      copying them from the setup table of the 100 periodic noise Grams (ml.NoiseRows.gram_table)
+    #   no_early_front     GPU: the next round's noiser lottery + Krum launch run at its own start instead of at
+    #                      the end of the previous round (engine._round_front): the chain must not change
     #   spec_tight         GPU: the speculative MSM's horizon is the leader's cap exactly (no margin, no slack): a
     #                      block reaching past its first cap arrivals is a speculative miss, topped up by the host
     #                      path (tests and measurements of that path): the chain must not change
@@ -101,7 +103,7 @@ class RunConfig:
     churn_round_s: ClassVar[float] = 25.44
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
-                                  "noise_gram_each_round", "spec_tight")
+                                  "noise_gram_each_round", "spec_tight", "no_early_front")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

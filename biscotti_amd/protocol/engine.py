@@ -203,6 +203,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.rounds_done = 0
         self._partitions = cfg.partitions()
         self._head = None
+        self._front = None            # the next round's front, started at the end of the previous round
+        self._front_planned = False
         self._warm_up()
         import atexit
         import weakref
@@ -368,44 +370,35 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         return iteration + 1 if self.cfg.deterministic_time else int(time.time())
 
     # ------------------------------------------------------------------ the round
-    def run_round(self, last: bool = False) -> RoundResult | None:
+    def run_round(self, last: bool = False, front: bool = True) -> RoundResult | None:
         """One protocol round.  last: the caller ends its run after this round (its final iteration), so the
         device VRF proofs still batched are launched with this round's instead of at drain() -- the same
-        proofs, one prover latency earlier.  The protocol's own last iteration (max_iterations) counts too."""
+        proofs, one prover latency earlier.  The protocol's own last iteration (max_iterations) counts too.
+        front=False: the next round's front (_round_front) is not started at the end of this one (bench.py's
+        last warm-up round, so a timed window holds exactly its own rounds' fronts)."""
         cfg, R, fsm, comm = self.cfg, self.R, self.fsm, self.comm
         t_round = time.perf_counter()
         tm = self.timer
-        with tm.phase("roles"):
-            head, self._head = self._head or self._open_round(), None
-            live, plan = head["live"], head["plan"]
-            if plan.done:
-                return None
-            it = plan.iteration
-            local_workers, inboxes = head["local_workers"], head["inboxes"]
-        krum_pre = head.get("krum_pre")
-        kst = None
-        with tm.phase("pre_vrf"):
-            # host work that does not need the VRF outputs, done while they are computed: the previous round's
-            # signature batch (starts once these outputs are known) and Krum's static tables
-            work, self._pre_vrf_work = self._pre_vrf_work, []
-            for f in work:
-                f(head["fut_noise"])
-            if head.get("vrf_proofs") is not None:
-                self.vrf_dev.submit(*head["vrf_proofs"], self.vrf_stream)
-                if last or it == cfg.max_iterations - 1:
-                    self.vrf_dev.flush(self.vrf_stream, urgent=True)   # the run's end waits for these
-            self._resolve_evals(wait=len(self._evals) > 3)   # a bounded backlog: the host rings hold 4
-            if krum_pre is not None and cfg.verification and inboxes and cfg.defense == "KRUM":
-                kst = head.get("kst") or self._krum_static(krum_pre["xrow"], krum_pre["U1"], plan, live, inboxes, head["spec"],
-                                        head.get("arrivals"))
-        with tm.phase("vrf_join"):
-            noisers = self._select_noisers(head["fut_noise"], head["stake"], local_workers, head.get("vrf_index"))
-        with tm.phase("noise"):
-            # with the phase-1 Gram the noised deltas are never materialised (only Krum reads them)
-            noised = None if krum_pre is not None else \
-                self._noise(head["delta"], head["row_of"], noisers, local_workers, it)
+        # the next round's front starts right after this round's block (engine._round_front): the host work of
+        # the audit wait that nothing before it needs (signature prep, evaluation read-backs) moves behind it
+        self._front_planned = front and not last and self._early_front_ok()
+        fr, self._front = self._front, None
+        if fr is None:
+            with tm.phase("roles"):
+                head, self._head = self._head or self._open_round(), None
+                if head["plan"].done:
+                    return None
+            fr = self._round_front(head, last)
+        else:
+            self.stats["early_fronts"] = self.stats.get("early_fronts", 0) + 1
+            if last and fr["head"].get("vrf_proofs") is not None:
+                self.vrf_dev.flush(self.vrf_stream, urgent=True)   # started before the caller said it is the last
+        head, noisers, noised = fr["head"], fr["noisers"], fr["noised"]
+        live, plan = head["live"], head["plan"]
+        it = plan.iteration
+        local_workers, inboxes = head["local_workers"], head["inboxes"]
         with tm.phase("verify"):
-            v = self._verification(head, noisers, noised, kst)
+            v = self._finish_verification(fr["verify"])
         approved, commit_of, signatures = v["approved"], v["commit_of"], v["signatures"]
         # ---------------------------------------------------------------- aggregation + block
         # host work nothing before the block needs: one rank runs it while it waits for the aggregate audit
@@ -454,6 +447,20 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 eval_pending = self.task.evaluate_async(self.W)
         with tm.phase("next_head"):
             self._head = self._open_round()   # next round's committee + VRF outputs start now
+        if self._front_planned:
+            if not self._head["plan"].done:
+                # the next round's front -- noiser lottery, Krum launch and the aggregation queued behind its
+                # selection -- before this round's remaining host work: the selection lands earlier and
+                # cancels the speculative MSM's rejected rows sooner; the work below fills the next round's waits
+                work, self._pre_vrf_work = self._pre_vrf_work, []   # this round's: after the launch
+                self._front = self._round_front(self._head, False)
+                self._head = None
+                self._pre_vrf_work = work + self._pre_vrf_work
+            with tm.phase("recover.idle"):
+                work, self._pre_vrf_work = self._pre_vrf_work, []
+                for f in work:
+                    f(None)
+                self._resolve_evals(wait=False)   # this round's evaluation was just queued: not waited for
         if self._idle_work is not None:  # every rank, same point: the collective stays aligned
             self._idle_work()
             self._idle_work = None
@@ -487,6 +494,57 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             S.rotate_holds()   # cross-stream tensors of two rounds ago are free to go
         self._maybe_fail(it)
         return res
+
+    def _round_front(self, head: dict, last: bool) -> dict:
+        """A round up to its verification's device launch: the host work that does not need the VRF outputs,
+        the noiser lottery (waits for them), the noise and the verification up to the committee's launch
+        (_verification_steps; the Multi-Krum path stops there, the rest runs through).  run_round finishes it
+        (_finish_verification) -- in the same call, or one round later when the previous round started it."""
+        cfg, tm = self.cfg, self.timer
+        live, plan = head["live"], head["plan"]
+        it = plan.iteration
+        local_workers, inboxes = head["local_workers"], head["inboxes"]
+        krum_pre = head.get("krum_pre")
+        kst = None
+        with tm.phase("pre_vrf"):
+            # host work that does not need the VRF outputs, done while they are computed: the previous round's
+            # signature batch (starts once these outputs are known) and Krum's static tables
+            work, self._pre_vrf_work = self._pre_vrf_work, []
+            for f in work:
+                f(head["fut_noise"])
+            if head.get("vrf_proofs") is not None:
+                self.vrf_dev.submit(*head["vrf_proofs"], self.vrf_stream)
+                if last or it == cfg.max_iterations - 1:
+                    self.vrf_dev.flush(self.vrf_stream, urgent=True)   # the run's end waits for these
+            self._resolve_evals(wait=len(self._evals) > 3)   # a bounded backlog: the host rings hold 4
+            if krum_pre is not None and cfg.verification and inboxes and cfg.defense == "KRUM":
+                kst = head.get("kst") or self._krum_static(krum_pre["xrow"], krum_pre["U1"], plan, live, inboxes, head["spec"],
+                                        head.get("arrivals"))
+        with tm.phase("vrf_join"):
+            noisers = self._select_noisers(head["fut_noise"], head["stake"], local_workers, head.get("vrf_index"))
+        with tm.phase("noise"):
+            # with the phase-1 Gram the noised deltas are never materialised (only Krum reads them)
+            noised = None if krum_pre is not None else \
+                self._noise(head["delta"], head["row_of"], noisers, local_workers, it)
+        with tm.phase("verify"):
+            steps = self._verification_steps(head, noisers, noised, kst)
+            try:
+                next(steps)
+                ver = steps
+            except StopIteration as done:
+                ver = done
+        return {"head": head, "noisers": noisers, "noised": noised, "verify": ver}
+
+    def _early_front_ok(self) -> bool:
+        """The next round's front runs at the end of this one: one rank per process on a GPU, the pipelined
+        noise-aware Multi-Krum path, no churn / partitions / fault injection (whose next round may differ from
+        the head built here) and no per-round phase records (trace, phase log, phase sync: their phases would
+        move to the previous round).  The no_early_front ablation turns it off; the chain is the same."""
+        cfg = self.cfg
+        return (self.gpu and self.comm.world == 1 and self._pipelined() and cfg.secure_agg and cfg.verification
+                and cfg.defense == "KRUM" and self._noise_krum() and not cfg.has("no_early_front")
+                and cfg.churn == 0 and cfg.churn_kill_per_min == 0 and not self._partitions
+                and cfg.fail_point()[0] < 0 and not cfg.phase_log and not cfg.phase_sync and not cfg.trace_file)
 
     # ------------------------------------------------------------------ logging
     def _log_round(self, r: RoundResult) -> None:

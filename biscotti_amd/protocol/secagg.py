@@ -338,11 +338,12 @@ class SecAggMixin:
                 # it slowed the outputs: vrf_join 0.03 -> 0.09 ms), the earlier rounds' evaluation read-backs and
                 # the next round's host preparation fill the audit wait
                 with tm.phase("recover.idle"):
-                    ej = self._early_vrf["job"] if self._early_vrf is not None else None
-                    work, self._pre_vrf_work = self._pre_vrf_work, []
-                    for f in work:
-                        f(ej)
-                    self._resolve_evals()
+                    if not self._front_planned:   # else run after the next round's front (run_round)
+                        ej = self._early_vrf["job"] if self._early_vrf is not None else None
+                        work, self._pre_vrf_work = self._pre_vrf_work, []
+                        for f in work:
+                            f(ej)
+                        self._resolve_evals()
                     self._prepare_next_in_wait()
             with tm.phase("recover.audit"):
                 ok = audit_ok()

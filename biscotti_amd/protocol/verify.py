@@ -288,10 +288,24 @@ class VerifyMixin:
             head["commit_gather"] = (rows, None)
         return got[1].reshape(-1, nn_).contiguous(), got[2].reshape(-1, nn_).contiguous()
 
-    def _verification(self, head: dict, noisers: dict, noised, kst) -> dict:
-        """The verifier committee's decisions and signatures for this round.  Returns approved workers,
-        the commitment table, signatures (where a consumer reads them), the device aggregation box and
-        the deferred signature join."""
+    @staticmethod
+    def _finish_verification(ver) -> dict:
+        """The result of _verification_steps: ver is the stopped generator (resumed to its end here) or the
+        StopIteration that already carries the result."""
+        if isinstance(ver, StopIteration):
+            return ver.value
+        try:
+            while True:
+                next(ver)
+        except StopIteration as done:
+            return done.value
+
+    def _verification_steps(self, head: dict, noisers: dict, noised, kst):
+        """The verifier committee's decisions and signatures for this round, as a generator that stops once
+        right after the Multi-Krum launch (the committee's selection and the aggregation behind it are queued on
+        the device; engine._round_front can start a round this far ahead) and returns (StopIteration.value)
+        approved workers, the commitment table, signatures (where a consumer reads them), the device
+        aggregation box and the deferred signature join."""
         cfg, R, fsm, comm, tm = self.cfg, self.R, self.fsm, self.comm, self.timer
         plan, live, it = head["plan"], head["live"], head["plan"].iteration
         workers, local_workers, inboxes = head["workers"], head["local_workers"], head["inboxes"]
@@ -371,8 +385,9 @@ class VerifyMixin:
                 with tm.phase("verify.defense"):
                     wait = self._launch_krum(X, xrow, plan, live, inboxes, spec, box, pre=krum_pre, nz=nz, sc=sc,
                                              static=kst)
-                    with tm.phase("verify.krum_wait"):
-                        acc_t, node_t = wait()
+                yield "launched"
+                with tm.phase("verify.defense"), tm.phase("verify.krum_wait"):
+                    acc_t, node_t = wait()
                 acc_np = acc_t.numpy().astype(np.uint8)   # [len(vs), ni]
                 acc_row = {v: k for k, v in enumerate(vs)}
                 if box.get("sa") is not None:   # the rows the device aggregation kept

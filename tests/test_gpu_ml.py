@@ -262,6 +262,39 @@ def test_pre_gram_and_early_vrf_keep_the_chain():
     assert stats[0].get("device_aggregations", 0) >= 4
 
 
+@pytest.mark.parametrize("extra", ["", "spec_tight"])
+def test_early_front_keeps_the_chain(extra):
+    """The next round's front (noiser lottery, Krum launch, the aggregation queued behind the selection) started
+    at the end of the previous round gives the chain of running it at the round's own start (no_early_front),
+    with poisoners (Krum's selection decides the blocks) and with spec_tight (speculative misses: the host path
+    aggregates behind an early-launched selection)."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    chains, stats = [], []
+    for abl in (extra, ",".join(a for a in (extra, "no_early_front") if a)):
+        cfg = RunConfig(num_nodes=30, dataset="mnist", seed=5, max_iterations=100, deterministic_time=True,
+                        poisoning=0.3, epsilon=1.0, ablation=abl)
+        eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
+        for k in range(10):
+            eng.run_round(front=k != 4, last=k == 9)   # one round without a front: the next starts its own
+        eng.drain()
+        ok, why = eng.fsm.chain.verify()
+        assert ok, why
+        chains.append([bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))])
+        stats.append(dict(eng.stats))
+        eng.close()
+    assert chains[0] == chains[1]
+    assert stats[0].get("early_fronts", 0) == 8 and "early_fronts" not in stats[1]
+    assert stats[0]["audit_failures"] == 0
+    if extra:   # a miss aggregates on the host-decided path
+        assert stats[0].get("spec_misses", 0) > 0, stats[0]
+        assert stats[0].get("device_aggregations", 0) + stats[0]["spec_misses"] >= 8, stats[0]
+    else:
+        assert stats[0].get("device_aggregations", 0) >= 6, stats[0]
+
+
 @pytest.mark.parametrize("U,n,V", [(94, 70, 3), (150, 140, 5), (256, 256, 3), (300, 200, 26)])
 def test_krum_committee_matches_reference(U, n, V):
     """Committee Multi-Krum (one Gram over the candidate rows, per-verifier inboxes, vote and leader
