@@ -611,26 +611,48 @@ extern "C" __global__ void __launch_bounds__(256) k_krum_rows(const double* gram
 // d-dimensional work (the Gram) runs before the noisers are known (they come from the workers' VRF
 // outputs on the host); only this O(n^2 nn^2) assembly waits for them.
 namespace {
-__device__ __forceinline__ double xx_dot(const double* gram, int T, int U1, const int* nz, const float* sc, int nn,
-                                         int a, int b) {
+// the noisers' ids and weights: device arrays, or (NoiseArg) the kernel's argument block -- the round's tables
+// are ~1.6 KB at 100 peers, so they ride in the launch instead of an upload copy the selection queues behind
+#define NOISE_ARG_MAX 400
+struct NoiseArg {
+  int nz[NOISE_ARG_MAX];
+  float sc[NOISE_ARG_MAX];
+};
+struct NoisePtr {
+  const int* z;
+  const float* s;
+  __device__ __forceinline__ int nz(int i) const { return z[i]; }
+  __device__ __forceinline__ float sc(int i) const { return s[i]; }
+};
+struct NoiseByVal {
+  const NoiseArg* a;
+  __device__ __forceinline__ int nz(int i) const { return a->nz[i]; }
+  __device__ __forceinline__ float sc(int i) const { return a->sc[i]; }
+};
+
+template <class N>
+__device__ __forceinline__ double xx_dot(const double* gram, int T, int U1, N q, int nn, int a, int b) {
   double v = gram_at(gram, T, a, b);
   const double inv = 1.0 / (double)nn;
   for (int t = 0; t < nn; ++t) {
-    v += inv * (double)sc[b * nn + t] * gram_at(gram, T, a, U1 + nz[b * nn + t]);
-    v += inv * (double)sc[a * nn + t] * gram_at(gram, T, U1 + nz[a * nn + t], b);
+    v += inv * (double)q.sc(b * nn + t) * gram_at(gram, T, a, U1 + q.nz(b * nn + t));
+    v += inv * (double)q.sc(a * nn + t) * gram_at(gram, T, U1 + q.nz(a * nn + t), b);
   }
   for (int s2 = 0; s2 < nn; ++s2)
     for (int t = 0; t < nn; ++t)
-      v += inv * inv * (double)sc[a * nn + s2] * (double)sc[b * nn + t] *
-           gram_at(gram, T, U1 + nz[a * nn + s2], U1 + nz[b * nn + t]);
+      v += inv * inv * (double)q.sc(a * nn + s2) * (double)q.sc(b * nn + t) *
+           gram_at(gram, T, U1 + q.nz(a * nn + s2), U1 + q.nz(b * nn + t));
   return v;
 }
-}  // namespace
+// wrapper kept for k_krum_rows_big (device arrays)
+__device__ __forceinline__ double xx_dot(const double* gram, int T, int U1, const int* nz, const float* sc, int nn,
+                                         int a, int b) {
+  return xx_dot(gram, T, U1, NoisePtr{nz, sc}, nn, a, b);
+}
 
-extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise(const double* gram, int T, int U1,
-                                                                   const int* nz, const float* sc, int nn,
-                                                                   const int* inbox, int n, int groupsize,
-                                                                   double* scores) {
+template <class N>
+__device__ __forceinline__ void krum_rows_noise_body(const double* gram, int T, int U1, N q, int nn, const int* inbox,
+                                                     int n, int groupsize, double* scores) {
   __shared__ double row[256];
   BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ double kept[256];
@@ -638,11 +660,11 @@ extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise(const double
   const int i = blockIdx.x, v = blockIdx.y, t = threadIdx.x;
   const int* box = inbox + (size_t)v * n;
   const int a = box[i];
-  if (t == 0) xaa = xx_dot(gram, T, U1, nz, sc, nn, a, a);
+  if (t == 0) xaa = xx_dot(gram, T, U1, q, nn, a, a);
   __syncthreads();
   if (t < n) {
     const int b = box[t];
-    row[t] = xaa + xx_dot(gram, T, U1, nz, sc, nn, b, b) - 2.0 * xx_dot(gram, T, U1, nz, sc, nn, a, b);
+    row[t] = xaa + xx_dot(gram, T, U1, q, nn, b, b) - 2.0 * xx_dot(gram, T, U1, q, nn, a, b);
   }
   __syncthreads();
   if (t < n) {
@@ -660,6 +682,20 @@ extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise(const double
     for (int j = 0; j < n; ++j) s += kept[j];
     scores[(size_t)v * n + i] = s;
   }
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise(const double* gram, int T, int U1,
+                                                                   const int* nz, const float* sc, int nn,
+                                                                   const int* inbox, int n, int groupsize,
+                                                                   double* scores) {
+  krum_rows_noise_body(gram, T, U1, NoisePtr{nz, sc}, nn, inbox, n, groupsize, scores);
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_krum_rows_noise_ka(const double* gram, int T, int U1, NoiseArg q,
+                                                                      int nn, const int* inbox, int n, int groupsize,
+                                                                      double* scores) {
+  krum_rows_noise_body(gram, T, U1, NoiseByVal{&q}, nn, inbox, n, groupsize, scores);
 }
 
 // h_acc / h_node (nullable): the same verdicts written straight into pinned host memory (the host reads them
@@ -1448,6 +1484,29 @@ extern "C" int bsc_krum_committee_noise2(const double* gram, int U1, int U, cons
     hipLaunchKernelGGL(k_krum_rows_big<true>, dim3(n, V), dim3(1024), (size_t)np2 * sizeof(double), s, gram, T, U1,
                        nz, sc, nn, inbox, n, np2, groupsize, scores);
   }
+  if (krum_vote_any(s, scores, inbox, V, n, n_accept, U1, need, lead_rank, cap, acc, node, ws, h_out, amap, nspec,
+                    alive) != 0)
+    return -1;
+  return (int)hipGetLastError();
+}
+// the same with the noisers' ids / weights read from HOST memory (nz_host / sc_host [U1][nn]) into the rows
+// kernel's argument block (U1 * nn <= NOISE_ARG_MAX, n <= 256; else -2: the caller uploads and uses the above)
+extern "C" int bsc_krum_committee_noise_ka(const double* gram, int U1, int U, const int* nz_host, const float* sc_host,
+                                           int nn, const int* inbox, int V, int n, int groupsize, int n_accept,
+                                           int need, const int* lead_rank, int cap, double* scores, int* acc, int* node,
+                                           int* ws, int* h_out, const int* amap, int nspec, int* alive, void* stream) {
+  if (U1 <= 0 || V <= 0 || n <= 0) return 0;
+  if (U > 8192 || U1 > 8192 || n > 4096 || V > 64 || n > U1 || nn <= 0 || nn > 16) return -1;
+  if ((long long)U1 * nn > NOISE_ARG_MAX || n > 256) return -2;
+  NoiseArg q;
+  for (int i = 0; i < U1 * nn; ++i) {
+    q.nz[i] = nz_host[i];
+    q.sc[i] = sc_host[i];
+  }
+  const int T = (U + 15) / 16;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_krum_rows_noise_ka, dim3(n, V), dim3(256), 0, s, gram, T, U1, q, nn, inbox, n, groupsize,
+                     scores);
   if (krum_vote_any(s, scores, inbox, V, n, n_accept, U1, need, lead_rank, cap, acc, node, ws, h_out, amap, nspec,
                     alive) != 0)
     return -1;

@@ -54,6 +54,7 @@ SIGNATURES = {
     "bsc_gram_stacked_range": [P, I, P, I, L, I, I, I, I, P, P, P, P, P],
     "bsc_krum_committee_noise": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P],
     "bsc_krum_committee_noise2": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, I, P, P],
+    "bsc_krum_committee_noise_ka": [P, I, I, P, P, I, P, I, I, I, I, I, P, I, P, P, P, P, P, P, I, P, P],
     "bsc_eval_error": [P, P, I, I, I, P, I, I, P, P],
     "bsc_eval_error_rb": [P, P, I, I, I, P, I, I, P, P, P],
     "bsc_eval_error_t_rb": [P, P, I, I, I, I, P, I, P, P, P],

@@ -565,18 +565,32 @@ def gram_adopt(pre: dict, gathered: torch.Tensor) -> None:
     del pre["split"]
 
 
+NOISE_ARG_MAX = 400   # kernels/ml.hip: noiser table entries the Krum rows kernel takes in its argument block
+
+
+def noise_tables_by_value(entries: int, n: int) -> bool:
+    """The noisers' ids / weights (entries = U1 * nn) fit the rows kernel's argument block (inbox n <= 256)."""
+    return 0 < entries <= NOISE_ARG_MAX and 0 < n <= 256
+
+
 def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accept: int, need: int, lead_rank,
                                cap: int, on_accept=None, flags=None):
     """Noise-aware committee Krum, phase 2: the noised rows x_a = delta_a + mean_s sc[a, s] t_{nz[a, s]}
     are never materialised -- their inner products are assembled from the phase-1 Gram.  nz int32 /
-    sc fp32 [U1, nn] (nz indexes the stacked noise rows); the rest as krum_committee_async.  The vote kernel
-    writes its verdicts straight into the pinned read-back buffer; flags = (amap, alive): it also sets the
-    speculative share MSM's row flags from the block mask (alive[i] = node[amap[i]])."""
+    sc fp32 [U1, nn] (nz indexes the stacked noise rows) -- device tensors, or (GPU, noise_tables_by_value)
+    host numpy arrays that travel in the rows kernel's arguments; the rest as krum_committee_async.  The vote
+    kernel writes its verdicts straight into the pinned read-back buffer; flags = (amap, alive): it also sets
+    the speculative share MSM's row flags from the block mask (alive[i] = node[amap[i]])."""
     U1, U = pre["U1"], pre["U"]
     V, n = inbox.shape
     nn = nz.shape[1]
+    host_tabs = isinstance(nz, np.ndarray)
+    if host_tabs:
+        nz = np.ascontiguousarray(nz, np.int32)
+        sc = np.ascontiguousarray(sc, np.float32)
+        assert "gram_full" not in pre and tuple(nz.shape) == (U1, nn) and noise_tables_by_value(nz.size, n)
     assert inbox.dtype == torch.int32 and lead_rank.dtype == torch.int32 and lead_rank.numel() == U1
-    assert nz.dtype == torch.int32 and sc.dtype == torch.float32 and tuple(nz.shape) == (U1, nn)
+    assert host_tabs or (nz.dtype == torch.int32 and sc.dtype == torch.float32 and tuple(nz.shape) == (U1, nn))
     assert 0 < n <= KRUM_MAX_INBOX and 0 < V <= 64 and n <= U1 and 0 < nn <= 16
     if "gram_full" in pre:   # CPU: the same assembly as k_krum_rows_noise, term by term in its order
         G, inv = pre["gram_full"], 1.0 / nn
@@ -599,11 +613,12 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
     ws = torch.empty((U1,), dtype=torch.int32, device=dev) if (U1 > 1024 or n > 256) else None
     host = pinned("krum_noise", out.shape, torch.int32)
     amap, alive = flags if flags is not None else (None, None)
-    _check(hip().bsc_krum_committee_noise2(_p(pre["gram"]), U1, U, _p(nz.contiguous()), _p(sc.contiguous()), nn,
-                                           _p(inbox.contiguous()), V, n, groupsize, n_accept, need,
-                                           _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _p(ws),
-                                           host.data_ptr(), _p(amap), alive.numel() if alive is not None else 0,
-                                           _p(alive), _stream()), "krum_committee_noise")
+    fn = hip().bsc_krum_committee_noise_ka if host_tabs else hip().bsc_krum_committee_noise2
+    _check(fn(_p(pre["gram"]), U1, U, nz.ctypes.data if host_tabs else _p(nz.contiguous()),
+              sc.ctypes.data if host_tabs else _p(sc.contiguous()), nn, _p(inbox.contiguous()), V, n, groupsize,
+              n_accept, need, _p(lead_rank.contiguous()), cap, _p(scores), _p(acc), _p(node), _p(ws),
+              host.data_ptr(), _p(amap), alive.numel() if alive is not None else 0, _p(alive), _stream()),
+           "krum_committee_noise")
     ev = S.record()
     if on_accept is not None:
         on_accept(node)

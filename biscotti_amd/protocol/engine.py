@@ -437,12 +437,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 self.W = torch.from_numpy(np.asarray(block.data.global_w, dtype=np.float64)).to(self.dev)
             if self.gpu:
                 # on the witness stream (low priority; nothing in the round waits for either): on the main
-                # stream the evaluation sat between the audit and the next round's Krum kernels
-                ws = self.witness_stream
-                S.wait(ws, S.current())
-                S.hold(self.W)   # read on another stream: kept for two rounds
-                with S.use(ws):
-                    eval_pending = self.task.evaluate_async(self.W)
+                # stream the evaluation sat between the audit and the next round's Krum kernels.  Launched
+                # after the next round's front when that runs (ordered on main's position here)
+                W_ev, W_eval = S.record(), self.W
             else:
                 eval_pending = self.task.evaluate_async(self.W)
         with tm.phase("next_head"):
@@ -461,6 +458,12 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 for f in work:
                     f(None)
                 self._resolve_evals(wait=False)   # this round's evaluation was just queued: not waited for
+        if self.gpu:
+            ws = self.witness_stream
+            ws.wait_event(W_ev)
+            S.hold(W_eval)   # read on another stream: kept for two rounds
+            with S.use(ws):
+                eval_pending = self.task.evaluate_async(W_eval)
         if self._idle_work is not None:  # every rank, same point: the collective stays aligned
             self._idle_work()
             self._idle_work = None

@@ -343,7 +343,10 @@ class VerifyMixin:
         if noise_aware and need_X and cfg.defense == "KRUM":
             if single:
                 nz_np, sc_np = self._noise_ids_np(noisers, local_workers)
-                nz, sc = h2d_many([(nz_np, torch.int32), (sc_np, torch.float32)], self.dev)
+                if self.gpu and K.noise_tables_by_value(nz_np.size, len(next(iter(inboxes.values()), []))):
+                    nz, sc = nz_np, sc_np   # host tables: they ride in the Krum kernel's arguments (no upload)
+                else:
+                    nz, sc = h2d_many([(nz_np, torch.int32), (sc_np, torch.float32)], self.dev)
             else:
                 nz, sc = self._gather_verify_inputs(head, noisers)
         elif not single:

@@ -344,6 +344,12 @@ def test_krum_committee_noise_aware_matches_explicit(U1, N, nn):
                                              rank.cuda(), 20)()
     assert torch.equal(acc, acc_ref)
     assert torch.equal(node, node_ref)
+    if K.noise_tables_by_value(U1 * nn, n):
+        # the host tables in the rows kernel's argument block (the one-rank round's path): the same decisions
+        acc2, node2 = K.krum_committee_noise_async(pre, nz.numpy(), sc.numpy(), inbox.cuda(), n - clip, n - clip, 1,
+                                                   rank.cuda(), 20)()
+        assert torch.equal(acc2, acc_ref)
+        assert torch.equal(node2, node_ref)
 
 
 def test_krum_committee_single_verifier_equals_krum():
