@@ -573,6 +573,9 @@ def noise_tables_by_value(entries: int, n: int) -> bool:
     return 0 < entries <= NOISE_ARG_MAX and 0 < n <= 256
 
 
+_KRUM_BUF: dict = {}   # (V, n, U1, device) -> resident outputs of krum_committee_noise_async
+
+
 def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accept: int, need: int, lead_rank,
                                cap: int, on_accept=None, flags=None):
     """Noise-aware committee Krum, phase 2: the noised rows x_a = delta_a + mean_s sc[a, s] t_{nz[a, s]}
@@ -607,11 +610,17 @@ def krum_committee_noise_async(pre: dict, nz, sc, inbox, groupsize: int, n_accep
             on_accept(node.to(torch.int32))
         return lambda: (acc, node)
     dev = pre["gram"].device
-    scores = torch.empty((V, n), dtype=torch.float64, device=dev)
-    out = torch.empty((V * n + U1,), dtype=torch.int32, device=dev)
-    acc, node = out[: V * n], out[V * n:]
-    ws = torch.empty((U1,), dtype=torch.int32, device=dev) if (U1 > 1024 or n > 256) else None
-    host = pinned("krum_noise", out.shape, torch.int32)
+    # resident outputs per shape (the launches are ordered on the caller's stream; the round reads the verdicts
+    # from the pinned copy): no allocator calls on the round's path
+    key = (V, n, U1, str(dev))
+    buf = _KRUM_BUF.get(key)
+    if buf is None:
+        out_ = torch.empty((V * n + U1,), dtype=torch.int32, device=dev)
+        buf = _KRUM_BUF[key] = (torch.empty((V, n), dtype=torch.float64, device=dev), out_, out_[: V * n],
+                                out_[V * n:], torch.empty((U1,), dtype=torch.int32, device=dev)
+                                if (U1 > 1024 or n > 256) else None)
+    scores, out, acc, node, ws = buf
+    host = pinned("krum_noise", out.shape, torch.int32)   # rotating: the last verdicts may still be read
     amap, alive = flags if flags is not None else (None, None)
     fn = hip().bsc_krum_committee_noise_ka if host_tabs else hip().bsc_krum_committee_noise2
     _check(fn(_p(pre["gram"]), U1, U, nz.ctypes.data if host_tabs else _p(nz.contiguous()),

@@ -515,11 +515,6 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             work, self._pre_vrf_work = self._pre_vrf_work, []
             for f in work:
                 f(head["fut_noise"])
-            if head.get("vrf_proofs") is not None:
-                self.vrf_dev.submit(*head["vrf_proofs"], self.vrf_stream)
-                if last or it == cfg.max_iterations - 1:
-                    self.vrf_dev.flush(self.vrf_stream, urgent=True)   # the run's end waits for these
-            self._resolve_evals(wait=len(self._evals) > 3)   # a bounded backlog: the host rings hold 4
             if krum_pre is not None and cfg.verification and inboxes and cfg.defense == "KRUM":
                 kst = head.get("kst") or self._krum_static(krum_pre["xrow"], krum_pre["U1"], plan, live, inboxes, head["spec"],
                                         head.get("arrivals"))
@@ -536,6 +531,15 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 ver = steps
             except StopIteration as done:
                 ver = done
+        with tm.phase("pre_vrf"):
+            # behind the committee's launch (nothing before it needs them): the unread VRF proofs go to the
+            # device prover, and the landed evaluation read-backs are taken
+            if head.get("vrf_proofs") is not None:
+                lw, lv, h = head["vrf_proofs"]
+                self.vrf_dev.submit(self._vrf_key_rows(lw, lv), h, self.vrf_stream)
+                if last or it == cfg.max_iterations - 1:
+                    self.vrf_dev.flush(self.vrf_stream, urgent=True)   # the run's end waits for these
+            self._resolve_evals(wait=len(self._evals) > 3)   # a bounded backlog: the host rings hold 4
         return {"head": head, "noisers": noisers, "noised": noised, "verify": ver}
 
     def _early_front_ok(self) -> bool:

@@ -163,7 +163,7 @@ class RoundHeadMixin:
             # the proofs nobody reads -- every noiser proof and the roles proofs -- go to the device prover
             # when the round runs (run_round's VRF wait), one launch per round on their own low-priority
             # stream: a timed window then contains exactly its rounds' proofs
-            head["vrf_proofs"] = (self._vrf_key_rows(local_workers, live), bytes(latest_hash))
+            head["vrf_proofs"] = (local_workers, live, bytes(latest_hash))   # key rows built at the submit
         return head
 
     def _vrf_key_rows(self, local_workers: list, live) -> "np.ndarray":
