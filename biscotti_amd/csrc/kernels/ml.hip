@@ -488,7 +488,6 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
   // the speculative share MSM from being dispatched until it ended (docs/PERF.md round 5); its work is ~10 us
   BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ double red[4][256];
-  __shared__ unsigned int last;
   // this launch covers the tile pairs [pair0, pair0 + gridDim.x) (several ranks split one Gram); part and
   // the arrival counters are indexed by the launch-local pair index, gram by the global one
   const int lp = blockIdx.x, pair = pair0 + lp, sp = blockIdx.y;
@@ -556,19 +555,29 @@ extern "C" __global__ void __launch_bounds__(256) k_gram_pairs(const float* X, i
   __syncthreads();
   const int e = threadIdx.x;  // 256 threads = the 16x16 tile
   part[((size_t)sp * npairs + lp) * 256 + e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
-  // split-K reduction in-kernel: the last split block of this tile pair to finish sums the partials
-  // in split order (bit-reproducible) and writes the reduced tile; it also re-arms the counter
-  __threadfence();
-  __syncthreads();
-  if (e == 0) last = atomicAdd(count + lp, 1u) == (unsigned)(gridDim.y - 1) ? 1u : 0u;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
+  // the split-K partials are summed by k_gram_reduce (the next launch on the stream).  An in-kernel
+  // last-block reduction needed an agent-scope release / acquire per block: on gfx950 that is an L2
+  // write-back + invalidate (buffer_wbl2 / buffer_inv sc1) in each of the ~1450 blocks -- ~100 us for ~10 us of
+  // MFMA work, and every kernel beside it (the share MSMs' table lookups) lost its L2 lines too
+}
+
+// KC1b: tile pair p's reduced Gram tile = sum of its split-K partials in split order (bit-reproducible, the
+// same order as before); the noise-only tile pairs were copied from the table by k_gram_pairs (split 0)
+extern "C" __global__ void __launch_bounds__(256) k_gram_reduce(const double* part, double* gram, int npairs,
+                                                               int nsplit, int pair0, int T, int tn0, int has_nn) {
+  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
+  const int lp = blockIdx.x, pair = pair0 + lp, e = threadIdx.x;
+  if (has_nn) {
+    int ti = 0, rem = pair;
+    while (rem >= T - ti) {
+      rem -= T - ti;
+      ++ti;
+    }
+    if (ti >= tn0) return;   // noise x noise: already in place
+  }
   double g = 0.0;
-  for (int q = 0; q < (int)gridDim.y; ++q)
-    g += __hip_atomic_load(part + ((size_t)q * npairs + lp) * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int q = 0; q < nsplit; ++q) g += part[((size_t)q * npairs + lp) * 256 + e];
   gram[(size_t)pair * 256 + e] = g;
-  if (e == 0) count[lp] = 0u;
 }
 
 extern "C" __global__ void __launch_bounds__(256) k_krum_rows(const double* gram, int T, const int* inbox, int n,
@@ -1119,19 +1128,21 @@ extern "C" __global__ void __launch_bounds__(256) k_eval_error_t(const float* Xt
     if (cnt0) atomicAdd(err, cnt0);
     if (cnt1) atomicAdd(err + 1, cnt1);
   }
-  // err_host: the last tile to finish (counter err[2]) copies the two counts into pinned host memory and
-  // resets err[0..2] for the next launch -- no fill and no copy blit around the kernel on the stream (each
-  // waited ~20-40 us for a CU slot behind the share MSMs).  err[0..2] must be zero before the first launch.
-  if (err_host != nullptr) {
-    __threadfence();   // this wave's counts are visible before its tile is counted as done
-    if (lane == 0 && atomicAdd(err + 2, 1u) == gridDim.x - 1) {
-      __threadfence();
-      const unsigned int e0 = atomicExch(err, 0u), e1 = atomicExch(err + 1, 0u);
-      atomicExch(err + 2, 0u);
-      err_host[0] = e0;
-      err_host[1] = e1;
-      __threadfence_system();
-    }
+  // err_host (bsc_eval_error_t_rb): k_eval_finish, the next launch, hands the counts to the host and re-zeroes
+  // them.  (A last-tile hand-off inside this kernel needed an agent-scope fence per wave -- on gfx950 an L2
+  // write-back + invalidate, ~625 of them beside the share MSMs.)
+  (void)err_host;
+}
+
+// the evaluation's two counts into pinned host memory, counters re-zeroed for the next launch: one wave, behind
+// k_eval_error_t on its stream (no fill and no copy blit: each waited ~20-40 us for a CU slot behind the MSMs)
+extern "C" __global__ void __launch_bounds__(64) k_eval_finish(unsigned int* err, unsigned int* err_host) {
+  if (threadIdx.x == 0) {
+    err_host[0] = err[0];
+    err_host[1] = err[1];
+    err[0] = 0u;
+    err[1] = 0u;
+    err[2] = 0u;
   }
 }
 
@@ -1309,7 +1320,8 @@ extern "C" __global__ void __launch_bounds__(256) k_recover_w(
       if (h_W != nullptr) h_W[idx] = w;   // pinned host mirror: the host reads it after the kernel's event
     }
   }
-  if (h_W != nullptr || h_status != nullptr) __threadfence_system();
+  // (no system-scope fence: the host reads the mirrors only after the kernel's completion event, whose
+  // end-of-kernel release makes them visible; a fence per block was an L2 write-back per block on the chain)
 }
 
 // =====================================================================================
@@ -1431,6 +1443,7 @@ extern "C" int bsc_krum_committee(const float* X, int U, int D, int kchunk, cons
   // count: npairs zeroed counters (re-armed by the kernel itself)
   hipLaunchKernelGGL(k_gram_pairs, dim3(npairs, nsplit), dim3(256), 0, s, X, U, D, kchunk, T, part, gram, count,
                      (const float*)nullptr, U, 0ll, 0, (const double*)nullptr, 0);
+  hipLaunchKernelGGL(k_gram_reduce, dim3(npairs), dim3(256), 0, s, part, gram, npairs, nsplit, 0, T, 0, 0);
   if (n <= 256) {
     hipLaunchKernelGGL(k_krum_rows, dim3(n, V), dim3(256), 0, s, gram, T, inbox, n, groupsize, scores);
   } else {
@@ -1459,6 +1472,8 @@ extern "C" int bsc_gram_stacked_range(const float* X, int U1, const float* X2, i
   const int nsplit = (D + kchunk - 1) / kchunk;
   hipLaunchKernelGGL(k_gram_pairs, dim3(p1 - p0, nsplit), dim3(256), 0, (hipStream_t)stream, X, U, D, kchunk, T, part,
                      gram, count, X2, U1, stride2, p0, nn, (U1 + 15) / 16);
+  hipLaunchKernelGGL(k_gram_reduce, dim3(p1 - p0), dim3(256), 0, (hipStream_t)stream, part, gram, p1 - p0, nsplit, p0,
+                     T, (U1 + 15) / 16, nn != nullptr ? 1 : 0);
   return (int)hipGetLastError();
 }
 extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2, long long stride2, int D, int kchunk,
@@ -1558,9 +1573,10 @@ extern "C" int bsc_eval_error_t_rb(const float* Xt, const int* y, int N, int KG,
     if (hipMemsetAsync(err, 0, 3 * sizeof(unsigned int), (hipStream_t)stream) != hipSuccess) return -1;
     return (int)hipMemcpyAsync(err_host, err, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, (hipStream_t)stream);
   }
-  // err: 3 zeroed counters (two error counts + tiles done); the kernel's last tile writes err_host and re-zeroes
+  // err: 3 zeroed counters; k_eval_finish writes err_host and re-zeroes them
   hipLaunchKernelGGL(k_eval_error_t, dim3((N + 15) / 16), dim3(256), 0, (hipStream_t)stream, Xt, y, N, KG, D_IN, D_OUT,
                      W, split, err, err_host);
+  hipLaunchKernelGGL(k_eval_finish, dim3(1), dim3(64), 0, (hipStream_t)stream, err, err_host);
   return (int)hipGetLastError();
 }
 

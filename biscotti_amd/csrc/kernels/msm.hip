@@ -495,10 +495,9 @@ extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* 
   if (t < nm) {
     const int v = jac_equal(ld_jac(sh), ld_jac(csum + 24 * ((size_t)t * nch + k))) ? 1 : 0;
     ok[(size_t)t * nch + k] = v;
-    if (h_ok != nullptr) {   // pinned host mirror: read after the kernel's event, no read-back copy
-      h_ok[(size_t)t * nch + k] = v;
-      __threadfence_system();
-    }
+    // pinned host mirror: read after the kernel's completion event (its end-of-kernel release makes it visible;
+    // no per-block system fence), no read-back copy
+    if (h_ok != nullptr) h_ok[(size_t)t * nch + k] = v;
   }
 }
 
@@ -582,10 +581,8 @@ extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* 
   if (threadIdx.x == 0) {
     const jac r = ld_jac(sh);
     st_jac(out + 24 * (size_t)g, r);
-    if (hout != nullptr) {   // pinned host mirror (the commitments' read-back without a copy)
-      st_jac(hout + 24 * (size_t)g, r);
-      __threadfence_system();
-    }
+    // pinned host mirror (the commitments' read-back without a copy), read after the kernel's event
+    if (hout != nullptr) st_jac(hout + 24 * (size_t)g, r);
   }
 }
 
