@@ -250,9 +250,10 @@ def main() -> int:
     seg0 = torch.cuda.memory_stats(comm.device).get("segment.all.allocated", 0) if eng.gpu else 0
     for k in range(a.steps):
         tr = time.perf_counter()
-        # the run's last timed round: the engine launches its still-batched device VRF proofs with this
-        # round's (they are computed inside the clock either way; drain() then waits less)
-        last = eng.run_round(last=k == a.steps - 1) if hasattr(eng, "drain") else eng.run_round()
+        # the run's end: the penultimate round's front launches the still-batched device VRF proofs and the last
+        # round proves its own on the host (all inside the clock; drain() then waits less)
+        last = eng.run_round(last=k == a.steps - 1, remaining=a.steps - k) if hasattr(eng, "_round_front") \
+            else eng.run_round(last=k == a.steps - 1) if hasattr(eng, "drain") else eng.run_round()
         walls.append(time.perf_counter() - tr)
         results.append(last)
         round_phases.append(last.phases)

@@ -440,7 +440,8 @@ static bool vrf_batch_enabled() {
 // One VRF batch on the native dispatcher: pass 1 computes every output (H, Gamma = x*H, beta), pass 2
 // the proofs unless outputs_only (the device prover makes them, kernels/vrf.hip).
 static std::shared_ptr<VrfJob> vrf_submit(const std::vector<Bytes>& seeds, const Bytes& alpha, int threads,
-                                          std::shared_ptr<VrfJob> after, bool outputs_only) {
+                                          std::shared_ptr<VrfJob> after, bool outputs_only,
+                                          bool whole_batches = false) {
   auto job = std::make_shared<VrfJob>();
   job->outputs_only = outputs_only;
   job->after = std::move(after);
@@ -451,7 +452,7 @@ static std::shared_ptr<VrfJob> vrf_submit(const std::vector<Bytes>& seeds, const
   VrfJob* jp = job.get();
   job->t_submit = std::chrono::steady_clock::now();
   job->started = true;
-  dispatcher().submit([jp, threads] {
+  dispatcher().submit([jp, threads, whole_batches] {
     if (jp->after) jp->after->done.wait();
     jp->t_start = std::chrono::steady_clock::now();
     bool beta_set = false;
@@ -459,7 +460,18 @@ static std::shared_ptr<VrfJob> vrf_submit(const std::vector<Bytes>& seeds, const
       // pass 1: every output (H, Gamma = x*H, beta); pass 2: the proofs (k*B, k*H, c, s) unless
       // they are produced elsewhere (outputs_only: the device prover, kernels/vrf.hip)
       const size_t n = jp->seeds.size();
-      if (jp->outputs_only && vrf_batch_enabled() && n >= 2 * size_t(std::max(1, threads))) {
+      if (whole_batches && !jp->outputs_only && vrf_batch_enabled()) {
+        // outputs AND proofs eight keys at a time (vrf_ifma.cpp prove8): for proofs nothing waits on between
+        // the two halves (the run's last round, whose device proofs would outlast it)
+        parallel_for((n + 7) / 8, threads, [&](size_t b) {
+          const size_t o = 8 * b, m = std::min<size_t>(8, n - o);
+          const VrfKey* ks[8];
+          Bytes be[8], pi[8];
+          for (size_t i = 0; i < m; ++i) ks[i] = &VrfKey::cached(jp->seeds[o + i]);
+          vrf_prove_batch(ks, int(m), jp->alpha, be, pi);
+          for (size_t i = 0; i < m; ++i) jp->out[o + i] = {std::move(be[i]), std::move(pi[i])};
+        });
+      } else if (jp->outputs_only && vrf_batch_enabled() && n >= 2 * size_t(std::max(1, threads))) {
         // eight outputs per AVX-512 IFMA batch (vrf_ifma.cpp, ~5x the outputs per core) once each thread would
         // otherwise compute two or more one by one: ~100 outputs on 14 threads take one batch's time
         parallel_for((n + 7) / 8, threads, [&](size_t b) {
@@ -481,7 +493,7 @@ static std::shared_ptr<VrfJob> vrf_submit(const std::vector<Bytes>& seeds, const
       }
       jp->beta_p.set_value();
       beta_set = true;
-      if (!jp->outputs_only) parallel_for(jp->seeds.size(), threads, [&](size_t i) {
+      if (!jp->outputs_only && !(whole_batches && vrf_batch_enabled())) parallel_for(jp->seeds.size(), threads, [&](size_t i) {
         jp->out[i].second = vrf_finish(VrfKey::cached(jp->seeds[i]), jp->stages[i]);
         jp->stages[i].st.reset();
       });
@@ -1070,6 +1082,26 @@ PYBIND11_MODULE(_biscotti_rt, m) {
     return vrf_submit(ss, B(alpha), threads, std::move(after), outputs_only);
   }, py::arg("seeds"), py::arg("alpha"), py::arg("threads"), py::arg("after") = nullptr,
      py::arg("outputs_only") = false);
+  // outputs + proofs in whole 8-key batches on AVX-512 IFMA (vrf_prove_batch), the outputs known only at the end:
+  // for proofs nobody reads before the job's join (the run's last round, engine._round_front)
+  m.def("vrf_proofs_async", [](std::vector<py::bytes> seeds, py::bytes alpha, int threads) {
+    std::vector<Bytes> ss;
+    for (auto& x : seeds) ss.push_back(B(x));
+    return vrf_submit(ss, B(alpha), threads, nullptr, false, true);
+  }, py::arg("seeds"), py::arg("alpha"), py::arg("threads"));
+  m.def("vrf_prove_batch_ifma", [](std::vector<py::bytes> seeds, py::bytes alpha) {
+    std::vector<const VrfKey*> ks;
+    for (auto& s : seeds) ks.push_back(&VrfKey::cached(B(s)));
+    const Bytes a = B(alpha);
+    std::vector<Bytes> be(ks.size()), pi(ks.size());
+    {
+      py::gil_scoped_release rel;
+      vrf_prove_batch(ks.data(), int(ks.size()), a, be.data(), pi.data());
+    }
+    py::list res;
+    for (size_t i = 0; i < ks.size(); ++i) res.append(py::make_tuple(P(be[i]), P(pi[i])));
+    return res;
+  });
 
   // ---------------------------------------------------------------- keys
   py::class_<CommitKey>(m, "CommitKey")

@@ -525,6 +525,16 @@ void fe51_consts(u64 d[5], u64 sqrtm1[5]) {
   memcpy(d, D().v, 5 * sizeof(u64));
   memcpy(sqrtm1, SQRTM1().v, 5 * sizeof(u64));
 }
+// the fixed-base table of B: entry (w, d) = (d + 1) * 16^w * B in cached form, 4 elements of 5 limbs
+const u64* base_table_limbs() {
+  static_assert(sizeof(GeCached) == 20 * sizeof(u64), "cached point layout");
+  return reinterpret_cast<const u64*>(base_table().t.data());
+}
+void sc_reduce64(u8 out[32], const u8 in[64]) { sc_reduce(out, in, 64); }
+void sc_muladd16(u8 out[32], const u8 k[32], const u8 c16[16], const u8 x[32]) { sc_muladd(out, k, c16, 16, x); }
+Bytes challenge(const Bytes& Y, const Bytes& H, const Bytes& G, const Bytes& U, const Bytes& V) {
+  return challenge_str(Y, H, G, U, V);
+}
 }  // namespace vrf_detail
 
 Bytes ed25519_public_from_seed(const Bytes& seed32) {

@@ -42,6 +42,9 @@ Bytes vrf_beta(const VrfKey& key, const Bytes& alpha);
 // (vrf_beta_batch_supported() false) take vrf_beta per key.  out: n outputs.
 bool vrf_beta_batch_supported();
 void vrf_beta_batch(const VrfKey* const* keys, int n, const Bytes& alpha, Bytes* out);
+// (beta, pi) of n keys (same alpha), the variable- and fixed-base multiplications eight at a time on AVX-512
+// IFMA lanes; byte-identical to vrf_prove (which CPUs without IFMA take per key).
+void vrf_prove_batch(const VrfKey* const* keys, int n, const Bytes& alpha, Bytes* beta, Bytes* pi);
 // The fixed-base table of B (64 signed radix-16 windows x 8 multiples, cached form) as 512 x 4
 // canonical 32-byte field encodings (Y+X, Y-X, 2Z, 2dT): the device prover's k*B table.
 Bytes vrf_base_table_bytes();

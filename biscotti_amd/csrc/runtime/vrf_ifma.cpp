@@ -31,6 +31,10 @@ namespace vrf_detail {
 void fe51_tobytes(u8 out[32], const u64 v[5]);
 void fe51_frombytes(u64 v[5], const u8 in[32]);
 void fe51_consts(u64 d[5], u64 sqrtm1[5]);
+const u64* base_table_limbs();
+void sc_reduce64(u8 out[32], const u8 in[64]);
+void sc_muladd16(u8 out[32], const u8 k[32], const u8 c16[16], const u8 x[32]);
+Bytes challenge(const Bytes& Y, const Bytes& H, const Bytes& G, const Bytes& U, const Bytes& V);
 }  // namespace vrf_detail
 
 namespace {
@@ -441,7 +445,141 @@ IFMA bool beta8(const VrfKey* const* keys, int n, const Bytes& alpha, Bytes* out
   return true;
 }
 
+// k * B with the resident fixed-base table of B (64 signed radix-16 windows x 8 cached multiples): no
+// doublings, one cached addition per window, each lane's entry selected by masked blends of broadcast entries
+IFMA F f_bcast_limbs(const u64* v) {
+  F r;
+  for (int k = 0; k < 5; ++k) r.l[k] = v1(v[k]);
+  return r;
+}
+IFMA P p_mul_base(const int64_t e[64][8]) {
+  const u64* bt = vrf_detail::base_table_limbs();   // [512][4][5]
+  const F one = f_one();
+  F two = f_zero();
+  two.l[0] = v1(2);
+  P r{f_zero(), one, one, f_zero()};
+  for (int w = 0; w < 64; ++w) {
+    const V d = _mm512_loadu_si512(e[w]);
+    const V ad = _mm512_abs_epi64(d);
+    C s{one, one, two, f_zero()};
+    for (int k = 0; k < 8; ++k) {
+      const __mmask8 m = _mm512_cmpeq_epi64_mask(ad, v1(u64(k + 1)));
+      if (!m) continue;
+      const u64* t = bt + (size_t)(w * 8 + k) * 20;
+      s.YpX = f_blend(m, s.YpX, f_bcast_limbs(t));
+      s.YmX = f_blend(m, s.YmX, f_bcast_limbs(t + 5));
+      s.Z2 = f_blend(m, s.Z2, f_bcast_limbs(t + 10));
+      s.T2d = f_blend(m, s.T2d, f_bcast_limbs(t + 15));
+    }
+    const __mmask8 neg = _mm512_cmplt_epi64_mask(d, vz());
+    if (neg) {
+      const F ypx = s.YpX;
+      s.YpX = f_blend(neg, s.YpX, s.YmX);
+      s.YmX = f_blend(neg, s.YmX, ypx);
+      s.T2d = f_blend(neg, s.T2d, f_neg(s.T2d));
+    }
+    r = p_add_cached(r, s);
+  }
+  return r;
+}
+
+// the RFC 8032 encodings of k points per lane (y with the sign of x in bit 255), one vector inversion
+IFMA void p_encode(const P* const* pts, int k, u8 (*out)[8][32]) {
+  F pre[4];
+  F acc = f_one();
+  for (int j = 0; j < k; ++j) {
+    pre[j] = acc;
+    acc = f_mul(acc, pts[j]->Z);
+  }
+  F inv = f_invert(acc);
+  for (int j = k - 1; j >= 0; --j) {
+    const F zi = f_mul(inv, pre[j]);
+    inv = f_mul(inv, pts[j]->Z);
+    u8 bx[8][32];
+    f_tobytes(f_mul(pts[j]->X, zi), bx);
+    f_tobytes(f_mul(pts[j]->Y, zi), out[j]);
+    for (int i = 0; i < 8; ++i)
+      if (bx[i][0] & 1) out[j][i][31] |= 0x80;
+  }
+}
+
+IFMA void digits8(const u8 (*sc)[32], int n, int64_t e[64][8]) {
+  for (int i = 0; i < 8; ++i) {
+    int8_t dg[64];
+    if (i < n) signed_digits(dg, sc[i]);
+    else memset(dg, 0, sizeof(dg));
+    for (int w = 0; w < 64; ++w) e[w][i] = dg[w];
+  }
+}
+
+// ECVRF prove (vrf.cpp vrf_output + vrf_finish) for up to 8 keys: H, Gamma = x*H, k*B and k*H as lane vectors
+IFMA bool prove8(const VrfKey* const* keys, int n, const Bytes& alpha, Bytes* beta, Bytes* pi) {
+  u64 dv[5], sv[5];
+  vrf_detail::fe51_consts(dv, sv);
+  const F d = f_bcast(dv), sqrtm1 = f_bcast(sv);
+  const F d2 = f_add(d, d);
+  P H;
+  if (!encode8(keys, n, alpha, d, sqrtm1, H)) return false;
+  u8 hb[1][8][32];
+  const P* hp[1] = {&H};
+  p_encode(hp, 1, hb);
+  u8 xs[8][32], ks[8][32];
+  for (int i = 0; i < 8; ++i) {
+    memset(xs[i], 0, 32);
+    memset(ks[i], 0, 32);
+    if (i >= n) continue;
+    memcpy(xs[i], keys[i]->x, 32);
+    Sha512 kh;   // nonce k = SHA-512(prefix || encode(H)) mod L (vrf_finish)
+    kh.update(keys[i]->prefix, 32);
+    kh.update(hb[0][i], 32);
+    u8 kd[64];
+    kh.final(kd);
+    vrf_detail::sc_reduce64(ks[i], kd);
+  }
+  alignas(64) int64_t ex[64][8], ek[64][8];
+  digits8(xs, n, ex);
+  digits8(ks, n, ek);
+  const P G = p_mul(H, ex, d2);
+  const P Vp = p_mul(H, ek, d2);
+  const P Up = p_mul_base(ek);
+  const P G8 = p_dbl(p_dbl(p_dbl(G)));
+  u8 enc[4][8][32];
+  const P* pts[4] = {&G, &Up, &Vp, &G8};
+  p_encode(pts, 4, enc);
+  for (int i = 0; i < n; ++i) {
+    Sha512 bh;
+    u8 pre[2] = {SUITE, 0x03};
+    bh.update(pre, 2);
+    bh.update(enc[3][i], 32);
+    u8 z = 0;
+    bh.update(&z, 1);
+    beta[i].assign(64, 0);
+    bh.final(beta[i].data());
+    const Bytes e0(enc[0][i], enc[0][i] + 32);
+    const Bytes c = vrf_detail::challenge(keys[i]->pk, Bytes(hb[0][i], hb[0][i] + 32), e0,
+                                          Bytes(enc[1][i], enc[1][i] + 32), Bytes(enc[2][i], enc[2][i] + 32));
+    u8 s[32];
+    vrf_detail::sc_muladd16(s, ks[i], c.data(), xs[i]);
+    pi[i] = e0;
+    pi[i].insert(pi[i].end(), c.begin(), c.end());
+    pi[i].insert(pi[i].end(), s, s + 32);
+  }
+  return true;
+}
+
 }  // namespace
+
+void vrf_prove_batch(const VrfKey* const* keys, int n, const Bytes& alpha, Bytes* beta, Bytes* pi) {
+  for (int off = 0; off < n; off += 8) {
+    const int m = n - off < 8 ? n - off : 8;
+    if (!vrf_beta_batch_supported() || !prove8(keys + off, m, alpha, beta + off, pi + off))
+      for (int i = 0; i < m; ++i) {
+        auto r = vrf_prove(*keys[off + i], alpha);
+        beta[off + i] = std::move(r.first);
+        pi[off + i] = std::move(r.second);
+      }
+  }
+}
 
 bool vrf_beta_batch_supported() {
   static const bool ok = [] {

@@ -204,6 +204,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self._partitions = cfg.partitions()
         self._head = None
         self._front = None            # the next round's front, started at the end of the previous round
+        self._host_proofs: list = []  # the run's last round's VRF proofs, proved on the host (joined by drain)
         self._front_planned = False
         self._warm_up()
         import atexit
@@ -305,6 +306,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             if self.vrf_dev is not None:
                 self.vrf_dev.drain(self.vrf_stream)
                 self.stats["vrf_device_proofs"] = self.vrf_dev.proofs
+            hp, self._host_proofs = self._host_proofs, []
+            for j in hp:
+                j.wait()
             t2 = time.perf_counter()
             joins, self._sign_joins = self._sign_joins, []
             for join in joins:
@@ -370,12 +374,14 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         return iteration + 1 if self.cfg.deterministic_time else int(time.time())
 
     # ------------------------------------------------------------------ the round
-    def run_round(self, last: bool = False, front: bool = True) -> RoundResult | None:
+    def run_round(self, last: bool = False, front: bool = True, remaining: int | None = None) -> RoundResult | None:
         """One protocol round.  last: the caller ends its run after this round (its final iteration), so the
         device VRF proofs still batched are launched with this round's instead of at drain() -- the same
         proofs, one prover latency earlier.  The protocol's own last iteration (max_iterations) counts too.
         front=False: the next round's front (_round_front) is not started at the end of this one (bench.py's
-        last warm-up round, so a timed window holds exactly its own rounds' fronts)."""
+        last warm-up round, so a timed window holds exactly its own rounds' fronts).  remaining: the caller's rounds
+        left, this one included -- the penultimate round's front sends the queued VRF proofs to the device and
+        the last round's front proves its own on the host (_round_front), so the run's end waits for neither."""
         cfg, R, fsm, comm = self.cfg, self.R, self.fsm, self.comm
         t_round = time.perf_counter()
         tm = self.timer
@@ -388,10 +394,10 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 head, self._head = self._head or self._open_round(), None
                 if head["plan"].done:
                     return None
-            fr = self._round_front(head, last)
+            fr = self._round_front(head, 1 if last else remaining)
         else:
             self.stats["early_fronts"] = self.stats.get("early_fronts", 0) + 1
-            if last and fr["head"].get("vrf_proofs") is not None:
+            if last and fr["head"].get("vrf_proofs") is not None and fr.get("remaining") != 1:
                 self.vrf_dev.flush(self.vrf_stream, urgent=True)   # started before the caller said it is the last
         head, noisers, noised = fr["head"], fr["noisers"], fr["noised"]
         live, plan = head["live"], head["plan"]
@@ -450,7 +456,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 # selection -- before this round's remaining host work: the selection lands earlier and
                 # cancels the speculative MSM's rejected rows sooner; the work below fills the next round's waits
                 work, self._pre_vrf_work = self._pre_vrf_work, []   # this round's: after the launch
-                self._front = self._round_front(self._head, False)
+                self._front = self._round_front(self._head, remaining - 1 if remaining else None)
                 self._head = None
                 self._pre_vrf_work = work + self._pre_vrf_work
             with tm.phase("recover.idle"):
@@ -498,7 +504,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self._maybe_fail(it)
         return res
 
-    def _round_front(self, head: dict, last: bool) -> dict:
+    def _round_front(self, head: dict, remaining: int | None) -> dict:
         """A round up to its verification's device launch: the host work that does not need the VRF outputs,
         the noiser lottery (waits for them), the noise and the verification up to the committee's launch
         (_verification_steps; the Multi-Krum path stops there, the rest runs through).  run_round finishes it
@@ -536,11 +542,27 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             # device prover, and the landed evaluation read-backs are taken
             if head.get("vrf_proofs") is not None:
                 lw, lv, h = head["vrf_proofs"]
-                self.vrf_dev.submit(self._vrf_key_rows(lw, lv), h, self.vrf_stream)
-                if last or it == cfg.max_iterations - 1:
-                    self.vrf_dev.flush(self.vrf_stream, urgent=True)   # the run's end waits for these
+                last = remaining == 1 or it == cfg.max_iterations - 1
+                if last:
+                    # the run's last round: the rounds queued so far go to the device now, this round's proofs
+                    # run on the host threads (AVX-512 IFMA, 8 keys a batch: ~0.3 ms for a round's ~200) -- one
+                    # device launch takes ~2.2 ms (a variable-base multiplication per proof), which the run's
+                    # end would otherwise wait out
+                    self.vrf_dev.flush(self.vrf_stream, urgent=True)
+                    seeds = [self.vrf_noise_seed[w] for w in lw]
+                    if cfg.roles_vrf_proof:
+                        seeds += [self.vrf_roles_seed[p] for p in self.local if lv[p]]
+                    if seeds:
+                        # (8 threads: the round's own host thread and the runtime keep cores of the quota)
+                        self._host_proofs.append(self.R.vrf_proofs_async(seeds, h,
+                                                                         max(1, min(8, cfg.host_threads - 2))))
+                        self.stats["vrf_host_proofs"] = self.stats.get("vrf_host_proofs", 0) + len(seeds)
+                else:
+                    self.vrf_dev.submit(self._vrf_key_rows(lw, lv), h, self.vrf_stream)
+                    if remaining == 2:   # the penultimate round: its launch (~2.2 ms) ends with the last round
+                        self.vrf_dev.flush(self.vrf_stream)
             self._resolve_evals(wait=len(self._evals) > 3)   # a bounded backlog: the host rings hold 4
-        return {"head": head, "noisers": noisers, "noised": noised, "verify": ver}
+        return {"head": head, "noisers": noisers, "noised": noised, "verify": ver, "remaining": remaining}
 
     def _early_front_ok(self) -> bool:
         """The next round's front runs at the end of this one: one rank per process on a GPU, the pipelined

@@ -295,6 +295,30 @@ def test_early_front_keeps_the_chain(extra):
         assert stats[0].get("device_aggregations", 0) >= 6, stats[0]
 
 
+def test_last_round_vrf_proofs_on_the_host():
+    """The run's last round (remaining = 1) proves its VRF proofs on the host threads (vrf_proofs_async,
+    AVX-512 IFMA batches) while the rounds before it go to the device prover: every proof is made, the drain
+    joins both, and the chain is the one of a run without the hint."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    chains, stats = [], []
+    for hint in (True, False):
+        cfg = RunConfig(num_nodes=20, dataset="mnist", seed=6, max_iterations=100, deterministic_time=True)
+        eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
+        for k in range(6):
+            eng.run_round(last=k == 5, remaining=6 - k if hint else None)
+        eng.drain()
+        chains.append([bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))])
+        stats.append(dict(eng.stats))
+        eng.close()
+    assert chains[0] == chains[1]
+    assert stats[0].get("vrf_host_proofs", 0) > 0 and "vrf_host_proofs" not in stats[1]
+    # the same proofs in total: the device's count plus the host's equals the all-device run's
+    assert stats[0]["vrf_device_proofs"] + stats[0]["vrf_host_proofs"] == stats[1]["vrf_device_proofs"]
+
+
 @pytest.mark.parametrize("U,n,V", [(94, 70, 3), (150, 140, 5), (256, 256, 3), (300, 200, 26)])
 def test_krum_committee_matches_reference(U, n, V):
     """Committee Multi-Krum (one Gram over the candidate rows, per-verifier inboxes, vote and leader

@@ -50,3 +50,18 @@ def test_outputs_only_job_uses_the_batch_and_matches():
         assert p.returncode == 0, p.stderr
         got.append(p.stdout.strip())
     assert got[0] == got[1]
+
+
+def test_batch_proofs_match_scalar_and_verify():
+    """vrf_prove_batch (outputs + proofs, eight keys per IFMA batch: encode_to_curve, x*H, k*H, the fixed-base
+    k*B and the three encodings with one inversion) is byte-identical to vrf_prove and verifies; also through
+    the job that proves the run's last round on the host (vrf_proofs_async)."""
+    R = rt()
+    seeds = _seeds(19, seed=3)
+    for alpha in (b"", b"block hash", bytes(range(40))):
+        got = R.vrf_prove_batch_ifma(seeds, alpha)
+        ref = [R.vrf_prove_batch_async([s], alpha, 1).result()[0] for s in seeds]
+        assert got == ref
+        assert R.vrf_proofs_async(seeds, alpha, 3).result() == ref
+        for s, (beta, pi) in zip(seeds, got):
+            assert R.vrf_verify(R.ed25519_public_key(s), alpha, pi) == beta
