@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <iterator>
 
 #include "hash.hpp"
 
@@ -243,10 +244,12 @@ std::vector<i64> RoundFSM::leader_cap(const std::vector<i64>& candidates) const 
   if (cap <= 0 || i64(candidates.size()) <= cap) {
     out = candidates;
   } else {
-    std::set<i64> cand(candidates.begin(), candidates.end());
+    std::vector<u8> cand(size_t(cfg.num_nodes), 0);   // a flag per peer instead of a node-based set
+    for (i64 w : candidates)
+      if (w >= 0 && w < cfg.num_nodes) cand[size_t(w)] = 1;
     for (i64 w : leader_arrivals()) {
       if (i64(out.size()) >= cap) break;
-      if (cand.count(w)) out.push_back(w);
+      if (cand[size_t(w)]) out.push_back(w);
     }
   }
   std::sort(out.begin(), out.end());
@@ -298,23 +301,30 @@ RoundFSM::LeaderView RoundFSM::leader_view(const std::map<i64, std::vector<std::
   if (!lv.leader_online) return lv;
   auto own = routes.find(L);
   if (own == routes.end() || own->second.empty()) return lv;  // leader has no shares -> empty block
-  std::set<i64> inter;
-  for (auto& wp : own->second) inter.insert(wp.first);
+  // sorted vectors, not node-based sets: this sits on the round's host path between the committee's selection
+  // and the block build (std::set allocations made it ~30 us at 60 approved workers)
+  auto sorted_ids = [](const std::vector<std::pair<i64, i64>>& v) {
+    std::vector<i64> ids;
+    ids.reserve(v.size());
+    for (auto& wp : v) ids.push_back(wp.first);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    return ids;
+  };
+  std::vector<i64> inter = sorted_ids(own->second), theirs, nx;
   lv.contributing_miners.push_back(L);
   for (i64 m : plan.miners) {
     if (m == L || !plan.live[size_t(m)]) continue;
     auto it = routes.find(m);
     if (it == routes.end() || it->second.empty()) continue;
-    std::set<i64> theirs;
-    for (auto& wp : it->second) theirs.insert(wp.first);
-    std::set<i64> nx;
-    for (i64 w : inter)
-      if (theirs.count(w)) nx.insert(w);
-    inter = nx;
+    theirs = sorted_ids(it->second);
+    nx.clear();
+    std::set_intersection(inter.begin(), inter.end(), theirs.begin(), theirs.end(), std::back_inserter(nx));
+    inter.swap(nx);
     lv.contributing_miners.push_back(m);
   }
   // the leader fires at NUM_SAMPLES/2 received shares (main.go:360): its list is the first arrivals
-  lv.node_list = leader_cap(std::vector<i64>(inter.begin(), inter.end()));
+  lv.node_list = leader_cap(inter);
   lv.quorum = cfg.shares_per_miner * i64(lv.contributing_miners.size()) >= cfg.poly_size &&
               lv.node_list.size() > 1;
   return lv;

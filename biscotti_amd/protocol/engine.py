@@ -417,8 +417,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             # the batch starts behind the next round's VRF outputs)
             self._idle_work = None
             self._sign_joins.append(pending_signatures)
-            while len(self._sign_joins) > 2:
-                self._sign_joins.pop(0)()
+            if not self._front_planned:   # else after the next round's front (the block build comes first)
+                while len(self._sign_joins) > 2:
+                    self._sign_joins.pop(0)()
         if cfg.secure_agg:
             block = self._secure_aggregation(plan, live, approved, head["qdelta"], local_workers, head["row_of"],
                                              commit_of, signatures, head["spec"],
@@ -464,6 +465,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 for f in work:
                     f(None)
                 self._resolve_evals(wait=False)   # this round's evaluation was just queued: not waited for
+            with tm.phase("verify.sign_join"):
+                while len(self._sign_joins) > 2:   # the signature batch of two rounds ago
+                    self._sign_joins.pop(0)()
         if self.gpu:
             ws = self.witness_stream
             ws.wait_event(W_ev)

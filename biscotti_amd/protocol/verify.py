@@ -58,18 +58,24 @@ class VerifyMixin:
         nz = np.zeros((self.maxlocal, nn_), np.int32)
         sc = np.zeros((self.maxlocal, nn_), np.float32)
         if local_workers and noisers:
-            at = np.asarray(local_workers, np.int64) - self.lo
+            # the rows of local_workers, cached per list (the round's head keeps one list object per round)
+            c = getattr(self, "_noise_at", None)
+            if c is None or c[0] is not local_workers:
+                c = self._noise_at = (local_workers, np.asarray(local_workers, np.int64) - self.lo)
+            at = c[1]
             arr = getattr(self, "_noise_arr", None)
             # the lottery's array (same ids, local_workers order) when it is this round's; else from the dict
-            ids = arr[1].astype(np.int64, copy=False).reshape(len(local_workers), -1) \
-                if arr is not None and arr[0] is local_workers else \
+            ids = arr[1].reshape(len(local_workers), -1) if arr is not None and arr[0] is local_workers else \
                 np.asarray([noisers[w] for w in local_workers], np.int64).reshape(len(local_workers), -1)
-            assert ids.min() >= 0 and ids.max() < self.N, "noiser id out of range"
+            if ids.size and not (0 <= int(ids.min()) and int(ids.max()) < self.N):
+                raise ValueError("noiser id out of range")
             nz[at] = ids
-            w = np.full(ids.shape, self.task.noise_scale(self.sigma), np.float32)
             if self.colluders:
+                w = np.full(ids.shape, self.task.noise_scale(self.sigma), np.float32)
                 w[np.isin(ids, self._colluder_arr())] = 0.0
-            sc[at] = w
+                sc[at] = w
+            else:
+                sc[at] = self.task.noise_scale(self.sigma)
         return nz, sc
 
     def _colluder_arr(self) -> np.ndarray:

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--warm", type=int, default=20)
     ap.add_argument("--set", action="append", default=[])
     ap.add_argument("--wrap", default="", help="comma-separated engine methods (or task./crypto. methods) timed as events")
+    ap.add_argument("--fsm-proxy", action="store_true", help="time every native RoundFSM call as an event (@fsm.name)")
     a = ap.parse_args()
     comm = Comm.init()
     torch.set_num_threads(min(4, torch.get_num_threads()))
@@ -89,6 +90,24 @@ def main():
             wrap(importlib.import_module(mod), fn, m[4:])
         else:
             wrap(eng, m, m)
+    if a.fsm_proxy:   # pybind methods cannot be patched: the engine's FSM behind a timing proxy instead
+        class FsmProxy:
+            def __init__(self, o):
+                object.__setattr__(self, "_o", o)
+
+            def __getattr__(self, k):
+                v = getattr(self._o, k)
+                if not callable(v):
+                    return v
+
+                def f(*args, **kw):
+                    s = time.perf_counter()
+                    try:
+                        return v(*args, **kw)
+                    finally:
+                        events.append(("@fsm." + k, s, time.perf_counter()))
+                return f
+        eng.fsm = FsmProxy(eng.fsm)
     for _ in range(a.warm):
         eng.run_round()
     torch.cuda.synchronize()
