@@ -572,7 +572,10 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         """The next round's front runs at the end of this one: one rank per process on a GPU, the pipelined
         noise-aware Multi-Krum path, no churn / partitions / fault injection (whose next round may differ from
         the head built here) and no per-round phase records (trace, phase log, phase sync: their phases would
-        move to the previous round).  The no_early_front ablation turns it off; the chain is the same."""
+        move to the previous round).  The no_early_front ablation turns it off; the chain is the same.  With
+        several ranks it measured slower (emulated rank 0 of 8: 0.99-1.02 vs 0.93-0.96 ms; the chains stay
+        identical): there the front's two collectives move ahead of the round's host work, and the device, not
+        the host, is no longer the limit (docs/PERF.md, round 5)."""
         cfg = self.cfg
         return (self.gpu and self.comm.world == 1 and self._pipelined() and cfg.secure_agg and cfg.verification
                 and cfg.defense == "KRUM" and self._noise_krum() and not cfg.has("no_early_front")
