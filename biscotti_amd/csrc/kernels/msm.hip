@@ -213,10 +213,11 @@ __device__ __forceinline__ void shares_msm_body(const long long* coeffs, int d, 
                                                 const int* compact, int group_rows, uint32_t* out_pts,
                                                 long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
-  // both share MSMs of a round end on its critical path: the speculative one gates the recovery, the pre-step's
-  // commitment MSM (commit_only == 1) the block build (the block carries the commitments); the commitment MSM is
-  // latency-bound (one lane per (row, chunk), ~1 wave per SIMD) and, launched first, wins the age tie-break
-  BSC_SET_PRIO(BSC_PRIO_SPEC);
+  // the pre-step's commitment MSM (commit_only == 1) at AHEAD: its outputs are read a round later (block, audit
+  // sums); after the fence fix the speculative MSM beside it gains (200 rounds: p50 0.711 vs 0.769 ms,
+  // profiles/r5/prio2; before it, round 4 measured the opposite)
+  if (commit_only == 1) BSC_SET_PRIO(BSC_PRIO_AHEAD);
+  else BSC_SET_PRIO(BSC_PRIO_SPEC);
   const int S = commit_only == 1 ? 1 : T + 1;   // output slots per (row, chunk)
   const int SL = commit_only == 2 ? T : S;      // lanes per (row, chunk)
   // compact (optional): [count, row...] -- only the listed rows are computed, packed densely over the
