@@ -213,9 +213,9 @@ __device__ __forceinline__ void shares_msm_body(const long long* coeffs, int d, 
                                                 const int* compact, int group_rows, uint32_t* out_pts,
                                                 long long* out_y) {
   const int nchunks = (d + poly - 1) / poly;
-  // the pre-step's commitment MSM (commit_only == 1) at AHEAD: its outputs are read a round later (block, audit
-  // sums); after the fence fix the speculative MSM beside it gains (200 rounds: p50 0.711 vs 0.769 ms,
-  // profiles/r5/prio2; before it, round 4 measured the opposite)
+  // the pre-step's commitment MSM (commit_only == 1) one class below the speculative MSM: both run side by side,
+  // the speculative one gates the recovery and the commitments are read only at the block build; after the
+  // fence fix this measured better (200 rounds: p50 0.711 vs 0.769 ms, profiles/r5/prio2; before it, worse)
   if (commit_only == 1) BSC_SET_PRIO(BSC_PRIO_AHEAD);
   else BSC_SET_PRIO(BSC_PRIO_SPEC);
   const int S = commit_only == 1 ? 1 : T + 1;   // output slots per (row, chunk)

@@ -6,8 +6,9 @@
 #pragma once
 #define BSC_PRIO_CRITICAL 3   // the round's latency chains: Krum scores / vote, selection flags, recovery, audit,
                               // the full commitments' sums
-#define BSC_PRIO_SPEC 2       // the share MSMs: speculative (gates the recovery), pre-step commitments (the block)
-#define BSC_PRIO_AHEAD 1      // needed later in the round: Gram, evaluation, pre-step step, early commitment sums
+#define BSC_PRIO_SPEC 2       // the speculative share MSM (gates the recovery)
+#define BSC_PRIO_AHEAD 1      // needed later in the round: the pre-step's commitment MSM (the block), evaluation,
+                              // early commitment sums
 // 0 (the hardware default): background -- the miners' witness sums (no consumer in the round), batched VRF
 // proofs (the run's final flush: CRITICAL), KZG audit sums.
 // The argument must be a constant; call it before the kernel's main work, under a wave-uniform condition (a

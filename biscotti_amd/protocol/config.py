@@ -97,13 +97,16 @@ class RunConfig:
     #   spec_tight         GPU: the speculative MSM's horizon is the leader's cap exactly (no margin, no slack): a
     #                      block reaching past its first cap arrivals is a speculative miss, topped up by the host
     #                      path (tests and measurements of that path): the chain must not change
+    #   wave_prio_multi    GPU: the round kernels' wave priority classes (kernels/wave_prio.h) also with several
+    #                      ranks (default: one rank only; the collectives' kernels run at the default class)
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
     churn_round_s: ClassVar[float] = 25.44
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
-                                  "noise_gram_each_round", "spec_tight", "no_early_front")
+                                  "noise_gram_each_round", "spec_tight", "no_early_front",
+                                  "wave_prio_multi")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

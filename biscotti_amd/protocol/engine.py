@@ -153,7 +153,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         if self.gpu:
             # wave priority classes (kernels/wave_prio.h): one rank drives its GPU alone; with several ranks the
             # collectives' kernels must not queue behind prio-2 share MSMs
-            B.set_wave_priorities(self.comm.world == 1)
+            B.set_wave_priorities(self.comm.world == 1 or cfg.has("wave_prio_multi"))
             S.set_spin(5e-3 if self.comm.world == 1 and not cfg.has("short_spin") else 2e-4)
             self._native = B.NativeSecAgg(self.crypto.eng, self.main_stream, self.side_stream, self.bg_stream,
                                           10.0 ** cfg.precision, witness=self.witness_stream)
