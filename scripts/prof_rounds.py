@@ -1,7 +1,9 @@
 """cProfile of steady-state headline rounds only (the engine built and warmed outside the profile): which Python
 functions and which torch / native calls hold the round's host thread.
 
-    python scripts/prof_rounds.py [--warm 30] [--rounds 200] [-o out.txt]
+    python scripts/prof_rounds.py [--warm 30] [--rounds 200] [--emulate-world N] [-o out.txt]
+
+--emulate-world N profiles rank 0 of an N-rank job (bench.py --emulate-world: the collectives filled locally).
 """
 import argparse
 import cProfile
@@ -22,9 +24,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--warm", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=200)
+    ap.add_argument("--emulate-world", type=int, default=0)
     ap.add_argument("-o", "--out", default=None)
     a = ap.parse_args()
-    comm = Comm.init()
+    comm = Comm.emulated(a.emulate_world) if a.emulate_world > 1 else Comm.init()
     torch.set_num_threads(1)
     eng = BiscottiEngine(RunConfig(num_nodes=100, seed=0, max_iterations=10**9, host_threads=14, lazy_eval=True), comm)
     for _ in range(a.warm):
