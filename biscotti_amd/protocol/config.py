@@ -111,7 +111,10 @@ class RunConfig:
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""
         assert ablation in self.ABLATIONS, ablation
-        return ablation in {a.strip() for a in self.ablation.split(",")}
+        got = self.__dict__.get("_ablation_set")   # the round asks ~11 times: parsed once per ablation string
+        if got is None or got[0] != self.ablation:
+            got = self.__dict__["_ablation_set"] = (self.ablation, frozenset(a.strip() for a in self.ablation.split(",")))
+        return ablation in got[1]
 
     @property
     def noise_independent(self) -> bool:

@@ -24,12 +24,14 @@ def test_phase_log_lines_parse_into_the_trace_phases(tmp_path):
     assert len(worker) >= 3
     verif = L.parse_verif(lines)
     assert len(verif) == len(worker)
+    # the log line is written next to the timer's reading, not at the same instant: a preempted thread (xdist
+    # workers on a loaded CPU) puts tens of us between them
     for got, t in zip(verif, worker):
-        assert abs(got - t["t_verify"]) < 5e-5, (got, t["t_verify"])
+        assert abs(got - t["t_verify"]) < 5e-4, (got, t["t_verify"])
     noise = L.parse_noise(lines)
     assert len(noise) == len(worker)
     for got, t in zip(noise, worker):
-        assert abs(got - t["t_noise"]) < 5e-5, (got, t["t_noise"])
+        assert abs(got - t["t_noise"]) < 5e-4, (got, t["t_noise"])
     aggr = L.parse_aggr(lines)
     assert [k for k, _ in aggr] == list(range(10))
     for (k, got), t in zip(aggr, trace):
