@@ -63,11 +63,26 @@ PRESETS = {
                         "perc_samples": 35}, None, 1 - 0.6310, {}, "nsdi-eval/credit/fed_50p"),
     "churn10": ({"churn": 0.1}, None, None, {}, "BASELINE.json config 5 (reference churn runs: 25-31 s/round)"),
     # process churn with state loss + rejoin (eval/eval_FT/runEval.sh: a node killed every 60/rate s,
-    # restarted 5 s before the next kill), 50 MNIST peers as in nsdi-eval/churn
-    "churn_kill4": ({"num_nodes": 50, "churn_kill_per_min": 4.0}, 30.92, 1 - 0.121, {}, "nsdi-eval/churn/15s.log"),
-    "churn_kill2": ({"num_nodes": 50, "churn_kill_per_min": 2.0}, 26.27, 1 - 0.210, {}, "nsdi-eval/churn/30s.log"),
-    "churn_kill1": ({"num_nodes": 50, "churn_kill_per_min": 1.0}, 25.71, 1 - 0.138, {}, "nsdi-eval/churn/60s.log"),
-    "churn_kill05": ({"num_nodes": 50, "churn_kill_per_min": 0.5}, 25.44, 1 - 0.191, {}, "nsdi-eval/churn/120s.log"),
+    # restarted 5 s before the next kill), 50 MNIST peers as in nsdi-eval/churn.  Those logs' leader fired at
+    # 5 shares ("As miner, I expect 5 shares", 60s.log:9686 -- 50 peers / 10, an older main.go), not at
+    # NUM_SAMPLES/2 = 17: the presets use that threshold (miner_threshold=tenth); *_half keep the live rule
+    "churn_kill4": ({"num_nodes": 50, "churn_kill_per_min": 4.0, "miner_threshold": "tenth"}, 30.92, 1 - 0.121, {},
+                    "nsdi-eval/churn/15s.log"),
+    "churn_kill2": ({"num_nodes": 50, "churn_kill_per_min": 2.0, "miner_threshold": "tenth"}, 26.27, 1 - 0.210, {},
+                    "nsdi-eval/churn/30s.log"),
+    "churn_kill1": ({"num_nodes": 50, "churn_kill_per_min": 1.0, "miner_threshold": "tenth"}, 25.71, 1 - 0.138, {},
+                    "nsdi-eval/churn/60s.log"),
+    "churn_kill05": ({"num_nodes": 50, "churn_kill_per_min": 0.5, "miner_threshold": "tenth"}, 25.44, 1 - 0.191, {},
+                     "nsdi-eval/churn/120s.log"),
+    "churn_kill1_half": ({"num_nodes": 50, "churn_kill_per_min": 1.0}, 25.71, 1 - 0.138, {},
+                         "nsdi-eval/churn/60s.log (leader at NUM_SAMPLES/2, main.go:360: not the logs' rule)"),
+    # the headline with the leader firing at N/8 shares (minBlockSize, main.go:348-352)
+    "headline_eighth": ({"miner_threshold": "eighth"}, 29.83, 0.877, {},
+                        "nsdi-eval/scaleup/bis_baseline_100 (leader at N/8 shares, main.go:348-352)"),
+    # weak scaling: 100 peers per rank, reference defaults otherwise (the reference's scaling axis is the peer
+    # count: nsdi-eval/increments/results.log:1-5, eval/eval_FedSys_scale); num_nodes = 100 x ranks
+    "scale_weak": ({"peers_per_rank": 100}, None, None, {},
+                   "nsdi-eval/increments/results.log:1-5 (peer-count axis; no published number at these sizes)"),
     # the long-parameter-vector ledger: LFW maleness softmax, d = 17486 (no reference number:
     # the reference's lfw pipeline is inconsistent, see data.dataset_dims)
     "lfw100": ({"dataset": "lfw"}, None, None, {}, "honest.go:211 'mnist/lfw for pytorch' (unpinned)"),
@@ -165,6 +180,9 @@ def main() -> int:
                          "rank 0's data): the per-rank cost of an N-GPU job, never a scaling number")
     ap.add_argument("--phase-sync", action="store_true",
                     help="synchronise the GPU at every phase boundary (per-phase GPU attribution, slower)")
+    ap.add_argument("--deterministic-time", action="store_true",
+                    help="block timestamps = iteration + 1 (RunConfig.deterministic_time): a seed's chain, and so "
+                         "its accuracy curve, is the same run to run (--seeds experiments)")
     a = ap.parse_args()
     if a.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -183,6 +201,9 @@ def main() -> int:
     over, ref_s, ref_acc, ref_extra, ref_src = PRESETS[a.config]
     over = dict(over)
     fedsys = over.pop("fedsys", False)
+    per_rank_peers = over.pop("peers_per_rank", None)
+    if per_rank_peers:   # weak scaling: the job's peers grow with its ranks (emulated ranks count)
+        over["num_nodes"] = per_rank_peers * max(world, a.emulate_world, 1)
 
     from biscotti_amd.parallel.comm import Comm
     from biscotti_amd.protocol.config import RunConfig
@@ -201,7 +222,8 @@ def main() -> int:
     # lazy_eval: each round's two evaluation numbers are read back one round later (the kernels still run
     # inside the round); the accuracies below are read after drain()
     kw = dict(num_nodes=100, dataset="mnist", seed=a.seed, max_iterations=10**9, trace_file=a.trace,
-              host_threads=_host_threads(), phase_sync=a.phase_sync, lazy_eval=True)
+              host_threads=_host_threads(), phase_sync=a.phase_sync, lazy_eval=True,
+              deterministic_time=a.deterministic_time)
     kw.update(over)
     if a.peers:
         kw["num_nodes"] = a.peers
@@ -346,6 +368,11 @@ def main() -> int:
     att10 = [st.mean([v for v in l[max(0, min(R, len(l)) - 10):min(R, len(l))] if v is not None]) for l in all_att]
     acc = finals[0]
     ok, why = eng.fsm.chain.verify() if not fedsys else (True, "")
+    # contributors per committed block (updates in the block; the reference's churn logs show it as the stake
+    # map's growth: stake_unit per contributor) and the stake total, for the churn comparisons
+    blocks = len(eng.fsm.chain) - 1 if not fedsys else None
+    contrib = (eng.stats.get("total_updates", 0) / max(1, eng.rounds_done)) if not fedsys else None
+    stake_total = int(sum(dict(eng.fsm.stake).values())) if not fedsys else None
     from biscotti_amd.utils import flush_logs
 
     flush_logs(eng.log)   # buffered log lines go out before the result line
@@ -415,6 +442,13 @@ def main() -> int:
             "phase_ms_per_round": {k: 1e3 * v / max(a.steps, 1) for k, v in sorted(phases.items())},
             "phase_sync": bool(a.phase_sync),
             "chain_valid": bool(ok),
+            "miner_threshold": getattr(cfg, "miner_threshold", None),
+            "leader_cap": eng.fsm.leader_cap_size() if not fedsys else None,
+            "contributors_per_block": contrib,
+            "stake_total": stake_total,
+            "stake_initial": cfg.num_nodes * cfg.default_stake,
+            "chain_blocks": blocks,
+            "deterministic_time": bool(cfg.deterministic_time),
         }
         if cfg.dataset == "mnist":
             out["final_attack_rate"] = att_final[0]

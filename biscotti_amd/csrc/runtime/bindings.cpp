@@ -1231,6 +1231,8 @@ PYBIND11_MODULE(_biscotti_rt, m) {
         const Bytes& h = c.latest().hash;
         return py::bytes(reinterpret_cast<const char*>(h.data()), h.size());
       })
+      // the latest block's iteration alone (net/rpc answers it on every admitted call: no block copy)
+      .def("latest_iteration", [](const Blockchain& c) { return c.latest().data.iteration; })
       .def("get", [](const Blockchain& c, i64 it) -> py::object {
         const Block* b = c.get(it);
         if (!b) return py::none();
@@ -1283,6 +1285,7 @@ PYBIND11_MODULE(_biscotti_rt, m) {
       .def_readwrite("seed", &ProtocolConfig::seed)
       .def_readwrite("shared_inbox", &ProtocolConfig::shared_inbox)
       .def_readwrite("miner_cap", &ProtocolConfig::miner_cap)
+      .def_readwrite("miner_block_div", &ProtocolConfig::miner_block_div)
       .def_readonly("num_samples", &ProtocolConfig::num_samples)
       .def_readonly("krum_thresh", &ProtocolConfig::krum_thresh)
       .def_readonly("total_shares", &ProtocolConfig::total_shares)

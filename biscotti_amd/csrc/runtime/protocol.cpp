@@ -15,7 +15,7 @@ void ProtocolConfig::derive() {
   krum_thresh = rand_sample ? num_nodes - num_verifiers - num_miners : num_samples;
   total_shares = i64(std::ceil(double(poly_size * 2) / double(num_miners))) * num_miners;
   shares_per_miner = total_shares / num_miners;
-  miner_share_thresh = num_samples / 2;
+  miner_share_thresh = miner_block_div > 0 ? std::max<i64>(num_nodes / miner_block_div, 2) : num_samples / 2;
   poisoning_index = i64(std::ceil(double(num_nodes) * (1.0 - poisoning)));
   collusion_thresh = i64(std::ceil(double(num_nodes) * (1.0 - double(colluders) / 100.0)));
 }
@@ -232,7 +232,8 @@ std::vector<i64> RoundFSM::leader_arrivals() const {
 
 i64 RoundFSM::leader_cap_size() const {
   if (!cfg.miner_cap) return 0;
-  // NUM_SAMPLES/2 (main.go:360), at least 2: the leader only builds a block from > 1 node
+  // NUM_SAMPLES/2 (main.go:360) or num_nodes / miner_block_div (minBlockSize, main.go:348-352), at least 2:
+  // the leader only builds a block from > 1 node
   // (main.go:2079) -- in the reference a second share lands while the leader queries the other
   // miners; the same floor as its minBlockSize rule (main.go:347-351)
   return std::max<i64>(cfg.miner_share_thresh, 2);

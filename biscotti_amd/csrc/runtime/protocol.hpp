@@ -48,6 +48,8 @@ struct ProtocolConfig {
   bool shared_inbox = false;  // every verifier sees the same inbox (round-1 model; the reference's
   //                             verifiers each keep their own first-arrivals list)
   bool miner_cap = true;   // leader fires at NUM_SAMPLES/2 shares (main.go:360): block = first arrivals
+  i64 miner_block_div = 0;  // 0: the NUM_SAMPLES/2 rule (main.go:360); k > 0: the leader fires at num_nodes / k
+  //                           shares, at least 2 (minBlockSize, main.go:348-352 with k = 8)
   // derived (call derive())
   i64 num_samples = 0, krum_thresh = 0, total_shares = 0, shares_per_miner = 0;
   i64 miner_share_thresh = 0, poisoning_index = 0, collusion_thresh = 0;

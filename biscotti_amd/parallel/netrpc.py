@@ -254,7 +254,8 @@ class PeerService:
         """The iteration this peer is working on: progress(), else its chain's latest block + 1."""
         if self._progress is not None:
             return int(self._progress())
-        return int(self.chain.latest().data.iteration) + 1
+        li = getattr(self.chain, "latest_iteration", None)   # native: no copy of the latest block (GlobalW)
+        return int(li() if li is not None else self.chain.latest().data.iteration) + 1
 
     def _admit(self, it: int) -> None:
         """Refuse a message whose iteration is outside [current - KEEP, current + AHEAD] and forget state

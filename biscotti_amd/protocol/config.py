@@ -63,6 +63,13 @@ class RunConfig:
     #                                 update to verifiers / miners, Got share for, Sending block of iteration) so its
     #                                 parseLogs.py phase breakdown works on our logs (protocol/golog.py)
     deterministic_time: bool = False  # block timestamps = iteration + 1 (reproducible chains in tests)
+    miner_threshold: str = "half_samples"  # when the leader miner builds its block from the shares it has
+    #                                 (secure path; its block holds the first arrivals up to that count):
+    #   half_samples  NUM_SAMPLES/2 shares (main.go:360, the reference's live rule; default)
+    #   eighth        numberOfNodes/8, at least 2 (minBlockSize, main.go:348-352: the commented-out rule)
+    #   tenth         numberOfNodes/10, at least 2: what the nsdi-eval/churn logs fired at ("As miner, I expect
+    #                 5 shares" with 50 peers, 60s.log:9686; an older main.go whose log lines are at :304-314)
+    #                 The plain path's leader keeps NUM_SAMPLES/2 updates (processUpdate, main.go:1222-1230).
     phase_sync: bool = False        # device sync at phase boundaries (diagnostics: per-phase GPU times)
     audit_aggregate: bool = True    # check the recovered aggregate against the miners' summed chunk
     #                                 commitments (verifyCommitment on the aggregate; not in the reference)
@@ -103,6 +110,7 @@ class RunConfig:
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
     churn_round_s: ClassVar[float] = 25.44
+    MINER_THRESHOLDS: ClassVar[dict] = {"half_samples": 0, "eighth": 8, "tenth": 10}   # -> miner_block_div
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
                                   "noise_gram_each_round", "spec_tight", "no_early_front",
@@ -183,6 +191,8 @@ class RunConfig:
             err.append(f"fail_at {self.fail_at!r}: expected IT or IT@RANK")
         if self.defense not in ("KRUM", "RONI", "LSH"):
             err.append(f"defense {self.defense!r}: expected KRUM | RONI | LSH")
+        if self.miner_threshold not in self.MINER_THRESHOLDS:
+            err.append(f"miner_threshold {self.miner_threshold!r}: expected {' | '.join(self.MINER_THRESHOLDS)}")
         if self.kzg_audit not in ("off", "consistent", "literal"):
             err.append(f"kzg_audit {self.kzg_audit!r}: expected off | consistent | literal")
         if err:
@@ -219,6 +229,7 @@ class RunConfig:
         pc.seed = self.seed & (2**64 - 1)
         pc.shared_inbox = self.has("shared_inbox")
         pc.miner_cap = not self.has("no_miner_cap")
+        pc.miner_block_div = self.MINER_THRESHOLDS.get(self.miner_threshold, 0) if self.secure_agg else 0
         pc.derive()
         return pc
 
@@ -273,6 +284,9 @@ def add_framework_flags(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--phase-log", action="store_true",
                     help="write the reference's role and phase log lines (parseLogs.py breakdowns)")
     ap.add_argument("--deterministic-time", action="store_true")
+    ap.add_argument("--miner-threshold", default="half_samples", choices=sorted(RunConfig.MINER_THRESHOLDS),
+                    help="shares the leader miner builds its block at: NUM_SAMPLES/2 (main.go:360), N/8 "
+                         "(main.go:348-352) or N/10 (the nsdi-eval/churn logs)")
     ap.add_argument("--phase-sync", action="store_true",
                     help="synchronise the device at every phase boundary (per-phase GPU times; slower)")
     ap.add_argument("--no-audit-aggregate", dest="audit_aggregate", action="store_false")

@@ -337,12 +337,23 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         if self.golog is not None:
             self.golog.flush()
         self.drain()
+        heads = []
+        fr, self._front = self._front, None
+        if fr is not None:
+            # the next round's front was started (its Krum, the aggregation behind it, the pre-step) but its round
+            # never ran: stop the suspended verification generator, join the head's VRF jobs, drop its tensors
+            ver = fr.get("verify")
+            if hasattr(ver, "close"):
+                ver.close()
+            heads.append(fr["head"])
         head, self._head = self._head, None
-        if head:
-            for k in ("fut_noise", "fut_roles"):
-                if head.get(k) is not None:
-                    head[k].result()
-        head = None  # drop the round's tensors while their streams are all still alive
+        heads.append(head)
+        for head in heads:
+            if head:
+                for k in ("fut_noise", "fut_roles"):
+                    if head.get(k) is not None:
+                        head[k].result()
+        fr = head = heads = None  # drop the round's tensors while their streams are all still alive
         self._pre = self._spec_next = None
         if self.gpu:
             torch.cuda.synchronize(self.dev)
@@ -369,6 +380,24 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 torch.cuda.empty_cache()
                 B.hip().bsc_stream_destroy(self.side_stream.cuda_stream)
             self.side_stream = None
+
+    EVAL_RING = 6   # evaluation inputs in flight (lazy_eval keeps at most 4 unread: _round_front)
+
+    def _eval_input(self, W: torch.Tensor) -> torch.Tensor:
+        """The model an evaluation reads, copied (current stream) into a slot of a ring of its own: the copy is
+        ordered after the recovery that wrote W and before any later round's recovery can rewrite W's ring
+        slot.  A slot is reused only after its previous evaluation has passed (an event wait that is
+        normally long satisfied: the evaluations lag by at most ~4 rounds)."""
+        ring = self.__dict__.get("_eval_ring")
+        if ring is None or ring[0].shape != W.shape:
+            ring = self._eval_ring = [torch.empty_like(W) for _ in range(self.EVAL_RING)]
+            self._eval_done = [None] * self.EVAL_RING
+            self._eval_k = -1
+        self._eval_k = k = (self._eval_k + 1) % self.EVAL_RING
+        if self._eval_done[k] is not None:
+            S.current().wait_event(self._eval_done[k])
+        ring[k].copy_(W)
+        return ring[k]
 
     def _now(self, iteration: int) -> int:
         return iteration + 1 if self.cfg.deterministic_time else int(time.time())
@@ -445,8 +474,11 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             if self.gpu:
                 # on the witness stream (low priority; nothing in the round waits for either): on the main
                 # stream the evaluation sat between the audit and the next round's Krum kernels.  Launched
-                # after the next round's front when that runs (ordered on main's position here)
-                W_ev, W_eval = S.record(), self.W
+                # after the next round's front when that runs (ordered on main's position here).  self.W is a
+                # slot of the native W ring, which a later round's recovery rewrites while a lagging evaluation
+                # may still read it: the evaluation reads a copy of its own (_eval_input)
+                W_eval = self._eval_input(self.W)
+                W_ev = S.record()
             else:
                 eval_pending = self.task.evaluate_async(self.W)
         with tm.phase("next_head"):
@@ -471,9 +503,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         if self.gpu:
             ws = self.witness_stream
             ws.wait_event(W_ev)
-            S.hold(W_eval)   # read on another stream: kept for two rounds
             with S.use(ws):
                 eval_pending = self.task.evaluate_async(W_eval)
+                self._eval_done[self._eval_k] = S.record(ws)   # the copy's slot is free again after this
         if self._idle_work is not None:  # every rank, same point: the collective stays aligned
             self._idle_work()
             self._idle_work = None

@@ -191,7 +191,8 @@ class SecAggMixin:
                "readback": readback, "contributing": list(contributing), "part": dict(part), "accepted": None,
                "node": node}
         if kzg:
-            out["kzg_in"], out["kzg_events"] = self._kzg_capture(lid, ycols_t, xs_t), []
+            out["kzg_in"] = self._kzg_capture(lid, ycols_t, xs_t)
+            out["kzg_events"] = [self._kzg_copied]   # the audit stream reads the copies (_kzg_adopt)
         return out
 
     def _kzg_capture(self, lid: int, ycols_t, xs_t):
@@ -200,7 +201,11 @@ class SecAggMixin:
         the contributing points ([nch, npts]: the recovered aggregate on one rank, this rank's send-row partials
         on several).  The next aggregation waits for the copies (_kzg_copied) before rewriting the buffers."""
         na, nch = self._native, self.nchunks
-        st = self.vrf_stream
+        # a stream of its own: on the VRF prover's stream the copies (which the next aggregation waits for) queued
+        # behind a whole ~2.2 ms prover launch
+        st = self.__dict__.get("kzg_stream")
+        if st is None:
+            st = self.kzg_stream = torch.cuda.Stream(device=self.dev, priority=torch.cuda.Stream.priority_range()[0])
         for src in (S.current(), self.side_stream, self.upload_stream, self.witness_stream):
             S.wait(st, src)
         with S.use(st):

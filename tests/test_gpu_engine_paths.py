@@ -240,3 +240,39 @@ def test_spec_horizon_same_chain_as_every_candidate(poisoning):
     assert s0["spec_rows_late"] < 0.9 * s1["spec_rows_late"], (s0["spec_rows_late"], s1["spec_rows_late"])
     print("rows launched after the window", s0["spec_rows_late"], "vs", s1["spec_rows_late"], "misses",
           s0.get("spec_misses", 0), "tight misses", s2.get("spec_misses", 0))
+
+
+def test_close_after_plain_rounds_with_a_pending_front():
+    """run_round() without last=True leaves the next round's front launched (its Krum, the aggregation queued
+    behind it, a suspended verification generator, unjoined VRF jobs): close() must stop and drop it before it
+    releases the streams, and a second engine must run normally afterwards."""
+    eng = _engine(num_nodes=30, lazy_eval=True)
+    for _ in range(4):
+        eng.run_round()
+    assert eng._front is not None and eng.stats.get("early_fronts", 0) >= 2
+    eng.close()
+    assert eng._front is None
+    eng2 = _engine(num_nodes=30)
+    r = eng2.run_round()
+    assert not r.empty and eng2.fsm.chain.verify()[0]
+    eng2.close()
+
+
+def test_lagging_evaluation_reads_its_own_model():
+    """The evaluation runs on the low-priority witness stream and may lag the main stream by several rounds,
+    while the native W ring slot it was given is rewritten by later recoveries: with the witness stream stalled
+    (a long sleep kernel queued on it every round) the reported test errors equal an unstalled run's."""
+    out = []
+    for stall in (False, True):
+        eng = _engine(num_nodes=30, lazy_eval=True)
+        errs = []
+        for k in range(8):
+            if stall:
+                with torch.cuda.stream(eng.witness_stream):
+                    torch.cuda._sleep(20_000_000)   # ~10 ms of the witness stream per round
+            errs.append(eng.run_round(last=k == 7))
+        eng.drain()
+        out.append([(r.iteration, r.test_error, r.attack_rate) for r in errs])
+        eng.close()
+    assert out[0] == out[1]
+    assert all(e == e for _, e, _ in out[1])

@@ -147,3 +147,23 @@ def test_gpu_spec_horizon_two_ranks_100_peers_over_rccl():
     assert out[0][1].get("spec_misses", 0) == out[1][1].get("spec_misses", 0) == s1.get("spec_misses", 0)
     # each rank launches its own peers' rows: together the single process's rows
     assert out[0][1]["spec_rows"] + out[1][1]["spec_rows"] == s1["spec_rows"], (out[0][1], out[1][1], s1)
+
+
+def test_gpu_eight_ranks_100_peers_over_rccl():
+    """The job an 8-GPU node runs at the headline size, rehearsed with 8 RCCL ranks sharing cuda:0: 100 peers
+    split 12/13 per rank, the speculative head forced on, every fast path on every rank in every round after the
+    first, no audit failure, and the chain equal to one process's byte for byte (the localTest.sh oracle,
+    DistSys/localTest.sh:47-87)."""
+    rounds = 6
+    kw = dict(num_nodes=100, dataset="mnist", seed=19, deterministic_time=True, max_iterations=100,
+              ablation="spec_head_shared", host_threads=2)
+    single, s1 = _run_stats(1, kw, rounds)[0]
+    out = _run_stats(8, kw, rounds, backend="nccl")
+    for r in range(8):
+        hashes, st = out[r]
+        assert hashes == single, f"rank {r} chain differs"
+        for k in ("pre_steps", "spec_head", "early_vrf"):
+            assert st.get(k, 0) >= rounds - 1, (r, k, st)
+        assert st.get("device_aggregations", 0) + st.get("spec_misses", 0) >= rounds - 1, (r, st)
+        assert st.get("audit_failures", 0) == 0, (r, st)
+    assert sum(out[r][1]["spec_rows"] for r in range(8)) == s1["spec_rows"]

@@ -279,7 +279,8 @@ def test_cli_defaults_match_runconfig():
     assert RunConfig().fail_point() == (-1, 0)
     import dataclasses
 
-    assert len(dataclasses.fields(RunConfig)) <= 50   # 49 + phase_log (the reference's phase lines, round 5)
+    # 49 + phase_log (the reference's phase lines, round 5) + miner_threshold (main.go:348-360, round 6)
+    assert len(dataclasses.fields(RunConfig)) <= 51
     import pytest
 
     with pytest.raises(ValueError):
@@ -352,3 +353,53 @@ def test_spec_horizon_policy():
     assert horizon(eng) == 35
     eng.cfg, eng.fsm = Cfg(), SimpleNamespace(leader_cap_size=lambda: 0)   # no leader cap: every candidate
     assert horizon(eng) == -1
+
+
+@pytest.mark.parametrize("rule,n,want", [("half_samples", 100, 35), ("eighth", 100, 12), ("eighth", 50, 6),
+                                         ("eighth", 12, 2), ("tenth", 50, 5), ("tenth", 14, 2)])
+def test_miner_threshold_rules(rt, rule, n, want):
+    """The leader miner's block size: NUM_SAMPLES/2 (main.go:360), numberOfNodes/8 (minBlockSize,
+    main.go:348-352) or /10 (what nsdi-eval/churn/*.log fired at: 'I expect 5 shares' with 50 peers), floor 2."""
+    from biscotti_amd.protocol.config import RunConfig
+
+    cfg = RunConfig(num_nodes=n, miner_threshold=rule)
+    cfg.validate()
+    pc = cfg.protocol(rt)
+    assert pc.miner_share_thresh == want
+    # the plain path's leader keeps NUM_SAMPLES/2 updates (processUpdate, main.go:1222-1230)
+    import dataclasses
+
+    assert dataclasses.replace(cfg, secure_agg=False).protocol(rt).miner_share_thresh == pc.num_samples // 2
+
+
+def test_runconfig_rejects_unknown_miner_threshold():
+    from biscotti_amd.protocol.config import RunConfig
+
+    with pytest.raises(ValueError, match="miner_threshold"):
+        RunConfig(miner_threshold="quarter").validate()
+
+
+def test_leader_fires_at_an_eighth_of_the_nodes():
+    """Secure rounds with miner_threshold=eighth: every non-empty block carries exactly floor(N/8) updates (the
+    leader's first arrivals among the approved; the approved always outnumber it here), the chain verifies and
+    the stake grows by stake_unit per contributor."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    n = 24
+    eng = BiscottiEngine(RunConfig(num_nodes=n, dataset="mnist", seed=3, max_iterations=100, deterministic_time=True,
+                                   miner_threshold="eighth", device="cpu"), Comm())
+    assert eng.fsm.leader_cap_size() == n // 8
+    stake0 = sum(dict(eng.fsm.stake).values())
+    sizes = []
+    for _ in range(3):
+        r = eng.run_round()
+        if not r.empty:
+            sizes.append(len(r.node_list))
+            assert len(r.approved) > n // 8
+    assert sizes and all(s == n // 8 for s in sizes), sizes
+    assert sum(dict(eng.fsm.stake).values()) == stake0 + 5 * sum(sizes)
+    ok, why = eng.fsm.chain.verify()
+    assert ok, why
+    eng.close()

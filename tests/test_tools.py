@@ -160,3 +160,27 @@ def test_vrf_security_models_and_lottery(tmp_path):
     V.plot_committee(str(tmp_path / "c.pdf"))
     V.plot_noise(str(tmp_path / "n.pdf"))
     assert (tmp_path / "c.pdf").stat().st_size > 0 and (tmp_path / "n.pdf").stat().st_size > 0
+
+
+def test_bench_scale_weak_preset_four_gloo_ranks():
+    """bench.py --config scale_weak on 4 gloo ranks (torchrun on 127.0.0.1): 100 peers per rank -> a 400-peer job
+    (creditcard keeps the CPU crypto cheap); the JSON names the job's peers and the per-rank packing, and the chain
+    verifies on every rank."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+                          "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", "4",
+                          "--config", "scale_weak", "--steps", "2", "--warmup", "1", "--rounds", "3",
+                          "--set", "dataset=creditcard", "--set", "noising=false", "--set", "host_threads=2"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads(next(ln for ln in out.stdout.splitlines() if ln.startswith("{")))
+    assert rec["config"]["name"] == "scale_weak" and rec["config"]["peers"] == 400 and rec["n_gpus"] == 4
+    assert rec["config"]["parallelism"].startswith("dp4") and "100/GPU" in rec["config"]["parallelism"]
+    assert rec["chain_valid"] and len(rec["per_rank"]) == 4
+    assert rec["contributors_per_block"] > 0 and rec["stake_initial"] == 4000
