@@ -400,6 +400,8 @@ def main() -> int:
             "accuracy_rounds": R,
             "seeds": a.seeds,
             "final_test_acc_mean_std": ms(finals),
+            "final_test_acc_per_seed": finals,
+            "test_acc_last10_per_seed": last10,
             "test_acc_last10_mean_std": ms(last10),
             "setup_s": setup_s,
             "drain_ms": 1e3 * drain_s,          # inside the timed window: joins of the last rounds' work
@@ -455,6 +457,7 @@ def main() -> int:
             out["attack_rate_last10_mean"] = att10[0]
             out["final_attack_rate_mean_std"] = ms(att_final)
             out["attack_rate_last10_mean_std"] = ms(att10)
+            out["attack_rate_last10_per_seed"] = att10
         for k, v in ref_extra.items():
             out[f"baseline_{k}"] = v
         if real_world > 1:
