@@ -37,8 +37,9 @@ print(sys.argv[2], 'ms', round(d['ms_per_step'], 3), 'med', round(med, 3), 'max'
       'rb', round(p.get('recover.readback', 0), 3), 'drain', round(d.get('drain_ms', 0), 2), flush=True)
 PY
 }
-bench() {   # bench NAME TIMEOUT ARGS...
-  local n="$1" t="$2"; shift 2
+bench() {   # bench NAME TIMEOUT ARGS...  (a NAME already used in OUT gets a suffix: repeated steps keep every run)
+  local n="$1" t="$2" k=2; shift 2
+  if [[ -e "$O/$n.txt" ]]; then while [[ -e "$O/${n}_$k.txt" ]]; do k=$((k + 1)); done; n="${n}_$k"; fi
   timeout -k 10 "$t" python bench.py "$@" > "$O/$n.txt" 2>&1 || { echo "FAIL $n"; tail -20 "$O/$n.txt"; exit 1; }
   summ "$O/$n.txt" "$n"
 }
