@@ -210,7 +210,9 @@ def test_mnist_label_flip_rejection_floor_default_noise():
     assert last10 <= DIGIT1_ERR_CEILING, last10
 
 
-DIGIT1_ERR_CEILING = 0.70   # this deterministic run measures 0.647 (rejection 0.756): + 0.05, docs/ROBUSTNESS.md
+# this deterministic run measures 0.647 (rejection 0.756); the reproducible 5-seed poison30 run (bench.py
+# --deterministic-time --seeds 5, round 6) gives 0.582 +- 0.065 with a worst seed of 0.644: ceiling 0.70
+DIGIT1_ERR_CEILING = 0.70
 
 
 @pytest.mark.parametrize("poisoning", [0.0, 0.3])
