@@ -16,8 +16,11 @@
 //
 // The launchers of the individual kernels (msm.hip, ml.hip) are called directly; every buffer is
 // resident (allocated once by the engine), so the call allocates nothing.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types only: the entry points are resolved at run time (bsc_rccl_load)
 #include <stdint.h>
+#include <string.h>
 
 #include <chrono>
 #include <thread>
@@ -58,6 +61,9 @@ extern "C" int bsc_gram_stacked(const float* X, int U1, const float* X2, int U2,
                                 double* part, double* gram, unsigned int* count, const double* nn, void* stream);
 extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
                                void* stream);
+extern "C" int bsc_gram_stacked_range(const float* X, int U1, const float* X2, int U2, long long stride2, int D,
+                                      int kchunk, int p0, int p1, double* part, double* gram, unsigned int* count,
+                                      const double* nn, void* stream);
 extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
                                int B0, int NW, uint32_t* partial, uint32_t* out, void* stream);
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
@@ -126,6 +132,26 @@ struct RoundCtx {
   hipEvent_t spec_done[8];
   bool spec_used[8], spec_filled[8];
   int nspec = 0, spec_cap = 0, spec_k = -1;
+  // several ranks (bsc_round_comm_init): the round's own RCCL communicator -- every collective of a round goes
+  // through it, on ONE comm stream, in the order the round issues them (the same on every rank) -- or, emulating
+  // rank 0 of a `cworld`-rank job on one GPU, local copies of rank 0's contribution into every slot
+  ncclComm_t comm = nullptr;
+  int cworld = 1, crank = 0, emulate = 0;
+  long long timeout_ns = 0;   // bsc_round_wait gives up (and aborts the communicator) after this; 0: never
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_c0 = nullptr, ev_c1 = nullptr;
+  // the multi-rank aggregation's resident buffers and the next Gram's inputs (bsc_round_bind_multi)
+  struct Multi {
+    int bound = 0;
+    unsigned char *send = nullptr, *recv = nullptr;
+    long long row_bytes = 0;
+    long long* h_clock = nullptr;
+    int maxlocal = 0, U1 = 0, p0 = 0, p1 = 0, chunk = 0;
+    float *pad = nullptr, *X = nullptr;      // [maxlocal][d] send buffer (ranks with fewer peers), [world maxlocal][d]
+    double* part = nullptr;                  // [nsplit][p1 - p0][256] split-K partials of this rank's tile pairs
+    unsigned char* vg_recv[2] = {nullptr, nullptr};   // the verification gather's rows (alternating by iteration)
+    long long vg_row_bytes = 0;
+  } m;
 };
 #define RC_CHECK(x)                        \
   do {                                     \
@@ -192,9 +218,26 @@ extern "C" int bsc_wave_prio(int on) {
   return bsc_wave_prio_vrf(on);
 }
 
+namespace {
+// The RCCL entry points of the library the process already runs (torch's, which owns the other communicators):
+// resolved once by bsc_rccl_load, so one RCCL instance serves the process.
+struct RcclApi {
+  void* h = nullptr;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+};
+RcclApi g_rccl;
+}  // namespace
+
 extern "C" void bsc_round_destroy(void* ctx) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return;
+  if (c->comm != nullptr && g_rccl.comm_destroy != nullptr) g_rccl.comm_destroy(c->comm);
+  if (c->ev_c0 != nullptr) (void)hipEventDestroy(c->ev_c0);
+  if (c->ev_c1 != nullptr) (void)hipEventDestroy(c->ev_c1);
   hipEventDestroy(c->ev_main);
   hipEventDestroy(c->ev_side);
   hipEventDestroy(c->ev_readback);
@@ -710,7 +753,7 @@ static long long g_spin_ns = 200000;   // bsc_set_host_spin_ns: the engine spins
 
 extern "C" void bsc_set_host_spin_ns(long long ns) { g_spin_ns = ns < 0 ? 0 : ns; }
 
-static int host_wait(hipEvent_t ev) {
+static int host_wait(hipEvent_t ev, long long timeout_ns = 0) {
   const long long SPIN_NS = g_spin_ns;
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
@@ -718,13 +761,217 @@ static int host_wait(hipEvent_t ev) {
     if (e != hipErrorNotReady) return (int)e;
     const long long ns =
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_ns > 0 && ns > timeout_ns) return -99;
     if (ns > SPIN_NS) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
 
-// which: 0 = the recovery read-back, 1 = the audit read-back
+// which: 0 = the recovery read-back, 1 = the audit read-back.  With the round's own communicator, a wait longer
+// than the collective timeout means a rank is gone (the reference's crashed peer): the communicator is aborted
+// -- its kernels return -- and -99 goes back to the engine, which fails the job for the elastic restart
+// (parallel/comm.py), as torch's watchdog does for its own collectives
 extern "C" int bsc_round_wait(void* ctx, int which) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return -1;
-  return host_wait(which == 0 ? c->ev_readback : c->ev_audit);
+  const int r = host_wait(which == 0 ? c->ev_readback : c->ev_audit, c->comm != nullptr ? c->timeout_ns : 0);
+  if (r == -99 && c->comm != nullptr && g_rccl.comm_abort != nullptr) {
+    g_rccl.comm_abort(c->comm);
+    c->comm = nullptr;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// The round's collectives, native (several ranks, one per GPU).  Each rank's round owns ONE RCCL communicator
+// (bsc_round_comm_init: the unique id travels over the job's process group once) and issues every collective
+// of its round on ONE comm stream, inside the fused calls that produce and consume the data:
+//   bsc_round_agg_multi     behind the committee's selection: this rank's partial sums -> all_gather of the
+//                           packed rows -> totals + exact recovery + read-back + the next pre-step -> all_gather
+//                           of the pre-step's deltas -> this rank's tile pairs of the next noise-aware Gram,
+//                           written into its slot of the next verification row
+//   bsc_round_vg_exchange   the verification row: pack -> all_gather in place -> unpack (ops/gather.py)
+// The order is the round's issue order, the same on every rank; RCCL pairs the ranks' operations op by op.  A
+// rank emulating rank 0 of a larger job (bench.py --emulate-world) fills the other ranks' slots with its own
+// contribution by device copies instead.  The library is the one torch already loaded (bsc_rccl_load).
+extern "C" int bsc_rccl_load(const char* path) {
+  if (g_rccl.all_gather != nullptr) return 0;
+  void* h = nullptr;
+  if (path != nullptr && path[0] != 0) {
+    h = dlopen(path, RTLD_NOW | RTLD_NOLOAD);   // the copy the process runs already
+    if (h == nullptr) h = dlopen(path, RTLD_NOW);
+  }
+  if (h == nullptr) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  if (h == nullptr) return -1;
+  g_rccl.get_unique_id = (decltype(g_rccl.get_unique_id))dlsym(h, "ncclGetUniqueId");
+  g_rccl.comm_init_rank = (decltype(g_rccl.comm_init_rank))dlsym(h, "ncclCommInitRank");
+  g_rccl.all_gather = (decltype(g_rccl.all_gather))dlsym(h, "ncclAllGather");
+  g_rccl.comm_destroy = (decltype(g_rccl.comm_destroy))dlsym(h, "ncclCommDestroy");
+  g_rccl.comm_abort = (decltype(g_rccl.comm_abort))dlsym(h, "ncclCommAbort");
+  if (!g_rccl.get_unique_id || !g_rccl.comm_init_rank || !g_rccl.all_gather || !g_rccl.comm_destroy ||
+      !g_rccl.comm_abort) {
+    g_rccl.all_gather = nullptr;
+    return -2;
+  }
+  g_rccl.h = h;
+  return 0;
+}
+
+extern "C" int bsc_rccl_unique_id(unsigned char* out) {
+  if (g_rccl.get_unique_id == nullptr) return -1;
+  ncclUniqueId id;
+  if (g_rccl.get_unique_id(&id) != ncclSuccess) return -2;
+  memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+// world ranks, this one `rank`; uid: the NCCL_UNIQUE_ID_BYTES rank 0 drew (every rank passes the same);
+// comm_stream: where the collectives run (nullptr: main); emulate: rank 0 alone (no communicator)
+extern "C" int bsc_round_comm_init(void* ctx, const unsigned char* uid, int world, int rank, void* comm_stream,
+                                   int emulate, double timeout_s) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || world < 2 || rank < 0 || rank >= world || c->comm != nullptr || (emulate && rank != 0)) return -1;
+  if (c->ev_c0 == nullptr) {
+    RC_CHECK(hipEventCreateWithFlags(&c->ev_c0, hipEventDisableTiming));
+    RC_CHECK(hipEventCreateWithFlags(&c->ev_c1, hipEventDisableTiming));
+  }
+  c->cworld = world;
+  c->crank = rank;
+  c->emulate = emulate ? 1 : 0;
+  c->cstream = comm_stream != nullptr ? (hipStream_t)comm_stream : c->main;
+  c->timeout_ns = timeout_s > 0 ? (long long)(timeout_s * 1e9) : 0;
+  if (!emulate) {
+    if (g_rccl.comm_init_rank == nullptr || uid == nullptr) return -2;
+    ncclUniqueId id;
+    memcpy(id.internal, uid, NCCL_UNIQUE_ID_BYTES);
+    const ncclResult_t r = g_rccl.comm_init_rank(&c->comm, world, id, rank);
+    if (r != ncclSuccess) {
+      c->comm = nullptr;
+      return -100 - (int)r;
+    }
+  }
+  return 0;
+}
+
+// all_gather of `bytes` per rank from `send` into recv [world][bytes] (in place when send is this rank's slot of
+// recv): the comm stream waits for the producer stream, the consumer stream for the collective
+static int round_all_gather(RoundCtx* c, const void* send, void* recv, size_t bytes, hipStream_t prod,
+                            hipStream_t cons) {
+  unsigned char* r = (unsigned char*)recv;
+  if (c->emulate) {   // rank 0 alone: every slot holds rank 0's contribution (same shapes, no transport)
+    if (send != r) RC_CHECK(hipMemcpyAsync(r, send, bytes, hipMemcpyDeviceToDevice, prod));
+    for (int k = 1; k < c->cworld; ++k)
+      RC_CHECK(hipMemcpyAsync(r + (size_t)k * bytes, r, bytes, hipMemcpyDeviceToDevice, prod));
+    if (cons != prod) {
+      RC_CHECK(hipEventRecord(c->ev_c1, prod));
+      RC_CHECK(hipStreamWaitEvent(cons, c->ev_c1, 0));
+    }
+    return 0;
+  }
+  if (c->comm == nullptr) return -30;
+  RC_CHECK(hipEventRecord(c->ev_c0, prod));
+  RC_CHECK(hipStreamWaitEvent(c->cstream, c->ev_c0, 0));
+  const ncclResult_t e = g_rccl.all_gather(send, recv, bytes, ncclUint8, c->comm, c->cstream);
+  if (e != ncclSuccess) return -100 - (int)e;
+  RC_CHECK(hipEventRecord(c->ev_c1, c->cstream));
+  RC_CHECK(hipStreamWaitEvent(cons, c->ev_c1, 0));
+  return 0;
+}
+
+// the resident buffers of the fused multi-rank calls: the aggregation's packed rows (send, recv [world][row_bytes],
+// pinned h_clock [world]); the next Gram's inputs -- pad [maxlocal][d] (zeroed: a rank with fewer peers sends its
+// rows then zeros), X [world maxlocal][d], part [nsplit][p1 - p0][256], this rank's tile pairs [p0, p1) of the
+// U1 + N row Gram -- and the verification rows (two, alternating by iteration, vg_row_bytes each per rank) whose
+// leading chunk x 256 doubles are each rank's Gram slot.  vg0 == nullptr: no packed verification row (the engine
+// then gathers the Gram's deltas itself)
+extern "C" int bsc_round_bind_multi(void* ctx, unsigned char* send, unsigned char* recv, long long row_bytes,
+                                    long long* h_clock, int maxlocal, float* pad, float* X, double* part, int U1, int p0,
+                                    int p1, unsigned char* vg0, unsigned char* vg1, long long vg_row_bytes) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || c->cworld < 2 || row_bytes < bsc_round_row_bytes(c->nch, c->T) || maxlocal <= 0) return -1;
+  auto& m = c->m;
+  m.send = send;
+  m.recv = recv;
+  m.row_bytes = row_bytes;
+  m.h_clock = h_clock;
+  m.maxlocal = maxlocal;
+  m.pad = pad;
+  m.X = X;
+  m.part = part;
+  m.U1 = U1;
+  m.p0 = p0;
+  m.p1 = p1;
+  m.vg_recv[0] = vg0;
+  m.vg_recv[1] = vg1;
+  m.vg_row_bytes = vg_row_bytes;
+  m.bound = 1;
+  return 0;
+}
+
+// the next round's noise-aware Gram on several ranks, on the Gram stream behind pre-step slot `slot`: the deltas'
+// all_gather (the rank's rows padded to maxlocal), then this rank's tile pairs into its verification-row slot of
+// iteration `it`; event ev_gram of the slot
+static int round_multi_gram(RoundCtx* c, int slot, int it) {
+  const TaskCfg& t = c->task;
+  const PreSlot& p = c->pre[slot];
+  auto& m = c->m;
+  if (t.noise == nullptr || m.vg_recv[0] == nullptr || m.X == nullptr) return -40;
+  hipStream_t gs = t.gram;
+  const size_t rowb = (size_t)c->d * sizeof(float);
+  const float* src = p.delta;
+  if (t.P != m.maxlocal) {
+    RC_CHECK(hipMemcpyAsync(m.pad, p.delta, (size_t)t.P * rowb, hipMemcpyDeviceToDevice, gs));
+    src = m.pad;
+  }
+  RC_CHECK(round_all_gather(c, src, m.X, (size_t)m.maxlocal * rowb, gs, gs));
+  double* out = (double*)(m.vg_recv[it % 2] + (size_t)c->crank * m.vg_row_bytes);
+  const int k = it % 100;   // the noisers' pre-sampled vectors of this iteration (client_obj.py:97-98)
+  RC_CHECK(bsc_gram_stacked_range(m.X, m.U1, t.noise + (size_t)k * c->d, t.noise_n, 100ll * c->d, c->d, t.kchunk, m.p0,
+                                  m.p1, m.part, out - (size_t)m.p0 * 256, t.counters,
+                                  t.nn_tab != nullptr ? t.nn_tab + (size_t)k * t.noise_n * t.noise_n : nullptr, gs));
+  RC_CHECK(hipEventRecord(p.ev_gram, gs));
+  return 0;
+}
+
+// Several ranks, behind the committee's selection, in one call: this rank's partials, the aggregation's
+// all_gather, totals + recovery + read-back + the next pre-step + the audit (bsc_round_after_gather), and with
+// gram the next Gram (round_multi_gram).  out as bsc_round_after_select.
+extern "C" int bsc_round_agg_multi(void* ctx, const int* node, const int* amap, int* alive, int nspec,
+                                   const int* spec_rows, void* spec_ev, const uint32_t* pts, const long long* ys,
+                                   int early_slot, void* upload, int layout, long long clock, const double* W,
+                                   int audit, int pre_it, int audit_now, int gram, int* out) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || !c->m.bound || c->cworld < 2) return -1;
+  RC_CHECK(bsc_round_select_partials(ctx, node, amap, alive, nspec, spec_rows, spec_ev, pts, ys, early_slot, upload,
+                                     layout, c->m.send, clock, audit));
+  RC_CHECK(round_all_gather(c, c->m.send, c->m.recv, (size_t)c->m.row_bytes, c->main, c->main));
+  RC_CHECK(bsc_round_after_gather(ctx, c->m.recv, c->cworld, c->m.row_bytes, layout, W, c->m.h_clock, audit, pre_it,
+                                  audit_now, out));
+  if (out[1] >= 0 && gram) RC_CHECK(round_multi_gram(c, out[1], pre_it));
+  return 0;
+}
+
+extern "C" int bsc_vg_pack(uint8_t* row, long long commit_off, long long nz_off, long long sc_off,
+                           const uint32_t* commits, int maxlocal, int pw, const int* src_row, const int* nz,
+                           const float* sc, int nnz, void* stream);
+extern "C" int bsc_vg_unpack(const uint8_t* recv, long long row_bytes, int chunk, int npairs, long long commit_off,
+                             long long nz_off, long long sc_off, int maxlocal, int pw, int nn, int world,
+                             const int* wrow, int nw, double* gram, int* nz, float* sc, uint32_t* commits_host,
+                             void* stream);
+
+// The verification row of iteration `it` (ops/gather.py): pack this rank's row, all_gather in place, unpack, on
+// `stream`; the Gram slot at the row's head was written by round_multi_gram (or the caller's Gram launch)
+extern "C" int bsc_round_vg_exchange(void* ctx, int it, long long commit_off, long long nz_off, long long sc_off,
+                                     const uint32_t* commits, int maxlocal, int pw, const int* src_row, const int* nz,
+                                     const float* sc, int nnz, int chunk, int npairs, int nn, const int* wrow, int nw,
+                                     double* gram, int* nz_out, float* sc_out, uint32_t* host, void* stream) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || !c->m.bound || c->m.vg_recv[0] == nullptr) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned char* buf = c->m.vg_recv[it % 2];
+  const size_t rb = (size_t)c->m.vg_row_bytes;
+  unsigned char* row = buf + (size_t)c->crank * rb;
+  RC_CHECK(bsc_vg_pack(row, commit_off, nz_off, sc_off, commits, maxlocal, pw, src_row, nz, sc, nnz, st));
+  RC_CHECK(round_all_gather(c, row, buf, rb, st, st));
+  return bsc_vg_unpack(buf, (long long)rb, chunk, npairs, commit_off, nz_off, sc_off, maxlocal, pw, nn, c->cworld, wrow,
+                       nw, gram, nz_out, sc_out, host, st);
 }

@@ -89,6 +89,12 @@ SIGNATURES = {
     "bsc_round_select_partials": [P, P, P, P, I, P, P, P, P, I, P, I, P, L, I],
     "bsc_round_after_gather": [P, P, I, L, I, P, P, I, I, I, P],
     "bsc_ring_pick": [P, I, P, P, P],
+    "bsc_rccl_load": [C.c_char_p],
+    "bsc_rccl_unique_id": [P],
+    "bsc_round_comm_init": [P, P, I, I, P, I, D],
+    "bsc_round_bind_multi": [P, P, P, L, P, I, P, P, P, I, I, I, P, P, L],
+    "bsc_round_agg_multi": [P, P, P, P, I, P, P, P, P, I, P, I, L, P, I, I, I, I, P],
+    "bsc_round_vg_exchange": [P, I, L, L, L, P, I, I, P, P, P, I, I, I, I, P, I, P, P, P, P, P],
     # gather.hip
     "bsc_vg_limits": [P],
     "bsc_vg_pack": [P, L, L, L, P, I, I, P, P, P, I, P],

@@ -553,6 +553,96 @@ class NativeSecAgg:
             raise RuntimeError(f"bsc_round_after_gather failed ({err})")
         return self.W_ring[o[0]], o[1]
 
+    # ---------------------------------------------------------------- several ranks, native collectives
+    native_comm = False   # the round's collectives run in the fused calls (comm_init)
+
+    def comm_init(self, comm, timeout_s: float = 0.0) -> bool:
+        """The round's own collectives (kernels/round.hip bsc_round_comm_init): RCCL ranks share ONE communicator
+        of their own -- rank 0's unique id travels over the job's process group once -- on the Comm's comm stream
+        (every collective of the round, native or torch's, then runs there in issue order); a rank emulating rank 0
+        of a larger job fills the other ranks' slots by device copies.  False: gloo (the round's collectives stay
+        torch's)."""
+        if comm.world < 2 or self.native_comm:
+            return self.native_comm
+        import ctypes
+        import os
+
+        if comm.emulating:
+            _check(hip().bsc_round_comm_init(self.ctx, None, comm.world, 0, None, 1, 0.0), "round_comm_init")
+        elif comm.backend == "nccl":
+            import torch.distributed as dist
+
+            # the RCCL instance torch runs (its librccl), not a second copy of the library
+            _check(hip().bsc_rccl_load(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so").encode()),
+                   "rccl_load")
+            uid = [None]
+            if comm.rank == 0:
+                buf = (ctypes.c_ubyte * 128)()
+                _check(hip().bsc_rccl_unique_id(buf), "rccl_unique_id")
+                uid = [bytes(buf)]
+            dist.broadcast_object_list(uid, src=0)
+            ub = (ctypes.c_ubyte * 128).from_buffer_copy(uid[0])
+            cs = comm._comm_stream()
+            torch.cuda.synchronize(self.eng.device)
+            _check(hip().bsc_round_comm_init(self.ctx, ub, comm.world, comm.rank, cs.cuda_stream, 0,
+                                             float(timeout_s or 0.0)), "round_comm_init")
+        else:
+            return False
+        self.native_comm = True
+        self.crank, self.cworld = comm.rank, comm.world
+        return True
+
+    def bind_multi(self, maxlocal: int, num_nodes: int, vg=None) -> None:
+        """The fused multi-rank calls' resident buffers: the aggregation's packed rows (gather_buffers), and with the
+        packed verification row vg (ops/gather.py) the next noise-aware Gram's inputs -- this rank's padded delta
+        rows, the gathered [world maxlocal, d] deltas, the split-K partials of its tile pairs."""
+        from . import ml as K
+
+        assert self.native_comm and self.world == self.cworld, "comm_init() and gather_buffers() first"
+        eng, dev, d = self.eng, self.eng.device, self.eng.d
+        U1 = self.cworld * maxlocal
+        p0, p1, chunk, _ = K.gram_split(U1 + num_nodes, self.crank, self.cworld)
+        nsplit = (d + 511) // 512
+        self.multi = {"pad": torch.zeros((maxlocal, d), dtype=torch.float32, device=dev),
+                      "X": torch.empty((U1, d), dtype=torch.float32, device=dev),
+                      "part": torch.empty((nsplit, max(1, p1 - p0), 256), dtype=torch.float64, device=dev),
+                      "U1": U1, "U": U1 + num_nodes, "split": (self.crank, chunk, p0, p1), "vg": vg}
+        mu = self.multi
+        _check(hip().bsc_round_bind_multi(self.ctx, self.send.data_ptr(), self.recv.data_ptr(), self.row_bytes,
+                                          self.h_clock.data_ptr(), maxlocal, _ptr(mu["pad"]), _ptr(mu["X"]),
+                                          _ptr(mu["part"]), U1, p0, p1,
+                                          vg.recv[0].data_ptr() if vg is not None else None,
+                                          vg.recv[1].data_ptr() if vg is not None else None,
+                                          vg.row_bytes if vg is not None else 0), "round_bind_multi")
+        torch.cuda.synchronize(dev)
+
+    def agg_multi(self, node, amap, sp, early_slot: int, upload, layout: int, clock: int, W, audit: int, pre_it: int,
+                  audit_now: bool, gram: bool):
+        """Several ranks with native collectives, behind the committee's selection in ONE call: partial sums, the
+        aggregation's all_gather, totals + recovery + read-back + the next pre-step + the audit and (gram) the next
+        noise-aware Gram's deltas gather and tile pairs.  Returns (W_new, pre-step slot or -1)."""
+        n = len(sp.rows) if sp is not None else 0
+        o = self._out
+        err = hip().bsc_round_agg_multi(
+            self.ctx, _ptr(node) if n and node is not None else None, _ptr(amap) if n else None,
+            _ptr(sp.alive) if n else None, n, _ptr(sp.rows_t) if n else None, sp.ev.cuda_event if n else None,
+            _ptr(sp.pts) if n else None, _ptr(sp.ys) if n else None, int(early_slot), upload.cuda_stream, int(layout),
+            int(clock), _ptr(W), int(audit), int(pre_it), int(audit_now), int(gram), o)
+        if err != 0:
+            raise RuntimeError(f"bsc_round_agg_multi failed ({err})")
+        return self.W_ring[o[0]], o[1]
+
+    def multi_gram_pre(self, k: int, W, it: int, xrow) -> dict:
+        """The pre dict of slot k whose noise-aware Gram agg_multi queued (its tile pairs in this rank's slot of
+        iteration it's verification row; the packed exchange completes it)."""
+        out = self._pre_out(k, W, it)
+        mu = self.multi
+        rank, chunk, p0, p1 = mu["split"]
+        npairs = ((mu["U"] + 15) // 16) * ((mu["U"] + 15) // 16 + 1) // 2
+        out["gram"] = {"gram": None, "U1": mu["U1"], "U": mu["U"], "split": (rank, chunk, npairs), "packed": True,
+                       "keep": (mu["X"], mu["part"]), "xrow": xrow, "it": it, "ev": self.slots[k]["ev"][3]}
+        return out
+
     SPEC_SLOTS = 3
     ROWARG_MAX = 248   # kernels/msm.hip: speculative rows that travel in the MSM kernel's arguments
 

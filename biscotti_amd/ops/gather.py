@@ -48,6 +48,7 @@ class VerifyGather:
         self.sc = torch.empty((world * maxlocal, nn), dtype=torch.float32, device=dev)
         self.host = [torch.empty((num_nodes, pw), dtype=torch.int32, pin_memory=True) for _ in range(self.HOST_DEPTH)]
         self._h = 0
+        self.native = None   # NativeSecAgg with the round's own collectives (bsc_round_vg_exchange), else torch's
 
     @staticmethod
     def fits(maxlocal: int, nn: int, num_nodes: int) -> bool:
@@ -73,13 +74,21 @@ class VerifyGather:
         nz_c = np.ascontiguousarray(nz_np, np.int32).reshape(-1)
         sc_c = np.ascontiguousarray(sc_np, np.float32).reshape(-1)
         assert nz_c.size == ml * nn and sc_c.size == ml * nn
-        _check(hip().bsc_vg_pack(row.data_ptr(), self.commit_off, self.nz_off, self.sc_off, commits.data_ptr(), ml,
-                                 self.pw, sr, nz_c.ctypes.data, sc_c.ctypes.data, ml * nn, S.raw()), "vg_pack")
-        self.comm.all_gather_into(buf, row)
         host = self.host[self._h]
         self._h = (self._h + 1) % self.HOST_DEPTH
         nw = len(worker_rows)
         wr = (ctypes.c_int * max(1, nw))(*worker_rows)
+        na = self.native
+        if na is not None:
+            # pack, the all_gather in place and unpack in ONE native call (the round's own communicator)
+            _check(hip().bsc_round_vg_exchange(na.ctx, it, self.commit_off, self.nz_off, self.sc_off, commits.data_ptr(),
+                                               ml, self.pw, sr, nz_c.ctypes.data, sc_c.ctypes.data, ml * nn, self.chunk,
+                                               self.npairs, nn, wr, nw, self.gram.data_ptr(), self.nz.data_ptr(),
+                                               self.sc.data_ptr(), host.data_ptr(), S.raw()), "round_vg_exchange")
+            return self.gram[: self.npairs], self.nz, self.sc, host[:nw], S.record()
+        _check(hip().bsc_vg_pack(row.data_ptr(), self.commit_off, self.nz_off, self.sc_off, commits.data_ptr(), ml,
+                                 self.pw, sr, nz_c.ctypes.data, sc_c.ctypes.data, ml * nn, S.raw()), "vg_pack")
+        self.comm.all_gather_into(buf, row)
         _check(hip().bsc_vg_unpack(buf.data_ptr(), self.row_bytes, self.chunk, self.npairs, self.commit_off,
                                    self.nz_off, self.sc_off, ml, self.pw, nn, self.comm.world, wr, nw,
                                    self.gram.data_ptr(), self.nz.data_ptr(), self.sc.data_ptr(), host.data_ptr(),

@@ -75,7 +75,7 @@ class Comm:
             if os.environ.get("BISCOTTI_RCCL_SHARED_DEVICE") == "1":
                 # rehearsal of the RCCL path with several ranks on one GPU: a distinct host id per rank
                 # makes RCCL connect them through its socket transport instead of refusing the
-                # duplicate device (test_gpu_multirank.py, scripts/gpu_rccl_bench.sh)
+                # duplicate device (test_gpu_multirank.py, scripts/archive/gpu_rccl_bench.sh)
                 os.environ.setdefault("NCCL_HOSTID", f"biscotti-rank{rank}")
                 os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
                 os.environ.setdefault("NCCL_IB_DISABLE", "1")

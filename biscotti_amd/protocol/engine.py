@@ -154,7 +154,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             # wave priority classes (kernels/wave_prio.h): one rank drives its GPU alone; with several ranks the
             # collectives' kernels must not queue behind prio-2 share MSMs
             B.set_wave_priorities(self.comm.world == 1 or cfg.has("wave_prio_multi"))
-            S.set_spin(5e-3 if self.comm.world == 1 and not cfg.has("short_spin") else 2e-4)
+            # host waits spin up to 5 ms before sleeping when this rank has its GPU (and a core of the quota) to
+            # itself -- one rank, or one rank per GPU; ranks sharing a GPU (rehearsals) spin 200 us
+            S.set_spin(5e-3 if not self._shared_device and not cfg.has("short_spin") else 2e-4)
             self._native = B.NativeSecAgg(self.crypto.eng, self.main_stream, self.side_stream, self.bg_stream,
                                           10.0 ** cfg.precision, witness=self.witness_stream)
             if self.comm.world > 1:
@@ -176,6 +178,16 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.noise_rows = None
         if cfg.noising and self.sigma > 0 and self.N * 100 * self.d * 4 <= (8 << 30):
             self.noise_rows = K.NoiseRows(self.N, self.d, cfg.seed, self.dev)
+        # several ranks with RCCL (or emulating rank 0): the round's collectives run inside the fused native calls on
+        # the round's own communicator (NativeSecAgg.comm_init); the next noise-aware Gram's deltas gather and tile
+        # pairs go with the aggregation's call when the packed verification row holds the layout (_multi_gram)
+        self._multi_gram = False
+        if self._native is not None and self.comm.world > 1 and self._native.comm_init(self.comm, cfg.comm_timeout_s):
+            vg = self._vgather()
+            if vg is not None:
+                vg.native = self._native
+            self._native.bind_multi(self.maxlocal, self.N, vg)
+            self._multi_gram = vg is not None and self._noise_krum()
         self.vrf_dev = None
         if self.gpu and cfg.vrf_device:
             from ..ops.vrf import DeviceVrfProver
@@ -609,7 +621,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         identical): there the front's two collectives move ahead of the round's host work, and the device, not
         the host, is no longer the limit (docs/PERF.md, round 5)."""
         cfg = self.cfg
-        return (self.gpu and self.comm.world == 1 and self._pipelined() and cfg.secure_agg and cfg.verification
+        return (self.gpu and (self.comm.world == 1 or self._multi_gram) and self._pipelined() and cfg.secure_agg
+                and cfg.verification
                 and cfg.defense == "KRUM" and self._noise_krum() and not cfg.has("no_early_front")
                 and cfg.churn == 0 and cfg.churn_kill_per_min == 0 and not self._partitions
                 and cfg.fail_point()[0] < 0 and not cfg.phase_log and not cfg.phase_sync and not cfg.trace_file)

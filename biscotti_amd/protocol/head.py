@@ -268,7 +268,8 @@ class RoundHeadMixin:
             gs = self.gram_stream
             with S.use(gs):
                 cnt = K._tile_counters(self.dev, 1024)
-            nk = self._noise_krum() and self.comm.world == 1
+            # the noise table drives the pre-step's own Gram (one rank) or the multi-rank call's (_multi_gram)
+            nk = self._noise_krum() and (self.comm.world == 1 or self._multi_gram)
             na.bind_task(self.task, gs, self.noise_rows.table if nk else None, cnt)
             if nk:
                 na.set_nn_table(self._noise_gram_table())

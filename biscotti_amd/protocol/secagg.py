@@ -178,7 +178,17 @@ class SecAggMixin:
             readback, clock = na.readback(), None
             if pre is not None:
                 pre = self._finish_pre(pre, nxt)
-        else:
+        elif na.native_comm:
+            # one call: partials, the all_gather, recovery, the next pre-step and its Gram's gather + tile pairs
+            gram = self._multi_gram and pre_it >= 0
+            W_new, k = na.agg_multi(sel, amap, sp, early, self.upload_stream, lid, now, self.W, audit, pre_it,
+                                    run_audit, gram)
+            pre = None
+            if k >= 0:
+                pre = na.multi_gram_pre(k, W_new, nxt, self.flat) if gram else \
+                    self._finish_pre(na._pre_out(k, W_new, nxt), nxt)
+            readback, clock = na.readback(clocks=True), True
+        else:   # gloo ranks on GPUs (tests): the collective is torch's, between the two native calls
             na.select_partials(sel, amap, sp, early, self.upload_stream, lid, now, audit)
             comm.all_gather_into(na.recv, na.send)
             W_new, k = na.after_gather(lid, self.W, audit, pre_it, audit_now=run_audit)
