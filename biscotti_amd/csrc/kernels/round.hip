@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <thread>
 
@@ -852,15 +853,26 @@ extern "C" int bsc_round_comm_init(void* ctx, const unsigned char* uid, int worl
   return 0;
 }
 
+// the emulated all_gather: every one of `world` rows of dst [world][n] (32-bit words) gets src [n] -- ONE launch,
+// as a real all_gather is one RCCL call (in place, src = dst's row 0, row 0 is rewritten with its own words)
+__global__ void __launch_bounds__(256) k_replicate_rows(const uint32_t* src, uint32_t* dst, long long n, int world) {
+  const long long total = n * world;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x)
+    dst[i] = src[i % n];
+}
+
 // all_gather of `bytes` per rank from `send` into recv [world][bytes] (in place when send is this rank's slot of
 // recv): the comm stream waits for the producer stream, the consumer stream for the collective
 static int round_all_gather(RoundCtx* c, const void* send, void* recv, size_t bytes, hipStream_t prod,
                             hipStream_t cons) {
   unsigned char* r = (unsigned char*)recv;
   if (c->emulate) {   // rank 0 alone: every slot holds rank 0's contribution (same shapes, no transport)
-    if (send != r) RC_CHECK(hipMemcpyAsync(r, send, bytes, hipMemcpyDeviceToDevice, prod));
-    for (int k = 1; k < c->cworld; ++k)
-      RC_CHECK(hipMemcpyAsync(r + (size_t)k * bytes, r, bytes, hipMemcpyDeviceToDevice, prod));
+    if (bytes % 4 != 0) return -31;
+    const long long n = (long long)(bytes / 4), total = n * c->cworld;
+    const int blocks = (int)std::min<long long>((total + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_replicate_rows, dim3(blocks), dim3(256), 0, prod, (const uint32_t*)send, (uint32_t*)r, n,
+                       c->cworld);
+    RC_CHECK(hipGetLastError());
     if (cons != prod) {
       RC_CHECK(hipEventRecord(c->ev_c1, prod));
       RC_CHECK(hipStreamWaitEvent(cons, c->ev_c1, 0));

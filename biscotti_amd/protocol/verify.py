@@ -287,7 +287,8 @@ class VerifyMixin:
         g_commit = got[0].reshape(-1, pw)
         rows = g_commit.index_select(0, h2d([self.flat[w] for w in head["workers"]], torch.long, self.dev))
         if self.gpu:
-            host = pinned("commit_gather", rows.shape, rows.dtype)
+            # (depth 4: the deferred signing reads these rows in the next round's VRF wait, commit_of.jac)
+            host = pinned("commit_gather", rows.shape, rows.dtype, depth=4)
             d2h_into(host, rows.contiguous())
             head["commit_gather"] = (host, S.record())
         else:
@@ -340,6 +341,10 @@ class VerifyMixin:
                         S.host_wait(ev)
                     return self.crypto.marshal_rows(host)
                 commit_of.fill_lazy(load, {w: i for i, w in enumerate(workers)})
+                if self.gpu and ev is not None:
+                    # the gathered rows are device-layout Jacobian points: the block build and the signing marshal
+                    # only the rows they use, natively (as with one rank's pre-step commitments)
+                    commit_of.jac = (host, ev)
             elif workers:   # every worker's commitment: one batched marshal of the gathered rows
                 sel = h2d([self.flat[w] for w in workers], torch.long, self.dev)
                 commit_of.fill(self.crypto.marshal_rows(g_commit.index_select(0, sel)),

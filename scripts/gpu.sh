@@ -18,6 +18,7 @@
 #   prof                  rocprofv3 --kernel-trace --stats of a driver-style run (OUT/prof/)
 #   hosttl                the host timeline of 4 steady rounds (scripts/host_timeline.py)
 #   mrprof:N              cProfile of rank 0 of an N-rank job (scripts/prof_rounds.py --emulate-world N)
+#   kt:TAG:A+B+C          rocprofv3 kernel + memory-copy trace of bench.py A B C (OUT/kt_TAG/; scripts/kt_timeline.py)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$PWD}"; cd "$R"
 O="gpurun_out/$1"; shift; mkdir -p "$O"
@@ -97,6 +98,11 @@ for step in "$@"; do
       timeout -k 10 300 python scripts/prof_rounds.py --emulate-world "$n" > "$O/mrprof_$n.txt" 2>&1 \
         || { echo "MRPROF FAILED"; tail -20 "$O/mrprof_$n.txt"; exit 1; }
       head -40 "$O/mrprof_$n.txt" ;;
+    kt:*)
+      s="${step#kt:}"; tag="${s%%:*}"; IFS='+' read -ra args <<< "${s#*:}"
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$O/kt_$tag" -o run -- python bench.py "${args[@]}" \
+        > "$O/kt_$tag.txt" 2>&1 || { echo "KT FAILED"; tail -20 "$O/kt_$tag.txt"; exit 1; }
+      summ "$O/kt_$tag.txt" "kt_$tag" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
