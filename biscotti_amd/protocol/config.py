@@ -106,6 +106,8 @@ class RunConfig:
     #                      path (tests and measurements of that path): the chain must not change
     #   wave_prio_multi    GPU: the round kernels' wave priority classes (kernels/wave_prio.h) also with several
     #                      ranks (default: one rank only; the collectives' kernels run at the default class)
+    #   multi_early_front  GPU, several ranks with the native collectives: the next round's front at the end of the
+    #                      previous round as with one rank (engine._early_front_ok; measured slower there)
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
@@ -114,7 +116,7 @@ class RunConfig:
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
                                   "noise_gram_each_round", "spec_tight", "no_early_front",
-                                  "wave_prio_multi")
+                                  "wave_prio_multi", "multi_early_front")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

@@ -617,12 +617,13 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         noise-aware Multi-Krum path, no churn / partitions / fault injection (whose next round may differ from
         the head built here) and no per-round phase records (trace, phase log, phase sync: their phases would
         move to the previous round).  The no_early_front ablation turns it off; the chain is the same.  With
-        several ranks it measured slower (emulated rank 0 of 8: 0.99-1.02 vs 0.93-0.96 ms; the chains stay
-        identical): there the front's two collectives move ahead of the round's host work, and the device, not
-        the host, is no longer the limit (docs/PERF.md, round 5)."""
+        several ranks it runs with the native collectives under the multi_early_front ablation only: same-box A/B
+        of emulated rank 0, 3 runs each (docs/PERF.md, round 6), 1.214 / 1.107 / 0.994 ms with it against 1.123 /
+        1.024 / 0.877 without at N = 2 / 4 / 8 -- the front's collectives and Krum wait on the device behind the
+        previous round's tail instead of the host work they used to overlap."""
         cfg = self.cfg
-        return (self.gpu and (self.comm.world == 1 or self._multi_gram) and self._pipelined() and cfg.secure_agg
-                and cfg.verification
+        return (self.gpu and (self.comm.world == 1 or (self._multi_gram and cfg.has("multi_early_front")))
+                and self._pipelined() and cfg.secure_agg and cfg.verification
                 and cfg.defense == "KRUM" and self._noise_krum() and not cfg.has("no_early_front")
                 and cfg.churn == 0 and cfg.churn_kill_per_min == 0 and not self._partitions
                 and cfg.fail_point()[0] < 0 and not cfg.phase_log and not cfg.phase_sync and not cfg.trace_file)

@@ -110,8 +110,8 @@ def test_gpu_two_ranks_over_rccl_match_single_process():
     assert multi[0] == single
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_gpu_one_rank_per_gpu_fast_path_over_rccl(world):
+@pytest.mark.parametrize("world,extra", [(2, ""), (4, ""), (2, ",multi_early_front"), (4, ",multi_early_front")])
+def test_gpu_one_rank_per_gpu_fast_path_over_rccl(world, extra):
     """The configuration an 8-GPU node runs (one rank per GPU): the speculative next-round head forced on
     (ablation spec_head_shared; it is off by default only because these ranks share cuda:0), the native pre-step
     (local step + chunk commitments), the Gram's tiles split across ranks, the native multi-rank
@@ -121,13 +121,15 @@ def test_gpu_one_rank_per_gpu_fast_path_over_rccl(world):
     kw = dict(num_nodes=20, dataset="mnist", seed=13, deterministic_time=True, max_iterations=100,
               ablation="spec_head_shared")
     single, s1 = _run_stats(1, kw, rounds)[0]
-    out = _run_stats(world, kw, rounds, backend="nccl")
+    out = _run_stats(world, dict(kw, ablation=kw["ablation"] + extra), rounds, backend="nccl")
     for r in range(world):
         hashes, st = out[r]
         assert hashes == single, f"rank {r} chain differs"
         for k in ("pre_steps", "spec_head", "device_aggregations", "early_vrf"):
             assert st.get(k, 0) >= rounds - 1, (r, k, st)
         assert st.get("spec_misses", 0) == 0 and st.get("audit_failures", 0) == 0, st
+        if extra:   # the next round's front started at the end of the previous one on every rank
+            assert st.get("early_fronts", 0) >= rounds - 2, (r, st)
     assert s1.get("spec_head", 0) >= rounds - 1, s1
 
 
