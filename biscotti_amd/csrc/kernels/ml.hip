@@ -1372,6 +1372,31 @@ extern "C" int bsc_sum_rows_i64(const long long* ys, int R, long long C, const i
   return (int)hipGetLastError();
 }
 
+// the same sums with one more int64 after them: out[C] = tail (the multi-rank send row's clock, kernels/round.hip)
+// -- written by the sums' own launch instead of two memset launches behind it on the critical path; R = 0: zeros
+extern "C" __global__ void __launch_bounds__(256) k_sum_rows_i64_tail(const long long* __restrict__ ys, int R,
+                                                                     long long C, const int* __restrict__ mask,
+                                                                     long long* __restrict__ out, long long tail) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > C) return;
+  if (c == C) {
+    out[C] = tail;
+    return;
+  }
+  long long s = 0;
+  for (int r = 0; r < R; ++r)
+    if (mask == nullptr || mask[r]) s += ys[(size_t)r * C + c];
+  out[c] = s;
+}
+
+extern "C" int bsc_sum_rows_i64_tail(const long long* ys, int R, long long C, const int* mask, long long* out,
+                                     long long tail, void* stream) {
+  if (C < 0 || R < 0 || (R > 0 && ys == nullptr)) return -1;
+  hipLaunchKernelGGL(k_sum_rows_i64_tail, dim3((unsigned)((C + 1 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     ys, R, C, mask, out, tail);
+  return (int)hipGetLastError();
+}
+
 extern "C" int bsc_softmax_step_ones(const float* X, const int* y, const long long* off, const int* ntrain,
                                      const int* pid, const double* W, int D_IN, int D_OUT, int B, int P,
                                      unsigned long long seed, int iteration, float max_norm, double qscale, float* delta,

@@ -44,6 +44,8 @@ extern "C" int bsc_chunk_check_h(const long long* coeffs, int d, int poly, const
                                  const uint32_t* csum, int nm, int nch, int* ok, int* h_ok, void* stream);
 extern "C" int bsc_sum_rows_i64(const long long* ys, int R, long long C, const int* rows, int nsel, const int* mask,
                                 long long* out, void* stream);
+extern "C" int bsc_sum_rows_i64_tail(const long long* ys, int R, long long C, const int* mask, long long* out,
+                                     long long tail, void* stream);
 extern "C" int bsc_sum_rows2_pos(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
                                  int ncols, const int* row_mask, uint32_t* out, void* stream);
 extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
@@ -141,6 +143,9 @@ struct RoundCtx {
   long long timeout_ns = 0;   // bsc_round_wait gives up (and aborts the communicator) after this; 0: never
   hipStream_t cstream = nullptr;
   hipEvent_t ev_c0 = nullptr, ev_c1 = nullptr;
+  hipStream_t aux = nullptr;        // bsc_round_agg_multi: the audit's commitment totals run here (its upload stream)
+  hipEvent_t ev_aux = nullptr;      // ... and the next gather into the same rows waits for them
+  bool aux_pending = false;
   // the multi-rank aggregation's resident buffers and the next Gram's inputs (bsc_round_bind_multi)
   struct Multi {
     int bound = 0;
@@ -239,6 +244,7 @@ extern "C" void bsc_round_destroy(void* ctx) {
   if (c->comm != nullptr && g_rccl.comm_destroy != nullptr) g_rccl.comm_destroy(c->comm);
   if (c->ev_c0 != nullptr) (void)hipEventDestroy(c->ev_c0);
   if (c->ev_c1 != nullptr) (void)hipEventDestroy(c->ev_c1);
+  if (c->ev_aux != nullptr) (void)hipEventDestroy(c->ev_aux);
   hipEventDestroy(c->ev_main);
   hipEventDestroy(c->ev_side);
   hipEventDestroy(c->ev_readback);
@@ -468,14 +474,13 @@ extern "C" int bsc_round_partials(void* ctx, const uint32_t* pts, int R, const l
       RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->wit));
       RC_CHECK(spec_mark_read(c, mask));
     }
-    RC_CHECK(bsc_sum_rows_i64(ys, R, (long long)nch * T, nullptr, R, mask, ys_slot, c->main));
-  } else {
-    RC_CHECK(hipMemsetAsync(ys_slot, 0, 8ull * nch * T, c->main));
-    if (audit != 0) RC_CHECK(hipMemsetAsync(cs_slot, 0, 96ull * nch, c->main));
+  } else if (audit != 0) {
+    RC_CHECK(hipMemsetAsync(cs_slot, 0, 96ull * nch, c->main));
   }
-  const unsigned long long u = (unsigned long long)clock;
-  RC_CHECK(hipMemsetD32Async((hipDeviceptr_t)clk, (int)(u & 0xffffffffull), 1, c->main));
-  RC_CHECK(hipMemsetD32Async((hipDeviceptr_t)(clk + 4), (int)(u >> 32), 1, c->main));
+  // the share-value sums (zeros without local rows) and the clock right behind them, in one launch
+  if ((long long*)clk != ys_slot + (long long)nch * T) return -1;
+  RC_CHECK(bsc_sum_rows_i64_tail(R > 0 ? ys : nullptr, R > 0 ? R : 0, (long long)nch * T, R > 0 ? mask : nullptr,
+                                 ys_slot, clock, c->main));
   if (R > 0 && audit != 0) RC_CHECK(hipStreamWaitEvent(c->main, c->ev_side, 0));
   return 0;
 }
@@ -489,9 +494,19 @@ extern "C" int bsc_round_combine(void* ctx, const unsigned char* recv, int world
   if (c == nullptr || world <= 0 || row_bytes % 96 != 0 || row_bytes < bsc_round_row_bytes(c->nch, c->T)) return -1;
   const int nch = c->nch, T = c->T;
   if (audit != 0) {
-    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv, (int)(row_bytes / 96), nullptr, world, nullptr, nch, nullptr, cs,
-                           c->main));
-    RC_CHECK(hipEventRecord(c->ev_side, c->main));   // bsc_round_audit waits for the sums through ev_side
+    // the audit's commitment totals over the ranks: beside the recovery (on the aux stream when the fused call
+    // names one) -- only the audit reads them; the next aggregation's gather waits for them (ev_aux)
+    hipStream_t st = c->aux != nullptr ? c->aux : c->main;
+    if (st != c->main) {
+      RC_CHECK(hipEventRecord(c->ev_main, c->main));
+      RC_CHECK(hipStreamWaitEvent(st, c->ev_main, 0));
+    }
+    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv, (int)(row_bytes / 96), nullptr, world, nullptr, nch, nullptr, cs, st));
+    RC_CHECK(hipEventRecord(c->ev_side, st));   // bsc_round_audit waits for the sums through ev_side
+    if (st != c->main && c->ev_aux != nullptr) {
+      RC_CHECK(hipEventRecord(c->ev_aux, st));
+      c->aux_pending = true;
+    }
   }
   RC_CHECK(bsc_recover_w_strided((const long long*)(recv + 96ll * nch), world, row_bytes / 8, nch, T, nullptr, ycols,
                                  xs, npts, A, basis, c->poly, shift, inv_lo, inv_hi, c->d, W, c->qscale, W_new, coeffs,
@@ -834,6 +849,7 @@ extern "C" int bsc_round_comm_init(void* ctx, const unsigned char* uid, int worl
   if (c->ev_c0 == nullptr) {
     RC_CHECK(hipEventCreateWithFlags(&c->ev_c0, hipEventDisableTiming));
     RC_CHECK(hipEventCreateWithFlags(&c->ev_c1, hipEventDisableTiming));
+    RC_CHECK(hipEventCreateWithFlags(&c->ev_aux, hipEventDisableTiming));
   }
   c->cworld = world;
   c->crank = rank;
@@ -955,9 +971,16 @@ extern "C" int bsc_round_agg_multi(void* ctx, const int* node, const int* amap, 
   if (c == nullptr || !c->m.bound || c->cworld < 2) return -1;
   RC_CHECK(bsc_round_select_partials(ctx, node, amap, alive, nspec, spec_rows, spec_ev, pts, ys, early_slot, upload,
                                      layout, c->m.send, clock, audit));
+  if (c->aux_pending) {   // the last aggregation's audit totals still read recv
+    RC_CHECK(hipStreamWaitEvent(c->main, c->ev_aux, 0));
+    c->aux_pending = false;
+  }
   RC_CHECK(round_all_gather(c, c->m.send, c->m.recv, (size_t)c->m.row_bytes, c->main, c->main));
-  RC_CHECK(bsc_round_after_gather(ctx, c->m.recv, c->cworld, c->m.row_bytes, layout, W, c->m.h_clock, audit, pre_it,
-                                  audit_now, out));
+  c->aux = (hipStream_t)upload;
+  const int e = bsc_round_after_gather(ctx, c->m.recv, c->cworld, c->m.row_bytes, layout, W, c->m.h_clock, audit,
+                                       pre_it, audit_now, out);
+  c->aux = nullptr;
+  RC_CHECK(e);
   if (out[1] >= 0 && gram) RC_CHECK(round_multi_gram(c, out[1], pre_it));
   return 0;
 }

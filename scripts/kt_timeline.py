@@ -2,14 +2,28 @@
 queue, start/end relative to the round's first kernel (the round boundary is k_recover_w, the exact
 recovery of W), and a per-kernel duration summary (first vs last quarter of the run).
 
-    python scripts/kt_timeline.py gpurun_out/kt/run_kernel_trace.csv [a b]"""
+    python scripts/kt_timeline.py gpurun_out/kt/run_kernel_trace.csv [a b]
+    python scripts/kt_timeline.py gpurun_out/kt/run_results.db [a b]     (rocprofv3's SQLite output)"""
 import collections
 import csv
 import sys
 
 
 def load(path):
-    rows = list(csv.DictReader(open(path)))
+    if path.endswith(".db"):   # rocprofv3's default rocpd (SQLite) output: its kernels view
+        import sqlite3
+
+        con = sqlite3.connect(path)
+        rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e, "Queue_Id": str(q), "Stream_Id": str(st)}
+                for n, s, e, q, st in con.execute("select name, start, end, queue_id, stream_id from kernels")]
+        try:   # blits and copies (--memory-copy-trace) as pseudo-kernels
+            rows += [{"Kernel_Name": f"copy_{k}", "Start_Timestamp": s, "End_Timestamp": e, "Queue_Id": "copy",
+                      "Stream_Id": str(st)}
+                     for k, s, e, st in con.execute("select name, start, end, stream_id from memory_copies")]
+        except sqlite3.Error:
+            pass
+    else:
+        rows = list(csv.DictReader(open(path)))
     for r in rows:
         r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         r["d"] = (r["e"] - r["s"]) / 1e3
