@@ -1256,8 +1256,12 @@ extern "C" __global__ void __launch_bounds__(256) k_recover_w(
     const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask, const int* ycols, const int* xs, int npts,
     const long long* A, const int* basis, int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi,
     int d, const double* W, double qscale, double* W_new, long long* coeffs, int* status, long long* agg_out,
-    double* h_W, int* h_status) {
+    double* h_W, int* h_status, long long* h_clock) {
   BSC_SET_PRIO(BSC_PRIO_CRITICAL);
+  // several ranks (h_clock): each rank's row carries its clock right after its share sums -- block 0 mirrors
+  // them to the host with the model (no strided read-back copy behind the kernel)
+  if (h_clock != nullptr && blockIdx.x == 0 && threadIdx.x < nrows)
+    h_clock[threadIdx.x] = ys[(size_t)threadIdx.x * rstride + (size_t)nch * T];
   __shared__ long long agg[RW_CPB][RW_MAXP];
   __shared__ __int128 cf[RW_CPB][RW_MAXC];
   __shared__ int ok[RW_CPB];
@@ -1634,18 +1638,29 @@ extern "C" int bsc_recover(const long long* ys, int nchunks, int npts, const int
 // rstride: int64 elements between consecutive rows of ys (nch * T for a dense [nrows][nch][T] tensor; the
 // packed row length when ys are the ranks' partials inside an all_gather buffer, round.hip)
 // h_W / h_status (nullable): pinned host mirrors of W_new / status written by the kernel (no read-back copies)
+// h_clock (nullable, several ranks): every row's int64 right after its nch x T sums, mirrored to pinned memory
+extern "C" int bsc_recover_w_clock(const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask,
+                                   const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
+                                   int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
+                                   const double* W, double qscale, double* W_new, long long* coeffs, int* status,
+                                   long long* agg_out, double* h_W, int* h_status, long long* h_clock, void* stream) {
+  if (nch <= 0) return 0;
+  if (npts > RW_MAXP || poly > RW_MAXC || poly > npts || shift < 0 || shift > 100 || nrows <= 0) return -1;
+  if (rstride < (long long)nch * T || (h_clock != nullptr && (nrows > 256 || rstride < (long long)nch * T + 1)))
+    return -1;
+  hipLaunchKernelGGL(k_recover_w, dim3(nblk(nch, RW_CPB)), dim3(256), 0, (hipStream_t)stream, ys, nrows, rstride, nch,
+                     T, mask, ycols, xs, npts, A, basis, poly, shift, inv_lo, inv_hi, d, W, qscale, W_new, coeffs,
+                     status, agg_out, h_W, h_status, h_clock);
+  return (int)hipGetLastError();
+}
+
 extern "C" int bsc_recover_w_strided(const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask,
                                      const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
                                      int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
                                      const double* W, double qscale, double* W_new, long long* coeffs, int* status,
                                      long long* agg_out, double* h_W, int* h_status, void* stream) {
-  if (nch <= 0) return 0;
-  if (npts > RW_MAXP || poly > RW_MAXC || poly > npts || shift < 0 || shift > 100 || nrows <= 0) return -1;
-  if (rstride < (long long)nch * T) return -1;
-  hipLaunchKernelGGL(k_recover_w, dim3(nblk(nch, RW_CPB)), dim3(256), 0, (hipStream_t)stream, ys, nrows, rstride, nch,
-                     T, mask, ycols, xs, npts, A, basis, poly, shift, inv_lo, inv_hi, d, W, qscale, W_new, coeffs,
-                     status, agg_out, h_W, h_status);
-  return (int)hipGetLastError();
+  return bsc_recover_w_clock(ys, nrows, rstride, nch, T, mask, ycols, xs, npts, A, basis, poly, shift, inv_lo, inv_hi, d,
+                             W, qscale, W_new, coeffs, status, agg_out, h_W, h_status, nullptr, stream);
 }
 
 extern "C" int bsc_recover_w(const long long* ys, int nrows, int nch, int T, const int* mask, const int* ycols,

@@ -38,6 +38,11 @@ extern "C" int bsc_recover_w_strided(const long long* ys, int nrows, long long r
                                      int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
                                      const double* W, double qscale, double* W_new, long long* coeffs, int* status,
                                      long long* agg_out, double* h_W, int* h_status, void* stream);
+extern "C" int bsc_recover_w_clock(const long long* ys, int nrows, long long rstride, int nch, int T, const int* mask,
+                                   const int* ycols, const int* xs, int npts, const long long* A, const int* basis,
+                                   int poly, int shift, unsigned long long inv_lo, unsigned long long inv_hi, int d,
+                                   const double* W, double qscale, double* W_new, long long* coeffs, int* status,
+                                   long long* agg_out, double* h_W, int* h_status, long long* h_clock, void* stream);
 extern "C" int bsc_segment_sum_h(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
                                  uint32_t* hout, void* stream);
 extern "C" int bsc_chunk_check_h(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,
@@ -508,11 +513,10 @@ extern "C" int bsc_round_combine(void* ctx, const unsigned char* recv, int world
       c->aux_pending = true;
     }
   }
-  RC_CHECK(bsc_recover_w_strided((const long long*)(recv + 96ll * nch), world, row_bytes / 8, nch, T, nullptr, ycols,
-                                 xs, npts, A, basis, c->poly, shift, inv_lo, inv_hi, c->d, W, c->qscale, W_new, coeffs,
-                                 status, agg, h_W, h_status, c->main));
-  RC_CHECK(hipMemcpy2DAsync(h_clock, sizeof(long long), recv + 96ll * nch + 8ll * nch * T, (size_t)row_bytes,
-                            sizeof(long long), (size_t)world, hipMemcpyDeviceToHost, c->main));
+  // (every rank's clock is mirrored to h_clock by the recovery itself: no strided read-back copy behind it)
+  RC_CHECK(bsc_recover_w_clock((const long long*)(recv + 96ll * nch), world, row_bytes / 8, nch, T, nullptr, ycols, xs,
+                               npts, A, basis, c->poly, shift, inv_lo, inv_hi, c->d, W, c->qscale, W_new, coeffs, status,
+                               agg, h_W, h_status, h_clock, c->main));
   RC_CHECK(hipEventRecord(c->ev_readback, c->main));
   return 0;
 }

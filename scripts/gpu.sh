@@ -19,6 +19,7 @@
 #   hosttl                the host timeline of 4 steady rounds (scripts/host_timeline.py)
 #   mrprof:N              cProfile of rank 0 of an N-rank job (scripts/prof_rounds.py --emulate-world N)
 #   kt:TAG:A+B+C          rocprofv3 kernel + memory-copy trace of bench.py A B C (OUT/kt_TAG/; scripts/kt_timeline.py)
+#   ht:TAG:A+B+C          rocprofv3 HIP API + kernel trace of bench.py A B C (OUT/ht_TAG/; scripts/hip_api_costs.py)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$PWD}"; cd "$R"
 O="gpurun_out/$1"; shift; mkdir -p "$O"
@@ -102,7 +103,18 @@ for step in "$@"; do
       s="${step#kt:}"; tag="${s%%:*}"; IFS='+' read -ra args <<< "${s#*:}"
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$O/kt_$tag" -o run -- python bench.py "${args[@]}" \
         > "$O/kt_$tag.txt" 2>&1 || { echo "KT FAILED"; tail -20 "$O/kt_$tag.txt"; exit 1; }
-      summ "$O/kt_$tag.txt" "kt_$tag" ;;
+      summ "$O/kt_$tag.txt" "kt_$tag"
+      # the timeline as text (the trace database is tens of MB: gpurun copies back at most 64 MiB)
+      python scripts/kt_timeline.py "$(ls "$O"/kt_$tag/*.db | head -1)" 30 34 > "$O/kt_${tag}_timeline.txt" 2>&1 || true
+      rm -rf "$O/kt_$tag" ;;
+    ht:*)
+      s="${step#ht:}"; tag="${s%%:*}"; IFS='+' read -ra args <<< "${s#*:}"
+      timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace -d "$O/ht_$tag" -o run -- python bench.py "${args[@]}" \
+        > "$O/ht_$tag.txt" 2>&1 || { echo "HT FAILED"; tail -20 "$O/ht_$tag.txt"; exit 1; }
+      summ "$O/ht_$tag.txt" "ht_$tag"
+      python scripts/hip_api_costs.py "$(ls "$O"/ht_$tag/*.db | head -1)" > "$O/ht_${tag}_api.txt" 2>&1 || true
+      python scripts/kt_timeline.py "$(ls "$O"/ht_$tag/*.db | head -1)" 30 34 > "$O/ht_${tag}_timeline.txt" 2>&1 || true
+      rm -rf "$O/ht_$tag" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,34 @@
+"""Host cost of the HIP runtime calls of a run, from a rocprofv3 --hip-trace database (rocpd SQLite):
+
+    python scripts/hip_api_costs.py gpurun_out/X/ht_TAG/run_results.db [rounds]
+
+Per API name on the busiest thread (the round's Python thread): calls, mean and total host microseconds, and the
+per-round share when the number of timed rounds is given."""
+import sqlite3
+import sys
+from collections import Counter, defaultdict
+
+
+def main(path: str, rounds: int = 0) -> None:
+    con = sqlite3.connect(path)
+    rows = list(con.execute("select tid, name, start, end from regions where category like '%HIP%'"))
+    if not rows:
+        print("no HIP API regions (run rocprofv3 with --hip-trace)")
+        return
+    main_tid = Counter(r[0] for r in rows).most_common(1)[0][0]
+    by = defaultdict(list)
+    for tid, name, s, e in rows:
+        if tid == main_tid:
+            by[name].append((e - s) / 1e3)
+    tot = sum(sum(v) for v in by.values())
+    print(f"thread {main_tid}: {sum(len(v) for v in by.values())} calls, {tot / 1e3:.1f} ms in HIP calls")
+    print(f"{'api':40s} {'calls':>7s} {'mean us':>8s} {'total ms':>9s}" + (f" {'us/round':>9s}" if rounds else ""))
+    for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1]))[:30]:
+        line = f"{name[:40]:40s} {len(v):7d} {sum(v) / len(v):8.2f} {sum(v) / 1e3:9.2f}"
+        if rounds:
+            line += f" {sum(v) / rounds:9.1f}"
+        print(line)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 0)
