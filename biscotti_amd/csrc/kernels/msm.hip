@@ -436,8 +436,9 @@ __device__ __forceinline__ jac aff_add_aff(const aff& p, const aff& q) {
 extern "C" __global__ void __launch_bounds__(64) k_chunk_check(const long long* coeffs, int d, int poly,
                                                               const uint32_t* tbl_pk, int B0, int NW,
                                                               const uint32_t* csum, int nm, int nch, int* ok,
-                                                              int* h_ok) {
-  BSC_SET_PRIO(BSC_PRIO_CRITICAL);
+                                                              int* h_ok, int low) {
+  if (low) BSC_SET_PRIO(BSC_PRIO_AHEAD);   // bsc_set_side_prio: below the speculative MSM
+  else BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ uint32_t sh[64 * 24];
   __shared__ int dig[16][9];      // signed digit of (coefficient j, window w); NW <= 9 (bsc_chunk_check)
   __shared__ uint32_t items[16 * 9];   // nonzero digits: table entry | sign bit
@@ -560,8 +561,11 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
 // Sum of a strided segment per group: out[g] = sum_{k<n} pts[(g*n + k)*stride + off], one block
 // per group, LDS tree.  Used for the full commitment = sum of chunk commitments.
 extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* pts, int n, int stride, int off,
-                                                               uint32_t* out, uint32_t* hout) {
-  BSC_SET_PRIO(BSC_PRIO_CRITICAL);   // the full commitments: the round's block build waits for them (a latency chain)
+                                                               uint32_t* out, uint32_t* hout, int low) {
+  // the full commitments: the round's block build waits for them (a latency chain) -- or, bsc_set_side_prio, below
+  // the speculative MSM they run beside (the next block build is a round away)
+  if (low) BSC_SET_PRIO(BSC_PRIO_AHEAD);
+  else BSC_SET_PRIO(BSC_PRIO_CRITICAL);
   __shared__ uint32_t sh[256 * 24];
   const int g = blockIdx.x;
   jac acc = jac_inf();
@@ -769,15 +773,24 @@ extern "C" int bsc_commit_rows(const long long* coeffs, int d, const int* rows, 
   hipLaunchKernelGGL(k_commit_rows, dim3(nrows * nslab), dim3(256), 0, (hipStream_t)stream, coeffs, d, rows, nrows,
                      tbl_pk, B0, NW, partial);
   hipLaunchKernelGGL(k_segment_sum, dim3(nrows), dim3(256), 0, (hipStream_t)stream, partial, nslab, 1, 0, out,
-                     (uint32_t*)nullptr);
+                     (uint32_t*)nullptr, 0);
   return (int)hipGetLastError();
+}
+
+// the round's side reductions (the pre-step's full-commitment sums, the aggregate audit) at the critical class
+// (default) or one below the speculative share MSM (1): experiments and A/Bs (RunConfig ablation side_prio_low)
+static int g_side_low = 0;
+extern "C" int bsc_set_side_prio(int low) {
+  g_side_low = low ? 1 : 0;
+  return 0;
 }
 
 // hout (nullable): pinned host mirror of out
 extern "C" int bsc_segment_sum_h(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
                                  uint32_t* hout, void* stream) {
   if (ngroups <= 0) return 0;
-  hipLaunchKernelGGL(k_segment_sum, dim3(ngroups), dim3(256), 0, (hipStream_t)stream, pts, n, stride, off, out, hout);
+  hipLaunchKernelGGL(k_segment_sum, dim3(ngroups), dim3(256), 0, (hipStream_t)stream, pts, n, stride, off, out, hout,
+                     g_side_low);
   return (int)hipGetLastError();
 }
 extern "C" int bsc_segment_sum(const uint32_t* pts, int ngroups, int n, int stride, int off, uint32_t* out,
@@ -792,7 +805,7 @@ extern "C" int bsc_chunk_check_h(const long long* coeffs, int d, int poly, const
   if (poly < 1 || poly > 16 || nm > 64 || B0 < 8 || B0 > 20 || B0 + 8 * (NW - 1) < 65 || NW > 9) return -1;
   if ((long long)nch * poly < d || (long long)(nch - 1) * poly >= d) return -1;
   hipLaunchKernelGGL(k_chunk_check, dim3(nch), dim3(64), 0, (hipStream_t)stream, coeffs, d, poly, tbl_pk, B0, NW,
-                     csum, nm, nch, ok, h_ok);
+                     csum, nm, nch, ok, h_ok, g_side_low);
   return (int)hipGetLastError();
 }
 extern "C" int bsc_chunk_check(const long long* coeffs, int d, int poly, const uint32_t* tbl_pk, int B0, int NW,

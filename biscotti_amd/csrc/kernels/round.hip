@@ -148,9 +148,6 @@ struct RoundCtx {
   long long timeout_ns = 0;   // bsc_round_wait gives up (and aborts the communicator) after this; 0: never
   hipStream_t cstream = nullptr;
   hipEvent_t ev_c0 = nullptr, ev_c1 = nullptr;
-  hipStream_t aux = nullptr;        // bsc_round_agg_multi: the audit's commitment totals run here (its upload stream)
-  hipEvent_t ev_aux = nullptr;      // ... and the next gather into the same rows waits for them
-  bool aux_pending = false;
   // the multi-rank aggregation's resident buffers and the next Gram's inputs (bsc_round_bind_multi)
   struct Multi {
     int bound = 0;
@@ -249,7 +246,6 @@ extern "C" void bsc_round_destroy(void* ctx) {
   if (c->comm != nullptr && g_rccl.comm_destroy != nullptr) g_rccl.comm_destroy(c->comm);
   if (c->ev_c0 != nullptr) (void)hipEventDestroy(c->ev_c0);
   if (c->ev_c1 != nullptr) (void)hipEventDestroy(c->ev_c1);
-  if (c->ev_aux != nullptr) (void)hipEventDestroy(c->ev_aux);
   hipEventDestroy(c->ev_main);
   hipEventDestroy(c->ev_side);
   hipEventDestroy(c->ev_readback);
@@ -442,6 +438,8 @@ extern "C" int bsc_round_prestep(void* ctx, void* gram_stream, const float* X, c
 // so the gathered buffer is at once a [world][row_bytes / 96][24] point array whose first nch columns are the
 // ranks' chunk-commitment partial sums (bsc_sum_rows2 sums them) and a strided [world][nch][T] share-sum
 // array (k_recover_w with a row stride sums and recovers).  No repacking on either side of the collective.
+// (The native path, bsc_round_agg_multi, gathers the same send row in two pieces -- [ys | clock] for the recovery
+// first, [cs] for the audit behind the early commitment sums -- into recv = [world][cs] + [world][ys | clock].)
 //
 // bsc_round_partials: this rank's partials of its kept rows, written straight into its send row -- the
 //   miners' share-value sums (main), the chunk-commitment sums (side, or already queued on another stream by
@@ -457,9 +455,20 @@ extern "C" int bsc_round_row_bytes(int nch, int T) {
   return (int)((raw + 95) / 96 * 96);
 }
 
+static int partials_impl(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask, const int* ccols,
+                         const int* wcols, int nwc, uint32_t* ws, unsigned char* send, long long clock, int audit,
+                         int wait_cs);
+
 extern "C" int bsc_round_partials(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask,
                                   const int* ccols, const int* wcols, int nwc, uint32_t* ws, unsigned char* send,
                                   long long clock, int audit) {
+  return partials_impl(ctx, pts, R, ys, mask, ccols, wcols, nwc, ws, send, clock, audit, 1);
+}
+
+// wait_cs = 0: main does not wait for the commitment partials (the native path gathers them separately)
+static int partials_impl(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask, const int* ccols,
+                         const int* wcols, int nwc, uint32_t* ws, unsigned char* send, long long clock, int audit,
+                         int wait_cs) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || R < 0) return -1;
   const int nch = c->nch, T = c->T;
@@ -486,7 +495,7 @@ extern "C" int bsc_round_partials(void* ctx, const uint32_t* pts, int R, const l
   if ((long long*)clk != ys_slot + (long long)nch * T) return -1;
   RC_CHECK(bsc_sum_rows_i64_tail(R > 0 ? ys : nullptr, R > 0 ? R : 0, (long long)nch * T, R > 0 ? mask : nullptr,
                                  ys_slot, clock, c->main));
-  if (R > 0 && audit != 0) RC_CHECK(hipStreamWaitEvent(c->main, c->ev_side, 0));
+  if (R > 0 && audit != 0 && wait_cs) RC_CHECK(hipStreamWaitEvent(c->main, c->ev_side, 0));
   return 0;
 }
 
@@ -499,19 +508,9 @@ extern "C" int bsc_round_combine(void* ctx, const unsigned char* recv, int world
   if (c == nullptr || world <= 0 || row_bytes % 96 != 0 || row_bytes < bsc_round_row_bytes(c->nch, c->T)) return -1;
   const int nch = c->nch, T = c->T;
   if (audit != 0) {
-    // the audit's commitment totals over the ranks: beside the recovery (on the aux stream when the fused call
-    // names one) -- only the audit reads them; the next aggregation's gather waits for them (ev_aux)
-    hipStream_t st = c->aux != nullptr ? c->aux : c->main;
-    if (st != c->main) {
-      RC_CHECK(hipEventRecord(c->ev_main, c->main));
-      RC_CHECK(hipStreamWaitEvent(st, c->ev_main, 0));
-    }
-    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv, (int)(row_bytes / 96), nullptr, world, nullptr, nch, nullptr, cs, st));
-    RC_CHECK(hipEventRecord(c->ev_side, st));   // bsc_round_audit waits for the sums through ev_side
-    if (st != c->main && c->ev_aux != nullptr) {
-      RC_CHECK(hipEventRecord(c->ev_aux, st));
-      c->aux_pending = true;
-    }
+    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv, (int)(row_bytes / 96), nullptr, world, nullptr, nch, nullptr, cs,
+                           c->main));
+    RC_CHECK(hipEventRecord(c->ev_side, c->main));   // bsc_round_audit waits for the sums through ev_side
   }
   // (every rank's clock is mirrored to h_clock by the recovery itself: no strided read-back copy behind it)
   RC_CHECK(bsc_recover_w_clock((const long long*)(recv + 96ll * nch), world, row_bytes / 8, nch, T, nullptr, ycols, xs,
@@ -729,17 +728,26 @@ extern "C" int bsc_round_after_select(void* ctx, const int* node, const int* ama
 
 // Several ranks, before the aggregation's all_gather: flags, early audit sums and this rank's partials into
 // the send row (nspec = 0: no local rows).
-extern "C" int bsc_round_select_partials(void* ctx, const int* node, const int* amap, int* alive, int nspec,
-                                         const int* spec_rows, void* spec_ev, const uint32_t* pts, const long long* ys,
-                                         int early_slot, void* upload, int layout, unsigned char* send, long long clock,
-                                         int audit) {
+static int select_partials_impl(void* ctx, const int* node, const int* amap, int* alive, int nspec,
+                                 const int* spec_rows, void* spec_ev, const uint32_t* pts, const long long* ys,
+                                 int early_slot, void* upload, int layout, unsigned char* send, long long clock, int audit,
+                                 int wait_cs) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || layout < 0 || layout >= c->nlayouts) return -1;
   const Layout& L = c->layouts[layout];
   RC_CHECK(select_head(c, node, amap, alive, nspec, spec_rows, nspec > 0 ? spec_ev : nullptr,
                        audit == 2 && nspec > 0 ? early_slot : -1, upload, (uint32_t*)send));
-  return bsc_round_partials(ctx, nspec > 0 ? pts : nullptr, nspec, nspec > 0 ? ys : nullptr, nspec > 0 ? alive : nullptr,
-                            L.ccols, L.wcols, nspec > 0 ? L.nwc : 0, L.ws, send, clock, nspec > 0 ? audit : (audit ? 1 : 0));
+  return partials_impl(ctx, nspec > 0 ? pts : nullptr, nspec, nspec > 0 ? ys : nullptr, nspec > 0 ? alive : nullptr,
+                       L.ccols, L.wcols, nspec > 0 ? L.nwc : 0, L.ws, send, clock, nspec > 0 ? audit : (audit ? 1 : 0),
+                       wait_cs);
+}
+
+extern "C" int bsc_round_select_partials(void* ctx, const int* node, const int* amap, int* alive, int nspec,
+                                         const int* spec_rows, void* spec_ev, const uint32_t* pts, const long long* ys,
+                                         int early_slot, void* upload, int layout, unsigned char* send, long long clock,
+                                         int audit) {
+  return select_partials_impl(ctx, node, amap, alive, nspec, spec_rows, spec_ev, pts, ys, early_slot, upload, layout,
+                              send, clock, audit, 1);
 }
 
 // Several ranks, behind the all_gather into recv: totals + recovery + read-back (clocks included), the next
@@ -853,7 +861,6 @@ extern "C" int bsc_round_comm_init(void* ctx, const unsigned char* uid, int worl
   if (c->ev_c0 == nullptr) {
     RC_CHECK(hipEventCreateWithFlags(&c->ev_c0, hipEventDisableTiming));
     RC_CHECK(hipEventCreateWithFlags(&c->ev_c1, hipEventDisableTiming));
-    RC_CHECK(hipEventCreateWithFlags(&c->ev_aux, hipEventDisableTiming));
   }
   c->cworld = world;
   c->crank = rank;
@@ -972,20 +979,43 @@ extern "C" int bsc_round_agg_multi(void* ctx, const int* node, const int* amap, 
                                    int early_slot, void* upload, int layout, long long clock, const double* W,
                                    int audit, int pre_it, int audit_now, int gram, int* out) {
   RoundCtx* c = (RoundCtx*)ctx;
-  if (c == nullptr || !c->m.bound || c->cworld < 2) return -1;
-  RC_CHECK(bsc_round_select_partials(ctx, node, amap, alive, nspec, spec_rows, spec_ev, pts, ys, early_slot, upload,
-                                     layout, c->m.send, clock, audit));
-  if (c->aux_pending) {   // the last aggregation's audit totals still read recv
-    RC_CHECK(hipStreamWaitEvent(c->main, c->ev_aux, 0));
-    c->aux_pending = false;
+  if (c == nullptr || !c->m.bound || c->cworld < 2 || layout < 0 || layout >= c->nlayouts || upload == nullptr) return -1;
+  const Layout& L = c->layouts[layout];
+  const int nch = c->nch, T = c->T, world = c->cworld;
+  // two gathers out of the one send row [cs | ys | clock]: the share sums + clocks (the recovery's input) first, on
+  // main; the chunk-commitment partials (the audit's input) behind the early audit sums, on the upload stream -- so
+  // the recovery never waits for the commitment sums.  recv = [world][cs] then [world][ys | clock].
+  const size_t cs_bytes = 96ull * nch, ys_bytes = 8ull * nch * T + 8;
+  if ((long long)(cs_bytes + ys_bytes) > c->m.row_bytes) return -1;
+  unsigned char* recv_cs = c->m.recv;
+  unsigned char* recv_ys = c->m.recv + (size_t)world * cs_bytes;
+  RC_CHECK(select_partials_impl(ctx, node, amap, alive, nspec, spec_rows, spec_ev, pts, ys, early_slot, upload, layout,
+                                c->m.send, clock, audit, 0));
+  RC_CHECK(round_all_gather(c, c->m.send + cs_bytes, recv_ys, ys_bytes, c->main, c->main));
+  if (audit != 0) {
+    hipStream_t up = (hipStream_t)upload;
+    RC_CHECK(hipEventRecord(c->ev_main, c->main));   // the partials (or, no local rows, the zeroed slot)
+    RC_CHECK(hipStreamWaitEvent(up, c->ev_main, 0));
+    if (nspec > 0) RC_CHECK(hipStreamWaitEvent(up, c->ev_side, 0));   // the commitment partials
+    RC_CHECK(round_all_gather(c, c->m.send, recv_cs, cs_bytes, up, up));
+    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv_cs, nch, nullptr, world, nullptr, nch, nullptr, c->cs, up));
+    RC_CHECK(hipEventRecord(c->ev_side, up));   // bsc_round_audit waits for the totals through ev_side
   }
-  RC_CHECK(round_all_gather(c, c->m.send, c->m.recv, (size_t)c->m.row_bytes, c->main, c->main));
-  c->aux = (hipStream_t)upload;
-  const int e = bsc_round_after_gather(ctx, c->m.recv, c->cworld, c->m.row_bytes, layout, W, c->m.h_clock, audit,
-                                       pre_it, audit_now, out);
-  c->aux = nullptr;
-  RC_CHECK(e);
-  if (out[1] >= 0 && gram) RC_CHECK(round_multi_gram(c, out[1], pre_it));
+  const int wk = bsc_round_pick_W(ctx, W);
+  if (wk < 0) return -2;
+  RC_CHECK(bsc_recover_w_clock((const long long*)recv_ys, world, (long long)(ys_bytes / 8), nch, T, nullptr, L.ycols, L.xs,
+                               L.npts, L.A, L.basis, c->poly, L.shift, L.inv_lo, L.inv_hi, c->d, W, c->qscale,
+                               c->W_ring[wk], c->coeffs, c->status, L.agg, c->h_W, c->h_status, c->m.h_clock, c->main));
+  RC_CHECK(hipEventRecord(c->ev_readback, c->main));
+  int ps = -1;
+  if (pre_it >= 0) {
+    ps = bsc_round_prestep_slot(ctx, c->W_ring[wk], pre_it, 0);
+    if (ps < 0) return -3;
+  }
+  if (audit != 0 && audit_now) RC_CHECK(bsc_round_audit(ctx, c->coeffs, c->cs, c->ok, c->h_ok));
+  out[0] = wk;
+  out[1] = ps;
+  if (ps >= 0 && gram) RC_CHECK(round_multi_gram(c, ps, pre_it));
   return 0;
 }
 

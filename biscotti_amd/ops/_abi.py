@@ -90,6 +90,7 @@ SIGNATURES = {
     "bsc_round_after_gather": [P, P, I, L, I, P, P, I, I, I, P],
     "bsc_ring_pick": [P, I, P, P, P],
     "bsc_rccl_load": [C.c_char_p],
+    "bsc_set_side_prio": [I],
     "bsc_rccl_unique_id": [P],
     "bsc_round_comm_init": [P, P, I, I, P, I, D],
     "bsc_round_bind_multi": [P, P, P, L, P, I, P, P, P, I, I, I, P, P, L],

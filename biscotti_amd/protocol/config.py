@@ -108,6 +108,8 @@ class RunConfig:
     #                      ranks (default: one rank only; the collectives' kernels run at the default class)
     #   multi_early_front  GPU, several ranks with the native collectives: the next round's front at the end of the
     #                      previous round as with one rank (engine._early_front_ok; measured slower there)
+    #   side_prio_low      GPU: the full-commitment sums (k_segment_sum) and the aggregate audit (k_chunk_check) one
+    #                      wave-priority class below the speculative share MSM instead of at the critical class
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
@@ -116,7 +118,7 @@ class RunConfig:
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
                                   "noise_gram_each_round", "spec_tight", "no_early_front",
-                                  "wave_prio_multi", "multi_early_front")
+                                  "wave_prio_multi", "multi_early_front", "side_prio_low")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""
