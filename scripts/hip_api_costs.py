@@ -2,8 +2,9 @@
 
     python scripts/hip_api_costs.py gpurun_out/X/ht_TAG/run_results.db [rounds]
 
-Per API name on the busiest thread (the round's Python thread): calls, mean and total host microseconds, and the
-per-round share when the number of timed rounds is given."""
+Per API name on the busiest thread (the round's Python thread), over the last 60 % of its calls (the steady
+state): calls, mean / median / p90 and total host microseconds, and the per-round share when the number of rounds
+in that window is given."""
 import sqlite3
 import sys
 from collections import Counter, defaultdict
@@ -16,15 +17,20 @@ def main(path: str, rounds: int = 0) -> None:
         print("no HIP API regions (run rocprofv3 with --hip-trace)")
         return
     main_tid = Counter(r[0] for r in rows).most_common(1)[0][0]
+    mine = sorted((s, e, name) for tid, name, s, e in rows if tid == main_tid)
+    # the steady state: the last 60 % of the thread's calls (set-up, tables and warm-up come first)
+    mine = mine[int(0.4 * len(mine)):]
     by = defaultdict(list)
-    for tid, name, s, e in rows:
-        if tid == main_tid:
-            by[name].append((e - s) / 1e3)
+    for s, e, name in mine:
+        by[name].append((e - s) / 1e3)
     tot = sum(sum(v) for v in by.values())
     print(f"thread {main_tid}: {sum(len(v) for v in by.values())} calls, {tot / 1e3:.1f} ms in HIP calls")
-    print(f"{'api':40s} {'calls':>7s} {'mean us':>8s} {'total ms':>9s}" + (f" {'us/round':>9s}" if rounds else ""))
+    print(f"{'api':40s} {'calls':>7s} {'mean us':>8s} {'p50 us':>7s} {'p90 us':>7s} {'total ms':>9s}"
+          + (f" {'us/round':>9s}" if rounds else ""))
     for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1]))[:30]:
-        line = f"{name[:40]:40s} {len(v):7d} {sum(v) / len(v):8.2f} {sum(v) / 1e3:9.2f}"
+        o = sorted(v)
+        line = (f"{name[:40]:40s} {len(v):7d} {sum(v) / len(v):8.2f} {o[len(o) // 2]:7.2f} {o[int(0.9 * (len(o) - 1))]:7.2f}"
+                f" {sum(v) / 1e3:9.2f}")
         if rounds:
             line += f" {sum(v) / rounds:9.1f}"
         print(line)
