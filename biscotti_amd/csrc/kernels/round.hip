@@ -457,7 +457,7 @@ extern "C" int bsc_round_row_bytes(int nch, int T) {
 
 static int partials_impl(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask, const int* ccols,
                          const int* wcols, int nwc, uint32_t* ws, unsigned char* send, long long clock, int audit,
-                         int wait_cs);
+                         int wait_cs, int defer_wit = 0);
 
 extern "C" int bsc_round_partials(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask,
                                   const int* ccols, const int* wcols, int nwc, uint32_t* ws, unsigned char* send,
@@ -465,10 +465,11 @@ extern "C" int bsc_round_partials(void* ctx, const uint32_t* pts, int R, const l
   return partials_impl(ctx, pts, R, ys, mask, ccols, wcols, nwc, ws, send, clock, audit, 1);
 }
 
-// wait_cs = 0: main does not wait for the commitment partials (the native path gathers them separately)
+// wait_cs = 0: main does not wait for the commitment partials (the native path gathers them separately);
+// defer_wit = 1: no witness sums here (the caller queues them after the recovery: they have no consumer in the round)
 static int partials_impl(void* ctx, const uint32_t* pts, int R, const long long* ys, const int* mask, const int* ccols,
                          const int* wcols, int nwc, uint32_t* ws, unsigned char* send, long long clock, int audit,
-                         int wait_cs) {
+                         int wait_cs, int defer_wit) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || R < 0) return -1;
   const int nch = c->nch, T = c->T;
@@ -483,7 +484,7 @@ static int partials_impl(void* ctx, const uint32_t* pts, int R, const long long*
       RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, ccols, nch, mask, cs_slot, c->side));
       RC_CHECK(hipEventRecord(c->ev_side, c->side));
     }
-    if (nwc > 0 && ws != nullptr) {
+    if (nwc > 0 && ws != nullptr && !defer_wit) {
       RC_CHECK(hipStreamWaitEvent(c->wit, c->ev_main, 0));
       RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->wit));
       RC_CHECK(spec_mark_read(c, mask));
@@ -731,7 +732,7 @@ extern "C" int bsc_round_after_select(void* ctx, const int* node, const int* ama
 static int select_partials_impl(void* ctx, const int* node, const int* amap, int* alive, int nspec,
                                  const int* spec_rows, void* spec_ev, const uint32_t* pts, const long long* ys,
                                  int early_slot, void* upload, int layout, unsigned char* send, long long clock, int audit,
-                                 int wait_cs) {
+                                 int wait_cs, int defer_wit = 0) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr || layout < 0 || layout >= c->nlayouts) return -1;
   const Layout& L = c->layouts[layout];
@@ -739,7 +740,7 @@ static int select_partials_impl(void* ctx, const int* node, const int* amap, int
                        audit == 2 && nspec > 0 ? early_slot : -1, upload, (uint32_t*)send));
   return partials_impl(ctx, nspec > 0 ? pts : nullptr, nspec, nspec > 0 ? ys : nullptr, nspec > 0 ? alive : nullptr,
                        L.ccols, L.wcols, nspec > 0 ? L.nwc : 0, L.ws, send, clock, nspec > 0 ? audit : (audit ? 1 : 0),
-                       wait_cs);
+                       wait_cs, defer_wit);
 }
 
 extern "C" int bsc_round_select_partials(void* ctx, const int* node, const int* amap, int* alive, int nspec,
@@ -989,24 +990,31 @@ extern "C" int bsc_round_agg_multi(void* ctx, const int* node, const int* amap, 
   if ((long long)(cs_bytes + ys_bytes) > c->m.row_bytes) return -1;
   unsigned char* recv_cs = c->m.recv;
   unsigned char* recv_ys = c->m.recv + (size_t)world * cs_bytes;
+  // issue order = the critical path first: partials -> share-sum gather -> recovery; then what only the audit, the
+  // witness sums and the next round read (the host issues ~5 us per launch: the recovery no longer queues behind them)
   RC_CHECK(select_partials_impl(ctx, node, amap, alive, nspec, spec_rows, spec_ev, pts, ys, early_slot, upload, layout,
-                                c->m.send, clock, audit, 0));
+                                c->m.send, clock, audit, 0, 1));
+  RC_CHECK(hipEventRecord(c->ev_main, c->main));   // the partials (or, no local rows, the zeroed commitment slot)
   RC_CHECK(round_all_gather(c, c->m.send + cs_bytes, recv_ys, ys_bytes, c->main, c->main));
-  if (audit != 0) {
-    hipStream_t up = (hipStream_t)upload;
-    RC_CHECK(hipEventRecord(c->ev_main, c->main));   // the partials (or, no local rows, the zeroed slot)
-    RC_CHECK(hipStreamWaitEvent(up, c->ev_main, 0));
-    if (nspec > 0) RC_CHECK(hipStreamWaitEvent(up, c->ev_side, 0));   // the commitment partials
-    RC_CHECK(round_all_gather(c, c->m.send, recv_cs, cs_bytes, up, up));
-    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv_cs, nch, nullptr, world, nullptr, nch, nullptr, c->cs, up));
-    RC_CHECK(hipEventRecord(c->ev_side, up));   // bsc_round_audit waits for the totals through ev_side
-  }
   const int wk = bsc_round_pick_W(ctx, W);
   if (wk < 0) return -2;
   RC_CHECK(bsc_recover_w_clock((const long long*)recv_ys, world, (long long)(ys_bytes / 8), nch, T, nullptr, L.ycols, L.xs,
                                L.npts, L.A, L.basis, c->poly, L.shift, L.inv_lo, L.inv_hi, c->d, W, c->qscale,
                                c->W_ring[wk], c->coeffs, c->status, L.agg, c->h_W, c->h_status, c->m.h_clock, c->main));
   RC_CHECK(hipEventRecord(c->ev_readback, c->main));
+  if (audit != 0) {
+    hipStream_t up = (hipStream_t)upload;
+    RC_CHECK(hipStreamWaitEvent(up, c->ev_main, 0));
+    if (nspec > 0) RC_CHECK(hipStreamWaitEvent(up, c->ev_side, 0));   // the commitment partials
+    RC_CHECK(round_all_gather(c, c->m.send, recv_cs, cs_bytes, up, up));
+    RC_CHECK(bsc_sum_rows2((const uint32_t*)recv_cs, nch, nullptr, world, nullptr, nch, nullptr, c->cs, up));
+    RC_CHECK(hipEventRecord(c->ev_side, up));   // bsc_round_audit waits for the totals through ev_side
+  }
+  if (nspec > 0 && L.nwc > 0) {   // the witness sums (per rank; no consumer in the round)
+    RC_CHECK(hipStreamWaitEvent(c->wit, c->ev_main, 0));
+    RC_CHECK(bsc_sum_rows2(pts, nch * (T + 1), nullptr, nspec, L.wcols, L.nwc, alive, L.ws, c->wit));
+    RC_CHECK(spec_mark_read(c, alive));
+  }
   int ps = -1;
   if (pre_it >= 0) {
     ps = bsc_round_prestep_slot(ctx, c->W_ring[wk], pre_it, 0);
