@@ -70,14 +70,17 @@ class VerifyGather:
         row = buf[self.comm.rank]
         ml, nn = self.maxlocal, self.nn
         assert commits.dtype == torch.int32 and commits.is_contiguous() and commits.shape[1] == self.pw
-        sr = (ctypes.c_int * ml)(*src_row)
+        # src_row / worker_rows: int32 numpy arrays (passed by address) or lists
+        sr_a = np.ascontiguousarray(src_row, np.int32)
+        wr_a = np.ascontiguousarray(worker_rows if len(worker_rows) else [0], np.int32)
+        assert sr_a.size == ml
+        sr, wr = sr_a.ctypes.data, wr_a.ctypes.data
         nz_c = np.ascontiguousarray(nz_np, np.int32).reshape(-1)
         sc_c = np.ascontiguousarray(sc_np, np.float32).reshape(-1)
         assert nz_c.size == ml * nn and sc_c.size == ml * nn
         host = self.host[self._h]
         self._h = (self._h + 1) % self.HOST_DEPTH
         nw = len(worker_rows)
-        wr = (ctypes.c_int * max(1, nw))(*worker_rows)
         na = self.native
         if na is not None:
             # pack, the all_gather in place and unpack in ONE native call (the round's own communicator)

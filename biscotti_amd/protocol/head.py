@@ -158,7 +158,7 @@ class RoundHeadMixin:
                     # the pre-step's delta holds every local peer (no row selection needed)
                     krum_pre = self._gram_rows(delta, None if use_pre else row_of, it)
         head.update(delta=delta, qdelta=qdelta, pending_commits=pending_commits, inboxes=inboxes, row_of=row_of,
-                    spec=spec, spec_cand=cand, krum_pre=krum_pre)
+                    row_is_slot=use_pre, spec=spec, spec_cand=cand, krum_pre=krum_pre)
         if self.vrf_dev is not None:
             # the proofs nobody reads -- every noiser proof and the roles proofs -- go to the device prover
             # when the round runs (run_round's VRF wait), one launch per round on their own low-priority

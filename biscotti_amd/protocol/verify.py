@@ -250,14 +250,21 @@ class VerifyMixin:
             rows = self.crypto.commit_rows_tensor(head["pending_commits"]).to(self.dev)
         else:   # no local worker this round (committee members, churn): every slot of the row is zeros
             rows = torch.zeros((1, self.crypto.point_width), dtype=torch.int32, device=self.dev)
-        src = [-1] * self.maxlocal
-        row_of = head["row_of"]
-        for w in head["local_workers"]:
-            src[w - self.lo] = row_of[w]
+        # slot j (local peer lo + j) -> its commitment row; the round's workers' flat rows: numpy gathers through
+        # tables built once (no per-element Python loop on the round's thread)
+        lw = np.asarray(head["local_workers"], np.int64)
+        src = np.full(self.maxlocal, -1, np.int32)
+        if lw.size:
+            # the pre-step's rows are the local peers themselves (head.py: row_of = {w: w - lo})
+            src[lw - self.lo] = (lw - self.lo) if head.get("row_is_slot") else \
+                np.fromiter((head["row_of"][w] for w in head["local_workers"]), np.int64, lw.size)
+        flat = self.__dict__.get("_flat_np")
+        if flat is None:
+            flat = self._flat_np = np.asarray([self.flat[p] for p in range(self.N)], np.int32)
         if self.gpu and "ev" in pre:   # the Gram slot is written on the Gram stream
             S.current().wait_event(pre["ev"])
         gram, nz, sc, host, ev = vg.exchange(pre["it"], rows.contiguous(), src, nz_np, sc_np,
-                                             [self.flat[w] for w in head["workers"]])
+                                             flat[np.asarray(head["workers"], np.int64)])
         pre["gram"] = gram
         pre.pop("split", None)
         head["commit_gather"] = (host, ev)
