@@ -558,6 +558,27 @@ extern "C" __global__ void __launch_bounds__(256) k_sum_rows2(const uint32_t* pt
   if (ry == 0 && i < ncols) st_jac(out + 24 * (size_t)i, ld_jac(&sh[0][cx][0]));
 }
 
+// Throughput form of the masked column sums, for sums nothing in the round waits for (the miners' witness sums:
+// per rank, read only by the KZG audit when it is on): one lane per output column adds the kept rows in order.
+// k_sum_rows2's 16-lane LDS tree buys latency with 15 more Jacobian additions per column -- ~30 % of the witness
+// sums' VALU work, issued while the share MSMs (VALU-bound) run beside them.  Background priority (class 0).
+extern "C" __global__ void __launch_bounds__(256) k_sum_cols_serial(const uint32_t* pts, int ncols_in, int nrows,
+                                                                   const int* cols, int ncols, const int* row_mask,
+                                                                   uint32_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncols) return;
+  const int col = cols != nullptr ? cols[i] : i;
+  jac acc = jac_inf();
+  bool any = false;
+  for (int r = 0; r < nrows; ++r) {
+    if (row_mask != nullptr && row_mask[r] == 0) continue;
+    const jac p = ld_jac(pts + 24 * ((size_t)r * ncols_in + col));
+    acc = any ? jac_add(acc, p) : p;
+    any = true;
+  }
+  st_jac(out + 24 * (size_t)i, acc);
+}
+
 // Sum of a strided segment per group: out[g] = sum_{k<n} pts[(g*n + k)*stride + off], one block
 // per group, LDS tree.  Used for the full commitment = sum of chunk commitments.
 extern "C" __global__ void __launch_bounds__(256) k_segment_sum(const uint32_t* pts, int n, int stride, int off,
@@ -750,6 +771,21 @@ extern "C" int bsc_sum_rows2(const uint32_t* pts, int ncols_in, const int* rows,
   if (ncols <= 0) return 0;
   hipLaunchKernelGGL(k_sum_rows2, dim3(blocks_for(ncols, 16)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
                      rows, nrows, cols, ncols, row_mask, 0, out);
+  return (int)hipGetLastError();
+}
+
+static int g_wit_tree = 0;   // bsc_set_witness_tree(1): the witness sums in the LDS-tree form (A/Bs)
+extern "C" int bsc_set_witness_tree(int on) {
+  g_wit_tree = on ? 1 : 0;
+  return 0;
+}
+
+extern "C" int bsc_sum_cols_serial(const uint32_t* pts, int ncols_in, int nrows, const int* cols, int ncols,
+                                   const int* row_mask, uint32_t* out, void* stream) {
+  if (ncols <= 0) return 0;
+  if (g_wit_tree) return bsc_sum_rows2(pts, ncols_in, nullptr, nrows, cols, ncols, row_mask, out, stream);
+  hipLaunchKernelGGL(k_sum_cols_serial, dim3(blocks_for(ncols, 256)), dim3(256), 0, (hipStream_t)stream, pts, ncols_in,
+                     nrows, cols, ncols, row_mask, out);
   return (int)hipGetLastError();
 }
 

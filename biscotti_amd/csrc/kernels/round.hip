@@ -51,6 +51,8 @@ extern "C" int bsc_sum_rows_i64(const long long* ys, int R, long long C, const i
                                 long long* out, void* stream);
 extern "C" int bsc_sum_rows_i64_tail(const long long* ys, int R, long long C, const int* mask, long long* out,
                                      long long tail, void* stream);
+extern "C" int bsc_sum_cols_serial(const uint32_t* pts, int ncols_in, int nrows, const int* cols, int ncols,
+                                   const int* row_mask, uint32_t* out, void* stream);
 extern "C" int bsc_sum_rows2_pos(const uint32_t* pts, int ncols_in, const int* rows, int nrows, const int* cols,
                                  int ncols, const int* row_mask, uint32_t* out, void* stream);
 extern "C" int bsc_shares_msm(const long long* coeffs, int d, const int* rows, int nrows, const uint32_t* tbl_pk,
@@ -277,7 +279,7 @@ extern "C" int bsc_round_secagg(void* ctx, const uint32_t* pts, int R, const lon
     RC_CHECK(hipEventRecord(c->ev_side, c->side));
   }
   RC_CHECK(hipStreamWaitEvent(c->wit, c->ev_main, 0));
-  RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->wit));
+  RC_CHECK(bsc_sum_cols_serial(pts, ncols_in, R, wcols, nwc, mask, ws, c->wit));
   RC_CHECK(spec_mark_read(c, mask));
   // the recovery writes (status, W_new) into the pinned read-back buffers itself: no copies behind it
   RC_CHECK(bsc_recover_w_strided(ys, R, (long long)c->nch * c->T, c->nch, c->T, mask, ycols, xs, npts, A, basis,
@@ -486,7 +488,7 @@ static int partials_impl(void* ctx, const uint32_t* pts, int R, const long long*
     }
     if (nwc > 0 && ws != nullptr && !defer_wit) {
       RC_CHECK(hipStreamWaitEvent(c->wit, c->ev_main, 0));
-      RC_CHECK(bsc_sum_rows2(pts, ncols_in, nullptr, R, wcols, nwc, mask, ws, c->wit));
+      RC_CHECK(bsc_sum_cols_serial(pts, ncols_in, R, wcols, nwc, mask, ws, c->wit));
       RC_CHECK(spec_mark_read(c, mask));
     }
   } else if (audit != 0) {
@@ -1012,7 +1014,7 @@ extern "C" int bsc_round_agg_multi(void* ctx, const int* node, const int* amap, 
   }
   if (nspec > 0 && L.nwc > 0) {   // the witness sums (per rank; no consumer in the round)
     RC_CHECK(hipStreamWaitEvent(c->wit, c->ev_main, 0));
-    RC_CHECK(bsc_sum_rows2(pts, nch * (T + 1), nullptr, nspec, L.wcols, L.nwc, alive, L.ws, c->wit));
+    RC_CHECK(bsc_sum_cols_serial(pts, nch * (T + 1), nspec, L.wcols, L.nwc, alive, L.ws, c->wit));
     RC_CHECK(spec_mark_read(c, alive));
   }
   int ps = -1;

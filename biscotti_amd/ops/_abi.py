@@ -91,6 +91,8 @@ SIGNATURES = {
     "bsc_ring_pick": [P, I, P, P, P],
     "bsc_rccl_load": [C.c_char_p],
     "bsc_set_side_prio": [I],
+    "bsc_sum_cols_serial": [P, I, I, P, I, P, P, P],
+    "bsc_set_witness_tree": [I],
     "bsc_rccl_unique_id": [P],
     "bsc_round_comm_init": [P, P, I, I, P, I, D],
     "bsc_round_bind_multi": [P, P, P, L, P, I, P, P, P, I, I, I, P, P, L],

@@ -110,6 +110,8 @@ class RunConfig:
     #                      previous round as with one rank (engine._early_front_ok; measured slower there)
     #   side_prio_low      GPU: the full-commitment sums (k_segment_sum) and the aggregate audit (k_chunk_check) one
     #                      wave-priority class below the speculative share MSM instead of at the critical class
+    #   witness_sums_tree  GPU: the miners' witness sums in k_sum_rows2's LDS-tree form (16 lanes a column) instead of
+    #                      one lane a column (k_sum_cols_serial: ~30 % fewer Jacobian additions)
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
@@ -118,7 +120,8 @@ class RunConfig:
     ABLATIONS: ClassVar[tuple] = ("noise_independent", "shared_inbox", "no_miner_cap", "no_roles_proof", "no_pipeline",
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
                                   "noise_gram_each_round", "spec_tight", "no_early_front",
-                                  "wave_prio_multi", "multi_early_front", "side_prio_low")
+                                  "wave_prio_multi", "multi_early_front", "side_prio_low",
+                                  "witness_sums_tree")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

@@ -155,6 +155,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             # collectives' kernels must not queue behind prio-2 share MSMs
             B.set_wave_priorities(self.comm.world == 1 or cfg.has("wave_prio_multi"))
             B.hip().bsc_set_side_prio(1 if cfg.has("side_prio_low") else 0)
+            B.hip().bsc_set_witness_tree(1 if cfg.has("witness_sums_tree") else 0)
             # host waits spin up to 5 ms before sleeping when this rank has its GPU (and a core of the quota) to
             # itself -- one rank, or one rank per GPU; ranks sharing a GPU (rehearsals) spin 200 us
             S.set_spin(5e-3 if not self._shared_device and not cfg.has("short_spin") else 2e-4)

@@ -223,3 +223,38 @@ def test_shares_msm_late_cancellation(rt):
     p, y = eng.shares(q, rows, alive=alive)
     for r in (2, 3):
         assert torch.equal(p[r], full_p[r]) and torch.equal(y[r], full_y[r])
+
+
+def test_sum_cols_serial_masked_witness_sums(rt):
+    """bsc_sum_cols_serial (the miners' witness sums: one lane per column, kept rows in order) gives the same group
+    elements as the LDS-tree form (k_sum_rows2) and as the host's aggregate witnesses (kyber.go:244-287 summed
+    homomorphically), with masked rows left out -- including a column set spanning miners' slots and a fully
+    masked input (the point at infinity)."""
+    from biscotti_amd.native import hip
+    from biscotti_amd.ops import bn256 as B
+    d = 30
+    key = rt.CommitKey.generate(d, 3)
+    eng = B.DeviceCommitEngine(key, 10, 21)
+    coeffs = np.random.default_rng(2).integers(-10**5, 10**5, size=(5, d), dtype=np.int64)
+    pts, _ = eng.shares(torch.from_numpy(coeffs).cuda(), torch.arange(5, dtype=torch.int32, device="cuda"))
+    flat = pts.reshape(5, -1, 24).contiguous()
+    ncols_in = flat.shape[1]
+    cols = torch.tensor([k * 22 + s for k in range(eng.nchunks) for s in (0, 3, 7, 20)], dtype=torch.int32,
+                        device="cuda")
+    for mask_l in ([1, 0, 1, 1, 0], [0, 0, 0, 0, 0]):
+        mask = torch.tensor(mask_l, dtype=torch.int32, device="cuda")
+        got = torch.empty((cols.numel(), 24), dtype=torch.int32, device="cuda")
+        assert hip().bsc_sum_cols_serial(flat.data_ptr(), ncols_in, 5, cols.data_ptr(), cols.numel(), mask.data_ptr(),
+                                         got.data_ptr(), None) == 0
+        ref = torch.empty_like(got)
+        assert hip().bsc_sum_rows2(flat.data_ptr(), ncols_in, None, 5, cols.data_ptr(), cols.numel(), mask.data_ptr(),
+                                   ref.data_ptr(), None) == 0
+        np.testing.assert_array_equal(B.marshal(got).cpu().numpy(), B.marshal(ref).cpu().numpy())
+        kept = [i for i, m in enumerate(mask_l) if m]
+        if kept:
+            _, _, _, wits = key.make_shares(coeffs[kept].sum(0), 10, 21)
+            g = B.marshal(got).cpu().numpy()
+            for i, (k, s) in enumerate((k, s) for k in range(eng.nchunks) for s in (0, 3, 7, 20)):
+                assert bytes(g[i]) == wits[k * 21 + s]
+        else:
+            assert not B.marshal(got).cpu().numpy().any()   # infinity marshals as zeros
