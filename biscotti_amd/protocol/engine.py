@@ -184,7 +184,17 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         # the round's own communicator (NativeSecAgg.comm_init); the next noise-aware Gram's deltas gather and tile
         # pairs go with the aggregation's call when the packed verification row holds the layout (_multi_gram)
         self._multi_gram = False
-        if self._native is not None and self.comm.world > 1 and self._native.comm_init(self.comm, cfg.comm_timeout_s):
+        native_comm = False
+        if self._native is not None and self.comm.world > 1:
+            try:
+                native_comm = self._native.comm_init(self.comm, cfg.comm_timeout_s)
+            except RuntimeError as e:   # (every rank fails alike: the unique id or the library is the problem)
+                import warnings
+
+                warnings.warn(f"native round collectives unavailable ({e}): torch's collectives instead",
+                              RuntimeWarning)
+        self._native_comm = native_comm
+        if native_comm:
             vg = self._vgather()
             if vg is not None:
                 vg.native = self._native
@@ -209,7 +219,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self._spec_next = None        # next round's share MSM launched at block build (_spec_head_launch)
         self._idle_work = None
         self._last_nodes: list = []
-        self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0, "vrf_outputs": 0}
+        self.stats = {"unmasked_updates": 0, "total_updates": 0, "audit_failures": 0, "vrf_outputs": 0,
+                      "native_collectives": int(self._native_comm)}
         self._kzg_init(cfg)
         self._churn = {"down": {}, "view": {}, "epoch": {}, "acc": 0.0, "kills": 0, "rejoins": 0,
                        "synced_blocks": 0}

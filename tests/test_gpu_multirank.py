@@ -128,6 +128,7 @@ def test_gpu_one_rank_per_gpu_fast_path_over_rccl(world, extra):
         for k in ("pre_steps", "spec_head", "device_aggregations", "early_vrf"):
             assert st.get(k, 0) >= rounds - 1, (r, k, st)
         assert st.get("spec_misses", 0) == 0 and st.get("audit_failures", 0) == 0, st
+        assert st.get("native_collectives") == 1, (r, st)
         if extra:   # the next round's front started at the end of the previous one on every rank
             assert st.get("early_fronts", 0) >= rounds - 2, (r, st)
     assert s1.get("spec_head", 0) >= rounds - 1, s1
@@ -168,4 +169,5 @@ def test_gpu_eight_ranks_100_peers_over_rccl():
             assert st.get(k, 0) >= rounds - 1, (r, k, st)
         assert st.get("device_aggregations", 0) + st.get("spec_misses", 0) >= rounds - 1, (r, st)
         assert st.get("audit_failures", 0) == 0, (r, st)
+        assert st.get("native_collectives") == 1, (r, st)   # the round's own RCCL communicator ran
     assert sum(out[r][1]["spec_rows"] for r in range(8)) == s1["spec_rows"]
