@@ -249,7 +249,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         VRF outputs / Krum, and the critical path keeps the rest)."""
         lo, hi = torch.cuda.Stream.priority_range()
         self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
-        self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, SIDE_STREAM_SKIP_EVERY)
+        self.side_stream, self.side_cus = B.cu_masked_stream(
+            self.dev, 0 if self.cfg.has("side_all_cus") else SIDE_STREAM_SKIP_EVERY)
         # work the round's end waits for at most (the pre-step's commitments: the block carries them)
         self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
         # work no consumer in the round waits for (the miners' witness sums): on bg they queued the
