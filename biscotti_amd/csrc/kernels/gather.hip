@@ -22,7 +22,7 @@
 
 #define VG_MAX_SLOTS 128   // local peer slots per rank
 #define VG_MAX_NZ 256      // maxlocal x nn noiser entries per rank
-#define VG_MAX_WORKERS 640 // workers whose commitment rows are read back
+#define VG_MAX_WORKERS 1024 // workers whose commitment rows are read back (weak scaling: 800 peers)
 
 struct VgPackArgs {
   int src_row[VG_MAX_SLOTS];   // slot j (local peer lo + j) -> row of the commitment source, -1: zeros
