@@ -50,12 +50,42 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build step failed: {cmd[0]} {cmd[-1]}")
 
 
+COMPILED: list = []   # the objects and libraries this process compiled or linked (build_record)
+
+
 def _compile_many(jobs: list[tuple[list[str], Path, list[Path]]], force: bool) -> list[Path]:
     todo = [(c, o) for c, o, deps in jobs if force or _stale(o, deps)]
     if todo:
         with cf.ThreadPoolExecutor(_jobs()) as ex:
             list(ex.map(lambda co: _run(co[0]), todo))
+        COMPILED.extend(str(o.relative_to(PKG.parent)) for _, o in todo)
     return [o for _, o, _ in jobs]
+
+
+def build_record(mode: str, t0: float) -> Path:
+    """build/build_record.json: what this build compiled (every object when forced), the toolchain, and the
+    sha256 of each source and each built library -- evidence that the libraries in the tree are this tree's."""
+    import hashlib
+    import json
+    import time
+
+    def sha(p: Path) -> str:
+        return hashlib.sha256(p.read_bytes()).hexdigest()[:16]
+
+    srcs = sorted(list((CSRC / "runtime").glob("*.[ch]pp")) + list((CSRC / "kernels").glob("*.hip"))
+                  + list((CSRC / "kernels").glob("*.h")))
+    libs = [PKG / RT_NAME, PKG / HIP_LIB]
+    rec = {"mode": mode, "arch": ARCH, "seconds": round(time.time() - t0, 1),
+           "finished_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+           "compiled": sorted(COMPILED), "n_compiled": len(COMPILED),
+           "hipcc": subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.splitlines()[:2]
+           if Path(HIPCC).exists() else None,
+           "sources_sha256_16": {str(p.relative_to(PKG.parent)): sha(p) for p in srcs},
+           "libraries_sha256_16": {str(p.relative_to(PKG.parent)): sha(p) for p in libs if p.exists()}}
+    BUILD.mkdir(parents=True, exist_ok=True)
+    out = BUILD / "build_record.json"
+    out.write_text(json.dumps(rec, indent=1) + "\n")
+    return out
 
 
 def build_runtime(force: bool = False) -> Path:
