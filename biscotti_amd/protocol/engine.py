@@ -505,9 +505,10 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 # stream the evaluation sat between the audit and the next round's Krum kernels.  Launched
                 # after the next round's front when that runs (ordered on main's position here).  self.W is a
                 # slot of the native W ring, which a later round's recovery rewrites while a lagging evaluation
-                # may still read it: the evaluation reads a copy of its own (_eval_input)
-                W_eval = self._eval_input(self.W)
-                W_ev = S.record()
+                # may still read it: the evaluation reads a copy of its own (_eval_input), taken where the evaluation is
+                # launched -- after the next round's front (the copy is not on the way to its Krum launch; no
+                # recovery queued in between can pick this model's ring slot, bsc_ring_pick)
+                W_eval_src = self.W
             else:
                 eval_pending = self.task.evaluate_async(self.W)
         with tm.phase("next_head"):
@@ -530,6 +531,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 while len(self._sign_joins) > 2:   # the signature batch of two rounds ago
                     self._sign_joins.pop(0)()
         if self.gpu:
+            W_eval = self._eval_input(W_eval_src)
+            W_ev = S.record()
             ws = self.witness_stream
             ws.wait_event(W_ev)
             with S.use(ws):
