@@ -112,8 +112,8 @@ class RunConfig:
     #                      wave-priority class below the speculative share MSM instead of at the critical class
     #   witness_sums_tree  GPU: the miners' witness sums in k_sum_rows2's LDS-tree form (16 lanes a column) instead of
     #                      one lane a column (k_sum_cols_serial: ~30 % fewer Jacobian additions)
-    #   side_all_cus       GPU: the speculative share MSM's stream on every CU also with one rank (default there: 3/4
-    #                      of them, the rest kept for the critical path; several ranks, one per GPU, use every CU)
+    #   side_all_cus       GPU: the speculative share MSM's stream on every CU (default: 3/4 of them, the rest kept for
+    #                      the critical path)
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)

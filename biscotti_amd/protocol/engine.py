@@ -249,10 +249,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         VRF outputs / Krum, and the critical path keeps the rest)."""
         lo, hi = torch.cuda.Stream.priority_range()
         self.main_stream = torch.cuda.Stream(device=self.dev, priority=hi)
-        # with several ranks (one per GPU) on every CU: a rank's share MSM is then the round's critical path on its
-        # device (the committee's selection lands after it), emulated rank 0 of 2: 0.959 vs 0.991 ms over 3 runs each
-        # (docs/PERF.md, round 6); one rank keeps a quarter of the CUs for the kernels its early front runs beside it
-        full = self.cfg.has("side_all_cus") or (self.comm.world > 1 and not self._shared_device)
+        # (side_all_cus: on every CU -- emulated rank 0 of 2 measured 0.959 vs 0.991 ms on one box and no different on
+        # another, docs/PERF.md round 6: the quarter stays with the critical path)
+        full = self.cfg.has("side_all_cus")
         self.side_stream, self.side_cus = B.cu_masked_stream(self.dev, 0 if full else SIDE_STREAM_SKIP_EVERY)
         # work the round's end waits for at most (the pre-step's commitments: the block carries them)
         self.bg_stream = torch.cuda.Stream(device=self.dev, priority=lo)
