@@ -98,7 +98,7 @@ for step in "$@"; do
       echo "host timeline: $O/host_tl.json" ;;
     mrprof:*)
       n="${step#mrprof:}"
-      timeout -k 10 300 python scripts/prof_rounds.py --emulate-world "$n" > "$O/mrprof_$n.txt" 2>&1 \
+      timeout -k 10 300 python scripts/prof_rounds.py --emulate-world "$n" -o "$O/mrprof_${n}_full.txt" > "$O/mrprof_$n.txt" 2>&1 \
         || { echo "MRPROF FAILED"; tail -20 "$O/mrprof_$n.txt"; exit 1; }
       head -40 "$O/mrprof_$n.txt" ;;
     kt:*)
