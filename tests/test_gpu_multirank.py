@@ -171,3 +171,21 @@ def test_gpu_eight_ranks_100_peers_over_rccl():
         assert st.get("audit_failures", 0) == 0, (r, st)
         assert st.get("native_collectives") == 1, (r, st)   # the round's own RCCL communicator ran
     assert sum(out[r][1]["spec_rows"] for r in range(8)) == s1["spec_rows"]
+
+
+def test_gpu_emulated_rank0_native_collectives():
+    """bench.py --emulate-world N: rank 0 of an N-rank job alone on the GPU -- its peers' work, the native fused calls
+    with every collective replaced by ONE replicate launch (rank 0's contribution in every slot) -- runs the multi-rank
+    fast paths (native collectives, packed verification row, the aggregation + next Gram in one call) and keeps a valid
+    chain."""
+    import subprocess
+    import json
+
+    out = subprocess.run([sys.executable, "bench.py", "--emulate-world", "4", "--steps", "4", "--warmup", "2",
+                          "--rounds", "8", "--peers", "24"], cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads(next(ln for ln in out.stdout.splitlines() if ln.startswith("{")))
+    st = rec["engine_stats"]
+    assert rec["emulated_world"] == 4 and rec["chain_valid"], rec
+    assert st["native_collectives"] == 1 and st.get("pre_steps", 0) >= 4 and st.get("device_aggregations", 0) >= 4, st
+    assert st["audit_failures"] == 0, st
