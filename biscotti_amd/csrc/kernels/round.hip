@@ -119,6 +119,10 @@ struct RoundCtx {
   hipStream_t main, side, bg;
   hipStream_t wit;   // the miners' witness sums (no consumer in the round; default: bg)
   hipEvent_t ev_main, ev_side, ev_readback, ev_audit, ev_pre;
+  // the audit's read-back is double-buffered (event + pinned row aud_k of h_ok): a round's audit can be read
+  // after the next round's aggregation was queued (the speculative front, engine._spec_front_launch)
+  hipEvent_t ev_audit1;
+  int aud_k = 0;
   const uint32_t* tbl_pk;
   int d, poly, T, nch, b0, nw;
   double qscale;
@@ -200,7 +204,7 @@ extern "C" void* bsc_round_create(void* main, void* side, void* bg, const uint32
   c->b0 = b0;
   c->nw = nw;
   c->qscale = qscale;
-  hipEvent_t* evs[5] = {&c->ev_main, &c->ev_side, &c->ev_readback, &c->ev_audit, &c->ev_pre};
+  hipEvent_t* evs[6] = {&c->ev_main, &c->ev_side, &c->ev_readback, &c->ev_audit, &c->ev_pre, &c->ev_audit1};
   for (hipEvent_t* e : evs)
     if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
       delete c;
@@ -252,6 +256,7 @@ extern "C" void bsc_round_destroy(void* ctx) {
   hipEventDestroy(c->ev_side);
   hipEventDestroy(c->ev_readback);
   hipEventDestroy(c->ev_audit);
+  hipEventDestroy(c->ev_audit1);
   hipEventDestroy(c->ev_pre);
   for (int i = 0; i < c->nspec; ++i) hipEventDestroy(c->spec_done[i]);
   delete c;
@@ -289,13 +294,22 @@ extern "C" int bsc_round_secagg(void* ctx, const uint32_t* pts, int R, const lon
   return 0;
 }
 
+// h_ok: [2][nch] pinned; this audit's verdicts go to row aud_k (flipped per audit, bsc_round_audit_slot)
 extern "C" int bsc_round_audit(void* ctx, const long long* coeffs, const uint32_t* cs, int* ok, int* h_ok) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return -1;
+  c->aud_k ^= 1;
   RC_CHECK(hipStreamWaitEvent(c->main, c->ev_side, 0));
-  RC_CHECK(bsc_chunk_check_h(coeffs, c->d, c->poly, c->tbl_pk, c->b0, c->nw, cs, 1, c->nch, ok, h_ok, c->main));
-  RC_CHECK(hipEventRecord(c->ev_audit, c->main));
+  RC_CHECK(bsc_chunk_check_h(coeffs, c->d, c->poly, c->tbl_pk, c->b0, c->nw, cs, 1, c->nch, ok,
+                             h_ok + (size_t)c->aud_k * c->nch, c->main));
+  RC_CHECK(hipEventRecord(c->aud_k ? c->ev_audit1 : c->ev_audit, c->main));
   return 0;
+}
+
+// the h_ok row (and bsc_round_wait's 2 + slot) of the audit queued last
+extern "C" int bsc_round_audit_slot(void* ctx) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  return c == nullptr ? -1 : c->aud_k;
 }
 
 // The audit's commitment sums taken early, from the pre-step's per-peer chunk commitments instead of the
@@ -797,14 +811,16 @@ static int host_wait(hipEvent_t ev, long long timeout_ns = 0) {
   }
 }
 
-// which: 0 = the recovery read-back, 1 = the audit read-back.  With the round's own communicator, a wait longer
+// which: 0 = the recovery read-back, 1 = the last audit's read-back, 2 / 3 = audit slot 0 / 1's.  With the round's own communicator, a wait longer
 // than the collective timeout means a rank is gone (the reference's crashed peer): the communicator is aborted
 // -- its kernels return -- and -99 goes back to the engine, which fails the job for the elastic restart
 // (parallel/comm.py), as torch's watchdog does for its own collectives
 extern "C" int bsc_round_wait(void* ctx, int which) {
   RoundCtx* c = (RoundCtx*)ctx;
   if (c == nullptr) return -1;
-  const int r = host_wait(which == 0 ? c->ev_readback : c->ev_audit, c->comm != nullptr ? c->timeout_ns : 0);
+  if (which == 1) which = 2 + c->aud_k;
+  const hipEvent_t ev = which == 0 ? c->ev_readback : which == 2 ? c->ev_audit : c->ev_audit1;
+  const int r = host_wait(ev, c->comm != nullptr ? c->timeout_ns : 0);
   if (r == -99 && c->comm != nullptr && g_rccl.comm_abort != nullptr) {
     g_rccl.comm_abort(c->comm);
     c->comm = nullptr;

@@ -1513,6 +1513,12 @@ PYBIND11_MODULE(_biscotti_rt, m) {
                                  std::vector<i64> selfs, i64 nn, i64 n) {
     return select_noisers_impl(stake, job, std::move(out_index), std::move(selfs), nn, n);
   });
+  // the lottery with the stake a block will leave the FSM with (commit_block: the block's map when it carries
+  // one) -- the speculative front draws the next round's noisers before the block is committed
+  m.def("select_noisers_job_after", [](const RoundFSM& f, const Block& b, VrfJob& job, std::vector<i64> out_index,
+                                       std::vector<i64> selfs, i64 nn, i64 n) {
+    return select_noisers_impl(b.stake.empty() ? f.stake : b.stake, job, std::move(out_index), std::move(selfs), nn, n);
+  });
   m.def("krum_scores", [](py::array_t<double, py::array::c_style | py::array::forcecast> X, i64 groupsize) {
     if (X.ndim() != 2) throw std::runtime_error("X must be 2-D");
     return krum_scores(X.data(), X.shape(0), X.shape(1), groupsize);

@@ -74,6 +74,7 @@ SIGNATURES = {
     "bsc_round_secagg": [P, P, I, P, P, P, P, I, P, P, I, P, P, I, U64, U64, P, P, P, P, P, P, P, P, P, I],
     "bsc_round_audit": [P, P, P, P, P],
     "bsc_round_wait": [P, I],
+    "bsc_round_audit_slot": [P],
     "bsc_set_host_spin_ns": [L],
     "bsc_round_row_bytes": [I, I],
     "bsc_round_partials": [P, P, I, P, P, P, P, I, P, P, L, I],

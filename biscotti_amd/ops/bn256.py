@@ -393,7 +393,7 @@ class NativeSecAgg:
         self.ok = torch.empty((1, nch), dtype=torch.int32, device=dev)
         self.h_status = torch.empty((nch,), dtype=torch.int32, pin_memory=True)
         self.h_W = torch.empty((d,), dtype=torch.float64, pin_memory=True)
-        self.h_ok = torch.empty((1, nch), dtype=torch.int32, pin_memory=True)
+        self.h_ok = torch.empty((2, nch), dtype=torch.int32, pin_memory=True)   # two audits in flight (bsc_round_audit)
         import ctypes
 
         ring = (ctypes.c_void_p * self.W_RING)(*[t.data_ptr() for t in self.W_ring])
@@ -712,9 +712,11 @@ class NativeSecAgg:
             _check(hip().bsc_round_audit(self.ctx, _ptr(self.coeffs), _ptr(self.cs), _ptr(self.ok),
                                          self.h_ok.data_ptr()), "round_audit")
 
+        k = int(hip().bsc_round_audit_slot(self.ctx))   # this audit's slot: a later one may be queued before the read
+
         def result():
-            _check(hip().bsc_round_wait(self.ctx, 1), "round_wait")
-            return self.h_ok.numpy()
+            _check(hip().bsc_round_wait(self.ctx, 2 + k), "round_wait")
+            return self.h_ok[k:k + 1].numpy()
         return result
 
     def close(self) -> None:

@@ -114,6 +114,9 @@ class RunConfig:
     #                      one lane a column (k_sum_cols_serial: ~30 % fewer Jacobian additions)
     #   side_all_cus       GPU: the speculative share MSM's stream on every CU (default: 3/4 of them, the rest kept for
     #                      the critical path)
+    #   no_spec_front      GPU, one rank: the next round's front at the commit of the block (after the audit wait and
+    #                      the read-back) instead of right after the block's build (engine._spec_front_launch): the
+    #                      chain must not change
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
@@ -123,7 +126,7 @@ class RunConfig:
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
                                   "noise_gram_each_round", "spec_tight", "no_early_front",
                                   "wave_prio_multi", "multi_early_front", "side_prio_low",
-                                  "witness_sums_tree", "side_all_cus")
+                                  "witness_sums_tree", "side_all_cus", "no_spec_front")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

@@ -43,7 +43,7 @@ from ..utils import streams as S
 from .config import RunConfig
 from .crypto_backends import DeviceCrypto, HostCrypto
 from .faults import FaultsMixin
-from .head import RoundHeadMixin
+from .head import PlanView, RoundHeadMixin
 from .kzg_audit import KzgAuditMixin
 from .secagg import SecAggMixin
 from .verify import VerifyMixin
@@ -231,6 +231,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self._front = None            # the next round's front, started at the end of the previous round
         self._host_proofs: list = []  # the run's last round's VRF proofs, proved on the host (joined by drain)
         self._front_planned = False
+        self._spec_front = None       # the next round's front launched before the block's commit (_spec_front_launch)
+        self._front_remaining = None
         self._warm_up()
         import atexit
         import weakref
@@ -366,6 +368,9 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             self.golog.flush()
         self.drain()
         heads = []
+        sf, self._spec_front = self._spec_front, None
+        if sf is not None:
+            self._drop_spec_front(sf)
         fr, self._front = self._front, None
         if fr is not None:
             # the next round's front was started (its Krum, the aggregation behind it, the pre-step) but its round
@@ -445,6 +450,7 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         # the next round's front starts right after this round's block (engine._round_front): the host work of
         # the audit wait that nothing before it needs (signature prep, evaluation read-backs) moves behind it
         self._front_planned = front and not last and self._early_front_ok()
+        self._front_remaining = remaining - 1 if remaining else None
         fr, self._front = self._front, None
         if fr is None:
             with tm.phase("roles"):
@@ -511,9 +517,13 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
             else:
                 eval_pending = self.task.evaluate_async(self.W)
         with tm.phase("next_head"):
-            self._head = self._open_round()   # next round's committee + VRF outputs start now
+            sf, self._spec_front = self._spec_front, None
+            if sf is not None:   # the next round's front, launched before this block's commit: adopted or dropped
+                self._adopt_spec_front(sf)
+            else:
+                self._head = self._open_round()   # next round's committee + VRF outputs start now
         if self._front_planned:
-            if not self._head["plan"].done:
+            if self._head is not None and not self._head["plan"].done:
                 # the next round's front -- noiser lottery, Krum launch and the aggregation queued behind its
                 # selection -- before this round's remaining host work: the selection lands earlier and
                 # cancels the speculative MSM's rejected rows sooner; the work below fills the next round's waits
@@ -592,7 +602,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                 kst = head.get("kst") or self._krum_static(krum_pre["xrow"], krum_pre["U1"], plan, live, inboxes, head["spec"],
                                         head.get("arrivals"))
         with tm.phase("vrf_join"):
-            noisers = self._select_noisers(head["fut_noise"], head["stake"], local_workers, head.get("vrf_index"))
+            noisers = self._select_noisers(head["fut_noise"], head["stake"], local_workers, head.get("vrf_index"),
+                                           after=head.get("after_block"))
         with tm.phase("noise"):
             # with the phase-1 Gram the noised deltas are never materialised (only Krum reads them)
             noised = None if krum_pre is not None else \
@@ -630,6 +641,85 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
                         self.vrf_dev.flush(self.vrf_stream)
             self._resolve_evals(wait=len(self._evals) > 3)   # a bounded backlog: the host rings hold 4
         return {"head": head, "noisers": noisers, "noised": noised, "verify": ver, "remaining": remaining}
+
+    def _spec_front_launch(self, block) -> None:
+        """The speculative front: the next round's front launched from the block just built, before its audit is
+        read and it is committed.  Everything the next head would hold is ready then -- the successor plan,
+        inboxes, candidates and share MSM (_spec_head_launch), the pre-step's deltas, commitments and Gram, the VRF
+        outputs started at the block build (_early_vrf_submit) and the stake the block leaves -- so a head is built
+        from them here and _round_front runs on it: the noiser lottery, the Krum launch and the aggregation behind
+        the selection are queued before the audit wait, the read-back and the commit instead of after them (the
+        selection cancels the speculative MSM's rejected rows sooner).  run_round adopts it when the committed
+        block and the FSM's plan match (_adopt_spec_front), else drops it (an audit failure empties the block)."""
+        sn, pre, ej = self._spec_next, self._pre, self._early_vrf
+        h = bytes(block.hash)
+        if not (self._front_planned and self._spec_front_ok() and sn is not None and ej is not None and pre is not None
+                and sn["hash"] == h and sn["pre"] is pre and ej["hash"] == h
+                and ej["ver"] == getattr(self, "_seed_version", 0) and pre.get("gram") is not None
+                and pre["W"] is self._W_next and not sn["plan"].done and sn["inboxes"]):
+            return
+        plan, lo = sn["plan"], self.lo
+        workers = sn["workers"]
+        local_workers = [w for w in workers if w in self.local]
+        if not local_workers:
+            return
+        self._spec_next = self._early_vrf = self._pre = None   # consumed (the pre-step's rows are the head's)
+        live = [1] * self.N
+        S.current().wait_event(pre["ev"])   # the step ran on the Gram stream
+        head = {"live": live, "plan": plan, "workers": workers, "local_workers": local_workers, "stake": None,
+                "after_block": block, "fut_noise": ej["job"], "fut_roles": None,
+                "vrf_index": [w - lo for w in local_workers], "delta": pre["delta"], "qdelta": pre["qdelta"],
+                "pending_commits": pre["commits"], "inboxes": sn["inboxes"], "row_of": {w: w - lo for w in local_workers},
+                "row_is_slot": True, "spec": sn["spec"], "spec_cand": sn["cand"], "arrivals": sn["arrivals"],
+                "cand_order": sn.get("cand_order"), "krum_pre": pre["gram"], "W": self._W_next,
+                "vrf_proofs": (local_workers, live, h)}
+        if sn.get("kst") is not None:
+            head["kst"] = sn["kst"]
+        with self.timer.phase("spec_front"):
+            work, self._pre_vrf_work = self._pre_vrf_work, []   # this round's: run in the audit wait, after the launch
+            fr = self._round_front(head, self._front_remaining)
+            self._pre_vrf_work = work + self._pre_vrf_work
+        self._spec_front = {"front": fr, "hash": h}
+
+    def _adopt_spec_front(self, sf: dict) -> None:
+        """Begin the round the speculative front was launched for; adopt the front when the committed block is the
+        one it was launched from and the plan is the one it used, else drop it and open the round afresh."""
+        live = self._live_mask()
+        plan = PlanView(self.fsm.begin_round(live))
+        sp = sf["front"]["head"]["plan"]
+        if (not plan.done and all(live) and bytes(self.fsm.chain.latest_hash()) == sf["hash"]
+                and plan.iteration == sp.iteration and plan.leader == sp.leader
+                and list(plan.verifiers) == list(sp.verifiers) and list(plan.miners) == list(sp.miners)
+                and list(plan.workers) == list(sp.workers)):
+            self._front = sf["front"]
+            st = self.stats
+            for k in ("spec_fronts", "early_vrf", "pre_steps", "spec_head"):
+                st[k] = st.get(k, 0) + 1
+            return
+        self._drop_spec_front(sf)
+        self._head = self._open_round(begun=(live, plan))
+
+    def _drop_spec_front(self, sf: dict) -> None:
+        """A speculative front whose round will not run from it: its verification generator is stopped and its VRF
+        job joined later; its device work (Krum, the aggregation, the pre-step behind it) is left to finish unread
+        -- the round that runs instead re-launches its own behind it on the same streams."""
+        fr = sf["front"]
+        ver = fr.get("verify")
+        if hasattr(ver, "close"):
+            ver.close()
+        job = fr["head"].get("fut_noise")
+        if job is not None:
+            self._stale_vrf.append(job)
+        self._pre = None   # the dropped aggregation's pre-step (from a model that is not the chain's)
+        self.stats["spec_front_drops"] = self.stats.get("spec_front_drops", 0) + 1
+
+    def _spec_front_ok(self) -> bool:
+        """The speculative front (_spec_front_launch) applies: one rank with the native round, the device VRF
+        prover (no host roles proofs to start with the head), no KZG audit (its capture of the aggregate follows
+        the commit), the noise-aware Krum input, and not the no_spec_front ablation."""
+        cfg = self.cfg
+        return (self.comm.world == 1 and self._native is not None and self.vrf_dev is not None
+                and cfg.kzg_audit == "off" and self._noise_krum() and not cfg.has("no_spec_front"))
 
     def _early_front_ok(self) -> bool:
         """The next round's front runs at the end of this one: one rank per process on a GPU, the pipelined

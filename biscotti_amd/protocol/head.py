@@ -44,13 +44,17 @@ class PlanView:
 
 class RoundHeadMixin:
     # ------------------------------------------------------------------ the head
-    def _open_round(self) -> dict:
+    def _open_round(self, begun: tuple | None = None) -> dict:
         """Round head: live set, committee plan, the VRF outputs and the device work of the round that
-        needs nothing but the latest block; consumed by run_round."""
+        needs nothing but the latest block; consumed by run_round.  begun: (live, PlanView) of a round the FSM
+        has begun already (a speculative front that was not adopted, engine._adopt_spec_front)."""
         cfg, R, fsm = self.cfg, self.R, self.fsm
         with self.timer.phase("head.plan"):
-            live = self._live_mask()
-            plan = PlanView(fsm.begin_round(live))
+            if begun is not None:
+                live, plan = begun
+            else:
+                live = self._live_mask()
+                plan = PlanView(fsm.begin_round(live))
         head = {"live": live, "plan": plan}
         if plan.done:
             return head

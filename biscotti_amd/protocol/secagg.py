@@ -142,7 +142,8 @@ class SecAggMixin:
             out["kzg_in"] = (cs_k, ws_k, agg if comm.world == 1 else y_k, xs_t)
         return out
 
-    def _spec_aggregate_native(self, sp, pred, node, amap, flags_set: bool = False) -> dict:
+    def _spec_aggregate_native(self, sp, pred, node, amap, flags_set: bool = False, it: int | None = None,
+                               W=None) -> dict:
         """The GPU secure aggregation through the fused native calls (kernels/round.hip) -- behind the committee's
         selection (sp: the speculative MSM) or on the host-decided path (sp: _Rows) alike.  One rank: ONE call
         queues the rows' flags, the early audit sums, the miners' sums + exact recovery + read-back, the next
@@ -166,14 +167,18 @@ class SecAggMixin:
                 raise RuntimeError("speculative MSM without commitment slots but no chunk commitments to audit with")
         if kzg and getattr(self, "_kzg_copied", None) is not None:
             S.current().wait_event(self._kzg_copied)   # the last aggregate's copies before its buffers are rewritten
-        nxt = self.fsm.iteration + 1            # fsm: the round being aggregated
+        # it: the round being aggregated (default: the FSM's, begun); W: the model it starts from (default: the engine's)
+        # -- a speculative front passes both, ahead of the previous block's commit (engine._spec_front_launch)
+        it = self.fsm.iteration if it is None else it
+        W = self.W if W is None else W
+        nxt = it + 1
         # the next round's pre-step behind the recovery (softmax tasks: binds the task at the first use)
         pre_it = nxt if (self._pipelined() and getattr(self.task, "stateless_step", False)
                          and self._native_prestep_ok()) else -1
-        now = self._now(self.fsm.iteration)
+        now = self._now(it)
         sel = None if flags_set else node   # None: the vote kernel (or the host path) has set the rows' flags
         if comm.world == 1:
-            W_new, pre = na.after_select(sel, amap, sp, early, self.upload_stream, lid, self.W, audit, pre_it,
+            W_new, pre = na.after_select(sel, amap, sp, early, self.upload_stream, lid, W, audit, pre_it,
                                          audit_now=run_audit)
             readback, clock = na.readback(), None
             if pre is not None:
@@ -181,7 +186,7 @@ class SecAggMixin:
         elif na.native_comm:
             # one call: partials, the all_gather, recovery, the next pre-step and its Gram's gather + tile pairs
             gram = self._multi_gram and pre_it >= 0
-            W_new, k = na.agg_multi(sel, amap, sp, early, self.upload_stream, lid, now, self.W, audit, pre_it,
+            W_new, k = na.agg_multi(sel, amap, sp, early, self.upload_stream, lid, now, W, audit, pre_it,
                                     run_audit, gram)
             pre = None
             if k >= 0:
@@ -191,7 +196,7 @@ class SecAggMixin:
         else:   # gloo ranks on GPUs (tests): the collective is torch's, between the two native calls
             na.select_partials(sel, amap, sp, early, self.upload_stream, lid, now, audit)
             comm.all_gather_into(na.recv, na.send)
-            W_new, k = na.after_gather(lid, self.W, audit, pre_it, audit_now=run_audit)
+            W_new, k = na.after_gather(lid, W, audit, pre_it, audit_now=run_audit)
             pre = self._finish_pre(na._pre_out(k, W_new, nxt), nxt) if k >= 0 else None
             readback, clock = na.readback(clocks=True), True
         if pre is not None:
@@ -343,6 +348,8 @@ class SecAggMixin:
         self._early_vrf_submit(block.hash)
         if self._W_next is not None:
             self._spec_head_launch(block)
+            # and its front (noiser lottery, Krum launch, the aggregation behind the selection) before the audit wait
+            self._spec_front_launch(block)
         if audit_ok is not None:
             if self._idle_work is not None:   # host-only work (no collective): overlap it with the audit
                 self._idle_work()
@@ -353,12 +360,17 @@ class SecAggMixin:
                 # it slowed the outputs: vrf_join 0.03 -> 0.09 ms), the earlier rounds' evaluation read-backs and
                 # the next round's host preparation fill the audit wait
                 with tm.phase("recover.idle"):
-                    if not self._front_planned:   # else run after the next round's front (run_round)
-                        ej = self._early_vrf["job"] if self._early_vrf is not None else None
+                    sf = self._spec_front
+                    # else (a front planned at the commit) run after the next round's front (run_round)
+                    if not self._front_planned or sf is not None:
+                        ej = sf["front"]["head"]["fut_noise"] if sf is not None else \
+                            self._early_vrf["job"] if self._early_vrf is not None else None
                         work, self._pre_vrf_work = self._pre_vrf_work, []
                         for f in work:
                             f(ej)
-                        self._resolve_evals()
+                        # (after a speculative front the previous round's evaluation was queued just before: only
+                        # the landed read-backs are taken)
+                        self._resolve_evals(wait=sf is None)
                     self._prepare_next_in_wait()
             with tm.phase("recover.audit"):
                 ok = audit_ok()

@@ -28,17 +28,22 @@ SIGN_THREADS = 4   # verifier signature batches: narrow, the pool's rest serves 
 
 class VerifyMixin:
     # ------------------------------------------------------------------ noisers and noise
-    def _select_noisers(self, fut_noise, stake, local_workers, index=None) -> dict:
+    def _select_noisers(self, fut_noise, stake, local_workers, index=None, after=None) -> dict:
         """Each worker's noisers from its own VRF output (getVRFNoisers, vrf.go:54-100).  Waits for the
         outputs only; the proofs finish on the native threads (or the device) and are joined later.
-        index: positions of local_workers in the job's output list (an early job covers more peers)."""
+        index: positions of local_workers in the job's output list (an early job covers more peers).
+        after: a block not committed yet whose stake the lottery uses (the speculative front)."""
         if fut_noise is None or not local_workers:
             return {}
         # the lottery reads the job's outputs natively (no 64-byte Python objects in between)
         idx = list(index) if index is not None else []
-        sel = self.fsm.select_noisers_job(fut_noise, idx, local_workers, self.cfg.num_noisers, self.N) \
-            if stake is None else self.R.select_noisers_job(stake, fut_noise, idx, local_workers, self.cfg.num_noisers,
-                                                             self.N)
+        nn = self.cfg.num_noisers
+        if after is not None:
+            sel = self.R.select_noisers_job_after(self.fsm, after, fut_noise, idx, local_workers, nn, self.N)
+        elif stake is None:
+            sel = self.fsm.select_noisers_job(fut_noise, idx, local_workers, nn, self.N)
+        else:
+            sel = self.R.select_noisers_job(stake, fut_noise, idx, local_workers, nn, self.N)
         self._noise_arr = (local_workers, sel)   # the same ids as an array, in local_workers order
         return dict(zip(local_workers, sel.tolist()))
 
@@ -198,7 +203,10 @@ class VerifyMixin:
         def on_accept(node):
             with self.timer.phase("verify.queue_agg"):
                 if fused:
-                    box["sa"] = self._spec_aggregate_native(sp, pred, node, amap_t, box.get("flags_set", False))
+                    # the round's iteration and the model it starts from: a speculative front runs before the
+                    # previous block is committed (engine._spec_front_launch)
+                    box["sa"] = self._spec_aggregate_native(sp, pred, node, amap_t, box.get("flags_set", False),
+                                                            it=plan.iteration, W=box.get("W"))
                 elif sp is not None:   # no aggregate behind the selection: cancel the rows the block drops
                     B.set_alive(node, amap_t, sp.alive)
                     sp.launch()
@@ -392,7 +400,7 @@ class VerifyMixin:
         signatures: dict = {}
         pending_signatures = None
         defer_sign = False
-        box: dict = {}
+        box: dict = {"W": head.get("W")}   # W: set by a speculative front (the block it starts from is not committed)
         if need_X:
             vs = [v for v in plan.verifiers if v in inboxes]   # live verifiers, plan order
             nv = len(plan.verifiers)

@@ -92,7 +92,7 @@ for step in "$@"; do
       echo "profiled: $(grep '^{' "$O/prof_bench.txt" | tail -1 | head -c 160)" ;;
     hosttl)
       timeout -k 10 300 python scripts/host_timeline.py --rounds 4 --warm 30 --set lazy_eval=true \
-        --wrap _early_vrf_submit,_spec_head_launch,_prepare_next_in_wait,_open_round,_select_noisers,_launch_krum,native.spec_msm,native.after_select,_finish_secagg,_secure_aggregation,_round_front,_finish_verification \
+        --wrap _early_vrf_submit,_spec_head_launch,_spec_front_launch,_adopt_spec_front,_prepare_next_in_wait,_open_round,_select_noisers,_launch_krum,native.spec_msm,native.after_select,_finish_secagg,_secure_aggregation,_round_front,_finish_verification \
         > "$O/host_tl.json" \
         2> "$O/host_tl.err" || { echo "HOST TL FAILED"; tail -20 "$O/host_tl.err"; exit 1; }
       echo "host timeline: $O/host_tl.json" ;;

@@ -278,3 +278,25 @@ def test_lagging_evaluation_reads_its_own_model():
         eng.close()
     assert out[0] == out[1]
     assert all(e == e for _, e, _ in out[1])
+
+
+def test_audit_read_back_is_per_audit():
+    """Two aggregate audits queued before either is read (the speculative front queues the next round's before the
+    current one's verdicts are read) each read back their own verdicts: the first over the last round's consistent
+    coefficients passes, the second over tampered ones fails one chunk."""
+    eng = _engine()
+    for _ in range(3):
+        eng.run_round()
+    eng.drain()
+    torch.cuda.synchronize()
+    na = eng._native
+    assert na is not None
+    first = na.audit(queue=True)
+    na.coeffs[0, 0] += 1   # stream-ordered after the first audit's read of the coefficients
+    second = na.audit(queue=True)
+    bad = second().copy()
+    good = first().copy()
+    assert good.all(), good
+    assert bad[0, 0] == 0 and bad.sum() == bad.size - 1, bad
+    na.coeffs[0, 0] -= 1
+    eng.close()

@@ -265,15 +265,17 @@ def test_pre_gram_and_early_vrf_keep_the_chain():
 @pytest.mark.parametrize("extra", ["", "spec_tight"])
 def test_early_front_keeps_the_chain(extra):
     """The next round's front (noiser lottery, Krum launch, the aggregation queued behind the selection) started
-    at the end of the previous round gives the chain of running it at the round's own start (no_early_front),
-    with poisoners (Krum's selection decides the blocks) and with spec_tight (speculative misses: the host path
-    aggregates behind an early-launched selection)."""
+    right after the previous round's block build (the speculative front), or at the previous round's commit
+    (no_spec_front), gives the chain of running it at the round's own start (no_early_front), with poisoners
+    (Krum's selection decides the blocks) and with spec_tight (speculative misses: the host path aggregates behind
+    an early-launched selection)."""
     from biscotti_amd.parallel.comm import Comm
     from biscotti_amd.protocol.config import RunConfig
     from biscotti_amd.protocol.engine import BiscottiEngine
 
     chains, stats = [], []
-    for abl in (extra, ",".join(a for a in (extra, "no_early_front") if a)):
+    for abl in (extra, ",".join(a for a in (extra, "no_early_front") if a),
+                ",".join(a for a in (extra, "no_spec_front") if a)):
         cfg = RunConfig(num_nodes=30, dataset="mnist", seed=5, max_iterations=100, deterministic_time=True,
                         poisoning=0.3, epsilon=1.0, ablation=abl)
         eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
@@ -285,14 +287,50 @@ def test_early_front_keeps_the_chain(extra):
         chains.append([bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))])
         stats.append(dict(eng.stats))
         eng.close()
-    assert chains[0] == chains[1]
+    assert chains[0] == chains[1] == chains[2]
     assert stats[0].get("early_fronts", 0) == 8 and "early_fronts" not in stats[1]
+    assert stats[2].get("early_fronts", 0) == 8 and "spec_fronts" not in stats[2]
+    assert stats[0].get("spec_fronts", 0) >= 6 and "spec_front_drops" not in stats[0], stats[0]
     assert stats[0]["audit_failures"] == 0
     if extra:   # a miss aggregates on the host-decided path
         assert stats[0].get("spec_misses", 0) > 0, stats[0]
         assert stats[0].get("device_aggregations", 0) + stats[0]["spec_misses"] >= 8, stats[0]
     else:
         assert stats[0].get("device_aggregations", 0) >= 6, stats[0]
+
+
+def test_spec_front_dropped_when_the_block_changes(monkeypatch):
+    """A speculative front whose block is not the one committed -- round 3's block replaced by an empty one after
+    its build, as a failed aggregate audit does -- is dropped (its generator stopped, its VRF job joined later) and
+    the round opened afresh from the already begun plan: the chain is the one of fronts launched at the commit
+    (no_spec_front)."""
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+    from biscotti_amd.protocol.secagg import SecAggMixin
+
+    real = SecAggMixin._finish_secagg
+
+    def empty_at_3(self, plan, *a):
+        blk = real(self, plan, *a)
+        return None if plan.iteration == 3 else blk
+    monkeypatch.setattr(SecAggMixin, "_finish_secagg", empty_at_3)
+    chains, stats = [], []
+    for abl in ("", "no_spec_front"):
+        cfg = RunConfig(num_nodes=30, dataset="mnist", seed=5, max_iterations=100, deterministic_time=True,
+                        poisoning=0.3, epsilon=1.0, ablation=abl)
+        eng = BiscottiEngine(cfg, Comm(device=torch.device("cuda", 0)))
+        for k in range(8):
+            eng.run_round(last=k == 7)
+        eng.drain()
+        ok, why = eng.fsm.chain.verify()
+        assert ok, why
+        chains.append([bytes(eng.fsm.chain.block(i).hash) for i in range(len(eng.fsm.chain))])
+        stats.append(dict(eng.stats))
+        eng.close()
+    assert chains[0] == chains[1]
+    assert stats[0].get("spec_front_drops", 0) == 1 and stats[0].get("spec_fronts", 0) >= 4, stats[0]
+    assert "spec_fronts" not in stats[1]
 
 
 def test_last_round_vrf_proofs_on_the_host():

@@ -185,6 +185,32 @@ def test_select_noisers_job_matches_per_worker_lottery():
         R.select_noisers_batch(stake, betas, list(range(60)), 2, 60)
 
 
+def test_select_noisers_after_block_uses_the_stake_it_leaves():
+    """The speculative front's noiser lottery (select_noisers_job_after) draws with the stake the block leaves the
+    FSM with once committed: the block's own map, or the FSM's when the block carries none."""
+    from biscotti_amd.native import rt
+    from biscotti_amd.parallel.comm import Comm
+    from biscotti_amd.protocol.config import RunConfig
+    from biscotti_amd.protocol.engine import BiscottiEngine
+
+    R = rt()
+    eng = BiscottiEngine(RunConfig(num_nodes=12, dataset="mnist", seed=5, max_iterations=100,
+                                   deterministic_time=True), Comm())
+    eng.run_round()
+    fsm, blk = eng.fsm, eng.fsm.chain.latest()
+    job = R.vrf_prove_batch_async([bytes([i]) * 32 for i in range(12)], bytes(blk.hash), 2, None, True)
+    ws = list(range(12))
+    other = {i: 1 + 5 * i for i in range(12)}
+    assert other != dict(fsm.stake)
+    blk.stake = other
+    got = R.select_noisers_job_after(fsm, blk, job, [], ws, 2, 12).tolist()
+    assert got == R.select_noisers_job(other, job, [], ws, 2, 12).tolist()
+    blk.stake = {}
+    got = R.select_noisers_job_after(fsm, blk, job, [], ws, 2, 12).tolist()
+    assert got == fsm.select_noisers_job(job, [], ws, 2, 12).tolist()
+    eng.close()
+
+
 def test_successor_gives_the_next_plan_before_commit():
     """fsm.successor(block) (used to launch the next round's share MSM before the block's audit is read)
     yields the same plan, verifier inboxes and leader arrival order as the FSM after the commit."""
