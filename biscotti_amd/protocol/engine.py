@@ -661,8 +661,8 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         plan, lo = sn["plan"], self.lo
         workers = sn["workers"]
         local_workers = [w for w in workers if w in self.local]
-        if not local_workers:
-            return
+        if not local_workers and self.comm.world == 1:
+            return   # (several ranks: every rank runs the front, with or without workers -- its collectives line up)
         self._spec_next = self._early_vrf = self._pre = None   # consumed (the pre-step's rows are the head's)
         live = [1] * self.N
         S.current().wait_event(pre["ev"])   # the step ran on the Gram stream
@@ -714,11 +714,14 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.stats["spec_front_drops"] = self.stats.get("spec_front_drops", 0) + 1
 
     def _spec_front_ok(self) -> bool:
-        """The speculative front (_spec_front_launch) applies: one rank with the native round, the device VRF
-        prover (no host roles proofs to start with the head), no KZG audit (its capture of the aggregate follows
-        the commit), the noise-aware Krum input, and not the no_spec_front ablation."""
+        """The speculative front (_spec_front_launch) applies: the native round (several ranks: with its own
+        collectives and the next Gram in its call, and the speculative MSM launched -- on a shared GPU only under
+        spec_head_shared), the device VRF prover (no host roles proofs to start with the head), no KZG audit (its
+        capture of the aggregate follows the commit), the noise-aware Krum input, and not the no_spec_front
+        ablation.  Every input is the same on every rank."""
         cfg = self.cfg
-        return (self.comm.world == 1 and self._native is not None and self.vrf_dev is not None
+        multi_ok = self._multi_gram and (not self._shared_device or cfg.has("spec_head_shared"))
+        return ((self.comm.world == 1 or multi_ok) and self._native is not None and self.vrf_dev is not None
                 and cfg.kzg_audit == "off" and self._noise_krum() and not cfg.has("no_spec_front"))
 
     def _early_front_ok(self) -> bool:
@@ -726,12 +729,16 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         noise-aware Multi-Krum path, no churn / partitions / fault injection (whose next round may differ from
         the head built here) and no per-round phase records (trace, phase log, phase sync: their phases would
         move to the previous round).  The no_early_front ablation turns it off; the chain is the same.  With
-        several ranks it runs with the native collectives under the multi_early_front ablation only: same-box A/B
+        several ranks it runs with the native collectives, as the speculative front (_spec_front_ok) or under the
+        multi_early_front ablation (at the commit): same-box A/B of the latter
         of emulated rank 0, 3 runs each (docs/PERF.md, round 6), 1.214 / 1.107 / 0.994 ms with it against 1.123 /
         1.024 / 0.877 without at N = 2 / 4 / 8 -- the front's collectives and Krum wait on the device behind the
         previous round's tail instead of the host work they used to overlap."""
         cfg = self.cfg
-        return (self.gpu and (self.comm.world == 1 or (self._multi_gram and cfg.has("multi_early_front")))
+        # (several ranks: the speculative front launches it before the commit; the front at the commit runs only
+        # where that front could not be launched)
+        multi = self._multi_gram and (cfg.has("multi_early_front") or self._spec_front_ok())
+        return (self.gpu and (self.comm.world == 1 or multi)
                 and self._pipelined() and cfg.secure_agg and cfg.verification
                 and cfg.defense == "KRUM" and self._noise_krum() and not cfg.has("no_early_front")
                 and cfg.churn == 0 and cfg.churn_kill_per_min == 0 and not self._partitions

@@ -326,8 +326,30 @@ class RoundHeadMixin:
             return
         plan, ibs, arrivals, spec_workers, cands = got[:5]
         order = got[-1]
-        if not spec_workers:
+        if not spec_workers and self.comm.world == 1:
             return
+        # several ranks: the successor plan is kept even without local rows to launch (spec None), so every rank
+        # makes the same speculative-front decision (engine._spec_front_launch: its collectives line up)
+        sp = self._spec_msm_launch(pre, spec_workers) if spec_workers else None
+        plan = PlanView(plan)
+        workers = plan.workers
+        inboxes = dict(zip(plan.verifiers, ibs))
+        cand = set(cands)
+        self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
+                           "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
+                           "arrivals": arrivals, "spec": (spec_workers, sp) if spec_workers else None, "pre": pre,
+                           "cand_order": order}
+        if krum and ibs:
+            n = len(ibs[0])
+            up = h2d_many([(got[5], torch.int32), (got[6], torch.int32), (got[7], torch.int32)], self.dev)
+            self._spec_next["kst"] = {"U": g["U1"], "n": n, "clip": self.fsm.krum_clip(n),
+                                      "need": len(plan.verifiers) // 2, "cap": self.fsm.leader_cap_size(),
+                                      "inbox": up[0], "rank": up[1], "amap": up[2]}
+
+    def _spec_msm_launch(self, pre: dict, spec_workers: list):
+        """The speculative share MSM over this rank's candidate rows (in the leader's arrival order) on the side
+        stream, behind the pre-step that produced them."""
+        cfg = self.cfg
         side = self.side_stream
         # the audit's commitment sums come from the pre-step's chunk commitments (the early audit sums of NativeSecAgg.after_select):
         # the MSM then computes the witness lanes only
@@ -346,19 +368,7 @@ class RoundHeadMixin:
             with S.use(self.upload_stream):
                 sp = self.crypto.shares_async(pre["qdelta"], rows, side, group_rows=SPEC_GROUP_ROWS,
                                               no_commit=no_commit)
-        plan = PlanView(plan)
-        workers = plan.workers
-        inboxes = dict(zip(plan.verifiers, ibs))
-        cand = set(cands)
-        self._spec_next = {"plan": plan, "hash": bytes(block.hash), "it": plan.iteration, "verifiers": list(plan.verifiers),
-                           "miners": list(plan.miners), "workers": workers, "inboxes": inboxes, "cand": cand,
-                           "arrivals": arrivals, "spec": (spec_workers, sp), "pre": pre, "cand_order": order}
-        if krum and ibs:
-            n = len(ibs[0])
-            up = h2d_many([(got[5], torch.int32), (got[6], torch.int32), (got[7], torch.int32)], self.dev)
-            self._spec_next["kst"] = {"U": g["U1"], "n": n, "clip": self.fsm.krum_clip(n),
-                                      "need": len(plan.verifiers) // 2, "cap": self.fsm.leader_cap_size(),
-                                      "inbox": up[0], "rank": up[1], "amap": up[2]}
+        return sp
 
     def _spec_horizon(self) -> int:
         """How far down the leader's arrival order of candidates the speculative MSM reaches, -1: every candidate

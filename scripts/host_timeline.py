@@ -1,7 +1,7 @@
 """Host-side timeline of engine rounds: every PhaseTimer phase with its start/end (us from the
 round's first phase), nested phases included, for a few steady-state rounds of the headline config.
 
-    python scripts/host_timeline.py [--rounds 3] [--warm 20] [--set field=value ...]
+    python scripts/host_timeline.py [--rounds 3] [--warm 20] [--set field=value ...] [--emulate-world N]
 """
 import argparse
 import dataclasses
@@ -26,8 +26,9 @@ def main():
     ap.add_argument("--set", action="append", default=[])
     ap.add_argument("--wrap", default="", help="comma-separated engine methods (or task./crypto. methods) timed as events")
     ap.add_argument("--fsm-proxy", action="store_true", help="time every native RoundFSM call as an event (@fsm.name)")
+    ap.add_argument("--emulate-world", type=int, default=0, help="rank 0 of an N-rank job (bench.py --emulate-world)")
     a = ap.parse_args()
-    comm = Comm.init()
+    comm = Comm.emulated(a.emulate_world) if a.emulate_world > 1 else Comm.init()
     torch.set_num_threads(min(4, torch.get_num_threads()))
     kw = dict(num_nodes=100, seed=0, max_iterations=10**9, host_threads=16)
     types = {f.name: f.type for f in dataclasses.fields(RunConfig)}
