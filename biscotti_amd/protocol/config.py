@@ -117,6 +117,8 @@ class RunConfig:
     #   no_spec_front      GPU, one rank: the next round's front at the commit of the block (after the audit wait and
     #                      the read-back) instead of right after the block's build (engine._spec_front_launch): the
     #                      chain must not change
+    #   multi_spec_front   GPU, several ranks with the native collectives: the speculative front as with one rank
+    #                      (engine._spec_front_ok; measured slower there)
 
     # seconds per reference round: maps the churn scripts' seconds onto rounds (the reference's churn runs
     # took 25-31 s per round, nsdi-eval/churn/*.log)
@@ -126,7 +128,8 @@ class RunConfig:
                                   "spec_head_shared", "spec_all_candidates", "short_spin",
                                   "noise_gram_each_round", "spec_tight", "no_early_front",
                                   "wave_prio_multi", "multi_early_front", "side_prio_low",
-                                  "witness_sums_tree", "side_all_cus", "no_spec_front")
+                                  "witness_sums_tree", "side_all_cus", "no_spec_front",
+                                  "multi_spec_front")
 
     def has(self, ablation: str) -> bool:
         """True when `ablation` (one of ABLATIONS) is switched on."""

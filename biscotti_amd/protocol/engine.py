@@ -714,13 +714,16 @@ class BiscottiEngine(RoundHeadMixin, VerifyMixin, SecAggMixin, KzgAuditMixin, Fa
         self.stats["spec_front_drops"] = self.stats.get("spec_front_drops", 0) + 1
 
     def _spec_front_ok(self) -> bool:
-        """The speculative front (_spec_front_launch) applies: the native round (several ranks: with its own
-        collectives and the next Gram in its call, and the speculative MSM launched -- on a shared GPU only under
-        spec_head_shared), the device VRF prover (no host roles proofs to start with the head), no KZG audit (its
+        """The speculative front (_spec_front_launch) applies: the native round (several ranks: the multi_spec_front
+        ablation, the round's own collectives and the next Gram in its call, and the speculative MSM launched -- on a
+        shared GPU only under spec_head_shared), the device VRF prover (no host roles proofs to start with the head), no KZG audit (its
         capture of the aggregate follows the commit), the noise-aware Krum input, and not the no_spec_front
         ablation.  Every input is the same on every rank."""
         cfg = self.cfg
-        multi_ok = self._multi_gram and (not self._shared_device or cfg.has("spec_head_shared"))
+        # several ranks: under multi_spec_front only -- emulated rank 0, same box (docs/PERF.md, round 6): N = 2
+        # 1.174 / 1.002 vs 0.954 / 0.979 ms, N = 8 0.895 vs 0.841 without it (the host, not the MSM, is the limit there)
+        multi_ok = (self._multi_gram and cfg.has("multi_spec_front")
+                    and (not self._shared_device or cfg.has("spec_head_shared")))
         return ((self.comm.world == 1 or multi_ok) and self._native is not None and self.vrf_dev is not None
                 and cfg.kzg_audit == "off" and self._noise_krum() and not cfg.has("no_spec_front"))
 
