@@ -117,6 +117,7 @@ for step in "$@"; do
       summ "$O/ht_$tag.txt" "ht_$tag"
       python scripts/hip_api_costs.py "$(ls "$O"/ht_$tag/*.db | head -1)" > "$O/ht_${tag}_api.txt" 2>&1 || true
       python scripts/kt_timeline.py "$(ls "$O"/ht_$tag/*.db | head -1)" 30 34 > "$O/ht_${tag}_timeline.txt" 2>&1 || true
+      python scripts/launch_gap.py "$(ls "$O"/ht_$tag/*.db | head -1)" > "$O/ht_${tag}_launch.txt" 2>&1 || true
       rm -rf "$O/ht_$tag" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
