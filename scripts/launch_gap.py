@@ -15,12 +15,21 @@ def cols(con, t):
 def main(path: str, names: str = "k_shares_msm_ka,k_krum_vote,k_recover_w") -> None:
     con = sqlite3.connect(path)
     kc, rc = cols(con, "kernels"), cols(con, "regions")
-    key = next((k for k in ("correlation_id", "corr_id", "stack_id") if k in kc and k in rc), None)
+    print("kernels:", kc)
+    print("regions:", rc)
+    for t in ("kernels", "regions"):
+        for row in con.execute(f"select * from {t} limit 2"):
+            print(t, row)
+    # rocprofv3 7.x: a kernel's stack_id is the id of the HIP API region that dispatched it
+    key = next((k for k in ("stack_id", "correlation_id") if k in kc and k in rc), None)
     if key is None:
-        print("kernels:", kc)
-        print("regions:", rc)
         return
-    launch = {c: s for c, s in con.execute(f"select {key}, start from regions where name like '%Launch%'")}
+    launch, lname = {}, {}
+    for c, st, nm in con.execute(f"select {key}, start, name from regions where {key} != 0"):
+        launch[c], lname[c] = st, nm
+    print(len(launch), "API regions with an id; launching APIs:",
+          sorted({lname.get(c) for _, _, _, c in con.execute(f"select name, start, end, {key} from kernels")
+                  if c in lname})[:8])
     ks = sorted(con.execute(f"select name, start, end, {key} from kernels"), key=lambda r: r[1])
     want = names.split(",")
     last_rec = None
@@ -33,7 +42,7 @@ def main(path: str, names: str = "k_shares_msm_ka,k_krum_vote,k_recover_w") -> N
             last_rec = e
         if last_rec is None or not any(w in n for w in want):
             continue
-        h = launch.get(c)
+        h = launch.get(c) if c else None
         rows.append((n, (h - last_rec) / 1e3 if h is not None else float("nan"), (s - last_rec) / 1e3,
                      (e - last_rec) / 1e3))
     rows = rows[len(rows) // 2:][:60]   # steady state
