@@ -18,8 +18,16 @@ def main(path: str, rounds: int = 0) -> None:
         return
     main_tid = Counter(r[0] for r in rows).most_common(1)[0][0]
     mine = sorted((s, e, name) for tid, name, s, e in rows if tid == main_tid)
-    # the steady state: the last 60 % of the thread's calls (set-up, tables and warm-up come first)
-    mine = mine[int(0.4 * len(mine)):]
+    # the steady state: between the ends of the last rounds' recoveries when their kernels are in the trace
+    # (rounds = the recoveries in the window), else the last 60 % of the thread's calls
+    rec = sorted(e for (e,) in con.execute("select end from kernels where name like 'k_recover_w%'"))
+    if len(rec) >= 12:
+        lo, hi = rec[-11], rec[-1]
+        mine = [m for m in mine if lo <= m[0] < hi]
+        rounds = 10
+        print(f"window: the last 10 rounds (recovery ends {lo} .. {hi})")
+    else:
+        mine = mine[int(0.4 * len(mine)):]
     by = defaultdict(list)
     for s, e, name in mine:
         by[name].append((e - s) / 1e3)
