@@ -44,5 +44,24 @@ def main(path: str, rounds: int = 0) -> None:
         print(line)
 
 
+def by_kernel(path: str) -> None:
+    """hipLaunchKernel host cost per launched kernel over the same window (kernels matched through stack_id)."""
+    con = sqlite3.connect(path)
+    rec = sorted(e for (e,) in con.execute("select end from kernels where name like 'k_recover_w%'"))
+    if len(rec) < 12:
+        return
+    lo, hi = rec[-11], rec[-1]
+    kname = {sid: n.split("(")[0] for n, sid in con.execute("select name, stack_id from kernels where stack_id != 0")}
+    by = defaultdict(list)
+    for sid, s, e in con.execute("select stack_id, start, end from regions where name = 'hipLaunchKernel'"):
+        if lo <= s < hi and sid in kname:
+            by[kname[sid]].append((e - s) / 1e3)
+    print(f"\n{'launched kernel':40s} {'calls':>7s} {'mean us':>8s} {'p50 us':>7s} {'us/round':>9s}")
+    for n, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+        o = sorted(v)
+        print(f"{n[:40]:40s} {len(v):7d} {sum(v) / len(v):8.2f} {o[len(o) // 2]:7.2f} {sum(v) / 10:9.1f}")
+
+
 if __name__ == "__main__":
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 0)
+    by_kernel(sys.argv[1])
