@@ -16,7 +16,8 @@
 #   set:K=V[,K=V][xK]     driver-style runs with --set K=V ... (A/B ablations)
 #   seeds:NAME:N          bench.py --config NAME --seeds N (accuracy over seeds)
 #   prof                  rocprofv3 --kernel-trace --stats of a driver-style run (OUT/prof/)
-#   hosttl[:N]            the host timeline of 4 steady rounds (scripts/host_timeline.py; :N emulated rank 0 of N)
+#   hosttl[:N|w:N]        the host timeline of 4 steady rounds (scripts/host_timeline.py; :N emulated rank 0 of N,
+#                         w:N the same with 100 peers per rank)
 #   mrprof:N              cProfile of rank 0 of an N-rank job (scripts/prof_rounds.py --emulate-world N)
 #   kt:TAG:A+B+C          rocprofv3 kernel + memory-copy trace of bench.py A B C (OUT/kt_TAG/; scripts/kt_timeline.py)
 #   ht:TAG:A+B+C          rocprofv3 HIP API + kernel trace of bench.py A B C (OUT/ht_TAG/; scripts/hip_api_costs.py)
@@ -92,6 +93,8 @@ for step in "$@"; do
       echo "profiled: $(grep '^{' "$O/prof_bench.txt" | tail -1 | head -c 160)" ;;
     hosttl*)
       e="${step#hosttl}"; ea=(); [[ -n "$e" ]] && ea=(--emulate-world "${e#:}")
+      # hosttlw:N -- weak scaling: 100 peers per emulated rank (bench.py's scale_weak)
+      [[ "$e" == w:* ]] && { e="${e#w}"; ea=(--emulate-world "${e#:}" --set "num_nodes=$((100 * ${e#:}))"); e="w${e#:}"; }
       timeout -k 10 300 python scripts/host_timeline.py --rounds 4 --warm 30 --set lazy_eval=true "${ea[@]}" \
         --wrap _early_vrf_submit,_spec_head_launch,_spec_front_launch,_adopt_spec_front,_prepare_next_in_wait,_open_round,_select_noisers,_launch_krum,native.spec_msm,native.after_select,native.agg_multi,_gather_verify_inputs,_finish_secagg,_secure_aggregation,_round_front,_finish_verification \
         > "$O/host_tl${e#:}.json" \
