@@ -331,6 +331,8 @@ class RoundHeadMixin:
         # several ranks: the successor plan is kept even without local rows to launch (spec None), so every rank
         # makes the same speculative-front decision (engine._spec_front_launch: its collectives line up)
         sp = self._spec_msm_launch(pre, spec_workers) if spec_workers else None
+        if not spec_workers:
+            self.stats["spec_head_no_rows"] = self.stats.get("spec_head_no_rows", 0) + 1
         plan = PlanView(plan)
         workers = plan.workers
         inboxes = dict(zip(plan.verifiers, ibs))

@@ -141,6 +141,25 @@ def test_gpu_one_rank_per_gpu_fast_path_over_rccl(world, extra):
     assert s1.get("spec_head", 0) >= rounds - 1, s1
 
 
+def test_gpu_rank_without_candidate_rows_keeps_the_chain():
+    """4 RCCL ranks of 5 peers with the speculative horizon at the leader's cap (spec_tight): some rank has no
+    candidate row within the horizon in some round and keeps the successor plan with no MSM to launch (the same
+    speculative-head decision as its peers: the Krum tables, the candidate set and the collectives stay the
+    same everywhere); misses are topped up on the host path; the chain equals one process's byte for byte."""
+    rounds = 10
+    kw = dict(num_nodes=20, dataset="mnist", seed=23, deterministic_time=True, max_iterations=100,
+              ablation="spec_head_shared,spec_tight")
+    single, s1 = _run_stats(1, kw, rounds)[0]
+    out = _run_stats(4, kw, rounds, backend="nccl")
+    for r in range(4):
+        hashes, st = out[r]
+        assert hashes == single, f"rank {r} chain differs"
+        assert st.get("spec_head", 0) >= rounds - 1 and st.get("audit_failures", 0) == 0, (r, st)
+    assert len({out[r][1].get("spec_misses", 0) for r in range(4)}) == 1   # the same top-up decisions
+    no_rows = [out[r][1].get("spec_head_no_rows", 0) for r in range(4)]
+    assert sum(no_rows) >= 1, no_rows   # (deterministic: rank 1 has one such round)
+
+
 def test_gpu_spec_horizon_two_ranks_100_peers_over_rccl():
     """The headline size (100 peers) on two RCCL ranks with the speculative head forced on: after 8 blocks
     the speculative MSM covers only the candidates up to the replicated horizon (head.py SPEC_MARGIN), every
