@@ -109,16 +109,20 @@ def build_runtime(force: bool = False) -> Path:
     return target
 
 
-def build_selftest(sanitize: bool = True) -> Path:
-    """Native self-test of the host runtime (csrc/selftest), with ASan + UBSan on the host code."""
+def build_selftest(sanitize: bool | str = True) -> Path:
+    """Native self-test of the host runtime (csrc/selftest) on the host code: sanitize True / "asan" -- ASan + UBSan;
+    "tsan" -- ThreadSanitizer (the pool / dispatcher stress: `selftest_tsan pool`); False -- none."""
     rt_dir = CSRC / "runtime"
-    out = BUILD / ("selftest_asan" if sanitize else "selftest")
+    mode = "asan" if sanitize is True else (sanitize or "")
+    out = BUILD / (f"selftest_{mode}" if mode else "selftest")
     out.parent.mkdir(parents=True, exist_ok=True)
     srcs = [s for s in sorted(rt_dir.glob("*.cpp")) if s.name != "bindings.cpp"]
     srcs.append(CSRC / "selftest" / "selftest.cpp")
     flags = ["-O1", "-g", "-std=c++17", "-pthread", f"-I{rt_dir}", "-fno-omit-frame-pointer"]
-    if sanitize:
+    if mode == "asan":
         flags += ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+    elif mode == "tsan":
+        flags += ["-fsanitize=thread"]
     _run(["g++", *flags, *map(str, srcs), "-o", str(out)])
     return out
 
@@ -152,7 +156,14 @@ def main(argv=None) -> None:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--sanitize", action="store_true",
                     help="build and run the host-runtime self-test under ASan + UBSan")
+    ap.add_argument("--tsan", action="store_true",
+                    help="build the host-runtime self-test under ThreadSanitizer and run its pool / dispatcher stress")
     a = ap.parse_args(argv)
+    if a.tsan:
+        exe = build_selftest("tsan")
+        print("built", exe)
+        r = subprocess.run([str(exe), "pool"], env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1"))
+        raise SystemExit(r.returncode)
     if a.sanitize:
         exe = build_selftest(True)
         print("built", exe)

@@ -1,10 +1,13 @@
 // Native self-test of the host runtime, built with AddressSanitizer + UBSan by
-// ``python -m biscotti_amd._build --sanitize`` (host code only: GPU sanitizers are not used).
-// It drives every runtime module from several threads at once and checks known answers, so
-// memory errors, UB and data races that the Python tests cannot see show up here.
+// ``python -m biscotti_amd._build --sanitize`` and with ThreadSanitizer by ``--tsan`` (host code only: GPU
+// sanitizers are not used).  It drives every runtime module from several threads at once and checks known
+// answers, and stresses the thread pool and job dispatcher the bindings run their batches on (overlapping
+// jobs from several submitting threads, jobs that wait on earlier jobs), so memory errors, UB and data races
+// that the Python tests cannot see show up here.
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <future>
 #include <thread>
 #include <vector>
 
@@ -13,6 +16,7 @@
 #include "keys.hpp"
 #include "ledger.hpp"
 #include "pairing.hpp"
+#include "pool.hpp"
 #include "protocol.hpp"
 #include "shares.hpp"
 #include "vrf.hpp"
@@ -116,7 +120,49 @@ static void test_protocol() {
   CHECK(select_noisers(stake, Sha256::digest(Bytes{8}), 4, 2, 30).size() == 2);
 }
 
-int main() {
+// The bindings' concurrency: several threads each run pool jobs (overlapping: the persistent workers help
+// whichever job has items left) and submit dispatcher tasks that themselves run pool jobs and wait on a task
+// submitted before them (the VrfJob::after / SignJob::after_vrf pattern).
+static void test_pool(int t) {
+  for (int rep = 0; rep < 4; ++rep) {
+    const size_t n = 200 + 37 * size_t(t) + size_t(rep);
+    std::vector<long long> out(n, 0);
+    parallel_for(n, 4 + t % 3, [&](size_t i) { out[i] = (long long)(i * i) + t; });
+    long long sum = 0;
+    for (size_t i = 0; i < n; ++i) sum += out[i];
+    long long want = 0;
+    for (size_t i = 0; i < n; ++i) want += (long long)(i * i) + t;
+    CHECK(sum == want);
+  }
+  std::promise<long long> first_p;
+  std::shared_future<long long> first = first_p.get_future().share();
+  std::promise<long long> second_p;
+  std::future<long long> second = second_p.get_future();
+  std::vector<long long> a(300, 0);
+  dispatcher().submit([&] {
+    parallel_for(a.size(), 3, [&](size_t i) { a[i] = (long long)i * 3; });
+    long long s = 0;
+    for (long long v : a) s += v;
+    first_p.set_value(s);
+  });
+  dispatcher().submit([&, first] {
+    const long long f = first.get();   // runs once the earlier task is done
+    second_p.set_value(f + a[299]);
+  });
+  const long long got = second.get();
+  CHECK(got == 3ll * 299 * 300 / 2 + 3ll * 299);
+  CHECK(first.get() == 3ll * 299 * 300 / 2);
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "pool") == 0) {
+    // the concurrency stress alone (ThreadSanitizer runs: the crypto modules are ~10x slower under it)
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 6; ++t) ts.emplace_back([t] { test_pool(t); test_hash(); test_protocol(); });
+    for (auto& t : ts) t.join();
+    std::printf("selftest pool: %s (%d failures)\n", failures ? "FAILED" : "ok", failures.load());
+    return failures ? 1 : 0;
+  }
   // run every module twice on 6 threads concurrently (lazy statics, caches and tables included)
   std::vector<std::thread> ts;
   for (int t = 0; t < 6; ++t)
@@ -128,6 +174,7 @@ int main() {
         test_vrf();
         test_shares_and_ledger();
         test_protocol();
+        test_pool(t);
       }
     });
   for (auto& t : ts) t.join();

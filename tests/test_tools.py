@@ -92,6 +92,17 @@ def test_native_selftest_under_asan_ubsan():
     assert "selftest: ok" in r.stdout
 
 
+def test_native_pool_under_tsan():
+    """The thread pool and job dispatcher the bindings run their VRF / Schnorr / KZG batches on, under
+    ThreadSanitizer: overlapping pool jobs from 6 submitting threads, dispatcher tasks that run pool jobs and wait
+    on an earlier task (SURVEY §5 race detection; the reference has none)."""
+    r = subprocess.run([sys.executable, "-m", "biscotti_amd._build", "--tsan"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "selftest pool: ok" in r.stdout
+    assert "ThreadSanitizer" not in r.stderr
+
+
 def test_centralblock_prototype():
     import numpy as np
 
