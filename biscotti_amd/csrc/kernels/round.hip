@@ -389,6 +389,32 @@ extern "C" int bsc_round_spec_msm2(void* ctx, int slot, void* ev_wait, const lon
                         nullptr, group_rows, pts, ys, c->side);
 }
 
+// A block that reaches past the speculative MSM's rows (a speculative miss: its horizon was too short): the missing
+// rows' shares go into the SAME ring slot behind its n rows, so one aggregation reads them all.  Behind everything
+// queued on main so far (the aggregation that already read the slot) the side stream uploads the slot's flags
+// (keep_host [n + m]: the host-decided block rows among the speculative ones, 1 for the new ones) and runs the MSM
+// over rows_host [m] into rows n.. of pts / ys; the new rows' device list goes up on `up` (event ev_up).
+extern "C" int bsc_round_spec_topup(void* ctx, int slot, const int* keep_host, int n, const int* rows_host, int m,
+                                    const long long* coeffs, const uint32_t* tbl_wb, int commit_only, int group_rows,
+                                    uint32_t* pts_n, long long* ys_n, int* rows_dev_n, void* up, void* ev_up) {
+  RoundCtx* c = (RoundCtx*)ctx;
+  if (c == nullptr || slot < 0 || slot >= c->nspec || n < 0 || m < 0 || n + m <= 0 || n + m > c->spec_cap ||
+      up == nullptr || ev_up == nullptr)
+    return -1;
+  int* alive = c->spec_alive[slot];
+  RC_CHECK(hipEventRecord(c->ev_main, c->main));
+  RC_CHECK(hipStreamWaitEvent(c->side, c->ev_main, 0));
+  RC_CHECK(hipMemcpyAsync(alive, keep_host, (size_t)(n + m) * sizeof(int), hipMemcpyHostToDevice, c->side));
+  hipStream_t st = (hipStream_t)up;
+  if (m > 0) {   // (m = 0: every block row was speculative -- only the flags change)
+    RC_CHECK(bsc_shares_msm_ka(coeffs, c->d, rows_host, m, c->tbl_pk, tbl_wb, c->poly, c->T, c->b0, c->nw,
+                               commit_only, alive + n, group_rows, pts_n, ys_n, c->side));
+    RC_CHECK(hipMemcpyAsync(rows_dev_n, rows_host, (size_t)m * sizeof(int), hipMemcpyHostToDevice, st));
+  }
+  RC_CHECK(hipEventRecord((hipEvent_t)ev_up, st));
+  return 0;   // (the aggregation that reads the slot again re-marks it read: spec_mark_read)
+}
+
 // The next round's pre-step (head.py _queue_pre_step) in one call, queued behind everything on main so far
 // (the recovery of W):
 //   gram stream: local SGD step of every local peer (delta, qdelta, loss), event ev_step; then, when

@@ -25,6 +25,7 @@ SIGNATURES = {
     "bsc_sum_rows2_pos": [P, I, P, I, P, I, P, P, P],
     "bsc_round_csum_early": [P, P, P, P, I, P, P, P],
     "bsc_round_spec_msm2": [P, I, P, P, P, I, P, I, I, P, P, P, P, P, P],
+    "bsc_round_spec_topup": [P, I, P, I, P, I, P, P, I, I, P, P, P, P, P],
     "bsc_round_set_spec_ring": [P, P, I, I],
     "bsc_round_set_witness_stream": [P, P],
     "bsc_wave_prio": [I],

@@ -694,6 +694,40 @@ class NativeSecAgg:
         sp.ev_flags = ev_flags
         return sp
 
+    def spec_topup(self, sp: "NativeSpec", keep, extra: list, group_rows: int, up, side) -> "NativeSpec":
+        """A speculative miss: the block's rows missing from sp's MSM (local peer rows `extra`) computed into the same
+        ring slot behind its rows, with the slot's flags re-set from the host-decided block (keep: int32 per sp row).
+        Returns the handle of all n + m rows (its event: the top-up's end on the side stream).  None when sp is not
+        the live slot's handle or the slot is too small (the caller recomputes the rows)."""
+        ring = self.__dict__.get("_spec_ring")
+        if ring is None:
+            return None
+        n, m, cap = len(sp.rows), len(extra), ring["cap"]
+        slot = next((k for k, sl in enumerate(ring["slots"]) if sl["pts"].data_ptr() == sp.pts.data_ptr()), -1)
+        if slot < 0 or n + m > cap or m > 248 or n + m == 0:
+            return None
+        sl = ring["slots"][slot]
+        kh = sl.get("keep")
+        if kh is None:
+            kh = sl["keep"] = torch.empty((cap,), dtype=torch.int32, pin_memory=True)
+        kn = kh.numpy()
+        kn[:n] = keep
+        kn[n:n + m] = 1
+        hn = sl["host"].numpy()
+        hn[n:n + m] = extra
+        ev_up = torch.cuda.Event()
+        ev_up.record(up)   # materialise the handle (re-recorded natively)
+        _check(hip().bsc_round_spec_topup(self.ctx, slot, kh.data_ptr(), n, sl["host"].data_ptr() + 4 * n, m,
+                                          sp.qdelta.data_ptr(), _ptr(self.eng.tbl_wb), 2 if sp.no_commit else 0,
+                                          int(group_rows), sl["pts"][n:].data_ptr(), sl["ys"][n:].data_ptr(),
+                                          sl["rows"].data_ptr() + 4 * n, up.cuda_stream, ev_up.cuda_event),
+               "round_spec_topup")
+        out = NativeSpec(sp.qdelta, list(sp.rows) + list(extra), sl["rows"][:n + m], sl["rows"][cap:cap + n + m],
+                         sl["pts"][:n + m], sl["ys"][:n + m], sp.no_commit)
+        out.record(side)
+        out.ev_up = ev_up
+        return out
+
     def readback(self, clocks: bool = False):
         """Callable: waits for the recovery's read-back -> [status, W_new(, every rank's clock)] numpy views
         (pinned)."""

@@ -20,6 +20,7 @@ from ..ops import bn256 as B
 from ..ops import ml as K
 from ..utils import d2h_into, h2d
 from ..utils import streams as S
+from .head import SPEC_GROUP_ROWS
 
 
 class _Rows:
@@ -287,6 +288,15 @@ class SecAggMixin:
         # computed; every rank takes this branch together (replicated decisions)
         with tm.phase("shares"):
             local_used = [w for w in node_list if w in self.local]
+            sp2 = self._spec_topup(spec, local_used, row_of, qdelta)
+        if sp2 is not None:
+            # a speculative miss: the block's rows the MSM did not cover go into its ring slot behind its rows, the
+            # slot's flags become the block's, and the aggregation reads them all (~2 ms recomputing every block row
+            # with its commitment lanes before; docs/PERF.md, round 6)
+            with tm.phase("recover"):
+                agg = self._spec_aggregate_native(sp2, (contributing, part_of), None, None, flags_set=True)
+                return self._finish_secagg(plan, node_list, commit_of, agg)
+        with tm.phase("shares"):
             pts = ys = ev = None
             rowsel: list = []
             if local_used:
@@ -308,6 +318,27 @@ class SecAggMixin:
             else:
                 agg = self._aggregate(pts, ys, rowsel, contributing, part_of, self._now(plan.iteration))
             return self._finish_secagg(plan, node_list, commit_of, agg)
+
+    def _spec_topup(self, spec, local_used: list, row_of: dict, qdelta):
+        """The host-decided aggregation's rows from the speculative MSM's ring slot, topped up with the block rows it did
+        not cover (NativeSecAgg.spec_topup) -- GPU, native round, an MSM without commitment lanes over this very
+        qdelta (the audit's sums then come from the pre-step's chunk commitments); None otherwise."""
+        na = self._native
+        if not (self.gpu and na is not None and spec is not None and local_used):
+            return None
+        sp = spec[1]
+        if not (sp.no_commit and getattr(sp, "qdelta", None) is qdelta and hasattr(sp, "ev_flags")):
+            return None
+        used = set(local_used)
+        keep = np.fromiter((w in used for w in spec[0]), np.int32, len(spec[0]))
+        have = set(spec[0])
+        extra = [row_of[w] for w in local_used if w not in have]
+        sp2 = na.spec_topup(sp, keep, extra, SPEC_GROUP_ROWS, self.upload_stream, self.side_stream)
+        if sp2 is None:
+            return None
+        S.current().wait_event(sp2.ev)   # the slot's flags and the new rows before the aggregation reads them
+        self.stats["spec_topups"] = self.stats.get("spec_topups", 0) + 1
+        return sp2
 
     def _finish_secagg(self, plan, node_list, commit_of, h):
         """Read back the recovered model (and the ranks' clocks), fall back to least squares for

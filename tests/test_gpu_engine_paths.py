@@ -238,6 +238,8 @@ def test_spec_horizon_same_chain_as_every_candidate(poisoning):
     assert h0 == h1 == h2
     if poisoning:
         assert s2.get("spec_misses", 0) > 0, s2   # rejections among the first cap arrivals: the host path ran
+        # ... topping the speculative slot up with the missing rows (not recomputing every block row)
+        assert s2.get("spec_topups", 0) == s2["spec_misses"], s2
     assert s0.get("spec_head", 0) >= 6 and s1.get("spec_head", 0) >= 6
     assert s0["spec_rows_late"] < 0.9 * s1["spec_rows_late"], (s0["spec_rows_late"], s1["spec_rows_late"])
     print("rows launched after the window", s0["spec_rows_late"], "vs", s1["spec_rows_late"], "misses",
