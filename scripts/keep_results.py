@@ -28,7 +28,8 @@ def main(src: str, dst: str) -> None:
                            f"final_acc {rec.get('final_test_acc')} contributors/block {rec.get('contributors_per_block')}")
         elif f.stem.startswith(("tests", "test_", "smoke")):
             tail = [ln for ln in lines if ln.strip()][-3:]
-            (d / f.name).write_text("\n".join(tail) + "\n")
+            # (a test step's file is named after its -k expression: no spaces in the kept name)
+            (d / f.name.replace(" ", "_")).write_text("\n".join(tail) + "\n")
             summary.append(f"{f.stem}: {tail[-1] if tail else ''}")
     (d / "summary.txt").write_text("\n".join(summary) + "\n")
     print("\n".join(summary))
